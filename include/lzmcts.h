@@ -1,0 +1,130 @@
+/* lzmcts.h — C ABI of the MI355X-native batched MuZero / EfficientZero MCTS tree
+ * (liblzmcts.so, built from lightzero_amd/csrc/lzm_kernels.hip for gfx950).
+ *
+ * Drop-in boundary for LightZero's ctree (reference paths relative to /root/reference):
+ *   lzero/mcts/ctree/ctree_muzero/mz_tree.pyx        (Roots, MinMaxStatsList, ResultsWrapper,
+ *                                                      batch_traverse, batch_backpropagate)
+ *   lzero/mcts/ctree/ctree_efficientzero/ez_tree.pyx (same, + is_reset)
+ *   lzero/mcts/tree_search/mcts_ctree.py:255-321     (per-simulation loop: gather, decode)
+ *   lzero/policy/scaling_transform.py:97-128         (InverseScalarTransform)
+ * Each entry point below names the reference interface it replaces.
+ *
+ * Conventions
+ *  - Every pointer argument is a DEVICE pointer (HBM), unless its name ends in _host.
+ *  - `stream` is a hipStream_t passed as void* (NULL = the null stream). All calls are
+ *    asynchronous on that stream and capture-safe (no host sync, no allocation) except
+ *    lzm_create / lzm_reserve / lzm_destroy.
+ *  - Return value: LZM_OK (0) or a negative lzm_status. No C++ exception crosses the ABI.
+ *  - One handle = one batch of roots (a CRoots + the CSearchResults of its last traverse).
+ *    Not thread-safe; use one handle per stream.
+ *  - Min-max statistics (CMinMaxStatsList) live in a caller-owned float[B*4] device buffer,
+ *    initialised by lzm_minmax_init, exactly as the reference creates one per search.
+ */
+#ifndef LZMCTS_H
+#define LZMCTS_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lzm_handle lzm_handle;
+
+enum lzm_status {
+  LZM_OK = 0,
+  LZM_ERR_ARG = -1,      /* bad argument (null pointer, size out of range) */
+  LZM_ERR_HIP = -2,      /* a HIP runtime call failed */
+  LZM_ERR_CAPACITY = -3, /* latent index beyond the reserved simulations: call lzm_reserve */
+  LZM_ERR_STATE = -4     /* call order violated (e.g. backprop before traverse) */
+};
+
+enum lzm_flags {
+  LZM_TREE_EZ = 1,  /* EfficientZero value-prefix tree (ctree_efficientzero) instead of MuZero */
+  LZM_RNG_FAST = 2  /* per-root counter-based (Philox4x32-10) tie-break stream instead of the
+                       batch-serial glibc rand() stream of the reference (parity mode) */
+};
+
+/* Creates a tree for `num_roots` roots, `action_space` actions, capacity for `max_sims`
+ * simulations per search (grown by lzm_reserve). Replaces Roots.__cinit__ (mz_tree.pyx:29-32)
+ * / CRoots::CRoots (ctree_muzero/lib/cnode.cpp:301-317). */
+int lzm_create(int num_roots, int action_space, int max_sims, int flags, lzm_handle **out);
+int lzm_destroy(lzm_handle *h); /* Roots.__dealloc__ (mz_tree.pyx:53-54) */
+int lzm_reserve(lzm_handle *h, int max_sims);
+int lzm_num_roots(const lzm_handle *h);
+int lzm_sims_capacity(const lzm_handle *h);
+int lzm_action_space(const lzm_handle *h);
+int lzm_flags(const lzm_handle *h);
+const char *lzm_last_error(void);
+
+/* MinMaxStatsList(n) + set_delta (mz_tree.pyx:5-16, common_lib/cminimax.cpp:7-66).
+ * minmax: float[n*4] = {maximum, minimum, value_delta_max, 0} per root. */
+int lzm_minmax_init(float *minmax, int n, float value_delta_max, void *stream);
+
+/* Roots.prepare / prepare_no_noise (mz_tree.pyx:34-40; cnode.cpp:321-358).
+ * legal_actions: int32[B*A], row i = the legal list of root i in the caller's order, padded;
+ * legal_count: int32[B]; noises: float[B*A] matched to legal order, or NULL for
+ * prepare_no_noise; rewards: float[B] (value_prefix for EZ); logits: float[B*A];
+ * to_play: int32[B]. */
+int lzm_roots_prepare(lzm_handle *h, const int32_t *legal_actions, const int32_t *legal_count,
+                      const float *noises, float noise_weight, const float *rewards,
+                      const float *logits, const int32_t *to_play, void *stream);
+
+/* batch_traverse (mz_tree.pyx:95-101; cbatch_traverse cnode.cpp:755-824).
+ * seed: device uint32 read by the kernel = the srand() seed of this call (parity mode) or the
+ * Philox key (fast mode). Outputs int32[B]: x = latent_state_index_in_search_path,
+ * y = latent_state_index_in_batch, action = last_actions, vtp = virtual_to_play_batchs,
+ * len = search_lens (ResultsWrapper.get_search_len). out_action_i64 (int64[B], may be NULL)
+ * is the same action list ready to feed model.recurrent_inference. */
+int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, float *minmax,
+                 const uint32_t *seed, const int32_t *virtual_to_play, int32_t *out_x, int32_t *out_y,
+                 int32_t *out_action, int64_t *out_action_i64, int32_t *out_vtp, int32_t *out_len,
+                 void *stream);
+
+/* Leaf gather: out[i, :] = latent_pool[x[i], i, :] over a pool laid out [S+1][B][row_elems]
+ * (replaces the host loop mcts_ctree.py:283-289). */
+int lzm_gather_latent(lzm_handle *h, const float *latent_pool, int64_t row_elems, const int32_t *x,
+                      float *out, void *stream);
+
+/* batch_backpropagate (mz_tree.pyx:74-80; cbatch_backpropagate cnode.cpp:480-500; EZ
+ * ez_tree.pyx:83-93 with is_reset, ctree_efficientzero/lib/cnode.cpp:577-601). rewards are
+ * value_prefixes for EZ; is_reset int32[B] (EZ only, may be NULL for MZ). */
+int lzm_backprop(lzm_handle *h, int current_latent_state_index, float discount, float *minmax,
+                 const float *rewards, const float *values, const float *logits, const int32_t *to_play,
+                 const int32_t *is_reset, void *stream);
+
+/* Fused decode + expand + backup for one simulation (mcts_ctree.py:300-318 in one kernel):
+ * reward/value heads given as support logits [B][support_len] (categorical != 0, softmax +
+ * expectation + h^-1 as InverseScalarTransform, scaling_transform.py:118-128) or as scalars
+ * [B][1] (categorical == 0, h^-1 only). lstm_horizon > 0 (EZ) applies the reset rule
+ * is_reset = search_len % lstm_horizon == 0 (mcts_ctree.py:810-814) and writes it to
+ * out_is_reset (int32[B], may be NULL). If next_latent and pool_slot are non-NULL the new
+ * latent rows [B][row_elems] are copied into pool_slot (mcts_ctree.py:305). out_decoded
+ * (float[B][2] = {reward, value} after h^-1, may be NULL) exposes what the tree consumed. */
+int lzm_decode_backprop(lzm_handle *h, int current_latent_state_index, float discount, float *minmax,
+                        const float *reward_logits, const float *value_logits, int support_len, int categorical,
+                        const float *policy_logits, const int32_t *to_play, int lstm_horizon,
+                        int32_t *out_is_reset, const float *next_latent, float *pool_slot, int64_t row_elems,
+                        float *out_decoded, void *stream);
+
+/* InverseScalarTransform.__call__ (scaling_transform.py:118-128) alone: out[i] = h^-1(E_p[support]). */
+int lzm_inverse_scalar_transform(const float *logits, int rows, int support_len, int categorical, float *out,
+                                 void *stream);
+
+/* Roots.get_distributions / get_values / get_trajectories (mz_tree.pyx:43-51;
+ * cnode.cpp:369-417). distributions: int32[B*A] in legal order, -1 padded;
+ * values: float[B]; trajectories: int32[B*tmax], -1 padded. */
+int lzm_get_distributions(lzm_handle *h, int32_t *out, void *stream);
+int lzm_get_values(lzm_handle *h, float *out, void *stream);
+int lzm_get_trajectories(lzm_handle *h, int32_t *out, int tmax, void *stream);
+
+/* Diagnostics: traverse passes used by the last parity-mode traverse (device int32[1]). */
+int lzm_last_traverse_passes(lzm_handle *h, int32_t *out, void *stream);
+
+/* Device-side numerics helpers exposed for exhaustive checks. */
+int lzm_debug_expf(const float *x, float *out, int64_t n, void *stream);
+int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream);
+int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*/, int n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

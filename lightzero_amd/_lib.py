@@ -1,0 +1,109 @@
+"""ctypes binding of liblzmcts.so (C ABI: include/lzmcts.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc --offload-arch=gfx950).
+There is no CPU fallback: if the library is missing or no GPU is visible, every entry
+point raises. torch is imported first so that the library binds to the HIP runtime torch
+already loaded (same soname, libamdhip64.so.7), and torch streams / device pointers are
+valid inside it.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblzmcts.so")
+
+LZM_OK = 0
+LZM_ERR_ARG = -1
+LZM_ERR_HIP = -2
+LZM_ERR_CAPACITY = -3
+LZM_ERR_STATE = -4
+LZM_TREE_EZ = 1
+LZM_RNG_FAST = 2
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_i64 = ctypes.c_int64
+_u32 = ctypes.c_uint32
+
+# name -> argtypes (all return int status unless listed in _RESTYPE)
+SIGNATURES = {
+    "lzm_create": [_i, _i, _i, _i, ctypes.POINTER(_vp)],
+    "lzm_destroy": [_vp],
+    "lzm_reserve": [_vp, _i],
+    "lzm_num_roots": [_vp],
+    "lzm_sims_capacity": [_vp],
+    "lzm_action_space": [_vp],
+    "lzm_flags": [_vp],
+    "lzm_last_error": [],
+    "lzm_minmax_init": [_vp, _i, _f, _vp],
+    "lzm_roots_prepare": [_vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp],
+    "lzm_traverse": [_vp, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_gather_latent": [_vp, _vp, _i64, _vp, _vp, _vp],
+    "lzm_backprop": [_vp, _i, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_decode_backprop": [_vp, _i, _f, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i64, _vp, _vp],
+    "lzm_inverse_scalar_transform": [_vp, _i, _i, _i, _vp, _vp],
+    "lzm_get_distributions": [_vp, _vp, _vp],
+    "lzm_get_values": [_vp, _vp, _vp],
+    "lzm_get_trajectories": [_vp, _vp, _i, _vp],
+    "lzm_last_traverse_passes": [_vp, _vp, _vp],
+    "lzm_debug_expf": [_vp, _vp, _i64, _vp],
+    "lzm_debug_glibc_rand": [_u32, _i, _vp, _vp],
+    "lzm_debug_philox": [_vp, _vp, _i, _vp],
+}
+_RESTYPE = {"lzm_last_error": ctypes.c_char_p}
+
+_lib = None
+
+
+class LzmError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load the library without touching the GPU (symbol table only)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise LzmError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(path)
+    for name, args in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
+    _lib = L
+    return L
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise LzmError("lightzero_amd needs a ROCm GPU (MI355X / gfx950); no CPU fallback exists")
+
+
+def check(rc, what):
+    if rc == LZM_OK:
+        return rc
+    msg = (_lib.lzm_last_error() or b"").decode(errors="replace")
+    if rc == LZM_ERR_ARG:
+        raise ValueError(f"{what}: {msg}")
+    raise LzmError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name, *args):
+    L = load()
+    return check(getattr(L, name)(*args), name)
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

@@ -1,0 +1,1218 @@
+// lzm_kernels.hip — MI355X (gfx950) batched MuZero / EfficientZero search tree.
+//
+// Replaces LightZero's ctree (lzero/mcts/ctree/ctree_{muzero,efficientzero}) and the per-
+// simulation glue of lzero/mcts/tree_search/mcts_ctree.py with device kernels over a
+// structure-of-arrays tree held in HBM. C ABI: include/lzmcts.h.
+//
+// Layout (per handle, B roots, A actions, node capacity C = 1 + A*(S_cap+1)):
+//   stat[node][root]  16 B {visit, value_sum, prior, reward|value_prefix}
+//   meta[node][root]  16 B {latent index (-1 = not expanded), to_play, best_action, is_reset}
+// node-major with the root index fastest, so lanes of a wave that sit on the same node id
+// (the root, its children) read one contiguous 1 KiB line per wave instruction. The node
+// expanded with latent index L (root 0, simulation k's leaf k+1) owns children
+// [1 + A*L, 1 + A*L + A) — the reference's std::map<int,CNode> children (cnode.h:26)
+// without allocation. Search paths of the last traverse: path[level][root].
+//
+// Arithmetic follows the reference expression by expression in fp32 (compiled with
+// -ffp-contract=off, IEEE division/sqrt), expf is the glibc port of lzm_numerics.h, and
+// log((N+base+1)/base)+init and sqrt(N) over the integer parent count N come from a host
+// table built with the host's libm (the very functions the reference calls).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "../../include/lzmcts.h"
+#include "lzm_numerics.h"
+
+namespace lzm {
+
+constexpr float kFloatMax = 1000000.0f;  // common_lib/cminimax.h:9-10
+constexpr float kFloatMin = -kFloatMax;
+constexpr int kMaxActions = 64;          // tie lists are held as one 64-bit mask
+constexpr int kMaxWG = 1024;
+
+struct alignas(16) NodeStat {
+  int visit;
+  float value_sum;
+  float prior;
+  float reward;  // value_prefix for EfficientZero
+};
+struct alignas(16) NodeMeta {
+  int latent;  // current_latent_state_index, -1 while not expanded
+  int to_play;
+  int best;  // best_action
+  int is_reset;
+};
+
+struct TreeView {
+  NodeStat *stat;
+  NodeMeta *meta;
+  const int32_t *legal;   // [B][A]
+  const int32_t *nlegal;  // [B]
+  int32_t *path;          // [D][B] node ids
+  int32_t *path_act;      // [D][B] actions
+  int32_t *pathlen;       // [B] edges of the last path
+  const float2 *lut;      // [N] {log((N+base+1)/base)+init, sqrt(N)}
+  int B, A, cap, lut_n, depth_cap;
+};
+
+__device__ inline size_t nidx(const TreeView &t, int node, int i) { return (size_t)node * t.B + i; }
+__device__ inline float node_value(const NodeStat &s) {  // CNode::value, cnode.cpp:219-235
+  return s.visit == 0 ? 0.0f : s.value_sum / (float)s.visit;
+}
+__device__ inline int legal_at(const TreeView &t, int i, int node, int j) {
+  return node == 0 ? t.legal[(size_t)i * t.A + j] : j;
+}
+__device__ inline int legal_n(const TreeView &t, int i, int node) { return node == 0 ? t.nlegal[i] : t.A; }
+
+// CMinMaxStats::normalize, common_lib/cminimax.cpp:33-45
+__device__ inline float mm_normalize(float4 mm, float v) {
+  float norm = v;
+  float delta = mm.x - mm.y;
+  if (delta > 0) {
+    if (delta < mm.z)
+      norm = (norm - mm.y) / mm.z;
+    else
+      norm = (norm - mm.y) / delta;
+  }
+  return norm;
+}
+
+// Result of one root's descent.
+struct Descent {
+  int len, x, action, vtp, leaf;
+};
+
+// One root's selection walk (cbatch_traverse body, cnode.cpp:783-823 with compute_mean_q
+// :169-203, cselect_child :551-596, cucb_score :655-699; EZ variants
+// ctree_efficientzero/lib/cnode.cpp:173-212, :756-814). `draw(level)` returns the rand()
+// value consumed at that level. Writes path/path_act; never writes tree state.
+template <bool EZ, typename Draw>
+__device__ inline Descent descend(const TreeView &t, int i, float4 mm, int players, int vtp, float disc, Draw draw) {
+  int node = 0, is_root = 1, len = 0, last_action = -1, parent = 0;
+  float parent_q = 0.0f;  // per root; the reference's cross-root carry is provably 0 wherever read
+  NodeStat s = t.stat[nidx(t, 0, i)];
+  NodeMeta m = t.meta[nidx(t, 0, i)];
+  t.path[i] = 0;
+  while (m.latent >= 0 && len < t.depth_cap - 1) {
+    const int n = legal_n(t, i, node);
+    const int base = 1 + t.A * m.latent;
+    const float pvp = s.reward;
+    const int preset = m.is_reset;
+    // compute_mean_q
+    float total_q = 0.0f;
+    int total_v = 0;
+    for (int j = 0; j < n; ++j) {
+      const int a = legal_at(t, i, node, j);
+      const NodeStat c = t.stat[nidx(t, base + a, i)];
+      if (c.visit > 0) {
+        float tr = c.reward;
+        if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
+        float qsa = tr + disc * node_value(c);
+        total_q += qsa;
+        total_v += 1;
+      }
+    }
+    float mean_q;
+    if (is_root && total_v > 0)
+      mean_q = total_q / (float)total_v;
+    else
+      mean_q = (parent_q + total_q) / (float)(total_v + 1);
+    is_root = 0;
+    parent_q = mean_q;
+    // cselect_child / cucb_score
+    int N = s.visit - 1;
+    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
+    const float2 L = t.lut[N];
+    float max_score = kFloatMin;
+    uint64_t mask = 0;
+    for (int j = 0; j < n; ++j) {
+      const int a = legal_at(t, i, node, j);
+      const NodeStat c = t.stat[nidx(t, base + a, i)];
+      float pb_c = L.x;
+      pb_c *= (L.y / (float)(c.visit + 1));
+      const float prior_score = pb_c * c.prior;
+      float vs;
+      if (c.visit == 0) {
+        vs = mean_q;
+      } else {
+        float tr = c.reward;
+        if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
+        if (players == 1)
+          vs = tr + disc * node_value(c);
+        else
+          vs = tr + disc * (-node_value(c));
+      }
+      vs = mm_normalize(mm, vs);
+      if (vs < 0) vs = 0;
+      if (vs > 1) vs = 1;
+      const float score = prior_score + vs;
+      if (max_score < score) {
+        max_score = score;
+        mask = 1ull << j;
+      } else if (score >= max_score - 0.000001f) {
+        mask |= 1ull << j;
+      }
+    }
+    const uint32_t r = draw(len);
+    const int nl = __popcll(mask);
+    int k = (int)(r % (uint32_t)nl);
+    uint64_t mm_ = mask;
+    for (; k > 0; --k) mm_ &= mm_ - 1;
+    const int jsel = __ffsll((long long)mm_) - 1;
+    const int action = legal_at(t, i, node, jsel);
+    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+    t.path_act[(size_t)len * t.B + i] = action;
+    parent = node;
+    node = base + action;
+    last_action = action;
+    ++len;
+    t.path[(size_t)len * t.B + i] = node;
+    s = t.stat[nidx(t, node, i)];
+    m = t.meta[nidx(t, node, i)];
+  }
+  Descent d;
+  d.len = len;
+  d.x = t.meta[nidx(t, parent, i)].latent;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
+struct TraverseArgs {
+  TreeView t;
+  const float4 *minmax;
+  const uint32_t *seed;
+  const int32_t *vtp_in;
+  int32_t *out_x, *out_y, *out_a, *out_vtp, *out_len;
+  long long *out_a64;
+  uint32_t *stream;  // raw glibc stream values (before >> 1)
+  int stream_cap;
+  const uint32_t *jfirst;  // [kMaxWG][31]
+  const uint32_t *jnext;   // [kMaxWG][31]
+  int32_t *off;            // [B]
+  int32_t *diag;           // [0] passes, [1] overflow-error
+  int32_t *hint;           // [0] stream length used by the previous call
+  float disc;
+};
+
+__device__ inline int block_players(const int32_t *vtp, int B) {
+  // players = (max(virtual_to_play) == -1) ? 1 : 2  (cnode.cpp:776-781)
+  __shared__ int s_max;
+  if (threadIdx.x == 0) s_max = INT_MIN;
+  __syncthreads();
+  int m = INT_MIN;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) m = max(m, vtp[i]);
+  atomicMax(&s_max, m);
+  __syncthreads();
+  int p = (s_max == -1) ? 1 : 2;
+  __syncthreads();
+  return p;
+}
+
+// Block-wide exclusive scan (blockDim multiple of 64, <= 1024).
+__device__ inline int block_excl_scan(int v, int *s_w, int &total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) s_w[wid] = x;
+  __syncthreads();
+  if (wid == 0) {
+    int w = lane < nw ? s_w[lane] : 0;
+#pragma unroll
+    for (int d = 1; d < 16; d <<= 1) {
+      int y = __shfl_up(w, d, 64);
+      if (lane >= d) w += y;
+    }
+    if (lane < nw) s_w[lane] = w;
+  }
+  __syncthreads();
+  const int pre = wid > 0 ? s_w[wid - 1] : 0;
+  total = s_w[nw - 1];
+  __syncthreads();
+  return pre + x - v;
+}
+
+// Parity-mode traverse: ONE workgroup walks every root, because the reference consumes one
+// process-wide rand() stream in root order (root i's draws start at sum_{j<i} depth_j).
+// The walk is speculative: descend every root with assumed offsets, scan the depths, and
+// repeat until the offsets reproduce themselves (the unique fixed point = the serial
+// order). A tie among unexpanded children never changes a depth, so two passes is typical.
+// The glibc stream is produced 1 block-width at a time by a jump matrix over Z/2^32:
+// z[n+m] = sum_j J[m][j] * z[n-31+j] (random_r is linear in its 31-word state).
+template <bool EZ>
+__global__ __launch_bounds__(1024) void traverse_glibc_kernel(TraverseArgs p) {
+  const TreeView &t = p.t;
+  const int W = blockDim.x, tid = threadIdx.x, B = t.B;
+  __shared__ uint32_t s_win[31];
+  __shared__ uint32_t s_z0[31];
+  __shared__ uint32_t s_tail[31];
+  __shared__ int s_w[16];
+  __shared__ int s_flag;
+  const int players = block_players(p.vtp_in, B);
+  if (tid == 0) glibc_seed_state(*p.seed, s_z0);
+  uint32_t jn[31];
+#pragma unroll
+  for (int j = 0; j < 31; ++j) jn[j] = p.jnext[tid * 31 + j];
+  __syncthreads();
+  int generated = 0;
+  auto gen_chunk = [&]() {
+    uint32_t v = 0;
+    if (generated == 0) {
+#pragma unroll
+      for (int j = 0; j < 31; ++j) v += p.jfirst[tid * 31 + j] * s_z0[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 31; ++j) v += jn[j] * s_win[j];
+    }
+    if (generated + tid < p.stream_cap) p.stream[generated + tid] = v;
+    if (tid >= W - 31) s_tail[tid - (W - 31)] = v;
+    __syncthreads();
+    if (tid < 31) s_win[tid] = s_tail[tid];
+    generated += W;
+    __syncthreads();
+  };
+  // first chunk(s): enough for the previous call's total
+  int want = *p.hint + W;
+  if (want > p.stream_cap) want = p.stream_cap;
+  do {
+    gen_chunk();
+  } while (generated < want);
+
+  const int rounds = (B + W - 1) / W;
+  for (int r = 0; r < rounds; ++r) {
+    int i = r * W + tid;
+    if (i < B) p.off[i] = 0;
+  }
+  __syncthreads();
+  int passes = 0;
+  for (;;) {
+    ++passes;
+    if (tid == 0) s_flag = 0;
+    __syncthreads();
+    int carry = 0, overflow = 0, changed = 0;
+    for (int r = 0; r < rounds; ++r) {
+      const int i = r * W + tid;
+      int depth = 0;
+      if (i < B) {
+        const int off = p.off[i];
+        const int gen = generated;
+        const uint32_t *st = p.stream;
+        auto draw = [&](int level) -> uint32_t {
+          const int pos = off + level;
+          if (pos < gen) return st[pos] >> 1;
+          overflow = 1;
+          return 0u;
+        };
+        Descent d = descend<EZ>(t, i, p.minmax[i], players, p.vtp_in[i], p.disc, draw);
+        depth = d.len;
+        p.out_x[i] = d.x;
+        p.out_y[i] = i;
+        p.out_a[i] = d.action;
+        if (p.out_a64) p.out_a64[i] = d.action;
+        p.out_vtp[i] = d.vtp;
+        p.out_len[i] = d.len;
+        t.pathlen[i] = d.len;
+      }
+      int total;
+      const int ex = block_excl_scan(depth, s_w, total);
+      if (i < B) {
+        const int noff = carry + ex;
+        if (noff != p.off[i]) changed = 1;
+        p.off[i] = noff;
+      }
+      carry += total;
+    }
+    if (changed || overflow) s_flag = 1;  // benign race: every writer stores 1
+    __syncthreads();
+    const int again = s_flag;
+    __syncthreads();
+    if (carry > generated && generated < p.stream_cap) {
+      while (generated < carry && generated < p.stream_cap) gen_chunk();
+    }
+    if (!again) {
+      if (tid == 0) *p.hint = carry;
+      break;
+    }
+    if (passes > B + 2) {  // cannot happen: the fixed point is reached in <= B+1 passes
+      if (tid == 0) p.diag[1] = 1;
+      break;
+    }
+  }
+  // commit best_action along the final paths (cnode.cpp:806)
+  for (int r = 0; r < rounds; ++r) {
+    const int i = r * W + tid;
+    if (i >= B) continue;
+    const int len = t.pathlen[i];
+    for (int l = 0; l < len; ++l) {
+      const int node = t.path[(size_t)l * B + i];
+      t.meta[nidx(t, node, i)].best = t.path_act[(size_t)l * B + i];
+    }
+  }
+  if (tid == 0) p.diag[0] = passes;
+}
+
+// Fast-mode traverse: roots are independent (Philox4x32-10 draw per (seed, root, level)), so
+// one lane per root over as many workgroups as needed.
+template <bool EZ>
+__global__ __launch_bounds__(256) void traverse_fast_kernel(TraverseArgs p) {
+  const TreeView &t = p.t;
+  const int players = block_players(p.vtp_in, t.B);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.B) return;
+  const uint32_t seed = *p.seed;
+  auto draw = [&](int level) -> uint32_t {
+    uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)i, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
+    return o.x >> 1;
+  };
+  Descent d = descend<EZ>(t, i, p.minmax[i], players, p.vtp_in[i], p.disc, draw);
+  p.out_x[i] = d.x;
+  p.out_y[i] = i;
+  p.out_a[i] = d.action;
+  if (p.out_a64) p.out_a64[i] = d.action;
+  p.out_vtp[i] = d.vtp;
+  p.out_len[i] = d.len;
+  t.pathlen[i] = d.len;
+  for (int l = 0; l < d.len; ++l) {
+    const int node = t.path[(size_t)l * t.B + i];
+    t.meta[nidx(t, node, i)].best = t.path_act[(size_t)l * t.B + i];
+  }
+}
+
+// CNode::expand of a non-root leaf (cnode.cpp:83-147): all A actions legal, masked-softmax
+// priors with glibc expf, sequential sum; children reset to CNode(prior, {}).
+__device__ inline void expand_leaf(const TreeView &t, int i, int leaf, int to_play, int latent, float reward,
+                                   const float *logits, int is_reset, bool ez) {
+  NodeMeta m = t.meta[nidx(t, leaf, i)];
+  m.latent = latent;
+  m.to_play = to_play;
+  if (ez) m.is_reset = is_reset;
+  t.meta[nidx(t, leaf, i)] = m;
+  t.stat[nidx(t, leaf, i)].reward = reward;
+  float pmax = kFloatMin;
+  for (int a = 0; a < t.A; ++a)
+    if (pmax < logits[a]) pmax = logits[a];
+  float sum = 0.0f;
+  for (int a = 0; a < t.A; ++a) sum += glibc_expf(logits[a] - pmax);
+  const int base = 1 + t.A * latent;
+  for (int a = 0; a < t.A; ++a) {
+    const float e = glibc_expf(logits[a] - pmax);
+    NodeStat c;
+    c.visit = 0;
+    c.value_sum = 0.0f;
+    c.prior = e / sum;
+    c.reward = 0.0f;
+    t.stat[nidx(t, base + a, i)] = c;
+    NodeMeta cm;
+    cm.latent = -1;
+    cm.to_play = 0;
+    cm.best = -1;
+    cm.is_reset = 0;
+    t.meta[nidx(t, base + a, i)] = cm;
+  }
+}
+
+// cbackpropagate: MuZero cnode.cpp:419-478, EfficientZero
+// ctree_efficientzero/lib/cnode.cpp:482-575.
+template <bool EZ>
+__device__ inline void backup(const TreeView &t, int i, float4 *mm_ptr, int to_play, float value, float disc) {
+  float4 mm = *mm_ptr;
+  const int len = t.pathlen[i];
+  float b = value;
+  float child_prefix_parent = 0.0f;  // unused for MZ
+  (void)child_prefix_parent;
+  for (int l = len; l >= 0; --l) {
+    const int node = t.path[(size_t)l * t.B + i];
+    NodeStat s = t.stat[nidx(t, node, i)];
+    const int ntp = t.meta[nidx(t, node, i)].to_play;
+    if (to_play == -1 || ntp == to_play)
+      s.value_sum += b;
+    else
+      s.value_sum += -b;
+    s.visit += 1;
+    t.stat[nidx(t, node, i)] = s;
+    const float v = node_value(s);
+    if (!EZ) {
+      const float tr = s.reward;
+      float q;
+      if (to_play == -1) {
+        q = tr + disc * v;
+        b = tr + disc * b;
+      } else {
+        q = tr + disc * -v;
+        b = (ntp == to_play) ? (-tr + disc * b) : (tr + disc * b);
+      }
+      if (q > mm.x) mm.x = q;
+      if (q < mm.y) mm.y = q;
+    } else {
+      float pvp = 0.0f;
+      int reset = 0;
+      if (l >= 1) {
+        const int pn = t.path[(size_t)(l - 1) * t.B + i];
+        pvp = t.stat[nidx(t, pn, i)].reward;
+        reset = t.meta[nidx(t, pn, i)].is_reset;
+      }
+      float tr = s.reward - pvp;
+      const float q = tr + disc * v;
+      if (q > mm.x) mm.x = q;
+      if (q < mm.y) mm.y = q;
+      if (reset == 1) tr = s.reward;
+      if (to_play == -1 || ntp != to_play)
+        b = tr + disc * b;
+      else
+        b = -tr + disc * b;
+    }
+  }
+  *mm_ptr = mm;
+}
+
+struct BackpropArgs {
+  TreeView t;
+  float4 *minmax;
+  const float *rewards, *values, *logits;
+  const int32_t *to_play, *is_reset;
+  int cur;
+  float disc;
+};
+
+template <bool EZ>
+__global__ __launch_bounds__(256) void backprop_kernel(BackpropArgs p) {
+  const TreeView &t = p.t;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.B) return;
+  const int leaf = t.path[(size_t)t.pathlen[i] * t.B + i];
+  const int tp = p.to_play[i];
+  expand_leaf(t, i, leaf, tp, p.cur, p.rewards[i], p.logits + (size_t)i * t.A, p.is_reset ? p.is_reset[i] : 0, EZ);
+  backup<EZ>(t, i, p.minmax + i, tp, p.values[i], p.disc);
+}
+
+// InverseScalarTransform (scaling_transform.py:118-128) of one row by one wave:
+// softmax (unless `raw`), expectation over support [-(V-1)/2 .. (V-1)/2], then h^-1.
+__device__ inline float wave_support_expectation(const float *row, int V, bool softmax) {
+  const int lane = threadIdx.x & 63;
+  const float half = (float)((V - 1) / 2);
+  if (!softmax) {
+    float acc = 0.0f;
+    for (int j = lane; j < V; j += 64) acc += row[j] * ((float)j - half);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+    return acc;
+  }
+  float mx = -INFINITY;
+  for (int j = lane; j < V; j += 64) mx = fmaxf(mx, row[j]);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+  float sum = 0.0f;
+  for (int j = lane; j < V; j += 64) sum += expf(row[j] - mx);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  float acc = 0.0f;
+  for (int j = lane; j < V; j += 64) acc += (expf(row[j] - mx) / sum) * ((float)j - half);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  return acc;
+}
+
+__device__ inline float h_inverse(float value) {
+  const float eps = 0.001f;
+  float tmp = (sqrtf(1.0f + 0.004f * (fabsf(value) + 1.0f + eps)) - 1.0f) * (1.0f / 0.002f);
+  float sgn = value > 0.0f ? 1.0f : (value < 0.0f ? -1.0f : 0.0f);
+  return sgn * (tmp * tmp - 1.0f);
+}
+
+__device__ inline float wave_row_sum(const float *row, int V) {
+  const int lane = threadIdx.x & 63;
+  float s = 0.0f;
+  for (int j = lane; j < V; j += 64) s += row[j];
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  return s;
+}
+
+struct DecodeArgs {
+  TreeView t;
+  float4 *minmax;
+  const float *reward_logits, *value_logits, *policy_logits;
+  const int32_t *to_play;
+  int32_t *out_is_reset;
+  const float *next_latent;
+  float *pool_slot;
+  long long row_elems;
+  int V, categorical, cur, horizon;
+  float disc;
+  float *out_decoded;  // [B][2] {reward, value} after h^-1, optional
+};
+
+// ensure_softmax (scaling_transform.py:36-62): softmax is skipped only when EVERY row of the
+// batch already sums to 1 within allclose(atol=1e-5, rtol=1e-5). Pass 1 clears a word per
+// call and tensor (flag[0]: reward rows, flag[1]: value rows — the reference calls the
+// transform once per head); this kernel ANDs each row's verdict into its word.
+__global__ __launch_bounds__(256) void normalized_check_kernel(const float *a, const float *b, int rows, int V,
+                                                               int32_t *flag) {
+  const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (w >= 2 * rows) return;
+  const float *row = (w < rows) ? a + (size_t)w * V : b + (size_t)(w - rows) * V;
+  const float s = wave_row_sum(row, V);
+  if ((threadIdx.x & 63) == 0 && !(fabsf(s - 1.0f) <= 1e-5f + 1e-5f)) atomicAnd(flag + (w < rows ? 0 : 1), 0);
+}
+
+template <bool EZ>
+__global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, const int32_t *norm_flag) {
+  const TreeView &t = p.t;
+  const int lane = threadIdx.x & 63;
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per root
+  if (i >= t.B) return;
+  // new latent row into the pool slot (mcts_ctree.py:305)
+  if (p.next_latent && p.pool_slot) {
+    const float *src = p.next_latent + (size_t)i * p.row_elems;
+    float *dst = p.pool_slot + (size_t)i * p.row_elems;
+    for (long long e = lane; e < p.row_elems; e += 64) dst[e] = src[e];
+  }
+  float r, v;
+  if (p.categorical) {
+    r = wave_support_expectation(p.reward_logits + (size_t)i * p.V, p.V, norm_flag[0] == 0);
+    v = wave_support_expectation(p.value_logits + (size_t)i * p.V, p.V, norm_flag[1] == 0);
+  } else {
+    r = p.reward_logits[(size_t)i * p.V];
+    v = p.value_logits[(size_t)i * p.V];
+  }
+  r = h_inverse(r);
+  v = h_inverse(v);
+  if (lane != 0) return;
+  if (p.out_decoded) {
+    p.out_decoded[2 * i] = r;
+    p.out_decoded[2 * i + 1] = v;
+  }
+  const int len = t.pathlen[i];
+  const int leaf = t.path[(size_t)len * t.B + i];
+  int is_reset = 0;
+  if (EZ && p.horizon > 0) is_reset = (len % p.horizon == 0) ? 1 : 0;
+  if (p.out_is_reset) p.out_is_reset[i] = is_reset;
+  const int tp = p.to_play[i];
+  expand_leaf(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, is_reset, EZ);
+  backup<EZ>(t, i, p.minmax + i, tp, v, p.disc);
+}
+
+__global__ __launch_bounds__(256) void inverse_transform_kernel(const float *logits, int rows, int V, int categorical,
+                                                                const int32_t *norm_flag, float *out) {
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (i >= rows) return;
+  float v;
+  if (categorical) {
+    v = wave_support_expectation(logits + (size_t)i * V, V, norm_flag[0] == 0);
+  } else {
+    v = logits[(size_t)i * V];
+  }
+  if ((threadIdx.x & 63) == 0) out[i] = h_inverse(v);
+}
+
+__global__ void set_word_kernel(int32_t *w, int32_t v) { *w = v; }
+
+// CRoots::prepare / prepare_no_noise (cnode.cpp:321-358): expand each root over its legal list
+// (an empty list means every action, cnode.cpp:101-107), optional Dirichlet mix
+// (add_exploration_noise :149-167), visit_count = 1.
+struct PrepareArgs {
+  NodeStat *stat;
+  NodeMeta *meta;
+  int32_t *legal, *nlegal;
+  const int32_t *legal_in, *count_in, *to_play;
+  const float *noises, *rewards, *logits;
+  float noise_weight;
+  int B, A;
+};
+
+__global__ __launch_bounds__(256) void prepare_kernel(PrepareArgs p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.B) return;
+  const int A = p.A;
+  int n = p.count_in[i];
+  if (n <= 0) {
+    n = A;
+    for (int a = 0; a < A; ++a) p.legal[(size_t)i * A + a] = a;
+  } else {
+    for (int j = 0; j < A; ++j) p.legal[(size_t)i * A + j] = j < n ? p.legal_in[(size_t)i * A + j] : -1;
+  }
+  p.nlegal[i] = n;
+  const float *lg = p.logits + (size_t)i * A;
+  float pmax = kFloatMin;
+  for (int j = 0; j < n; ++j) {
+    const float l = lg[p.legal[(size_t)i * A + j]];
+    if (pmax < l) pmax = l;
+  }
+  float sum = 0.0f;
+  for (int j = 0; j < n; ++j) sum += glibc_expf(lg[p.legal[(size_t)i * A + j]] - pmax);
+  const float f = p.noise_weight;
+  for (int j = 0; j < n; ++j) {
+    const int a = p.legal[(size_t)i * A + j];
+    float prior = glibc_expf(lg[a] - pmax) / sum;
+    if (p.noises) {
+      const float noise = p.noises[(size_t)i * A + j];
+      prior = prior * (1 - f) + noise * f;
+    }
+    NodeStat c;
+    c.visit = 0;
+    c.value_sum = 0.0f;
+    c.prior = prior;
+    c.reward = 0.0f;
+    p.stat[(size_t)(1 + a) * p.B + i] = c;
+    NodeMeta cm;
+    cm.latent = -1;
+    cm.to_play = 0;
+    cm.best = -1;
+    cm.is_reset = 0;
+    p.meta[(size_t)(1 + a) * p.B + i] = cm;
+  }
+  NodeStat r;
+  r.visit = 1;
+  r.value_sum = 0.0f;
+  r.prior = 0.0f;
+  r.reward = p.rewards[i];
+  p.stat[i] = r;
+  NodeMeta rm;
+  rm.latent = 0;
+  rm.to_play = p.to_play[i];
+  rm.best = -1;
+  rm.is_reset = 0;
+  p.meta[i] = rm;
+}
+
+__global__ void minmax_init_kernel(float4 *mm, int n, float delta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) mm[i] = make_float4(kFloatMin, kFloatMax, delta, 0.0f);
+}
+
+__global__ void gather_kernel(const float *pool, long long row, int B, const int32_t *x, float *out) {
+  const long long total = (long long)B * row;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(e / row);
+    const long long c = e - (long long)i * row;
+    out[e] = pool[((long long)x[i] * B + i) * row + c];
+  }
+}
+
+__global__ void gather_kernel_v4(const float4 *pool, long long row4, int B, const int32_t *x, float4 *out) {
+  const long long total = (long long)B * row4;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(e / row4);
+    const long long c = e - (long long)i * row4;
+    out[e] = pool[((long long)x[i] * B + i) * row4 + c];
+  }
+}
+
+__global__ void distributions_kernel(TreeView t, int32_t *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.B) return;
+  const NodeMeta rm = t.meta[i];
+  for (int j = 0; j < t.A; ++j) {
+    int v = -1;
+    if (rm.latent >= 0 && j < t.nlegal[i]) v = t.stat[nidx(t, 1 + t.A * rm.latent + t.legal[(size_t)i * t.A + j], i)].visit;
+    out[(size_t)i * t.A + j] = v;
+  }
+}
+
+__global__ void values_kernel(TreeView t, float *out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < t.B) out[i] = node_value(t.stat[i]);
+}
+
+__global__ void trajectories_kernel(TreeView t, int32_t *out, int tmax) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.B) return;
+  int node = 0, n = 0;
+  NodeMeta m = t.meta[nidx(t, 0, i)];
+  while (m.best >= 0 && n < tmax && m.latent >= 0) {
+    out[(size_t)i * tmax + n++] = m.best;
+    node = 1 + t.A * m.latent + m.best;
+    m = t.meta[nidx(t, node, i)];
+  }
+  for (; n < tmax; ++n) out[(size_t)i * tmax + n] = -1;
+}
+
+__global__ void debug_expf_kernel(const float *x, float *out, long long n) {
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long long)gridDim.x * blockDim.x)
+    out[e] = glibc_expf(x[e]);
+}
+
+__global__ void debug_philox_kernel(const uint32_t *ck, uint32_t *out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t *c = ck + (size_t)i * 6;
+  uint4 o = philox4x32_10(make_uint4(c[0], c[1], c[2], c[3]), make_uint2(c[4], c[5]));
+  out[(size_t)i * 4 + 0] = o.x;
+  out[(size_t)i * 4 + 1] = o.y;
+  out[(size_t)i * 4 + 2] = o.z;
+  out[(size_t)i * 4 + 3] = o.w;
+}
+
+__global__ void debug_glibc_kernel(uint32_t seed, int n, int32_t *out, const uint32_t *jfirst, const uint32_t *jnext) {
+  // single workgroup; exercises the same jump-matrix generator as traverse_glibc_kernel
+  __shared__ uint32_t s_z0[31], s_win[31], s_tail[31];
+  const int W = blockDim.x, tid = threadIdx.x;
+  if (tid == 0) glibc_seed_state(seed, s_z0);
+  __syncthreads();
+  for (int g = 0; g < n; g += W) {
+    uint32_t v = 0;
+    for (int j = 0; j < 31; ++j) v += (g == 0 ? jfirst[tid * 31 + j] * s_z0[j] : jnext[tid * 31 + j] * s_win[j]);
+    if (g + tid < n) out[g + tid] = (int32_t)(v >> 1);
+    if (tid >= W - 31) s_tail[tid - (W - 31)] = v;
+    __syncthreads();
+    if (tid < 31) s_win[tid] = s_tail[tid];
+    __syncthreads();
+  }
+}
+
+}  // namespace lzm
+
+// ============================================================================ host side
+using namespace lzm;
+
+static thread_local char g_err[512];
+static void set_err(const char *msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
+#define LZM_HIP(call)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess) {                                                                        \
+      snprintf(g_err, sizeof(g_err), "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return LZM_ERR_HIP;                                                                          \
+    }                                                                                              \
+  } while (0)
+#define LZM_CHECK_LAUNCH() LZM_HIP(hipGetLastError())
+
+struct lzm_handle {
+  int B, A, flags, sims_cap, cap, depth_cap;
+  NodeStat *stat = nullptr;
+  NodeMeta *meta = nullptr;
+  int32_t *legal = nullptr, *nlegal = nullptr, *path = nullptr, *path_act = nullptr, *pathlen = nullptr;
+  int32_t *off = nullptr, *diag = nullptr, *hint = nullptr, *norm_flag = nullptr;
+  uint32_t *stream = nullptr;
+  int stream_cap = 0;
+  float2 *lut = nullptr;
+  int lut_n = 0;
+  int lut_base = -1;
+  float lut_init = -1.0f;
+  uint32_t *jmat = nullptr;  // [2][kMaxWG][31]
+};
+
+// Jump matrices of glibc random_r: row m of J_first expresses z[344+m] (the m-th rand()
+// output before >>1) in the 31-word seeded state; row m of J_next expresses z[n+m] in the
+// window z[n-31..n-1]. Coefficients over Z/2^32 (wrapping uint32 arithmetic).
+static void build_jump_matrices(std::vector<uint32_t> &jf, std::vector<uint32_t> &jn) {
+  const int W = kMaxWG;
+  jf.assign((size_t)W * 31, 0u);
+  jn.assign((size_t)W * 31, 0u);
+  {
+    const int N = 344 + W;
+    std::vector<uint32_t> z((size_t)N * 31, 0u);
+    for (int j = 0; j < 31; ++j) z[(size_t)j * 31 + j] = 1u;
+    for (int j = 31; j < 34; ++j)
+      for (int c = 0; c < 31; ++c) z[(size_t)j * 31 + c] = z[(size_t)(j - 31) * 31 + c];
+    for (int n = 34; n < N; ++n)
+      for (int c = 0; c < 31; ++c) z[(size_t)n * 31 + c] = z[(size_t)(n - 31) * 31 + c] + z[(size_t)(n - 3) * 31 + c];
+    for (int m = 0; m < W; ++m)
+      for (int c = 0; c < 31; ++c) jf[(size_t)m * 31 + c] = z[(size_t)(344 + m) * 31 + c];
+  }
+  {
+    const int N = 31 + W;
+    std::vector<uint32_t> z((size_t)N * 31, 0u);
+    for (int j = 0; j < 31; ++j) z[(size_t)j * 31 + j] = 1u;
+    for (int n = 31; n < N; ++n)
+      for (int c = 0; c < 31; ++c) z[(size_t)n * 31 + c] = z[(size_t)(n - 31) * 31 + c] + z[(size_t)(n - 3) * 31 + c];
+    for (int m = 0; m < W; ++m)
+      for (int c = 0; c < 31; ++c) jn[(size_t)m * 31 + c] = z[(size_t)(31 + m) * 31 + c];
+  }
+}
+
+static TreeView view(lzm_handle *h) {
+  TreeView t;
+  t.stat = h->stat;
+  t.meta = h->meta;
+  t.legal = h->legal;
+  t.nlegal = h->nlegal;
+  t.path = h->path;
+  t.path_act = h->path_act;
+  t.pathlen = h->pathlen;
+  t.lut = h->lut;
+  t.B = h->B;
+  t.A = h->A;
+  t.cap = h->cap;
+  t.lut_n = h->lut_n;
+  t.depth_cap = h->depth_cap;
+  return t;
+}
+
+static void dfree(void *p) {
+  if (p) (void)hipFree(p);
+}
+
+static void free_tree(lzm_handle *h) {
+  dfree(h->stat); dfree(h->meta); dfree(h->path); dfree(h->path_act); dfree(h->stream); dfree(h->lut);
+  h->stat = nullptr; h->meta = nullptr; h->path = nullptr; h->path_act = nullptr; h->stream = nullptr; h->lut = nullptr;
+}
+
+// pb_c table over the integer parent count N = visit-1 (cucb_score, cnode.cpp:673-674):
+// {logf(((N + base) + 1) / base) + init, sqrtf(N)} with the host libm, -ffp-contract=off.
+static int fill_lut(lzm_handle *h, int base, float init) {
+  if (h->lut_base == base && h->lut_init == init) return LZM_OK;
+  std::vector<float2> lut(h->lut_n);
+  const float fb = (float)base;
+  for (int n = 0; n < h->lut_n; ++n) {
+    volatile float N = (float)n;
+    volatile float num = N + fb;
+    num = num + 1;
+    volatile float q = num / fb;
+    float pbc = logf(q) + init;
+    lut[n] = make_float2(pbc, sqrtf(N));
+  }
+  LZM_HIP(hipMemcpy(h->lut, lut.data(), sizeof(float2) * h->lut_n, hipMemcpyHostToDevice));
+  h->lut_base = base;
+  h->lut_init = init;
+  return LZM_OK;
+}
+
+static int alloc_tree(lzm_handle *h, int sims) {
+  h->sims_cap = sims;
+  h->cap = 1 + h->A * (sims + 1);
+  h->depth_cap = sims + 2;
+  const size_t nodes = (size_t)h->cap * h->B;
+  LZM_HIP(hipMalloc(&h->stat, nodes * sizeof(NodeStat)));
+  LZM_HIP(hipMalloc(&h->meta, nodes * sizeof(NodeMeta)));
+  LZM_HIP(hipMemset(h->meta, 0xff, nodes * sizeof(NodeMeta)));  // latent -1: nothing expanded
+  LZM_HIP(hipMemset(h->stat, 0, nodes * sizeof(NodeStat)));
+  LZM_HIP(hipMalloc(&h->path, sizeof(int32_t) * (size_t)h->depth_cap * h->B));
+  LZM_HIP(hipMalloc(&h->path_act, sizeof(int32_t) * (size_t)h->depth_cap * h->B));
+  h->stream_cap = h->B * (sims + 2) + 2 * kMaxWG;
+  LZM_HIP(hipMalloc(&h->stream, sizeof(uint32_t) * (size_t)h->stream_cap));
+  h->lut_n = sims + 8;
+  LZM_HIP(hipMalloc(&h->lut, sizeof(float2) * h->lut_n));
+  h->lut_base = -1;
+  return fill_lut(h, 19652, 1.25f);
+}
+
+extern "C" {
+
+const char *lzm_last_error(void) { return g_err; }
+
+int lzm_create(int B, int A, int max_sims, int flags, lzm_handle **out) {
+  if (!out || B <= 0 || A <= 0 || A > kMaxActions || max_sims < 0) {
+    set_err("lzm_create: need num_roots > 0, 0 < action_space <= 64, max_sims >= 0");
+    return LZM_ERR_ARG;
+  }
+  lzm_handle *h = new lzm_handle();
+  h->B = B;
+  h->A = A;
+  h->flags = flags;
+  int rc;
+#define TRY(x) do { rc = (x); if (rc != LZM_OK) { lzm_destroy(h); return rc; } } while (0)
+  TRY(hipMalloc(&h->legal, sizeof(int32_t) * (size_t)B * A) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->nlegal, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->pathlen, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->off, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->diag, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->hint, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->norm_flag, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMemset(h->diag, 0, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMemset(h->hint, 0, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMemset(h->pathlen, 0, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  {
+    std::vector<uint32_t> jf, jn;
+    build_jump_matrices(jf, jn);
+    TRY(hipMalloc(&h->jmat, sizeof(uint32_t) * 2 * kMaxWG * 31) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+    TRY(hipMemcpy(h->jmat, jf.data(), sizeof(uint32_t) * kMaxWG * 31, hipMemcpyHostToDevice) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+    TRY(hipMemcpy(h->jmat + kMaxWG * 31, jn.data(), sizeof(uint32_t) * kMaxWG * 31, hipMemcpyHostToDevice) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  }
+  TRY(alloc_tree(h, max_sims));
+#undef TRY
+  *out = h;
+  return LZM_OK;
+}
+
+int lzm_destroy(lzm_handle *h) {
+  if (!h) return LZM_OK;
+  free_tree(h);
+  dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag);
+  dfree(h->hint); dfree(h->norm_flag); dfree(h->jmat);
+  delete h;
+  return LZM_OK;
+}
+
+// Grows the node pool, keeping the tree: node-major storage means the old pool is a prefix
+// of the new one (same for the [level][root] path arrays). Synchronises the device.
+int lzm_reserve(lzm_handle *h, int max_sims) {
+  if (!h || max_sims < 0) return LZM_ERR_ARG;
+  if (max_sims <= h->sims_cap) return LZM_OK;
+  LZM_HIP(hipDeviceSynchronize());
+  lzm_handle old = *h;
+  h->stat = nullptr; h->meta = nullptr; h->path = nullptr; h->path_act = nullptr; h->stream = nullptr; h->lut = nullptr;
+  int rc = alloc_tree(h, max_sims);
+  if (rc == LZM_OK) {
+    const size_t nodes = (size_t)old.cap * old.B;
+    LZM_HIP(hipMemcpy(h->stat, old.stat, nodes * sizeof(NodeStat), hipMemcpyDeviceToDevice));
+    LZM_HIP(hipMemcpy(h->meta, old.meta, nodes * sizeof(NodeMeta), hipMemcpyDeviceToDevice));
+    LZM_HIP(hipMemcpy(h->path, old.path, sizeof(int32_t) * (size_t)old.depth_cap * old.B, hipMemcpyDeviceToDevice));
+    LZM_HIP(hipMemcpy(h->path_act, old.path_act, sizeof(int32_t) * (size_t)old.depth_cap * old.B, hipMemcpyDeviceToDevice));
+    if (old.lut_base >= 0) rc = fill_lut(h, old.lut_base, old.lut_init);
+  }
+  free_tree(&old);
+  return rc;
+}
+
+int lzm_num_roots(const lzm_handle *h) { return h ? h->B : LZM_ERR_ARG; }
+int lzm_sims_capacity(const lzm_handle *h) { return h ? h->sims_cap : LZM_ERR_ARG; }
+int lzm_action_space(const lzm_handle *h) { return h ? h->A : LZM_ERR_ARG; }
+int lzm_flags(const lzm_handle *h) { return h ? h->flags : LZM_ERR_ARG; }
+
+int lzm_minmax_init(float *mm, int n, float delta, void *stream) {
+  if (!mm || n <= 0) return LZM_ERR_ARG;
+  hipLaunchKernelGGL(minmax_init_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (float4 *)mm, n, delta);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_roots_prepare(lzm_handle *h, const int32_t *legal, const int32_t *count, const float *noises, float noise_weight,
+                      const float *rewards, const float *logits, const int32_t *to_play, void *stream) {
+  if (!h || !legal || !count || !rewards || !logits || !to_play) {
+    set_err("lzm_roots_prepare: null argument");
+    return LZM_ERR_ARG;
+  }
+  PrepareArgs p;
+  p.stat = h->stat; p.meta = h->meta; p.legal = h->legal; p.nlegal = h->nlegal;
+  p.legal_in = legal; p.count_in = count; p.to_play = to_play; p.noises = noises; p.rewards = rewards;
+  p.logits = logits; p.noise_weight = noise_weight; p.B = h->B; p.A = h->A;
+  hipLaunchKernelGGL(prepare_kernel, dim3((h->B + 255) / 256), dim3(256), 0, (hipStream_t)stream, p);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, float *minmax, const uint32_t *seed,
+                 const int32_t *vtp_in, int32_t *out_x, int32_t *out_y, int32_t *out_a, int64_t *out_a64,
+                 int32_t *out_vtp, int32_t *out_len, void *stream) {
+  if (!h || !minmax || !seed || !vtp_in || !out_x || !out_y || !out_a || !out_vtp || !out_len) {
+    set_err("lzm_traverse: null argument");
+    return LZM_ERR_ARG;
+  }
+  if (pb_c_base <= 0) {
+    set_err("lzm_traverse: pb_c_base must be positive");
+    return LZM_ERR_ARG;
+  }
+  int rc = fill_lut(h, pb_c_base, pb_c_init);
+  if (rc != LZM_OK) return rc;
+  TraverseArgs p;
+  p.t = view(h);
+  p.minmax = (const float4 *)minmax;
+  p.seed = seed;
+  p.vtp_in = vtp_in;
+  p.out_x = out_x; p.out_y = out_y; p.out_a = out_a; p.out_vtp = out_vtp; p.out_len = out_len;
+  p.out_a64 = (long long *)out_a64;
+  p.stream = h->stream;
+  p.stream_cap = h->stream_cap;
+  p.jfirst = h->jmat;
+  p.jnext = h->jmat + kMaxWG * 31;
+  p.off = h->off;
+  p.diag = h->diag;
+  p.hint = h->hint;
+  p.disc = discount;
+  const bool ez = h->flags & LZM_TREE_EZ;
+  hipStream_t s = (hipStream_t)stream;
+  if (h->flags & LZM_RNG_FAST) {
+    dim3 g((h->B + 255) / 256), b(256);
+    if (ez) hipLaunchKernelGGL(traverse_fast_kernel<true>, g, b, 0, s, p);
+    else hipLaunchKernelGGL(traverse_fast_kernel<false>, g, b, 0, s, p);
+  } else {
+    int W = ((h->B + 63) / 64) * 64;
+    if (W > kMaxWG) W = kMaxWG;
+    if (W < 64) W = 64;
+    if (ez) hipLaunchKernelGGL(traverse_glibc_kernel<true>, dim3(1), dim3(W), 0, s, p);
+    else hipLaunchKernelGGL(traverse_glibc_kernel<false>, dim3(1), dim3(W), 0, s, p);
+  }
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_gather_latent(lzm_handle *h, const float *pool, int64_t row, const int32_t *x, float *out, void *stream) {
+  if (!h || !pool || !x || !out || row <= 0) return LZM_ERR_ARG;
+  const long long total = (long long)h->B * row;
+  hipStream_t s = (hipStream_t)stream;
+  if (row % 4 == 0 && ((uintptr_t)pool % 16 == 0) && ((uintptr_t)out % 16 == 0)) {
+    const long long t4 = total / 4;
+    int grid = (int)((t4 + 255) / 256);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(gather_kernel_v4, dim3(grid), dim3(256), 0, s, (const float4 *)pool, (long long)(row / 4), h->B, x,
+                       (float4 *)out);
+  } else {
+    int grid = (int)((total + 255) / 256);
+    if (grid > 4096) grid = 4096;
+    hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, s, pool, (long long)row, h->B, x, out);
+  }
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+static int check_cur(lzm_handle *h, int cur) {
+  if (cur < 1 || 1 + h->A * (cur + 1) > h->cap) {
+    snprintf(g_err, sizeof(g_err), "latent index %d outside reserved capacity (%d simulations)", cur, h->sims_cap);
+    return LZM_ERR_CAPACITY;
+  }
+  return LZM_OK;
+}
+
+int lzm_backprop(lzm_handle *h, int cur, float discount, float *minmax, const float *rewards, const float *values,
+                 const float *logits, const int32_t *to_play, const int32_t *is_reset, void *stream) {
+  if (!h || !minmax || !rewards || !values || !logits || !to_play) {
+    set_err("lzm_backprop: null argument");
+    return LZM_ERR_ARG;
+  }
+  int rc = check_cur(h, cur);
+  if (rc != LZM_OK) return rc;
+  BackpropArgs p;
+  p.t = view(h);
+  p.minmax = (float4 *)minmax;
+  p.rewards = rewards; p.values = values; p.logits = logits; p.to_play = to_play; p.is_reset = is_reset;
+  p.cur = cur;
+  p.disc = discount;
+  dim3 g((h->B + 255) / 256), b(256);
+  if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(backprop_kernel<true>, g, b, 0, (hipStream_t)stream, p);
+  else hipLaunchKernelGGL(backprop_kernel<false>, g, b, 0, (hipStream_t)stream, p);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+static int launch_norm_check(lzm_handle *hflag_owner, int32_t *flag, const float *a, const float *b, int rows, int V,
+                             hipStream_t s) {
+  (void)hflag_owner;
+  hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, flag, 1);
+  hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, flag + 1, 1);
+  const int waves = 2 * rows;
+  hipLaunchKernelGGL(normalized_check_kernel, dim3((waves * 64 + 255) / 256), dim3(256), 0, s, a, b, rows, V, flag);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_decode_backprop(lzm_handle *h, int cur, float discount, float *minmax, const float *reward_logits,
+                        const float *value_logits, int support_len, int categorical, const float *policy_logits,
+                        const int32_t *to_play, int lstm_horizon, int32_t *out_is_reset, const float *next_latent,
+                        float *pool_slot, int64_t row_elems, float *out_decoded, void *stream) {
+  if (!h || !minmax || !reward_logits || !value_logits || !policy_logits || !to_play || support_len <= 0) {
+    set_err("lzm_decode_backprop: null argument");
+    return LZM_ERR_ARG;
+  }
+  if (categorical && support_len % 2 == 0) {
+    set_err("lzm_decode_backprop: categorical support length must be odd (2*support_scale+1)");
+    return LZM_ERR_ARG;
+  }
+  int rc = check_cur(h, cur);
+  if (rc != LZM_OK) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (categorical) {
+    rc = launch_norm_check(h, h->norm_flag, reward_logits, value_logits, h->B, support_len, s);
+    if (rc != LZM_OK) return rc;
+  }
+  DecodeArgs p;
+  p.t = view(h);
+  p.minmax = (float4 *)minmax;
+  p.reward_logits = reward_logits; p.value_logits = value_logits; p.policy_logits = policy_logits;
+  p.to_play = to_play; p.out_is_reset = out_is_reset; p.next_latent = next_latent; p.pool_slot = pool_slot;
+  p.row_elems = row_elems; p.V = support_len; p.categorical = categorical; p.cur = cur; p.horizon = lstm_horizon;
+  p.disc = discount; p.out_decoded = out_decoded;
+  dim3 g((h->B * 64 + 255) / 256), b(256);
+  const int32_t *nf = categorical ? h->norm_flag : nullptr;
+  if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(decode_backprop_kernel<true>, g, b, 0, s, p, nf);
+  else hipLaunchKernelGGL(decode_backprop_kernel<false>, g, b, 0, s, p, nf);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+static int32_t *g_scratch_flag = nullptr;
+static std::mutex g_scratch_mu;
+
+int lzm_inverse_scalar_transform(const float *logits, int rows, int V, int categorical, float *out, void *stream) {
+  if (!logits || !out || rows <= 0 || V <= 0) return LZM_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (!g_scratch_flag) LZM_HIP(hipMalloc(&g_scratch_flag, 64));
+  }
+  if (categorical) {
+    hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, g_scratch_flag, 1);
+    hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, g_scratch_flag + 1, 1);
+    hipLaunchKernelGGL(normalized_check_kernel, dim3((2 * rows * 64 + 255) / 256), dim3(256), 0, s, logits, logits,
+                       rows, V, g_scratch_flag);
+  }
+  hipLaunchKernelGGL(inverse_transform_kernel, dim3((rows * 64 + 255) / 256), dim3(256), 0, s, logits, rows, V,
+                     categorical, g_scratch_flag, out);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_get_distributions(lzm_handle *h, int32_t *out, void *stream) {
+  if (!h || !out) return LZM_ERR_ARG;
+  hipLaunchKernelGGL(distributions_kernel, dim3((h->B + 255) / 256), dim3(256), 0, (hipStream_t)stream, view(h), out);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_get_values(lzm_handle *h, float *out, void *stream) {
+  if (!h || !out) return LZM_ERR_ARG;
+  hipLaunchKernelGGL(values_kernel, dim3((h->B + 255) / 256), dim3(256), 0, (hipStream_t)stream, view(h), out);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_get_trajectories(lzm_handle *h, int32_t *out, int tmax, void *stream) {
+  if (!h || !out || tmax <= 0) return LZM_ERR_ARG;
+  hipLaunchKernelGGL(trajectories_kernel, dim3((h->B + 255) / 256), dim3(256), 0, (hipStream_t)stream, view(h), out,
+                     tmax);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_last_traverse_passes(lzm_handle *h, int32_t *out, void *stream) {
+  if (!h || !out) return LZM_ERR_ARG;
+  LZM_HIP(hipMemcpyAsync(out, h->diag, sizeof(int32_t) * 2, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return LZM_OK;
+}
+
+int lzm_debug_expf(const float *x, float *out, int64_t n, void *stream) {
+  if (!x || !out || n <= 0) return LZM_ERR_ARG;
+  long long grid = (n + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(debug_expf_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, x, out, (long long)n);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_debug_philox(const uint32_t *ck, uint32_t *out, int n, void *stream) {
+  if (!ck || !out || n <= 0) return LZM_ERR_ARG;
+  hipLaunchKernelGGL(debug_philox_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, ck, out, n);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream) {
+  if (!out || n <= 0) return LZM_ERR_ARG;
+  static uint32_t *jm = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    if (!jm) {
+      std::vector<uint32_t> jf, jn;
+      build_jump_matrices(jf, jn);
+      LZM_HIP(hipMalloc(&jm, sizeof(uint32_t) * 2 * kMaxWG * 31));
+      LZM_HIP(hipMemcpy(jm, jf.data(), sizeof(uint32_t) * kMaxWG * 31, hipMemcpyHostToDevice));
+      LZM_HIP(hipMemcpy(jm + kMaxWG * 31, jn.data(), sizeof(uint32_t) * kMaxWG * 31, hipMemcpyHostToDevice));
+    }
+  }
+  hipLaunchKernelGGL(debug_glibc_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, seed, n, out, jm, jm + kMaxWG * 31);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+}  // extern "C"

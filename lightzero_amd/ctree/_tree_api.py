@@ -1,0 +1,202 @@
+"""List-in / list-out tree API with the exact surface of LightZero's Cython ctree modules.
+
+Mirrors ``lzero/mcts/ctree/ctree_muzero/mz_tree.pyx:5-107`` (MuZero) and
+``lzero/mcts/ctree/ctree_efficientzero/ez_tree.pyx:6-121`` (EfficientZero, ``is_reset``):
+classes ``MinMaxStatsList``, ``ResultsWrapper``, ``Roots`` and the functions
+``batch_traverse`` / ``batch_backpropagate``. Arguments typed ``list`` in the .pyx raise
+``TypeError`` for anything else, as Cython does. The trees live on the GPU (lightzero_amd.tree);
+each call stages its Python lists through HBM. The fast path that keeps everything on the
+device is ``lightzero_amd.mcts_ctree`` (search loop) — this module is the compatibility
+surface for code that drives the tree by hand.
+"""
+import numpy as np
+import torch
+
+from ..tree import POOL, new_minmax, next_seed, seed_tensor
+
+_DEFAULT_SIMS = 64
+
+
+def _require_list(name, v):
+    if not isinstance(v, list):
+        raise TypeError(f"Argument '{name}' has incorrect type (expected list, got {type(v).__name__})")
+
+
+def _f32(v):
+    return float(np.float32(v))
+
+
+class MinMaxStatsList:
+    """CMinMaxStatsList (common_lib/cminimax.cpp:47-66): one (max, min, delta) per root, in HBM."""
+
+    def __init__(self, num):
+        self.num = int(num)
+        self._delta = 0.0
+        self._buf = None
+
+    def set_delta(self, value_delta_max):
+        self._delta = _f32(value_delta_max)
+        if self._buf is not None:
+            self._buf[:, 2] = self._delta
+
+    def _device(self, device):
+        if self._buf is None or self._buf.device != device:
+            self._buf = new_minmax(self.num, self._delta, device)
+        return self._buf
+
+
+class ResultsWrapper:
+    """CSearchResults holder (mz_tree.pyx:18-25); the search paths themselves stay in the tree."""
+
+    def __init__(self, num):
+        self.num = int(num)
+        self._search_lens = []
+
+    def get_search_len(self):
+        return list(self._search_lens)
+
+
+class _RootsBase:
+    EZ = False
+
+    def __init__(self, root_num, legal_actions_list, fast_rng=False):
+        self.fast_rng = bool(fast_rng)
+        self.root_num = int(root_num)
+        self.legal_actions_list = [list(map(int, l)) for l in legal_actions_list]
+        if len(self.legal_actions_list) < self.root_num:
+            raise IndexError("legal_actions_list shorter than root_num")
+        self.tree = None
+        self._sims = _DEFAULT_SIMS
+
+    @property
+    def num(self):
+        return self.root_num
+
+    def _acquire(self, A, device):
+        if self.tree is not None and self.tree.A == A and self.tree.device == device:
+            return self.tree
+        if self.tree is not None:
+            POOL.release(self.tree)
+        self.tree = POOL.acquire(self.root_num, A, self._sims, self.EZ, self.fast_rng, device)
+        return self.tree
+
+    def _prepare(self, noise_weight, noises, rewards, logits, to_play, device=None):
+        B = self.root_num
+        logits = np.asarray(logits, dtype=np.float32).reshape(B, -1)
+        A = logits.shape[1]
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        t = self._acquire(A, dev)
+        legal = np.full((B, A), -1, np.int32)
+        count = np.zeros(B, np.int32)
+        nz = np.zeros((B, A), np.float32) if noises is not None else None
+        for i in range(B):
+            l = self.legal_actions_list[i]
+            if len(l) > A or any(a < 0 or a >= A for a in l):
+                raise ValueError(f"root {i}: legal actions {l} outside action space {A}")
+            legal[i, :len(l)] = l
+            count[i] = len(l)
+            if nz is not None:
+                row = np.asarray(noises[i], dtype=np.float32).reshape(-1)
+                n = len(l) if len(l) > 0 else A
+                if row.shape[0] < n:
+                    raise IndexError(f"root {i}: {row.shape[0]} noises for {n} legal actions")
+                nz[i, :n] = row[:n]
+        g = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev, non_blocking=False)
+        t.prepare(g(legal, np.int32), g(count, np.int32), None if nz is None else g(nz, np.float32),
+                  _f32(noise_weight), g(np.asarray(rewards, np.float32).reshape(B), np.float32), g(logits, np.float32),
+                  g(np.asarray(to_play, np.int32).reshape(B), np.int32))
+
+    def prepare(self, root_noise_weight, noises, value_prefix_pool, policy_logits_pool, to_play_batch):
+        _require_list("noises", noises)
+        _require_list("value_prefix_pool", value_prefix_pool)
+        _require_list("policy_logits_pool", policy_logits_pool)
+        self._prepare(root_noise_weight, noises, value_prefix_pool, policy_logits_pool, list(to_play_batch))
+
+    def prepare_no_noise(self, value_prefix_pool, policy_logits_pool, to_play_batch):
+        _require_list("value_prefix_pool", value_prefix_pool)
+        _require_list("policy_logits_pool", policy_logits_pool)
+        self._prepare(0.0, None, value_prefix_pool, policy_logits_pool, list(to_play_batch))
+
+    def prepare_device(self, root_noise_weight, noises, rewards, logits, to_play):
+        """Device-tensor variant (not in the reference): all arguments torch tensors on the GPU."""
+        B = self.root_num
+        A = logits.shape[-1]
+        t = self._acquire(A, logits.device)
+        legal = torch.full((B, A), -1, dtype=torch.int32)
+        count = torch.zeros(B, dtype=torch.int32)
+        for i, l in enumerate(self.legal_actions_list[:B]):
+            legal[i, :len(l)] = torch.tensor(l, dtype=torch.int32)
+            count[i] = len(l)
+        dev = logits.device
+        t.prepare(legal.to(dev), count.to(dev),
+                  None if noises is None else noises.to(dev, torch.float32).contiguous(), _f32(root_noise_weight),
+                  rewards.to(dev, torch.float32).contiguous(), logits.to(dev, torch.float32).contiguous(),
+                  to_play.to(dev, torch.int32).contiguous())
+
+    def get_trajectories(self):
+        if self.tree is None:
+            return [[] for _ in range(self.root_num)]
+        tr = self.tree.trajectories(self.tree.sims_capacity + 2).cpu().numpy()
+        return [[int(a) for a in row if a >= 0] for row in tr]
+
+    def get_distributions(self):
+        if self.tree is None:
+            return [[] for _ in range(self.root_num)]
+        d = self.tree.distributions().cpu().numpy()
+        return [[int(v) for v in row if v >= 0] for row in d]
+
+    def get_values(self):
+        if self.tree is None:
+            return [0.0] * self.root_num
+        return [float(v) for v in self.tree.values().cpu().numpy()]
+
+    def clear(self):
+        if self.tree is not None:
+            POOL.release(self.tree)
+            self.tree = None
+
+    def __del__(self):
+        try:
+            self.clear()
+        except Exception:
+            pass
+
+
+def _traverse(roots, pb_c_base, pb_c_init, discount_factor, min_max_stats_lst, results, virtual_to_play_batch,
+              seed=None):
+    if not isinstance(pb_c_base, (int, np.integer)):
+        raise TypeError("an integer is required for pb_c_base")
+    _require_list("virtual_to_play_batch", virtual_to_play_batch)
+    t = roots.tree
+    if t is None:
+        raise RuntimeError("batch_traverse: roots not prepared")
+    dev = t.device
+    mm = min_max_stats_lst._device(dev)
+    vtp = torch.tensor(np.asarray(virtual_to_play_batch, np.int32)[:t.B], device=dev)
+    s = seed_tensor(next_seed() if seed is None else seed, dev)
+    t.traverse(mm, s, vtp, int(pb_c_base), _f32(pb_c_init), _f32(discount_factor))
+    out = torch.stack([t.x, t.y, t.action, t.vtp, t.search_len]).cpu().numpy()
+    results._search_lens = out[4].tolist()
+    results._tree = t
+    return out[0].tolist(), out[1].tolist(), out[2].tolist(), out[3].tolist()
+
+
+def _backprop(current_latent_state_index, discount_factor, value_prefixs, values, policies, min_max_stats_lst,
+              results, to_play_batch, is_reset_list=None):
+    _require_list("value_prefixs", value_prefixs)
+    _require_list("values", values)
+    _require_list("policies", policies)
+    _require_list("to_play_batch", to_play_batch)
+    t = getattr(results, "_tree", None)
+    if t is None:
+        raise RuntimeError("batch_backpropagate: results do not come from batch_traverse")
+    cur = int(current_latent_state_index)
+    if 1 + t.A * (cur + 1) > 1 + t.A * (t.sims_capacity + 1):
+        t.reserve(max(cur + 1, 2 * t.sims_capacity))
+    dev = t.device
+    B = t.B
+    g = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)
+    rs = None if is_reset_list is None else g(np.asarray(is_reset_list, np.int32).reshape(B), np.int32)
+    t.backprop(cur, _f32(discount_factor), min_max_stats_lst._device(dev), g(np.asarray(value_prefixs).reshape(B), np.float32),
+               g(np.asarray(values).reshape(B), np.float32), g(np.asarray(policies, np.float32).reshape(B, t.A), np.float32),
+               g(np.asarray(to_play_batch, np.int32).reshape(B), np.int32), rs)

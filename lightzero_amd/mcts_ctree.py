@@ -1,0 +1,247 @@
+"""Drop-in ``MuZeroMCTSCtree`` / ``EfficientZeroMCTSCtree`` with the search loop on the GPU.
+
+Same class surface as /root/reference/lzero/mcts/tree_search/mcts_ctree.py:172-420 (MuZero) and
+:623-827 (EfficientZero): class attribute ``config``, ``default_config()``, ``__init__(cfg)``,
+classmethod ``roots(n, legal_actions)`` and ``search(...)``. The difference is where the
+per-simulation loop (mcts_ctree.py:255-321) runs: here every step is a device kernel or a
+device-resident model call on one stream —
+
+    traverse (select, HIP)  ->  gather leaf latents (HIP)  ->  model.recurrent_inference
+    ->  decode value/reward supports + expand + backup (one HIP kernel, also files the new
+        latents into the [S+1, B, ...] pool in HBM)
+
+with no host round trip inside a search. The tree and the tie-break RNG follow the reference
+bit for bit in the default parity mode (glibc rand() stream seeded per traverse, exactly one
+draw per tree level), see lzm_kernels.hip.
+"""
+import copy
+from typing import Any, List, Union
+
+import numpy as np
+import torch
+
+from .ctree import ez_tree, mz_tree
+from .scaling_transform import InverseScalarTransform
+from .tree import new_minmax, next_seed
+from .utils import EasyDict
+
+
+def _seeds(n, device):
+    s = np.array([next_seed() for _ in range(n)], dtype=np.uint32).view(np.int32)
+    return torch.from_numpy(s).to(device)
+
+
+def _to_play_tensor(to_play_batch, B, device):
+    if isinstance(to_play_batch, torch.Tensor):
+        return to_play_batch.to(device=device, dtype=torch.int32).reshape(B)
+    if isinstance(to_play_batch, (int, np.integer)):
+        return torch.full((B,), int(to_play_batch), dtype=torch.int32, device=device)
+    return torch.as_tensor(np.asarray(to_play_batch, dtype=np.int32).reshape(B), device=device)
+
+
+def _latent_tensor(x, device):
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=torch.float32)
+    if isinstance(x, (list, tuple)):
+        x = np.asarray(x)
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(device)
+
+
+class _Recorder:
+    """Optional per-simulation record of what the tree requested and consumed (tests, tracing)."""
+
+    def __init__(self, S, B, A, device):
+        i32 = dict(dtype=torch.int32, device=device)
+        self.x = torch.zeros((S, B), **i32)
+        self.action = torch.zeros((S, B), **i32)
+        self.search_len = torch.zeros((S, B), **i32)
+        self.vtp = torch.zeros((S, B), **i32)
+        self.decoded = torch.zeros((S, B, 2), dtype=torch.float32, device=device)
+        self.policy_logits = torch.zeros((S, B, A), dtype=torch.float32, device=device)
+        self.seeds = None
+
+    def step(self, k, t, policy_logits):
+        self.x[k].copy_(t.x)
+        self.action[k].copy_(t.action)
+        self.search_len[k].copy_(t.search_len)
+        self.vtp[k].copy_(t.vtp)
+        self.policy_logits[k].copy_(policy_logits)
+
+    def numpy(self):
+        return {k: getattr(self, k).cpu().numpy() for k in
+                ("x", "action", "search_len", "vtp", "decoded", "policy_logits")} | {"seeds": self.seeds}
+
+
+class _SearchBuffers:
+    """Per (B, S, latent shape) device buffers reused across searches."""
+
+    def __init__(self):
+        self.key = None
+
+    def get(self, B, S, shape, device, extra=()):
+        key = (B, S, tuple(shape), str(device), tuple(extra))
+        if key != self.key:
+            self.pool = torch.empty((S + 1, B) + tuple(shape), dtype=torch.float32, device=device)
+            self.net_in = torch.empty((B,) + tuple(shape), dtype=torch.float32, device=device)
+            self.extra = [torch.empty((S + 1, B, e), dtype=torch.float32, device=device) for e in extra]
+            self.extra_in = [torch.empty((B, e), dtype=torch.float32, device=device) for e in extra]
+            self.key = key
+        return self
+
+
+class MuZeroMCTSCtree(object):
+    """MCTS for MuZero on the GPU (reference: mcts_ctree.py:172-321)."""
+
+    config = dict(
+        root_dirichlet_alpha=0.3,
+        root_noise_weight=0.25,
+        pb_c_base=19652,
+        pb_c_init=1.25,
+        value_delta_max=0.01,
+        env_type='not_board_games',
+    )
+
+    @classmethod
+    def default_config(cls: type) -> EasyDict:
+        cfg = EasyDict(copy.deepcopy(cls.config))
+        cfg.cfg_type = cls.__name__ + 'Dict'
+        return cfg
+
+    def __init__(self, cfg: EasyDict = None) -> None:
+        default_config = self.default_config()
+        default_config.update(cfg)
+        self._cfg = default_config
+        self.inverse_scalar_transform_handle = InverseScalarTransform(
+            self._cfg.model.support_scale, self._cfg.device, self._cfg.model.categorical_distribution
+        )
+        self._buf = _SearchBuffers()
+
+    # 'glibc': the reference's tie-break stream, bit-exact (default); 'philox': independent
+    # counter-based stream per root (LZM_RNG_FAST), no batch-serial dependency.
+    rng_mode = 'glibc'
+
+    @classmethod
+    def roots(cls: int, active_collect_env_num: int, legal_actions: List[Any]) -> "mz_tree.Roots":
+        return mz_tree.Roots(active_collect_env_num, legal_actions, fast_rng=(cls.rng_mode == 'philox'))
+
+    def _categorical(self):
+        return bool(self._cfg.model.get('categorical_distribution', True))
+
+    def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
+               to_play_batch: Union[int, List[Any]]) -> None:
+        with torch.no_grad():
+            model.eval()
+            t = roots.tree
+            if t is None:
+                raise RuntimeError("search: roots must be prepared (Roots.prepare / prepare_no_noise) first")
+            B, S = roots.num, int(self._cfg.num_simulations)
+            t.reserve(S)
+            dev = t.device
+            lat0 = _latent_tensor(latent_state_roots, dev)
+            shape = lat0.shape[1:]
+            row = int(np.prod(shape)) if len(shape) else 1
+            buf = self._buf.get(B, S, shape, dev)
+            buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
+            cfg = self._cfg
+            disc = float(np.float32(cfg.discount_factor))
+            mm = new_minmax(B, cfg.value_delta_max, dev)
+            vtp_in = _to_play_tensor(to_play_batch, B, dev)
+            seeds = _seeds(S, dev)
+            cat = self._categorical()
+            rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
+            if rec is not None:
+                rec.seeds = seeds.cpu().numpy().view(np.uint32)
+            for k in range(S):
+                t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+                t.gather(buf.pool, row, buf.net_in)
+                out = model.recurrent_inference(buf.net_in, t.action64)
+                logits = out.policy_logits.float().contiguous()
+                if rec is not None:
+                    rec.step(k, t, logits)
+                t.decode_backprop(k + 1, disc, mm, out.reward.float().contiguous(), out.value.float().contiguous(), cat,
+                                  logits, t.vtp, next_latent=out.latent_state.float().contiguous(),
+                                  pool_slot=buf.pool[k + 1], row_elems=row,
+                                  out_decoded=None if rec is None else rec.decoded[k])
+            roots._last_minmax = mm
+            self.last_record = rec
+
+
+class EfficientZeroMCTSCtree(object):
+    """MCTS for EfficientZero on the GPU (reference: mcts_ctree.py:623-827)."""
+
+    config = dict(
+        root_dirichlet_alpha=0.3,
+        root_noise_weight=0.25,
+        pb_c_base=19652,
+        pb_c_init=1.25,
+        value_delta_max=0.01,
+        env_type='not_board_games',
+    )
+
+    @classmethod
+    def default_config(cls: type) -> EasyDict:
+        cfg = EasyDict(copy.deepcopy(cls.config))
+        cfg.cfg_type = cls.__name__ + 'Dict'
+        return cfg
+
+    def __init__(self, cfg: EasyDict = None) -> None:
+        default_config = self.default_config()
+        default_config.update(cfg)
+        self._cfg = default_config
+        self.inverse_scalar_transform_handle = InverseScalarTransform(
+            self._cfg.model.support_scale, self._cfg.device, self._cfg.model.categorical_distribution
+        )
+        self._buf = _SearchBuffers()
+
+    rng_mode = 'glibc'
+
+    @classmethod
+    def roots(cls: int, active_collect_env_num: int, legal_actions: List[Any]) -> "ez_tree.Roots":
+        return ez_tree.Roots(active_collect_env_num, legal_actions, fast_rng=(cls.rng_mode == 'philox'))
+
+    def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
+               reward_hidden_state_roots: List[Any], to_play_batch: Union[int, List[Any]]) -> None:
+        with torch.no_grad():
+            model.eval()
+            t = roots.tree
+            if t is None:
+                raise RuntimeError("search: roots must be prepared (Roots.prepare / prepare_no_noise) first")
+            B, S = roots.num, int(self._cfg.num_simulations)
+            t.reserve(S)
+            dev = t.device
+            lat0 = _latent_tensor(latent_state_roots, dev)
+            shape = lat0.shape[1:]
+            row = int(np.prod(shape)) if len(shape) else 1
+            hc0 = _latent_tensor(reward_hidden_state_roots[0], dev).reshape(B, -1)
+            hh0 = _latent_tensor(reward_hidden_state_roots[1], dev).reshape(B, -1)
+            Hl = hc0.shape[1]
+            buf = self._buf.get(B, S, shape, dev, extra=(Hl, Hl))
+            buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
+            buf.extra[0][0].copy_(hc0)
+            buf.extra[1][0].copy_(hh0)
+            cfg = self._cfg
+            disc = float(np.float32(cfg.discount_factor))
+            horizon = int(cfg.lstm_horizon_len)
+            if horizon <= 0:
+                raise ValueError("lstm_horizon_len must be > 0 (mcts_ctree.py:809)")
+            mm = new_minmax(B, cfg.value_delta_max, dev)
+            vtp_in = _to_play_tensor(to_play_batch, B, dev)
+            seeds = _seeds(S, dev)
+            cat = bool(cfg.model.get('categorical_distribution', True))
+            for k in range(S):
+                t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+                t.gather(buf.pool, row, buf.net_in)
+                t.gather(buf.extra[0], Hl, buf.extra_in[0])
+                t.gather(buf.extra[1], Hl, buf.extra_in[1])
+                out = model.recurrent_inference(buf.net_in, (buf.extra_in[0].unsqueeze(0), buf.extra_in[1].unsqueeze(0)),
+                                                t.action64)
+                t.decode_backprop(k + 1, disc, mm, out.value_prefix.float().contiguous(), out.value.float().contiguous(),
+                                  cat, out.policy_logits.float().contiguous(), t.vtp, lstm_horizon=horizon,
+                                  out_is_reset=t.is_reset, next_latent=out.latent_state.float().contiguous(),
+                                  pool_slot=buf.pool[k + 1], row_elems=row)
+                # reset the LSTM state of roots whose search_len % horizon == 0 (mcts_ctree.py:810-816)
+                keep = (1 - t.is_reset).to(torch.float32).unsqueeze(1)
+                hc, hh = out.reward_hidden_state
+                torch.mul(hc.reshape(B, Hl).float(), keep, out=buf.extra[0][k + 1])
+                torch.mul(hh.reshape(B, Hl).float(), keep, out=buf.extra[1][k + 1])
+            roots._last_minmax = mm

@@ -1,0 +1,180 @@
+"""DeviceTree: one lzm_handle (a batch of search trees resident in HBM) plus its result buffers.
+
+Host-side owner of the structures the reference keeps in ``CRoots`` + ``CSearchResults``
+(/root/reference/lzero/mcts/ctree/ctree_muzero/lib/cnode.h:48-79). All tensors are on the GPU;
+every method enqueues work on the current torch stream and never synchronises.
+"""
+import ctypes
+import threading
+import time
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, ptr, stream_ptr
+
+# ----------------------------------------------------------------------------- seeds
+_seed_lock = threading.Lock()
+_seed_source = None
+
+
+def reference_time_seed():
+    """The reference seeds every batch_traverse with gettimeofday().tv_usec (common_lib/utils.cpp:25)."""
+    return int(time.time_ns() // 1000 % 1000000)
+
+
+def set_seed_source(fn):
+    """Install a callable returning the next traverse seed (None restores the time seed)."""
+    global _seed_source
+    with _seed_lock:
+        _seed_source = fn
+
+
+def next_seed():
+    with _seed_lock:
+        fn = _seed_source
+    return int(fn() if fn is not None else reference_time_seed()) & 0xFFFFFFFF
+
+
+class SequentialSeeds:
+    """Deterministic seed source: usec_k = (1000003*seed + k) mod 1e6."""
+
+    def __init__(self, seed):
+        self.seed, self.k = int(seed), 0
+
+    def __call__(self):
+        v = (1000003 * self.seed + self.k) % 1000000
+        self.k += 1
+        return v
+
+
+# ----------------------------------------------------------------------------- handle
+class DeviceTree:
+    def __init__(self, num_roots, action_space, max_sims=64, ez=False, fast_rng=False, device=None):
+        _lib.require_gpu()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.B, self.A = int(num_roots), int(action_space)
+        self.ez, self.fast_rng = bool(ez), bool(fast_rng)
+        flags = (_lib.LZM_TREE_EZ if ez else 0) | (_lib.LZM_RNG_FAST if fast_rng else 0)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            call("lzm_create", self.B, self.A, int(max_sims), flags, ctypes.byref(h))
+        self.h = h
+        i32 = dict(dtype=torch.int32, device=self.device)
+        B = self.B
+        self.x = torch.zeros(B, **i32)
+        self.y = torch.zeros(B, **i32)
+        self.action = torch.zeros(B, **i32)
+        self.action64 = torch.zeros(B, dtype=torch.int64, device=self.device)
+        self.vtp = torch.zeros(B, **i32)
+        self.search_len = torch.zeros(B, **i32)
+        self.is_reset = torch.zeros(B, **i32)
+        self.seed_buf = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    @property
+    def sims_capacity(self):
+        return _lib.load().lzm_sims_capacity(self.h)
+
+    def reserve(self, max_sims):
+        if max_sims > self.sims_capacity:
+            with torch.cuda.device(self.device):
+                call("lzm_reserve", self.h, int(max_sims))
+
+    def close(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                _lib.load().lzm_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+        self.h = None
+
+    def __del__(self):
+        self.close()
+
+    # -- calls ---------------------------------------------------------------------------
+    def prepare(self, legal, count, noises, noise_weight, rewards, logits, to_play, stream=None):
+        call("lzm_roots_prepare", self.h, ptr(legal), ptr(count), ptr(noises), float(noise_weight), ptr(rewards),
+             ptr(logits), ptr(to_play), stream_ptr(stream))
+
+    def traverse(self, minmax, seed, vtp_in, pb_c_base=19652, pb_c_init=1.25, discount=0.997, stream=None):
+        """seed: 1-element device tensor (int32/uint32 bits)."""
+        call("lzm_traverse", self.h, int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax), ptr(seed),
+             ptr(vtp_in), ptr(self.x), ptr(self.y), ptr(self.action), ptr(self.action64), ptr(self.vtp),
+             ptr(self.search_len), stream_ptr(stream))
+
+    def gather(self, pool, row_elems, out, stream=None):
+        call("lzm_gather_latent", self.h, ptr(pool), int(row_elems), ptr(self.x), ptr(out), stream_ptr(stream))
+
+    def backprop(self, cur, discount, minmax, rewards, values, logits, to_play, is_reset=None, stream=None):
+        call("lzm_backprop", self.h, int(cur), float(discount), ptr(minmax), ptr(rewards), ptr(values), ptr(logits),
+             ptr(to_play), ptr(is_reset), stream_ptr(stream))
+
+    def decode_backprop(self, cur, discount, minmax, reward_logits, value_logits, categorical, policy_logits, to_play,
+                        lstm_horizon=0, out_is_reset=None, next_latent=None, pool_slot=None, row_elems=0,
+                        out_decoded=None, stream=None):
+        V = reward_logits.shape[-1] if categorical else 1
+        call("lzm_decode_backprop", self.h, int(cur), float(discount), ptr(minmax), ptr(reward_logits),
+             ptr(value_logits), int(V), int(bool(categorical)), ptr(policy_logits), ptr(to_play), int(lstm_horizon),
+             ptr(out_is_reset), ptr(next_latent), ptr(pool_slot), int(row_elems), ptr(out_decoded), stream_ptr(stream))
+
+    def distributions(self, stream=None):
+        out = torch.empty((self.B, self.A), dtype=torch.int32, device=self.device)
+        call("lzm_get_distributions", self.h, ptr(out), stream_ptr(stream))
+        return out
+
+    def values(self, stream=None):
+        out = torch.empty(self.B, dtype=torch.float32, device=self.device)
+        call("lzm_get_values", self.h, ptr(out), stream_ptr(stream))
+        return out
+
+    def trajectories(self, tmax=64, stream=None):
+        out = torch.empty((self.B, tmax), dtype=torch.int32, device=self.device)
+        call("lzm_get_trajectories", self.h, ptr(out), int(tmax), stream_ptr(stream))
+        return out
+
+    def traverse_passes(self):
+        out = torch.zeros(2, dtype=torch.int32, device=self.device)
+        call("lzm_last_traverse_passes", self.h, ptr(out), stream_ptr())
+        return out.cpu().tolist()
+
+
+def new_minmax(n, value_delta_max, device, stream=None):
+    mm = torch.empty((n, 4), dtype=torch.float32, device=device)
+    call("lzm_minmax_init", ptr(mm), int(n), float(np.float32(value_delta_max)), stream_ptr(stream))
+    return mm
+
+
+def seed_tensor(seed, device):
+    return torch.tensor([np.uint32(seed).view(np.int32)], dtype=torch.int32, device=device)
+
+
+# ----------------------------------------------------------------------------- handle pool
+class TreePool:
+    """Re-uses handles across searches so device pointers stay stable (graph replay)."""
+
+    def __init__(self):
+        self._free = {}
+        self._lock = threading.Lock()
+
+    def acquire(self, B, A, max_sims, ez, fast_rng, device):
+        key = (B, A, ez, fast_rng, str(device))
+        with self._lock:
+            lst = self._free.get(key)
+            t = lst.pop() if lst else None
+        if t is None:
+            t = DeviceTree(B, A, max_sims, ez=ez, fast_rng=fast_rng, device=device)
+        else:
+            t.reserve(max_sims)
+        return t
+
+    def release(self, t):
+        if t is None or t.h is None:
+            return
+        key = (t.B, t.A, t.ez, t.fast_rng, str(t.device))
+        with self._lock:
+            self._free.setdefault(key, []).append(t)
+
+
+POOL = TreePool()

@@ -268,8 +268,9 @@ static float ucb_score(const lzo_tree *t, int i, size_t p, size_t c, float paren
 }
 
 /* cselect_child, cnode.cpp:551-596: order-dependent 1e-6 tie list, exactly one rand() */
+static int32_t draw_next_fwd(void *d, int root, int level);
 static int select_child(const lzo_tree *t, int i, int node, int pb_c_base, float pb_c_init, float disc,
-                        float mean_q, int players, lzo_glibc_rng *g) {
+                        float mean_q, int players, void *dr, int level) {
   size_t p = NODE(t, i, node);
   float max_score = LZO_FLOAT_MIN;
   const float epsilon = 0.000001f;
@@ -286,17 +287,47 @@ static int select_child(const lzo_tree *t, int i, int node, int pb_c_base, float
       lst[nl++] = a;
     }
   }
-  if (nl > 0) action = lst[lzo_glibc_rand(g) % nl];
+  if (nl > 0) action = lst[draw_next_fwd(dr, i, level) % nl];
   return action;
 }
 
-/* cbatch_traverse, cnode.cpp:755-824 */
-void lzo_traverse(lzo_tree *t, int pb_c_base, float pb_c_init, float disc, uint32_t seed, const int32_t *vtp_in,
-                  int32_t *out_x, int32_t *out_y, int32_t *out_a, int32_t *out_vtp, int32_t *out_len) {
+/* Philox4x32-10 (Salmon et al., SC'11), for the LZM_RNG_FAST tie-break stream:
+ * draw(root i, level l) = philox(ctr = {l, i, 0, 0}, key = {seed, 0x4c5a4d43}).x >> 1 */
+void lzo_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+  uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3], k0 = key_in[0], k1 = key_in[1];
+  int r;
+  for (r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0, hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* draw source: glibc stream (serial over roots) or philox per (root, level) */
+typedef struct {
+  int fast;
+  uint32_t seed;
   lzo_glibc_rng g;
+} lzo_draws;
+
+static int32_t draw_next(lzo_draws *d, int root, int level) {
+  if (!d->fast) return lzo_glibc_rand(&d->g);
+  {
+    uint32_t ctr[4] = {(uint32_t)level, (uint32_t)root, 0u, 0u}, key[2] = {d->seed, 0x4c5a4d43u}, o[4];
+    lzo_philox4x32_10(ctr, key, o);
+    return (int32_t)(o[0] >> 1);
+  }
+}
+
+/* cbatch_traverse, cnode.cpp:755-824 */
+static void traverse_impl(lzo_tree *t, int pb_c_base, float pb_c_init, float disc, lzo_draws *dr, const int32_t *vtp_in,
+                          int32_t *out_x, int32_t *out_y, int32_t *out_a, int32_t *out_vtp, int32_t *out_len) {
   int i, players, largest = vtp_in[0], last_action = -1;
   float parent_q = 0.0f; /* declared once per call and carried across roots, cnode.cpp:773 */
-  lzo_glibc_srand(&g, seed);
   for (i = 1; i < t->B; ++i)
     if (vtp_in[i] > largest) largest = vtp_in[i];
   players = (largest == -1) ? 1 : 2;
@@ -310,7 +341,7 @@ void lzo_traverse(lzo_tree *t, int pb_c_base, float pb_c_init, float disc, uint3
       int action;
       is_root = 0;
       parent_q = mean_q;
-      action = select_child(t, i, node, pb_c_base, pb_c_init, disc, mean_q, players, &g);
+      action = select_child(t, i, node, pb_c_base, pb_c_init, disc, mean_q, players, dr, search_len);
       if (players > 1) vtp = (vtp == 1) ? 2 : 1;
       t->best[NODE(t, i, node)] = action;
       node = child_of(t, i, node, action);
@@ -328,6 +359,25 @@ void lzo_traverse(lzo_tree *t, int pb_c_base, float pb_c_init, float disc, uint3
     out_len[i] = search_len;
     out_vtp[i] = vtp;
   }
+}
+
+static int32_t draw_next_fwd(void *d, int root, int level) { return draw_next((lzo_draws *)d, root, level); }
+
+void lzo_traverse(lzo_tree *t, int pb_c_base, float pb_c_init, float disc, uint32_t seed, const int32_t *vtp_in,
+                  int32_t *out_x, int32_t *out_y, int32_t *out_a, int32_t *out_vtp, int32_t *out_len) {
+  lzo_draws d;
+  d.fast = 0;
+  d.seed = seed;
+  lzo_glibc_srand(&d.g, seed); /* srand(tv_usec), common_lib/utils.cpp:25 */
+  traverse_impl(t, pb_c_base, pb_c_init, disc, &d, vtp_in, out_x, out_y, out_a, out_vtp, out_len);
+}
+
+void lzo_traverse_fast(lzo_tree *t, int pb_c_base, float pb_c_init, float disc, uint32_t seed, const int32_t *vtp_in,
+                       int32_t *out_x, int32_t *out_y, int32_t *out_a, int32_t *out_vtp, int32_t *out_len) {
+  lzo_draws d;
+  d.fast = 1;
+  d.seed = seed;
+  traverse_impl(t, pb_c_base, pb_c_init, disc, &d, vtp_in, out_x, out_y, out_a, out_vtp, out_len);
 }
 
 /* cbackpropagate, mz: cnode.cpp:419-478; ez: ctree_efficientzero/lib/cnode.cpp:482-575 */
@@ -488,4 +538,48 @@ double lzo_bench_tree_only(int B, int A, int S, int threads, int searches, uint3
   clock_gettime(CLOCK_MONOTONIC, &t1);
   (void)base;
   return (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+}
+
+/* ---------------------------------------------------------------- expf exhaustive checker */
+typedef struct {
+  uint32_t first;
+  int64_t lo, hi;
+  const float *got;
+  long bad;
+} expf_arg;
+
+static void *expf_worker(void *p) {
+  expf_arg *a = (expf_arg *)p;
+  int64_t k;
+  for (k = a->lo; k < a->hi; ++k) {
+    uint32_t u = a->first + (uint32_t)k;
+    float x, e;
+    memcpy(&x, &u, 4);
+    e = expf(x);
+    if (memcmp(&e, &a->got[k], 4) != 0) a->bad++;
+  }
+  return NULL;
+}
+
+/* Counts k in [0,n) where host libm expf(bits(first+k)) differs bitwise from got[k]. */
+long lzo_expf_mismatches(uint32_t first, int64_t n, const float *got, int threads) {
+  pthread_t th[64];
+  expf_arg args[64];
+  int w;
+  long bad = 0;
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  for (w = 0; w < threads; ++w) {
+    args[w].first = first;
+    args[w].lo = n * w / threads;
+    args[w].hi = n * (w + 1) / threads;
+    args[w].got = got;
+    args[w].bad = 0;
+    pthread_create(&th[w], NULL, expf_worker, &args[w]);
+  }
+  for (w = 0; w < threads; ++w) {
+    pthread_join(th[w], NULL);
+    bad += args[w].bad;
+  }
+  return bad;
 }

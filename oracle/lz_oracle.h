@@ -38,6 +38,11 @@ void lzo_prepare(lzo_tree *t, float noise_weight, const float *noises, const flo
 void lzo_traverse(lzo_tree *t, int pb_c_base, float pb_c_init, float discount, uint32_t seed,
                   const int32_t *virtual_to_play, int32_t *out_x, int32_t *out_y, int32_t *out_a,
                   int32_t *out_vtp, int32_t *out_len);
+/* Same walk with the LZM_RNG_FAST draw stream (Philox4x32-10 per root and level). */
+void lzo_traverse_fast(lzo_tree *t, int pb_c_base, float pb_c_init, float discount, uint32_t seed,
+                       const int32_t *virtual_to_play, int32_t *out_x, int32_t *out_y, int32_t *out_a,
+                       int32_t *out_vtp, int32_t *out_len);
+void lzo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 void lzo_backprop(lzo_tree *t, int current_latent_state_index, float discount, const float *rewards,
                   const float *values, const float *logits, const int32_t *is_reset,
                   const int32_t *to_play);
@@ -49,6 +54,10 @@ int lzo_get_trajectories(const lzo_tree *t, int32_t *out /*[B][tmax], -1 padded*
  * `threads` pthreads (each shard its own batch + RNG stream, i.e. shard-local parity).
  * Returns wall seconds for `searches` full searches of B roots x S simulations. */
 double lzo_bench_tree_only(int B, int A, int S, int threads, int searches, uint32_t seed);
+
+/* Exhaustive-check helper: number of k in [0, n) where host libm expf(bit pattern first+k)
+ * differs bitwise from got[k] (pins the device glibc-expf port, lzm_numerics.h). */
+long lzo_expf_mismatches(uint32_t first, int64_t n, const float *got, int threads);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(HERE, "liblzoracle.so")
 
 _i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
 _f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
 _lib = None
 
 
@@ -41,6 +42,8 @@ def lib():
         L.lzo_prepare.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p, _f32p, _f32p, _i32p]
         L.lzo_traverse.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_float, ctypes.c_uint32,
                                    _i32p, _i32p, _i32p, _i32p, _i32p, _i32p]
+        L.lzo_traverse_fast.argtypes = L.lzo_traverse.argtypes
+        L.lzo_philox4x32_10.argtypes = [_u32p, _u32p, _u32p]
         L.lzo_backprop.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, _f32p, _f32p, _f32p,
                                    ctypes.c_void_p, _i32p]
         L.lzo_get_distributions.argtypes = [ctypes.c_void_p, _i32p]
@@ -50,10 +53,18 @@ def lib():
         L.lzo_glibc_srand.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
         L.lzo_glibc_rand.restype = ctypes.c_int32
         L.lzo_glibc_rand.argtypes = [ctypes.c_void_p]
+        L.lzo_expf_mismatches.restype = ctypes.c_long
+        L.lzo_expf_mismatches.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]
         L.lzo_bench_tree_only.restype = ctypes.c_double
         L.lzo_bench_tree_only.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint32]
         _lib = L
     return _lib
+
+
+def philox4x32_10(ctr, key):
+    out = np.zeros(4, np.uint32)
+    lib().lzo_philox4x32_10(np.ascontiguousarray(ctr, np.uint32), np.ascontiguousarray(key, np.uint32), out)
+    return out
 
 
 def glibc_rand_stream(seed, n):
@@ -66,8 +77,9 @@ def glibc_rand_stream(seed, n):
 class OracleTree:
     """One batch of roots (CRoots + CMinMaxStatsList + CSearchResults of the reference)."""
 
-    def __init__(self, num_roots, action_space, max_sims, ez=False):
+    def __init__(self, num_roots, action_space, max_sims, ez=False, fast_rng=False):
         self.B, self.A = num_roots, action_space
+        self.fast_rng = fast_rng
         self._h = lib().lzo_create(num_roots, action_space, max_sims, int(ez))
 
     def __del__(self):
@@ -92,7 +104,8 @@ class OracleTree:
     def traverse(self, pb_c_base, pb_c_init, discount, seed, virtual_to_play):
         B = self.B
         outs = [np.zeros(B, np.int32) for _ in range(5)]
-        lib().lzo_traverse(self._h, int(pb_c_base), pb_c_init, discount, int(seed),
+        fn = lib().lzo_traverse_fast if self.fast_rng else lib().lzo_traverse
+        fn(self._h, int(pb_c_base), pb_c_init, discount, int(seed),
                            np.ascontiguousarray(virtual_to_play, np.int32), *outs)
         return tuple(outs)  # x, y, action, vtp, search_len
 
