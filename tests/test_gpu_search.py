@@ -4,7 +4,7 @@ Scalar heads (categorical_distribution=False): the whole search is bit-exact aga
 restatement of mcts_ctree.py:228-321 with the oracle tree (tests/helpers.py).
 Categorical heads: the tree is bit-exact given the values the decode kernel produced (recorded
 per simulation), and those decoded values match a torch fp32 InverseScalarTransform within
-rtol 1e-5 / atol 1e-4.
+rtol 1e-5 / atol 1e-5*support_scale (fp32 summation-order bound over the support).
 """
 import numpy as np
 import pytest
@@ -107,8 +107,10 @@ def test_categorical_search_tree_exact_given_decoded_values():
             r = torch_inverse_scalar_transform(out.reward, 300).squeeze(1)
             v = torch_inverse_scalar_transform(out.value, 300).squeeze(1)
             dec = torch.from_numpy(rec["decoded"][k]).to(DEV)
-            torch.testing.assert_close(dec[:, 0], r, rtol=1e-5, atol=1e-4)
-            torch.testing.assert_close(dec[:, 1], v, rtol=1e-5, atol=1e-4)
+            # fp32 expectation over 601 supports in [-300, 300]: the two summation orders differ
+            # by up to ~V*eps32*|s| -> tolerance scales with the support (3e-3 at scale 300)
+            torch.testing.assert_close(dec[:, 0], r, rtol=1e-5, atol=1e-5 * 300)
+            torch.testing.assert_close(dec[:, 1], v, rtol=1e-5, atol=1e-5 * 300)
             pool.append(out.latent_state)
 
 
