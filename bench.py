@@ -1,0 +1,261 @@
+"""bench.py — MCTS simulations/sec of the batched MuZero search (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): CartPole-v0 MuZero, 256 envs x 50 simulations per GPU,
+MuZeroModelMLP (latent 128, support 601, residual dynamics, BN) with random weights, synthetic
+observations. One step = one self-play search pass over the batch exactly as
+MuZeroPolicy._forward_collect runs it (lzero/policy/muzero.py:617-690): initial_inference ->
+Roots.prepare (Dirichlet-mixed priors) -> MuZeroMCTSCtree.search (50 simulations) -> root
+visit distributions and values. Inputs are resident in HBM before the timed region.
+
+Multi-GPU: one process per GPU (torchrun); every rank searches its own 256 envs (envs are
+independent trees: weak scaling, no collective in the data path). value = all ranks' sims / the
+slowest rank's time.
+
+Extra objects on the JSON line:
+  roofline     - dominant HIP kernel of the step, algorithmic bytes per launch / its live
+                 HIP-event duration vs the HBM peak (profiles/ holds the matching rocprof stats)
+  cpu_baseline - the oracle's CPU restatement of the reference ctree driving the same network on
+                 the host cores (the reference's architecture with device='cpu'), bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--envs", type=int, default=256)
+    p.add_argument("--sims", type=int, default=50)
+    p.add_argument("--rng", choices=["glibc", "philox"], default="glibc")
+    p.add_argument("--graph", type=int, default=1, help="replay each search as one HIP graph")
+    p.add_argument("--cpu-baseline-secs", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--zero-heads", action="store_true", help="reference zero-init last layers (all-tie search)")
+    return p.parse_args()
+
+
+def build_model(device, zero_heads, seed):
+    from lightzero_amd.model_mlp import cartpole_muzero_model
+    torch.manual_seed(seed)
+    m = cartpole_muzero_model(random_heads=not zero_heads)
+    # random BatchNorm statistics so eval-mode BN is not the identity
+    g = torch.Generator().manual_seed(seed + 1)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm1d):
+            with torch.no_grad():
+                mod.running_mean.copy_(torch.randn(mod.running_mean.shape, generator=g) * 0.1)
+                mod.running_var.copy_(torch.rand(mod.running_var.shape, generator=g) * 0.5 + 0.75)
+                mod.weight.copy_(torch.rand(mod.weight.shape, generator=g) * 0.5 + 0.75)
+                mod.bias.copy_(torch.randn(mod.bias.shape, generator=g) * 0.1)
+    return m.to(device).eval()
+
+
+class GpuStep:
+    """One collect-time search pass (muzero.py:660-690) on the GPU drop-in."""
+
+    def __init__(self, B, S, model, device, rng_mode, graph, seed):
+        from lightzero_amd.mcts_ctree import MuZeroMCTSCtree
+        from lightzero_amd.utils import EasyDict
+        from lightzero_amd.tree import SequentialSeeds, set_seed_source
+        self.B, self.S, self.model, self.device = B, S, model, device
+        MuZeroMCTSCtree.rng_mode = rng_mode
+        self.cls = MuZeroMCTSCtree
+        cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=device, use_hip_graph=bool(graph),
+                            model=dict(support_scale=300, categorical_distribution=True)))
+        self.mcts = MuZeroMCTSCtree(cfg)
+        rng = np.random.default_rng(seed)
+        self.obs = torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32)).to(device)
+        self.noises = torch.from_numpy(rng.dirichlet([0.3, 0.3], size=B).astype(np.float32)).to(device)
+        self.legal = [[0, 1] for _ in range(B)]
+        self.to_play = torch.full((B,), -1, dtype=torch.int32, device=device)
+        self.zero = torch.zeros(B, dtype=torch.float32, device=device)
+        set_seed_source(SequentialSeeds(seed))
+        self.last = None
+
+    def __call__(self):
+        with torch.no_grad():
+            out = self.model.initial_inference(self.obs)
+            roots = self.cls.roots(self.B, self.legal)
+            roots.prepare_device(0.25, self.noises, self.zero, out.policy_logits, self.to_play)
+            self.mcts.search(roots, self.model, out.latent_state, self.to_play)
+            t = roots.tree
+            self.last = (t.distributions(), t.values(), t.search_len)
+            roots.clear()
+
+
+def kernel_timing(step, n_search=2):
+    """Live per-kernel durations (HIP events on the launch stream) of the tree kernels over
+    `n_search` eager searches, plus the mean search depth d-bar from the kernels' own output."""
+    from lightzero_amd import mcts_ctree as mc
+    mcts = step.mcts
+    orig_traverse, orig_decode = mc.DeviceTree.traverse, mc.DeviceTree.decode_backprop
+    acc = {"traverse": [], "decode_backprop": []}
+    depth = []
+
+    def timed(name, fn):
+        def w(self, *a, **k):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn(self, *a, **k)
+            e1.record()
+            acc[name].append((e0, e1))
+            if name == "traverse":
+                depth.append(self.search_len.clone())
+        return w
+
+    use_graph = mcts._cfg.use_hip_graph
+    mcts._cfg.use_hip_graph = False
+    mc.DeviceTree.traverse = timed("traverse", orig_traverse)
+    mc.DeviceTree.decode_backprop = timed("decode_backprop", orig_decode)
+    try:
+        for _ in range(n_search):
+            step()
+        torch.cuda.synchronize()
+    finally:
+        mc.DeviceTree.traverse, mc.DeviceTree.decode_backprop = orig_traverse, orig_decode
+        mcts._cfg.use_hip_graph = use_graph
+    ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in acc.items()}
+    dbar = float(torch.stack(depth).float().mean().item())
+    return ms, dbar
+
+
+def algorithmic_bytes(B, A, H, V, dbar):
+    """Bytes each kernel must move per launch (this layout: 16-B node records).
+    traverse: per level the parent's stat+meta records (32 B) and A child stat records (16 A),
+    path + action writes (8 B); per root the six result words (28 B).
+    decode_backprop: two support rows (8 V) + policy logits (4 A) + the new latent row read and
+    filed into the pool (8 H) + A child records written (32 A) + leaf meta (16) + the backup
+    read-modify-write of (d+1) stat records and their meta (48 (d+1)) + min-max (16)."""
+    trav = B * (dbar * (32 + 16 * A + 8) + 28)
+    dec = B * (8 * V + 4 * A + 8 * H + 32 * A + 16 + 48 * (dbar + 1) + 16)
+    return {"traverse": trav, "decode_backprop": dec}
+
+
+def cpu_reference_search(B, S, model_cpu, secs, threads):
+    """The reference's architecture on the host: oracle ctree (restated cnode.cpp) + the same
+    network on torch CPU + InverseScalarTransform + list glue, as mcts_ctree.py:228-321 runs
+    with device='cpu'. Returns (sims/s, searches run)."""
+    from oracle.oracle import OracleTree
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    obs = torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32))
+    support = torch.arange(-300, 301, dtype=torch.float64).unsqueeze(0)
+
+    def inv(logits):
+        p = torch.softmax(logits, dim=1)
+        v = p.mul_(support).sum(1, keepdim=True)
+        tmp = (torch.sqrt(1 + 4 * 0.001 * (torch.abs(v) + 1 + 0.001)) - 1) / (2 * 0.001)
+        return (torch.sign(v) * (tmp * tmp - 1)).float()
+
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            out = model_cpu.initial_inference(obs)
+            tree = OracleTree(B, 2, S)
+            tree.set_delta(np.float32(0.01))
+            noises = rng.dirichlet([0.3, 0.3], size=B).astype(np.float32)
+            tree.prepare(np.float32(0.25), noises, np.zeros(B, np.float32), out.policy_logits.numpy(),
+                         np.full(B, -1, np.int32))
+            pool = [out.latent_state.numpy()]
+            tp = np.full(B, -1, np.int32)
+            for k in range(S):
+                x, y, a, vtp, _ = tree.traverse(19652, np.float32(1.25), np.float32(0.997), k, tp)
+                lat = torch.from_numpy(np.asarray([pool[ix][iy] for ix, iy in zip(x, y)]))
+                o = model_cpu.recurrent_inference(lat, torch.from_numpy(a.astype(np.int64)))
+                pool.append(o.latent_state.numpy())
+                tree.backprop(k + 1, np.float32(0.997), inv(o.reward).numpy().reshape(-1),
+                              inv(o.value).numpy().reshape(-1), o.policy_logits.numpy(), vtp)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return n * B * S / el, n, el
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    B, S = args.envs, args.sims
+    model = build_model(device, args.zero_heads, seed=0)
+    step = GpuStep(B, S, model, device, args.rng, args.graph, seed=1000 + rank)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    sims = world * B * S * args.steps
+    value = sims / el
+
+    # sanity: every root received exactly S visits
+    dsum = step.last[0].sum(dim=1)
+    assert bool((dsum == S).all()), "visit counts do not sum to num_simulations"
+
+    roofline = None
+    cpu = None
+    if rank == 0:
+        ms, dbar = kernel_timing(step)
+        byt = algorithmic_bytes(B, 2, 128, 601, dbar)
+        dom = max(ms, key=lambda k: ms[k])
+        achieved = byt[dom] / (ms[dom] * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                    "alg_bytes_per_launch": int(byt[dom]), "launch_us": round(ms[dom] * 1e3, 2),
+                    "kernels_us": {k: round(v * 1e3, 2) for k, v in ms.items()}, "mean_search_len": round(dbar, 3)}
+        if world == 1 and not args.no_cpu_baseline:
+            cores = min(16, os.cpu_count() or 1)
+            model_cpu = build_model(torch.device("cpu"), args.zero_heads, seed=0)
+            v, n, secs = cpu_reference_search(B, S, model_cpu, args.cpu_baseline_secs, cores)
+            cpu = {"value": round(v, 1), "unit": "sims/s", "cores": cores, "kind": "port",
+                   "sample": f"{n} full searches (B={B}, S={S}, same MLP on torch-CPU, oracle ctree restatement, "
+                             f"{secs:.1f}s)"}
+    if rank == 0:
+        line = {"metric": "MCTS simulations/sec (whole node), 256 parallel envs x 50 sims/step",
+                "value": round(value, 1), "unit": "sims/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                "config": {"workload": "CartPole-v0 MuZero search, MuZeroModelMLP (latent 128, support 601), "
+                                       f"{B} envs x {S} sims per GPU",
+                           "global_batch": world * B, "num_simulations": S, "rng": args.rng,
+                           "hip_graph": bool(args.graph), "heads": "zero" if args.zero_heads else "random",
+                           "parallelism": f"env-sharded x{world}"},
+                "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

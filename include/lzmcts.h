@@ -55,6 +55,14 @@ int lzm_action_space(const lzm_handle *h);
 int lzm_flags(const lzm_handle *h);
 const char *lzm_last_error(void);
 
+/* Builds the pUCT table {log((N+base+1)/base)+init, sqrt(N)} for these constants with the host
+ * libm (synchronous H2D; call outside stream capture). lzm_traverse rebuilds it on demand. */
+int lzm_set_pb_c(lzm_handle *h, int pb_c_base, float pb_c_init);
+
+/* Copies the whole tree state (nodes, root legal lists, last search paths) of `src` into `dst`
+ * (same num_roots / action_space; dst capacity >= src). */
+int lzm_copy_tree(lzm_handle *dst, const lzm_handle *src, void *stream);
+
 /* MinMaxStatsList(n) + set_delta (mz_tree.pyx:5-16, common_lib/cminimax.cpp:7-66).
  * minmax: float[n*4] = {maximum, minimum, value_delta_max, 0} per root. */
 int lzm_minmax_init(float *minmax, int n, float value_delta_max, void *stream);

@@ -38,6 +38,8 @@ SIGNATURES = {
     "lzm_action_space": [_vp],
     "lzm_flags": [_vp],
     "lzm_last_error": [],
+    "lzm_set_pb_c": [_vp, _i, _f],
+    "lzm_copy_tree": [_vp, _vp, _vp],
     "lzm_minmax_init": [_vp, _i, _f, _vp],
     "lzm_roots_prepare": [_vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp],
     "lzm_traverse": [_vp, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],

@@ -696,7 +696,8 @@ __global__ void gather_kernel(const float *pool, long long row, int B, const int
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
     const int i = (int)(e / row);
     const long long c = e - (long long)i * row;
-    out[e] = pool[((long long)x[i] * B + i) * row + c];
+    const int xi = max(x[i], 0);
+    out[e] = pool[((long long)xi * B + i) * row + c];
   }
 }
 
@@ -705,7 +706,8 @@ __global__ void gather_kernel_v4(const float4 *pool, long long row4, int B, cons
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
     const int i = (int)(e / row4);
     const long long c = e - (long long)i * row4;
-    out[e] = pool[((long long)x[i] * B + i) * row4 + c];
+    const int xi = max(x[i], 0);  // an unexpanded root reports -1 (reference: UB); never read before the pool
+    out[e] = pool[((long long)xi * B + i) * row4 + c];
   }
 }
 
@@ -964,6 +966,28 @@ int lzm_reserve(lzm_handle *h, int max_sims) {
   }
   free_tree(&old);
   return rc;
+}
+
+int lzm_set_pb_c(lzm_handle *h, int pb_c_base, float pb_c_init) {
+  if (!h || pb_c_base <= 0) return LZM_ERR_ARG;
+  return fill_lut(h, pb_c_base, pb_c_init);
+}
+
+int lzm_copy_tree(lzm_handle *dst, const lzm_handle *src, void *stream) {
+  if (!dst || !src || dst->B != src->B || dst->A != src->A || dst->sims_cap < src->sims_cap) {
+    set_err("lzm_copy_tree: handles differ in shape or destination is smaller");
+    return LZM_ERR_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const size_t nodes = (size_t)src->cap * src->B;
+  LZM_HIP(hipMemcpyAsync(dst->stat, src->stat, nodes * sizeof(NodeStat), hipMemcpyDeviceToDevice, s));
+  LZM_HIP(hipMemcpyAsync(dst->meta, src->meta, nodes * sizeof(NodeMeta), hipMemcpyDeviceToDevice, s));
+  LZM_HIP(hipMemcpyAsync(dst->legal, src->legal, sizeof(int32_t) * (size_t)src->B * src->A, hipMemcpyDeviceToDevice, s));
+  LZM_HIP(hipMemcpyAsync(dst->nlegal, src->nlegal, sizeof(int32_t) * src->B, hipMemcpyDeviceToDevice, s));
+  LZM_HIP(hipMemcpyAsync(dst->path, src->path, sizeof(int32_t) * (size_t)src->depth_cap * src->B, hipMemcpyDeviceToDevice, s));
+  LZM_HIP(hipMemcpyAsync(dst->path_act, src->path_act, sizeof(int32_t) * (size_t)src->depth_cap * src->B, hipMemcpyDeviceToDevice, s));
+  LZM_HIP(hipMemcpyAsync(dst->pathlen, src->pathlen, sizeof(int32_t) * src->B, hipMemcpyDeviceToDevice, s));
+  return LZM_OK;
 }
 
 int lzm_num_roots(const lzm_handle *h) { return h ? h->B : LZM_ERR_ARG; }

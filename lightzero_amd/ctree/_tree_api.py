@@ -122,13 +122,20 @@ class _RootsBase:
         B = self.root_num
         A = logits.shape[-1]
         t = self._acquire(A, logits.device)
-        legal = torch.full((B, A), -1, dtype=torch.int32)
-        count = torch.zeros(B, dtype=torch.int32)
-        for i, l in enumerate(self.legal_actions_list[:B]):
-            legal[i, :len(l)] = torch.tensor(l, dtype=torch.int32)
-            count[i] = len(l)
+        rows = self.legal_actions_list[:B]
+        if all(len(l) == A for l in rows):
+            legal = np.asarray(rows, dtype=np.int32).reshape(B, A)
+            count = np.full(B, A, np.int32)
+        else:
+            legal = np.full((B, A), -1, np.int32)
+            count = np.zeros(B, np.int32)
+            for i, l in enumerate(rows):
+                legal[i, :len(l)] = l
+                count[i] = len(l)
         dev = logits.device
-        t.prepare(legal.to(dev), count.to(dev),
+        legal = torch.from_numpy(legal).to(dev)
+        count = torch.from_numpy(count).to(dev)
+        t.prepare(legal, count,
                   None if noises is None else noises.to(dev, torch.float32).contiguous(), _f32(root_noise_weight),
                   rewards.to(dev, torch.float32).contiguous(), logits.to(dev, torch.float32).contiguous(),
                   to_play.to(dev, torch.int32).contiguous())

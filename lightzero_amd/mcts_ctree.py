@@ -22,7 +22,7 @@ import torch
 
 from .ctree import ez_tree, mz_tree
 from .scaling_transform import InverseScalarTransform
-from .tree import new_minmax, next_seed
+from .tree import DeviceTree, new_minmax, next_seed
 from .utils import EasyDict
 
 
@@ -85,6 +85,9 @@ class _SearchBuffers:
             self.net_in = torch.empty((B,) + tuple(shape), dtype=torch.float32, device=device)
             self.extra = [torch.empty((S + 1, B, e), dtype=torch.float32, device=device) for e in extra]
             self.extra_in = [torch.empty((B, e), dtype=torch.float32, device=device) for e in extra]
+            self.mm = torch.empty((B, 4), dtype=torch.float32, device=device)
+            self.vtp_in = torch.empty(B, dtype=torch.int32, device=device)
+            self.seeds = torch.empty(S, dtype=torch.int32, device=device)
             self.key = key
         return self
 
@@ -115,6 +118,7 @@ class MuZeroMCTSCtree(object):
             self._cfg.model.support_scale, self._cfg.device, self._cfg.model.categorical_distribution
         )
         self._buf = _SearchBuffers()
+        self._graphs = {}
 
     # 'glibc': the reference's tie-break stream, bit-exact (default); 'philox': independent
     # counter-based stream per root (LZM_RNG_FAST), no batch-serial dependency.
@@ -127,6 +131,24 @@ class MuZeroMCTSCtree(object):
     def _categorical(self):
         return bool(self._cfg.model.get('categorical_distribution', True))
 
+    def _loop(self, t, model, buf, mm, vtp_in, seeds, S, row, rec=None):
+        """The S simulations (mcts_ctree.py:255-321), all enqueued on the current stream."""
+        cfg = self._cfg
+        disc = float(np.float32(cfg.discount_factor))
+        cat = self._categorical()
+        new_minmax(t.B, cfg.value_delta_max, t.device, out=mm)
+        for k in range(S):
+            t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+            t.gather(buf.pool, row, buf.net_in)
+            out = model.recurrent_inference(buf.net_in, t.action64)
+            logits = out.policy_logits.float().contiguous()
+            if rec is not None:
+                rec.step(k, t, logits)
+            t.decode_backprop(k + 1, disc, mm, out.reward.float().contiguous(), out.value.float().contiguous(), cat,
+                              logits, t.vtp, next_latent=out.latent_state.float().contiguous(),
+                              pool_slot=buf.pool[k + 1], row_elems=row,
+                              out_decoded=None if rec is None else rec.decoded[k])
+
     def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
                to_play_batch: Union[int, List[Any]]) -> None:
         with torch.no_grad():
@@ -136,34 +158,43 @@ class MuZeroMCTSCtree(object):
                 raise RuntimeError("search: roots must be prepared (Roots.prepare / prepare_no_noise) first")
             B, S = roots.num, int(self._cfg.num_simulations)
             t.reserve(S)
+            t.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
             dev = t.device
             lat0 = _latent_tensor(latent_state_roots, dev)
             shape = lat0.shape[1:]
             row = int(np.prod(shape)) if len(shape) else 1
             buf = self._buf.get(B, S, shape, dev)
             buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
-            cfg = self._cfg
-            disc = float(np.float32(cfg.discount_factor))
-            mm = new_minmax(B, cfg.value_delta_max, dev)
-            vtp_in = _to_play_tensor(to_play_batch, B, dev)
-            seeds = _seeds(S, dev)
-            cat = self._categorical()
+            buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
+            buf.seeds.copy_(_seeds(S, dev))
             rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
             if rec is not None:
-                rec.seeds = seeds.cpu().numpy().view(np.uint32)
-            for k in range(S):
-                t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
-                t.gather(buf.pool, row, buf.net_in)
-                out = model.recurrent_inference(buf.net_in, t.action64)
-                logits = out.policy_logits.float().contiguous()
-                if rec is not None:
-                    rec.step(k, t, logits)
-                t.decode_backprop(k + 1, disc, mm, out.reward.float().contiguous(), out.value.float().contiguous(), cat,
-                                  logits, t.vtp, next_latent=out.latent_state.float().contiguous(),
-                                  pool_slot=buf.pool[k + 1], row_elems=row,
-                                  out_decoded=None if rec is None else rec.decoded[k])
-            roots._last_minmax = mm
+                rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
+            if rec is None and self._cfg.get('use_hip_graph', False):
+                self._graph_search(t, model, buf, S, row)
+            else:
+                self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, rec)
+            roots._last_minmax = buf.mm
             self.last_record = rec
+
+    def _graph_search(self, t, model, buf, S, row):
+        """Replays the whole S-simulation loop as one HIP graph (captured once per tree handle,
+        model and shape; inputs are the static buffers filled just before)."""
+        key = (t.h.value, t.generation, id(model), buf.key)
+        g = self._graphs.get(key)
+        if g is None:
+            # warm up every kernel and library handle on a scratch tree (must not touch `t`)
+            scratch = DeviceTree(t.B, t.A, max(S, t.sims_capacity), ez=t.ez, fast_rng=t.fast_rng, device=t.device)
+            scratch.copy_roots_from(t)
+            scratch.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
+            self._loop(scratch, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row)
+            torch.cuda.synchronize(t.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row)
+            self._graphs[key] = g
+            scratch.close()
+        g.replay()
 
 
 class EfficientZeroMCTSCtree(object):

@@ -61,6 +61,8 @@ class DeviceTree:
         with torch.cuda.device(self.device):
             call("lzm_create", self.B, self.A, int(max_sims), flags, ctypes.byref(h))
         self.h = h
+        self.generation = 0
+        self._pb_c = (19652, 1.25)  # lzm_create builds the table for the reference defaults
         i32 = dict(dtype=torch.int32, device=self.device)
         B = self.B
         self.x = torch.zeros(B, **i32)
@@ -80,6 +82,17 @@ class DeviceTree:
         if max_sims > self.sims_capacity:
             with torch.cuda.device(self.device):
                 call("lzm_reserve", self.h, int(max_sims))
+            self.generation += 1  # device buffers moved: captured graphs are stale
+
+    def set_pb_c(self, pb_c_base, pb_c_init):
+        key = (int(pb_c_base), float(np.float32(pb_c_init)))
+        if key != self._pb_c:
+            with torch.cuda.device(self.device):
+                call("lzm_set_pb_c", self.h, key[0], key[1])
+            self._pb_c = key
+
+    def copy_roots_from(self, other, stream=None):
+        call("lzm_copy_tree", self.h, other.h, stream_ptr(stream))
 
     def close(self):
         h = getattr(self, "h", None)
@@ -140,8 +153,8 @@ class DeviceTree:
         return out.cpu().tolist()
 
 
-def new_minmax(n, value_delta_max, device, stream=None):
-    mm = torch.empty((n, 4), dtype=torch.float32, device=device)
+def new_minmax(n, value_delta_max, device, stream=None, out=None):
+    mm = torch.empty((n, 4), dtype=torch.float32, device=device) if out is None else out
     call("lzm_minmax_init", ptr(mm), int(n), float(np.float32(value_delta_max)), stream_ptr(stream))
     return mm
 
