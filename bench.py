@@ -31,6 +31,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (matrix = vector rate on gfx950, MI355X_MICROARCH.md)
 
 
 def parse():
@@ -41,7 +42,10 @@ def parse():
     p.add_argument("--envs", type=int, default=256)
     p.add_argument("--sims", type=int, default=50)
     p.add_argument("--rng", choices=["glibc", "philox"], default="glibc")
-    p.add_argument("--graph", type=int, default=1, help="replay each search as one HIP graph")
+    p.add_argument("--path", choices=["fused", "generic"], default="fused",
+                   help="fused: one lzm_search_mlp launch per search; generic: HIP tree kernels around the "
+                        "PyTorch network (any model)")
+    p.add_argument("--graph", type=int, default=1, help="generic path: replay each search as one HIP graph")
     p.add_argument("--cpu-baseline-secs", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--zero-heads", action="store_true", help="reference zero-init last layers (all-tie search)")
@@ -67,7 +71,7 @@ def build_model(device, zero_heads, seed):
 class GpuStep:
     """One collect-time search pass (muzero.py:660-690) on the GPU drop-in."""
 
-    def __init__(self, B, S, model, device, rng_mode, graph, seed):
+    def __init__(self, B, S, model, device, rng_mode, graph, seed, fused=True):
         from lightzero_amd.mcts_ctree import MuZeroMCTSCtree
         from lightzero_amd.utils import EasyDict
         from lightzero_amd.tree import SequentialSeeds, set_seed_source
@@ -75,6 +79,7 @@ class GpuStep:
         MuZeroMCTSCtree.rng_mode = rng_mode
         self.cls = MuZeroMCTSCtree
         cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=device, use_hip_graph=bool(graph),
+                            fused_search=bool(fused),
                             model=dict(support_scale=300, categorical_distribution=True)))
         self.mcts = MuZeroMCTSCtree(cfg)
         rng = np.random.default_rng(seed)
@@ -97,13 +102,15 @@ class GpuStep:
             roots.clear()
 
 
-def kernel_timing(step, n_search=2):
-    """Live per-kernel durations (HIP events on the launch stream) of the tree kernels over
-    `n_search` eager searches, plus the mean search depth d-bar from the kernels' own output."""
+def kernel_timing(step, n_search=3):
+    """Live per-launch durations (HIP events on the launch stream — torch's current stream, the
+    one every lzm_* call is enqueued on) of the search kernels over `n_search` searches, plus
+    the mean search depth d-bar from the kernels' own search_len output."""
     from lightzero_amd import mcts_ctree as mc
     mcts = step.mcts
-    orig_traverse, orig_decode = mc.DeviceTree.traverse, mc.DeviceTree.decode_backprop
-    acc = {"traverse": [], "decode_backprop": []}
+    names = ("traverse", "decode_backprop", "search_mlp")
+    orig = {n: getattr(mc.DeviceTree, n) for n in names}
+    acc = {n: [] for n in names}
     depth = []
 
     def timed(name, fn):
@@ -119,18 +126,35 @@ def kernel_timing(step, n_search=2):
 
     use_graph = mcts._cfg.use_hip_graph
     mcts._cfg.use_hip_graph = False
-    mc.DeviceTree.traverse = timed("traverse", orig_traverse)
-    mc.DeviceTree.decode_backprop = timed("decode_backprop", orig_decode)
+    for n in names:
+        setattr(mc.DeviceTree, n, timed(n, orig[n]))
+    mcts.record = True
     try:
         for _ in range(n_search):
             step()
+            if mcts.last_record is not None and not acc["traverse"]:
+                depth.append(mcts.last_record.search_len.clone())
         torch.cuda.synchronize()
     finally:
-        mc.DeviceTree.traverse, mc.DeviceTree.decode_backprop = orig_traverse, orig_decode
+        for n in names:
+            setattr(mc.DeviceTree, n, orig[n])
         mcts._cfg.use_hip_graph = use_graph
-    ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in acc.items()}
-    dbar = float(torch.stack(depth).float().mean().item())
+        mcts.record = False
+    ms = {k: float(np.mean([a.elapsed_time(b) for a, b in v])) for k, v in acc.items() if v}
+    dbar = float(torch.cat([d.reshape(-1) for d in depth]).float().mean().item())
     return ms, dbar
+
+
+def mlp_flops_per_sim(H, A, F, V, res=True):
+    """2 x multiply-adds of one recurrent_inference row (149,376 MAC at
+    H=128, A=2, F=32, V=601)."""
+    mac = (H + A) * H + H * H          # fc_dynamics(_1)
+    mac += 2 * H * H if res else 0     # fc_dynamics_2
+    mac += H * F + F * V               # fc_reward_head
+    mac += 2 * H * H                   # fc_prediction_common
+    mac += H * F + F * V               # fc_value_head
+    mac += H * F + F * A               # fc_policy_head
+    return 2 * mac
 
 
 def algorithmic_bytes(B, A, H, V, dbar):
@@ -197,7 +221,7 @@ def main():
     torch.cuda.set_device(device)
     B, S = args.envs, args.sims
     model = build_model(device, args.zero_heads, seed=0)
-    step = GpuStep(B, S, model, device, args.rng, args.graph, seed=1000 + rank)
+    step = GpuStep(B, S, model, device, args.rng, args.graph, seed=1000 + rank, fused=args.path == "fused")
 
     for _ in range(args.warmup):
         step()
@@ -227,13 +251,26 @@ def main():
     cpu = None
     if rank == 0:
         ms, dbar = kernel_timing(step)
-        byt = algorithmic_bytes(B, 2, 128, 601, dbar)
-        dom = max(ms, key=lambda k: ms[k])
-        achieved = byt[dom] / (ms[dom] * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                    "alg_bytes_per_launch": int(byt[dom]), "launch_us": round(ms[dom] * 1e3, 2),
-                    "kernels_us": {k: round(v * 1e3, 2) for k, v in ms.items()}, "mean_search_len": round(dbar, 3)}
+        if "search_mlp" in ms:
+            # fused whole-search kernel: one launch = B x S simulations; fp32 FMA network dominates
+            flops = B * S * mlp_flops_per_sim(128, 2, 32, 601)
+            hbm = B * (S * 8 * 128 + 2 * 32 * (1 + 2 * (S + 1)))  # latent gather+file per sim, tree slice in/out
+            sec = ms["search_mlp"] * 1e-3
+            achieved = flops / sec / 1e12
+            roofline = {"bound": "mfma", "kernel": "search_mlp_kernel", "achieved": round(achieved, 3),
+                        "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
+                        "traffic": None, "alg_flops_per_launch": int(flops), "alg_hbm_bytes_per_launch": int(hbm),
+                        "hbm_achieved_GBs": round(hbm / sec / 1e9, 2), "launch_us": round(ms["search_mlp"] * 1e3, 1),
+                        "sims_per_launch": B * S, "mean_search_len": round(dbar, 3)}
+        else:
+            byt = algorithmic_bytes(B, 2, 128, 601, dbar)
+            dom = max(ms, key=lambda k: ms[k])
+            achieved = byt[dom] / (ms[dom] * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                        "alg_bytes_per_launch": int(byt[dom]), "launch_us": round(ms[dom] * 1e3, 2),
+                        "kernels_us": {k: round(v * 1e3, 2) for k, v in ms.items()},
+                        "mean_search_len": round(dbar, 3)}
         if world == 1 and not args.no_cpu_baseline:
             cores = min(16, os.cpu_count() or 1)
             model_cpu = build_model(torch.device("cpu"), args.zero_heads, seed=0)
@@ -249,7 +286,8 @@ def main():
                 "config": {"workload": "CartPole-v0 MuZero search, MuZeroModelMLP (latent 128, support 601), "
                                        f"{B} envs x {S} sims per GPU",
                            "global_batch": world * B, "num_simulations": S, "rng": args.rng,
-                           "hip_graph": bool(args.graph), "heads": "zero" if args.zero_heads else "random",
+                           "path": args.path, "hip_graph": bool(args.graph) and args.path == "generic",
+                           "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
                 "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)

@@ -124,6 +124,32 @@ int lzm_get_distributions(lzm_handle *h, int32_t *out, void *stream);
 int lzm_get_values(lzm_handle *h, float *out, void *stream);
 int lzm_get_trajectories(lzm_handle *h, int32_t *out, int tmax, void *stream);
 
+/* ---- Fused whole search for the MuZeroModelMLP family (lzero/model/muzero_model_mlp.py) ----
+ * One launch runs all `num_simulations` simulations of MuZeroMCTSCtree.search
+ * (mcts_ctree.py:255-321) for every root: selection, leaf-latent gather, recurrent_inference
+ * (dynamics + reward head + prediction heads, BatchNorm folded into the Linears), support decode
+ * (InverseScalarTransform, softmax always applied: the heads are Linear logits), expansion and
+ * backup. Roots must be prepared (lzm_roots_prepare) and minmax initialised (lzm_minmax_init).
+ * weights: device float buffer, lzm_mlp_packed_floats() floats, layers in the order
+ *   fc_dynamics(_1)[0] (K = hidden + actions: latent rows then one-hot action rows),
+ *   fc_dynamics(_1)[1], [fc_dynamics_2[0], fc_dynamics_2[1] if res_dynamics],
+ *   fc_reward_head[0] (hidden -> head_hidden), fc_reward_head[1] (head_hidden -> support),
+ *   fc_prediction_common[0], [1], fc_value_head[0], [1], fc_policy_head[0], [1] (-> actions);
+ * each as W[K][N] (input-major, i.e. torch weight transposed) followed by bias[N]; ReLU after
+ * every layer except the three head outputs; res_dynamics adds the input latent after
+ * fc_dynamics_1 (muzero_model_mlp.py:427-431). latent_pool: float[S+1][B][hidden] with slot 0 =
+ * root latents; slots 1..S receive the new latents. seeds: uint32[S] (traverse k uses seeds[k]).
+ * rec_* (nullable, [S][B] / [S][B][2] / [S][B][actions]): per-simulation x, last action,
+ * search_len, decoded {reward, value} and policy logits. */
+int64_t lzm_mlp_packed_floats(int hidden, int actions, int head_hidden, int support, int res_dynamics);
+int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int res_dynamics, const float *weights,
+                   int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
+                   const uint32_t *seeds, const int32_t *virtual_to_play, float *latent_pool, int32_t *rec_x,
+                   int32_t *rec_a, int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream);
+/* int32[2]: {look-back spin timeouts (must stay 0), slices resolved serially (ties that reached
+ * an expanded child)} accumulated over the handle's fused searches. */
+int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream);
+
 /* Diagnostics: traverse passes used by the last parity-mode traverse (device int32[1]). */
 int lzm_last_traverse_passes(lzm_handle *h, int32_t *out, void *stream);
 

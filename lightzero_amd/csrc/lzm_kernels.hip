@@ -28,162 +28,10 @@
 
 #include "../../include/lzmcts.h"
 #include "lzm_numerics.h"
+#include "lzm_tree.h"
+#include "lzm_search_mlp.h"
 
 namespace lzm {
-
-constexpr float kFloatMax = 1000000.0f;  // common_lib/cminimax.h:9-10
-constexpr float kFloatMin = -kFloatMax;
-constexpr int kMaxActions = 64;          // tie lists are held as one 64-bit mask
-constexpr int kMaxWG = 1024;
-
-struct alignas(16) NodeStat {
-  int visit;
-  float value_sum;
-  float prior;
-  float reward;  // value_prefix for EfficientZero
-};
-struct alignas(16) NodeMeta {
-  int latent;  // current_latent_state_index, -1 while not expanded
-  int to_play;
-  int best;  // best_action
-  int is_reset;
-};
-
-struct TreeView {
-  NodeStat *stat;
-  NodeMeta *meta;
-  const int32_t *legal;   // [B][A]
-  const int32_t *nlegal;  // [B]
-  int32_t *path;          // [D][B] node ids
-  int32_t *path_act;      // [D][B] actions
-  int32_t *pathlen;       // [B] edges of the last path
-  const float2 *lut;      // [N] {log((N+base+1)/base)+init, sqrt(N)}
-  int B, A, cap, lut_n, depth_cap;
-};
-
-__device__ inline size_t nidx(const TreeView &t, int node, int i) { return (size_t)node * t.B + i; }
-__device__ inline float node_value(const NodeStat &s) {  // CNode::value, cnode.cpp:219-235
-  return s.visit == 0 ? 0.0f : s.value_sum / (float)s.visit;
-}
-__device__ inline int legal_at(const TreeView &t, int i, int node, int j) {
-  return node == 0 ? t.legal[(size_t)i * t.A + j] : j;
-}
-__device__ inline int legal_n(const TreeView &t, int i, int node) { return node == 0 ? t.nlegal[i] : t.A; }
-
-// CMinMaxStats::normalize, common_lib/cminimax.cpp:33-45
-__device__ inline float mm_normalize(float4 mm, float v) {
-  float norm = v;
-  float delta = mm.x - mm.y;
-  if (delta > 0) {
-    if (delta < mm.z)
-      norm = (norm - mm.y) / mm.z;
-    else
-      norm = (norm - mm.y) / delta;
-  }
-  return norm;
-}
-
-// Result of one root's descent.
-struct Descent {
-  int len, x, action, vtp, leaf;
-};
-
-// One root's selection walk (cbatch_traverse body, cnode.cpp:783-823 with compute_mean_q
-// :169-203, cselect_child :551-596, cucb_score :655-699; EZ variants
-// ctree_efficientzero/lib/cnode.cpp:173-212, :756-814). `draw(level)` returns the rand()
-// value consumed at that level. Writes path/path_act; never writes tree state.
-template <bool EZ, typename Draw>
-__device__ inline Descent descend(const TreeView &t, int i, float4 mm, int players, int vtp, float disc, Draw draw) {
-  int node = 0, is_root = 1, len = 0, last_action = -1, parent = 0;
-  float parent_q = 0.0f;  // per root; the reference's cross-root carry is provably 0 wherever read
-  NodeStat s = t.stat[nidx(t, 0, i)];
-  NodeMeta m = t.meta[nidx(t, 0, i)];
-  t.path[i] = 0;
-  while (m.latent >= 0 && len < t.depth_cap - 1) {
-    const int n = legal_n(t, i, node);
-    const int base = 1 + t.A * m.latent;
-    const float pvp = s.reward;
-    const int preset = m.is_reset;
-    // compute_mean_q
-    float total_q = 0.0f;
-    int total_v = 0;
-    for (int j = 0; j < n; ++j) {
-      const int a = legal_at(t, i, node, j);
-      const NodeStat c = t.stat[nidx(t, base + a, i)];
-      if (c.visit > 0) {
-        float tr = c.reward;
-        if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
-        float qsa = tr + disc * node_value(c);
-        total_q += qsa;
-        total_v += 1;
-      }
-    }
-    float mean_q;
-    if (is_root && total_v > 0)
-      mean_q = total_q / (float)total_v;
-    else
-      mean_q = (parent_q + total_q) / (float)(total_v + 1);
-    is_root = 0;
-    parent_q = mean_q;
-    // cselect_child / cucb_score
-    int N = s.visit - 1;
-    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
-    const float2 L = t.lut[N];
-    float max_score = kFloatMin;
-    uint64_t mask = 0;
-    for (int j = 0; j < n; ++j) {
-      const int a = legal_at(t, i, node, j);
-      const NodeStat c = t.stat[nidx(t, base + a, i)];
-      float pb_c = L.x;
-      pb_c *= (L.y / (float)(c.visit + 1));
-      const float prior_score = pb_c * c.prior;
-      float vs;
-      if (c.visit == 0) {
-        vs = mean_q;
-      } else {
-        float tr = c.reward;
-        if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
-        if (players == 1)
-          vs = tr + disc * node_value(c);
-        else
-          vs = tr + disc * (-node_value(c));
-      }
-      vs = mm_normalize(mm, vs);
-      if (vs < 0) vs = 0;
-      if (vs > 1) vs = 1;
-      const float score = prior_score + vs;
-      if (max_score < score) {
-        max_score = score;
-        mask = 1ull << j;
-      } else if (score >= max_score - 0.000001f) {
-        mask |= 1ull << j;
-      }
-    }
-    const uint32_t r = draw(len);
-    const int nl = __popcll(mask);
-    int k = (int)(r % (uint32_t)nl);
-    uint64_t mm_ = mask;
-    for (; k > 0; --k) mm_ &= mm_ - 1;
-    const int jsel = __ffsll((long long)mm_) - 1;
-    const int action = legal_at(t, i, node, jsel);
-    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
-    t.path_act[(size_t)len * t.B + i] = action;
-    parent = node;
-    node = base + action;
-    last_action = action;
-    ++len;
-    t.path[(size_t)len * t.B + i] = node;
-    s = t.stat[nidx(t, node, i)];
-    m = t.meta[nidx(t, node, i)];
-  }
-  Descent d;
-  d.len = len;
-  d.x = t.meta[nidx(t, parent, i)].latent;
-  d.action = last_action;
-  d.vtp = vtp;
-  d.leaf = node;
-  return d;
-}
 
 struct TraverseArgs {
   TreeView t;
@@ -389,92 +237,6 @@ __global__ __launch_bounds__(256) void traverse_fast_kernel(TraverseArgs p) {
   }
 }
 
-// CNode::expand of a non-root leaf (cnode.cpp:83-147): all A actions legal, masked-softmax
-// priors with glibc expf, sequential sum; children reset to CNode(prior, {}).
-__device__ inline void expand_leaf(const TreeView &t, int i, int leaf, int to_play, int latent, float reward,
-                                   const float *logits, int is_reset, bool ez) {
-  NodeMeta m = t.meta[nidx(t, leaf, i)];
-  m.latent = latent;
-  m.to_play = to_play;
-  if (ez) m.is_reset = is_reset;
-  t.meta[nidx(t, leaf, i)] = m;
-  t.stat[nidx(t, leaf, i)].reward = reward;
-  float pmax = kFloatMin;
-  for (int a = 0; a < t.A; ++a)
-    if (pmax < logits[a]) pmax = logits[a];
-  float sum = 0.0f;
-  for (int a = 0; a < t.A; ++a) sum += glibc_expf(logits[a] - pmax);
-  const int base = 1 + t.A * latent;
-  for (int a = 0; a < t.A; ++a) {
-    const float e = glibc_expf(logits[a] - pmax);
-    NodeStat c;
-    c.visit = 0;
-    c.value_sum = 0.0f;
-    c.prior = e / sum;
-    c.reward = 0.0f;
-    t.stat[nidx(t, base + a, i)] = c;
-    NodeMeta cm;
-    cm.latent = -1;
-    cm.to_play = 0;
-    cm.best = -1;
-    cm.is_reset = 0;
-    t.meta[nidx(t, base + a, i)] = cm;
-  }
-}
-
-// cbackpropagate: MuZero cnode.cpp:419-478, EfficientZero
-// ctree_efficientzero/lib/cnode.cpp:482-575.
-template <bool EZ>
-__device__ inline void backup(const TreeView &t, int i, float4 *mm_ptr, int to_play, float value, float disc) {
-  float4 mm = *mm_ptr;
-  const int len = t.pathlen[i];
-  float b = value;
-  float child_prefix_parent = 0.0f;  // unused for MZ
-  (void)child_prefix_parent;
-  for (int l = len; l >= 0; --l) {
-    const int node = t.path[(size_t)l * t.B + i];
-    NodeStat s = t.stat[nidx(t, node, i)];
-    const int ntp = t.meta[nidx(t, node, i)].to_play;
-    if (to_play == -1 || ntp == to_play)
-      s.value_sum += b;
-    else
-      s.value_sum += -b;
-    s.visit += 1;
-    t.stat[nidx(t, node, i)] = s;
-    const float v = node_value(s);
-    if (!EZ) {
-      const float tr = s.reward;
-      float q;
-      if (to_play == -1) {
-        q = tr + disc * v;
-        b = tr + disc * b;
-      } else {
-        q = tr + disc * -v;
-        b = (ntp == to_play) ? (-tr + disc * b) : (tr + disc * b);
-      }
-      if (q > mm.x) mm.x = q;
-      if (q < mm.y) mm.y = q;
-    } else {
-      float pvp = 0.0f;
-      int reset = 0;
-      if (l >= 1) {
-        const int pn = t.path[(size_t)(l - 1) * t.B + i];
-        pvp = t.stat[nidx(t, pn, i)].reward;
-        reset = t.meta[nidx(t, pn, i)].is_reset;
-      }
-      float tr = s.reward - pvp;
-      const float q = tr + disc * v;
-      if (q > mm.x) mm.x = q;
-      if (q < mm.y) mm.y = q;
-      if (reset == 1) tr = s.reward;
-      if (to_play == -1 || ntp != to_play)
-        b = tr + disc * b;
-      else
-        b = -tr + disc * b;
-    }
-  }
-  *mm_ptr = mm;
-}
 
 struct BackpropArgs {
   TreeView t;
@@ -523,12 +285,6 @@ __device__ inline float wave_support_expectation(const float *row, int V, bool s
   return acc;
 }
 
-__device__ inline float h_inverse(float value) {
-  const float eps = 0.001f;
-  float tmp = (sqrtf(1.0f + 0.004f * (fabsf(value) + 1.0f + eps)) - 1.0f) * (1.0f / 0.002f);
-  float sgn = value > 0.0f ? 1.0f : (value < 0.0f ? -1.0f : 0.0f);
-  return sgn * (tmp * tmp - 1.0f);
-}
 
 __device__ inline float wave_row_sum(const float *row, int V) {
   const int lane = threadIdx.x & 63;
@@ -803,6 +559,14 @@ struct lzm_handle {
   int lut_base = -1;
   float lut_init = -1.0f;
   uint32_t *jmat = nullptr;  // [2][kMaxWG][31]
+  // fused whole-search state (lzm_search_mlp)
+  uint32_t *coef = nullptr;  // [coef_positions][31] glibc draw coefficients
+  int coef_positions = 0;
+  uint32_t *pow16807 = nullptr;            // [31]
+  unsigned long long *lb_flags = nullptr;  // [flag_sims][G] look-back words
+  int flag_sims = 0;
+  uint32_t *epoch = nullptr;               // [2] launch epoch, done counter
+  int32_t *search_diag = nullptr;          // [2]
 };
 
 // Jump matrices of glibc random_r: row m of J_first expresses z[344+m] (the m-th rand()
@@ -943,6 +707,7 @@ int lzm_destroy(lzm_handle *h) {
   free_tree(h);
   dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag);
   dfree(h->hint); dfree(h->norm_flag); dfree(h->jmat);
+  dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag);
   delete h;
   return LZM_OK;
 }
@@ -1236,6 +1001,204 @@ int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream) {
   }
   hipLaunchKernelGGL(debug_glibc_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, seed, n, out, jm, jm + kMaxWG * 31);
   LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------- fused whole-search (MLP)
+namespace {
+
+// Layer shapes of the packed MuZeroModelMLP recurrent network (lzm_search_mlp.h order).
+struct LayerShape {
+  int krows, K, N;
+};
+void mlp_shapes(int H, int A, int F, int V, LayerShape *s) {
+  s[0] = {H + A, H, H};  // fc_dynamics(_1)[0]: input [latent; one-hot action]
+  s[1] = {H, H, H};
+  s[2] = {H, H, H};      // fc_dynamics_2 (res_connection_in_dynamics)
+  s[3] = {H, H, H};
+  s[4] = {H, H, F};      // fc_reward_head
+  s[5] = {F, F, V};
+  s[6] = {H, H, H};      // fc_prediction_common
+  s[7] = {H, H, H};
+  s[8] = {H, H, F};      // fc_value_head
+  s[9] = {F, F, V};
+  s[10] = {H, H, F};     // fc_policy_head
+  s[11] = {F, F, A};
+}
+
+// Coefficients of z[344 + p] (the p-th rand() output before >> 1) over the 31 seeded words.
+int ensure_coef(lzm_handle *h, int positions) {
+  if (h->coef_positions >= positions) return LZM_OK;
+  std::vector<uint32_t> tab((size_t)positions * 31);
+  std::vector<uint32_t> ring((size_t)34 * 31, 0u);  // z[n] for n mod 34
+  auto row = [&](long n) { return &ring[(size_t)(n % 34) * 31]; };
+  for (int j = 0; j < 31; ++j) {
+    uint32_t *r = row(j);
+    for (int c = 0; c < 31; ++c) r[c] = (c == j);
+  }
+  for (int j = 31; j < 34; ++j) memcpy(row(j), row(j - 31), 31 * sizeof(uint32_t));
+  const long last = 344L + positions;
+  for (long n = 34; n < last; ++n) {
+    uint32_t tmp[31];
+    const uint32_t *a = row(n - 31), *b = row(n - 3);
+    for (int c = 0; c < 31; ++c) tmp[c] = a[c] + b[c];
+    memcpy(row(n), tmp, sizeof(tmp));
+    if (n >= 344) memcpy(&tab[(size_t)(n - 344) * 31], tmp, sizeof(tmp));
+  }
+  dfree(h->coef);
+  h->coef = nullptr;
+  LZM_HIP(hipMalloc(&h->coef, tab.size() * sizeof(uint32_t)));
+  LZM_HIP(hipMemcpy(h->coef, tab.data(), tab.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  h->coef_positions = positions;
+  if (!h->pow16807) {
+    uint32_t pw[31];
+    unsigned long long x = 1;
+    for (int i = 0; i < 31; ++i) {
+      pw[i] = (uint32_t)x;
+      x = (x * 16807ull) % 2147483647ull;
+    }
+    LZM_HIP(hipMalloc(&h->pow16807, sizeof(pw)));
+    LZM_HIP(hipMemcpy(h->pow16807, pw, sizeof(pw), hipMemcpyHostToDevice));
+  }
+  return LZM_OK;
+}
+
+int ensure_flags(lzm_handle *h, int sims, int G) {
+  if (!h->epoch) {
+    LZM_HIP(hipMalloc(&h->epoch, 2 * sizeof(uint32_t)));
+    const uint32_t init[2] = {1u, 0u};
+    LZM_HIP(hipMemcpy(h->epoch, init, sizeof(init), hipMemcpyHostToDevice));
+    LZM_HIP(hipMalloc(&h->search_diag, 2 * sizeof(int32_t)));
+    LZM_HIP(hipMemset(h->search_diag, 0, 2 * sizeof(int32_t)));
+  }
+  if (h->flag_sims >= sims) return LZM_OK;
+  dfree(h->lb_flags);
+  h->lb_flags = nullptr;
+  const size_t n = (size_t)sims * G;
+  LZM_HIP(hipMalloc(&h->lb_flags, n * sizeof(unsigned long long)));
+  LZM_HIP(hipMemset(h->lb_flags, 0, n * sizeof(unsigned long long)));  // epoch 0 never matches
+  h->flag_sims = sims;
+  return LZM_OK;
+}
+
+constexpr int kRoots = 8;  // roots per workgroup in the fused search
+constexpr size_t kMaxLds = 160 * 1024 - 1024;
+
+size_t round4(size_t x) { return (x + 3) & ~(size_t)3; }
+
+}  // namespace
+
+extern "C" {
+
+int64_t lzm_mlp_packed_floats(int hidden, int actions, int head_hidden, int support, int res_dynamics) {
+  if (hidden <= 0 || actions <= 0 || head_hidden <= 0 || support <= 0) return -1;
+  LayerShape s[12];
+  mlp_shapes(hidden, actions, head_hidden, support, s);
+  int64_t n = 0;
+  for (int l = 0; l < 12; ++l) {
+    if (!res_dynamics && (l == 2 || l == 3)) continue;
+    n += (int64_t)s[l].krows * s[l].N + s[l].N;
+  }
+  return n;
+}
+
+int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int res_dynamics, const float *weights,
+                   int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
+                   const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, int32_t *rec_x, int32_t *rec_a,
+                   int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream) {
+  if (!h || !weights || !minmax || !seeds || !vtp_in || !latent_pool || num_simulations <= 0) {
+    set_err("lzm_search_mlp: null argument or no simulations");
+    return LZM_ERR_ARG;
+  }
+  if (h->flags & LZM_TREE_EZ) {
+    set_err("lzm_search_mlp: MuZero trees only");
+    return LZM_ERR_ARG;
+  }
+  const int H = hidden, F = head_hidden, V = support, A = h->A, S = num_simulations;
+  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || A > H) {
+    set_err("lzm_search_mlp: unsupported network shape");
+    return LZM_ERR_ARG;
+  }
+  if (S > h->sims_cap) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_mlp: %d simulations > reserved %d (lzm_reserve)", S, h->sims_cap);
+    return LZM_ERR_CAPACITY;
+  }
+  int rc = fill_lut(h, pb_c_base, pb_c_init);
+  if (rc != LZM_OK) return rc;
+  const int R = kRoots;
+  const int G = (h->B + R - 1) / R;
+  const bool fast = (h->flags & LZM_RNG_FAST) != 0;
+  if (!fast) {
+    rc = ensure_coef(h, h->B * (S + 1) + 64);
+    if (rc != LZM_OK) return rc;
+  }
+  rc = ensure_flags(h, S, G);
+  if (rc != LZM_OK) return rc;
+
+  SearchArgs p;
+  memset(&p, 0, sizeof(p));
+  p.stat = h->stat; p.meta = h->meta; p.legal = h->legal; p.nlegal = h->nlegal;
+  p.path = h->path; p.path_act = h->path_act; p.pathlen = h->pathlen; p.lut = h->lut;
+  p.B = h->B; p.A = A; p.cap = h->cap; p.lut_n = h->lut_n; p.depth_cap = h->depth_cap;
+  p.S = S; p.disc = discount; p.seeds = seeds; p.vtp_in = vtp_in; p.minmax = (float4 *)minmax; p.pool = latent_pool;
+  p.H = H; p.F = F; p.V = V; p.res = res_dynamics ? 1 : 0;
+  {
+    LayerShape s[12];
+    mlp_shapes(H, A, F, V, s);
+    size_t off = 0;
+    for (int l = 0; l < 12; ++l) {
+      if (!res_dynamics && (l == 2 || l == 3)) {
+        p.L[l] = MlpLayer{nullptr, nullptr, 0, 0, 0};
+        continue;
+      }
+      p.L[l].w = weights + off;
+      p.L[l].b = weights + off + (size_t)s[l].krows * s[l].N;
+      p.L[l].K = s[l].K;
+      p.L[l].N = s[l].N;
+      p.L[l].ldw = s[l].N;
+      off += (size_t)s[l].krows * s[l].N + s[l].N;
+    }
+  }
+  p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
+  p.flags = h->lb_flags; p.epoch = h->epoch; p.diag = h->search_diag; p.fast = fast ? 1 : 0;
+  p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
+  // dynamic LDS plan (float offsets, 16-B aligned)
+  size_t o = 0;
+  const size_t tree_floats = (size_t)h->cap * R * 4;
+  p.tree_in_lds = (2 * tree_floats * sizeof(float) <= 96 * 1024) ? 1 : 0;
+  p.off_stat = o; if (p.tree_in_lds) o += tree_floats;
+  p.off_meta = o; if (p.tree_in_lds) o += tree_floats;
+  p.off_path = o; o += round4((size_t)h->depth_cap * R);
+  p.off_pact = o; o += round4((size_t)h->depth_cap * R);
+  p.off_x0 = o; o += round4((size_t)H * R);
+  p.off_x1 = o; o += round4((size_t)H * R);
+  p.off_x2 = o; o += round4((size_t)H * R);
+  p.off_n = o; o += round4((size_t)H * R);
+  p.off_h = o; o += round4((size_t)F * R);
+  p.off_logit = o; o += round4((size_t)(V + 1) * R);
+  p.off_part = o; o += round4((size_t)256 * R);
+  p.off_misc = o;
+  const size_t lds = o * sizeof(float);
+  if (lds > kMaxLds) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_mlp: %zu B of LDS needed (network too wide)", lds);
+    return LZM_ERR_ARG;
+  }
+  LZM_HIP(hipFuncSetAttribute((const void *)search_mlp_kernel<kRoots>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds));
+  hipLaunchKernelGGL(search_mlp_kernel<kRoots>, dim3(G), dim3(kThreads), lds, (hipStream_t)stream, p);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream) {
+  if (!h || !out) return LZM_ERR_ARG;
+  if (!h->search_diag) {
+    LZM_HIP(hipMemsetAsync(out, 0, 2 * sizeof(int32_t), (hipStream_t)stream));
+    return LZM_OK;
+  }
+  LZM_HIP(hipMemcpyAsync(out, h->search_diag, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return LZM_OK;
 }
 

@@ -1,0 +1,310 @@
+// lzm_tree.h — device-side tree semantics shared by every tree kernel (gfx950).
+//
+// One restatement of LightZero's ctree node rules (reference paths under /root/reference):
+// selection walk cbatch_traverse / compute_mean_q / cselect_child / cucb_score
+// (lzero/mcts/ctree/ctree_muzero/lib/cnode.cpp:169-203, :551-596, :655-699, :755-824),
+// CNode::expand (:83-147), cbackpropagate (:419-478) and the EfficientZero value-prefix
+// variants (ctree_efficientzero/lib/cnode.cpp:173-212, :482-575, :756-814).
+//
+// TreeView addresses nodes as stat/meta[node * B + i]: over the whole batch in HBM (B = roots,
+// i = root) or over a workgroup's slice staged in LDS (B = slice width, i = local root).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lzm_numerics.h"
+
+namespace lzm {
+
+constexpr float kFloatMax = 1000000.0f;  // common_lib/cminimax.h:9-10
+constexpr float kFloatMin = -kFloatMax;
+constexpr int kMaxActions = 64;          // tie lists are held as one 64-bit mask
+constexpr int kMaxWG = 1024;
+
+struct alignas(16) NodeStat {
+  int visit;
+  float value_sum;
+  float prior;
+  float reward;  // value_prefix for EfficientZero
+};
+struct alignas(16) NodeMeta {
+  int latent;  // current_latent_state_index, -1 while not expanded
+  int to_play;
+  int best;  // best_action
+  int is_reset;
+};
+
+struct TreeView {
+  NodeStat *stat;
+  NodeMeta *meta;
+  const int32_t *legal;   // [B][A]
+  const int32_t *nlegal;  // [B]
+  int32_t *path;          // [D][B] node ids
+  int32_t *path_act;      // [D][B] actions
+  int32_t *pathlen;       // [B] edges of the last path
+  const float2 *lut;      // [N] {log((N+base+1)/base)+init, sqrt(N)}
+  int B, A, cap, lut_n, depth_cap;
+};
+
+__device__ inline size_t nidx(const TreeView &t, int node, int i) { return (size_t)node * t.B + i; }
+__device__ inline float node_value(const NodeStat &s) {  // CNode::value, cnode.cpp:219-235
+  return s.visit == 0 ? 0.0f : s.value_sum / (float)s.visit;
+}
+__device__ inline int legal_at(const TreeView &t, int i, int node, int j) {
+  return node == 0 ? t.legal[(size_t)i * t.A + j] : j;
+}
+__device__ inline int legal_n(const TreeView &t, int i, int node) { return node == 0 ? t.nlegal[i] : t.A; }
+
+// CMinMaxStats::normalize, common_lib/cminimax.cpp:33-45
+__device__ inline float mm_normalize(float4 mm, float v) {
+  float norm = v;
+  float delta = mm.x - mm.y;
+  if (delta > 0) {
+    if (delta < mm.z)
+      norm = (norm - mm.y) / mm.z;
+    else
+      norm = (norm - mm.y) / delta;
+  }
+  return norm;
+}
+
+// Result of one root's descent.
+struct Descent {
+  int len, x, action, vtp, leaf;
+};
+
+// One root's selection walk (cbatch_traverse body, cnode.cpp:783-823 with compute_mean_q
+// :169-203, cselect_child :551-596, cucb_score :655-699; EZ variants
+// ctree_efficientzero/lib/cnode.cpp:173-212, :756-814). `draw(level)` returns the rand()
+// value consumed at that level. Writes path/path_act; never writes tree state.
+// Tie information of a draw-free classification walk (descend with CLASSIFY = true).
+struct TieInfo {
+  int status;  // 0: walk complete, no tie; 1: stopped at a tie among unexpanded children (depth
+               // known, child pending a draw); 2: stopped at a tie involving an expanded child
+  int level;
+  unsigned long long mask;  // tie candidates as legal positions
+};
+
+// i indexes the tree (stat/meta[node * t.B + i]); li / ps index the path arrays
+// (path[level * ps + li]), which may live in LDS while the tree stays in HBM.
+// CLASSIFY: stop at the first tie with more than one candidate and report it in `tie` instead
+// of consuming a draw (forced levels still count as one draw each, like the reference).
+template <bool EZ, bool CLASSIFY, typename Draw>
+__device__ inline Descent descend_slice(const TreeView &t, int i, int li, int ps, float4 mm, int players, int vtp,
+                                        float disc, Draw draw, TieInfo *tie) {
+  int node = 0, is_root = 1, len = 0, last_action = -1, parent = 0;
+  float parent_q = 0.0f;  // per root; the reference's cross-root carry is provably 0 wherever read
+  NodeStat s = t.stat[nidx(t, 0, i)];
+  NodeMeta m = t.meta[nidx(t, 0, i)];
+  t.path[li] = 0;
+  if (CLASSIFY) tie->status = 0;
+  while (m.latent >= 0 && len < t.depth_cap - 1) {
+    const int n = legal_n(t, i, node);
+    const int base = 1 + t.A * m.latent;
+    const float pvp = s.reward;
+    const int preset = m.is_reset;
+    // compute_mean_q
+    float total_q = 0.0f;
+    int total_v = 0;
+    for (int j = 0; j < n; ++j) {
+      const int a = legal_at(t, i, node, j);
+      const NodeStat c = t.stat[nidx(t, base + a, i)];
+      if (c.visit > 0) {
+        float tr = c.reward;
+        if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
+        float qsa = tr + disc * node_value(c);
+        total_q += qsa;
+        total_v += 1;
+      }
+    }
+    float mean_q;
+    if (is_root && total_v > 0)
+      mean_q = total_q / (float)total_v;
+    else
+      mean_q = (parent_q + total_q) / (float)(total_v + 1);
+    is_root = 0;
+    parent_q = mean_q;
+    // cselect_child / cucb_score
+    int N = s.visit - 1;
+    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
+    const float2 L = t.lut[N];
+    float max_score = kFloatMin;
+    uint64_t mask = 0;
+    for (int j = 0; j < n; ++j) {
+      const int a = legal_at(t, i, node, j);
+      const NodeStat c = t.stat[nidx(t, base + a, i)];
+      float pb_c = L.x;
+      pb_c *= (L.y / (float)(c.visit + 1));
+      const float prior_score = pb_c * c.prior;
+      float vs;
+      if (c.visit == 0) {
+        vs = mean_q;
+      } else {
+        float tr = c.reward;
+        if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
+        if (players == 1)
+          vs = tr + disc * node_value(c);
+        else
+          vs = tr + disc * (-node_value(c));
+      }
+      vs = mm_normalize(mm, vs);
+      if (vs < 0) vs = 0;
+      if (vs > 1) vs = 1;
+      const float score = prior_score + vs;
+      if (max_score < score) {
+        max_score = score;
+        mask = 1ull << j;
+      } else if (score >= max_score - 0.000001f) {
+        mask |= 1ull << j;
+      }
+    }
+    const int nl = __popcll(mask);
+    if (CLASSIFY && nl > 1) {
+      bool all_leaves = true;
+      for (uint64_t q = mask; q; q &= q - 1) {
+        const int a = legal_at(t, i, node, __ffsll((long long)q) - 1);
+        if (t.meta[nidx(t, base + a, i)].latent >= 0) all_leaves = false;
+      }
+      if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+      tie->status = all_leaves ? 1 : 2;
+      tie->level = len;
+      tie->mask = mask;
+      Descent d;
+      d.len = len + 1;
+      d.x = m.latent;
+      d.action = -1;
+      d.vtp = vtp;
+      d.leaf = -1;
+      return d;
+    }
+    const uint32_t r = CLASSIFY ? 0u : draw(len);
+    int k = (int)(r % (uint32_t)nl);
+    uint64_t mm_ = mask;
+    for (; k > 0; --k) mm_ &= mm_ - 1;
+    const int jsel = __ffsll((long long)mm_) - 1;
+    const int action = legal_at(t, i, node, jsel);
+    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+    t.path_act[(size_t)len * ps + li] = action;
+    parent = node;
+    node = base + action;
+    last_action = action;
+    ++len;
+    t.path[(size_t)len * ps + li] = node;
+    s = t.stat[nidx(t, node, i)];
+    m = t.meta[nidx(t, node, i)];
+  }
+  Descent d;
+  d.len = len;
+  d.x = t.meta[nidx(t, parent, i)].latent;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
+template <bool EZ, typename Draw>
+__device__ inline Descent descend(const TreeView &t, int i, float4 mm, int players, int vtp, float disc, Draw draw) {
+  return descend_slice<EZ, false>(t, i, i, t.B, mm, players, vtp, disc, draw, nullptr);
+}
+
+
+// CNode::expand of a non-root leaf (cnode.cpp:83-147): all A actions legal, masked-softmax
+// priors with glibc expf, sequential sum; children reset to CNode(prior, {}).
+__device__ inline void expand_leaf(const TreeView &t, int i, int leaf, int to_play, int latent, float reward,
+                                   const float *logits, int is_reset, bool ez) {
+  NodeMeta m = t.meta[nidx(t, leaf, i)];
+  m.latent = latent;
+  m.to_play = to_play;
+  if (ez) m.is_reset = is_reset;
+  t.meta[nidx(t, leaf, i)] = m;
+  t.stat[nidx(t, leaf, i)].reward = reward;
+  float pmax = kFloatMin;
+  for (int a = 0; a < t.A; ++a)
+    if (pmax < logits[a]) pmax = logits[a];
+  float sum = 0.0f;
+  for (int a = 0; a < t.A; ++a) sum += glibc_expf(logits[a] - pmax);
+  const int base = 1 + t.A * latent;
+  for (int a = 0; a < t.A; ++a) {
+    const float e = glibc_expf(logits[a] - pmax);
+    NodeStat c;
+    c.visit = 0;
+    c.value_sum = 0.0f;
+    c.prior = e / sum;
+    c.reward = 0.0f;
+    t.stat[nidx(t, base + a, i)] = c;
+    NodeMeta cm;
+    cm.latent = -1;
+    cm.to_play = 0;
+    cm.best = -1;
+    cm.is_reset = 0;
+    t.meta[nidx(t, base + a, i)] = cm;
+  }
+}
+
+// cbackpropagate: MuZero cnode.cpp:419-478, EfficientZero
+// ctree_efficientzero/lib/cnode.cpp:482-575.
+template <bool EZ>
+__device__ inline void backup_slice(const TreeView &t, int i, int li, int ps, float4 *mm_ptr, int to_play,
+                                    float value, float disc) {
+  float4 mm = *mm_ptr;
+  const int len = t.pathlen[li];
+  float b = value;
+  for (int l = len; l >= 0; --l) {
+    const int node = t.path[(size_t)l * ps + li];
+    NodeStat s = t.stat[nidx(t, node, i)];
+    const int ntp = t.meta[nidx(t, node, i)].to_play;
+    if (to_play == -1 || ntp == to_play)
+      s.value_sum += b;
+    else
+      s.value_sum += -b;
+    s.visit += 1;
+    t.stat[nidx(t, node, i)] = s;
+    const float v = node_value(s);
+    if (!EZ) {
+      const float tr = s.reward;
+      float q;
+      if (to_play == -1) {
+        q = tr + disc * v;
+        b = tr + disc * b;
+      } else {
+        q = tr + disc * -v;
+        b = (ntp == to_play) ? (-tr + disc * b) : (tr + disc * b);
+      }
+      if (q > mm.x) mm.x = q;
+      if (q < mm.y) mm.y = q;
+    } else {
+      float pvp = 0.0f;
+      int reset = 0;
+      if (l >= 1) {
+        const int pn = t.path[(size_t)(l - 1) * ps + li];
+        pvp = t.stat[nidx(t, pn, i)].reward;
+        reset = t.meta[nidx(t, pn, i)].is_reset;
+      }
+      float tr = s.reward - pvp;
+      const float q = tr + disc * v;
+      if (q > mm.x) mm.x = q;
+      if (q < mm.y) mm.y = q;
+      if (reset == 1) tr = s.reward;
+      if (to_play == -1 || ntp != to_play)
+        b = tr + disc * b;
+      else
+        b = -tr + disc * b;
+    }
+  }
+  *mm_ptr = mm;
+}
+
+template <bool EZ>
+__device__ inline void backup(const TreeView &t, int i, float4 *mm_ptr, int to_play, float value, float disc) {
+  backup_slice<EZ>(t, i, i, t.B, mm_ptr, to_play, value, disc);
+}
+
+// h^-1 of InverseScalarTransform (scaling_transform.py:123-127), eps = 0.001.
+__device__ inline float h_inverse(float value) {
+  const float eps = 0.001f;
+  float tmp = (sqrtf(1.0f + 0.004f * (fabsf(value) + 1.0f + eps)) - 1.0f) * (1.0f / 0.002f);
+  float sgn = value > 0.0f ? 1.0f : (value < 0.0f ? -1.0f : 0.0f);
+  return sgn * (tmp * tmp - 1.0f);
+}
+
+}  // namespace lzm

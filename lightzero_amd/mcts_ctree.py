@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from .ctree import ez_tree, mz_tree
+from .fused import NotPackable, PackedCache
 from .scaling_transform import InverseScalarTransform
 from .tree import DeviceTree, new_minmax, next_seed
 from .utils import EasyDict
@@ -119,6 +120,7 @@ class MuZeroMCTSCtree(object):
         )
         self._buf = _SearchBuffers()
         self._graphs = {}
+        self._packed = PackedCache()
 
     # 'glibc': the reference's tie-break stream, bit-exact (default); 'philox': independent
     # counter-based stream per root (LZM_RNG_FAST), no batch-serial dependency.
@@ -130,6 +132,19 @@ class MuZeroMCTSCtree(object):
 
     def _categorical(self):
         return bool(self._cfg.model.get('categorical_distribution', True))
+
+    def _fused(self, model, t):
+        """(packed weights, dims) when the whole search can run as one lzm_search_mlp launch:
+        a MuZeroModelMLP-shaped network with categorical heads, eval-mode BatchNorm and ReLU."""
+        if not self._cfg.get('fused_search', True) or not self._categorical() or t.ez:
+            return None
+        try:
+            packed, dims = self._packed.get(model, t.device)
+        except NotPackable:
+            return None
+        if dims["actions"] != t.A or dims["support"] != 2 * int(self._cfg.model.support_scale) + 1:
+            return None
+        return packed, dims
 
     def _loop(self, t, model, buf, mm, vtp_in, seeds, S, row, rec=None):
         """The S simulations (mcts_ctree.py:255-321), all enqueued on the current stream."""
@@ -170,7 +185,14 @@ class MuZeroMCTSCtree(object):
             rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
             if rec is not None:
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
-            if rec is None and self._cfg.get('use_hip_graph', False):
+            fz = self._fused(model, t)
+            if fz is not None:
+                packed, dims = fz
+                cfg = self._cfg
+                new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
+                t.search_mlp(dims, packed, S, buf.mm, buf.seeds, buf.vtp_in, buf.pool, int(cfg.pb_c_base),
+                             float(cfg.pb_c_init), float(np.float32(cfg.discount_factor)), rec=rec)
+            elif rec is None and self._cfg.get('use_hip_graph', False):
                 self._graph_search(t, model, buf, S, row)
             else:
                 self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, rec)

@@ -132,6 +132,20 @@ class DeviceTree:
              ptr(value_logits), int(V), int(bool(categorical)), ptr(policy_logits), ptr(to_play), int(lstm_horizon),
              ptr(out_is_reset), ptr(next_latent), ptr(pool_slot), int(row_elems), ptr(out_decoded), stream_ptr(stream))
 
+    def search_mlp(self, dims, weights, S, minmax, seeds, vtp_in, pool, pb_c_base=19652, pb_c_init=1.25,
+                   discount=0.997, rec=None, stream=None):
+        """One launch for the whole search (lzm_search_mlp); rec: optional _Recorder-like object."""
+        r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n)))
+        call("lzm_search_mlp", self.h, dims["hidden"], dims["head_hidden"], dims["support"], int(dims["res"]),
+             ptr(weights), int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax), ptr(seeds),
+             ptr(vtp_in), ptr(pool), r("x"), r("action"), r("search_len"), r("decoded"), r("policy_logits"),
+             stream_ptr(stream))
+
+    def search_diagnostics(self):
+        out = torch.zeros(2, dtype=torch.int32, device=self.device)
+        call("lzm_search_diagnostics", self.h, ptr(out), stream_ptr())
+        return out.cpu().tolist()
+
     def distributions(self, stream=None):
         out = torch.empty((self.B, self.A), dtype=torch.int32, device=self.device)
         call("lzm_get_distributions", self.h, ptr(out), stream_ptr(stream))
