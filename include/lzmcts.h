@@ -156,6 +156,12 @@ int lzm_last_traverse_passes(lzm_handle *h, int32_t *out, void *stream);
 /* Device-side numerics helpers exposed for exhaustive checks. */
 int lzm_debug_expf(const float *x, float *out, int64_t n, void *stream);
 int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream);
+/* Shader-clock cycles per phase of the fused search, summed over workgroups, when the process
+ * runs with LZM_PHASE_TIMING=1 (synchronous; reset != 0 clears the counters). Phases: 0 select,
+ * 1 draw offsets + look-back, 2 leaf gather, 3 dynamics, 4 reward head + decode, 5 prediction
+ * trunk, 6 value head + decode, 7 policy head, 8 latent filing, 9 expand + backup, 10 stage-in,
+ * 11 write-back. */
+int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset);
 int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*/, int n, void *stream);
 
 #ifdef __cplusplus

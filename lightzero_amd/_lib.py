@@ -57,6 +57,7 @@ SIGNATURES = {
     "lzm_debug_expf": [_vp, _vp, _i64, _vp],
     "lzm_debug_glibc_rand": [_u32, _i, _vp, _vp],
     "lzm_debug_philox": [_vp, _vp, _i, _vp],
+    "lzm_debug_phase_cycles": [_vp, _vp, _i],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64}
 

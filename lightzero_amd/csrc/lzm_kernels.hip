@@ -21,6 +21,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -567,6 +568,7 @@ struct lzm_handle {
   int flag_sims = 0;
   uint32_t *epoch = nullptr;               // [2] launch epoch, done counter
   int32_t *search_diag = nullptr;          // [2]
+  unsigned long long *phase = nullptr;     // [16] diagnostic phase cycles (LZM_PHASE_TIMING=1)
 };
 
 // Jump matrices of glibc random_r: row m of J_first expresses z[344+m] (the m-th rand()
@@ -707,7 +709,7 @@ int lzm_destroy(lzm_handle *h) {
   free_tree(h);
   dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag);
   dfree(h->hint); dfree(h->norm_flag); dfree(h->jmat);
-  dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag);
+  dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag); dfree(h->phase);
   delete h;
   return LZM_OK;
 }
@@ -1117,8 +1119,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     return LZM_ERR_ARG;
   }
   const int H = hidden, F = head_hidden, V = support, A = h->A, S = num_simulations;
-  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || A > H) {
-    set_err("lzm_search_mlp: unsupported network shape");
+  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || A > H || H % kKC != 0 || F % kKC != 0) {
+    set_err("lzm_search_mlp: unsupported network shape (hidden and head widths must be multiples of 16)");
     return LZM_ERR_ARG;
   }
   if (S > h->sims_cap) {
@@ -1163,6 +1165,11 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   }
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
   p.flags = h->lb_flags; p.epoch = h->epoch; p.diag = h->search_diag; p.fast = fast ? 1 : 0;
+  if (!h->phase && getenv("LZM_PHASE_TIMING") && atoi(getenv("LZM_PHASE_TIMING")) > 0) {
+    LZM_HIP(hipMalloc(&h->phase, 16 * sizeof(unsigned long long)));
+    LZM_HIP(hipMemset(h->phase, 0, 16 * sizeof(unsigned long long)));
+  }
+  p.phase = h->phase;
   p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
   // dynamic LDS plan (float offsets, 16-B aligned)
   size_t o = 0;
@@ -1170,6 +1177,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.tree_in_lds = (2 * tree_floats * sizeof(float) <= 96 * 1024) ? 1 : 0;
   p.off_stat = o; if (p.tree_in_lds) o += tree_floats;
   p.off_meta = o; if (p.tree_in_lds) o += tree_floats;
+  p.off_lut = o; if (p.tree_in_lds) o += round4((size_t)2 * h->lut_n);
+  p.off_legal = o; if (p.tree_in_lds) o += round4((size_t)R * A + R);
   p.off_path = o; o += round4((size_t)h->depth_cap * R);
   p.off_pact = o; o += round4((size_t)h->depth_cap * R);
   p.off_x0 = o; o += round4((size_t)H * R);
@@ -1178,17 +1187,35 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.off_n = o; o += round4((size_t)H * R);
   p.off_h = o; o += round4((size_t)F * R);
   p.off_logit = o; o += round4((size_t)(V + 1) * R);
-  p.off_part = o; o += round4((size_t)256 * R);
-  p.off_misc = o;
+  p.off_part = o; o += round4((size_t)kThreads * R);
+  p.off_misc = o; o += round4((size_t)S + 32);  // staged seeds[S] + 16807^i table
   const size_t lds = o * sizeof(float);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_mlp: %zu B of LDS needed (network too wide)", lds);
     return LZM_ERR_ARG;
   }
-  LZM_HIP(hipFuncSetAttribute((const void *)search_mlp_kernel<kRoots>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds));
-  hipLaunchKernelGGL(search_mlp_kernel<kRoots>, dim3(G), dim3(kThreads), lds, (hipStream_t)stream, p);
+  if (p.tree_in_lds) {
+    LZM_HIP(hipFuncSetAttribute((const void *)search_mlp_kernel<kRoots, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((search_mlp_kernel<kRoots, true>), dim3(G), dim3(kThreads), lds, (hipStream_t)stream, p);
+  } else {
+    LZM_HIP(hipFuncSetAttribute((const void *)search_mlp_kernel<kRoots, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((search_mlp_kernel<kRoots, false>), dim3(G), dim3(kThreads), lds, (hipStream_t)stream, p);
+  }
   LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset) {
+  if (!h || !out_host) return LZM_ERR_ARG;
+  if (!h->phase) {
+    memset(out_host, 0, 16 * sizeof(uint64_t));
+    return LZM_OK;
+  }
+  LZM_HIP(hipDeviceSynchronize());
+  LZM_HIP(hipMemcpy(out_host, h->phase, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (reset) LZM_HIP(hipMemset(h->phase, 0, 16 * sizeof(unsigned long long)));
   return LZM_OK;
 }
 

@@ -29,7 +29,7 @@
 
 namespace lzm {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 512;  // 8 waves: two per SIMD, so one's memory wait hides under the other's FMAs
 
 struct MlpLayer {
   const float *w;  // [K][ldw] (input-major), zero-padded columns
@@ -62,13 +62,14 @@ struct SearchArgs {
   unsigned long long *flags;  // [S][G]
   uint32_t *epoch;            // [2]: epoch, done counter
   int32_t *diag;              // [0] errors (spin timeouts), [1] ambiguous resolutions
+  unsigned long long *phase;  // optional [16] per-phase shader-clock cycles (diagnostic builds)
   int fast;
   // optional per-simulation record (tests / tracing), may be null
   int32_t *rec_x, *rec_a, *rec_len;
   float *rec_dec, *rec_logits;
   // dynamic LDS layout (float offsets)
   int tree_in_lds;
-  size_t off_stat, off_meta, off_path, off_pact, off_x0, off_x1, off_x2, off_n, off_h, off_logit, off_part,
+  size_t off_stat, off_meta, off_lut, off_legal, off_path, off_pact, off_x0, off_x1, off_x2, off_n, off_h, off_logit, off_part,
       off_misc;
 };
 
@@ -78,25 +79,63 @@ __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const fl
 // out_T[n][r] (or out[r][n] when rowmajor) = act(in_T . W + b (+ W[H+a_r] one-hot row)) (+ resid_T)
 // Each weight element is read from L2 by exactly one lane: a lane owns one output column for all
 // R rows; spare lanes split K and reduce through LDS partials.
+constexpr int kKC = 16;  // weights held in registers per lane before the FMAs that use them
+typedef const __attribute__((address_space(1))) float *gfloat_p;  // global (not flat) loads
+
+// acc[r] += sum_{k in [k0, k1)} inT[k][r] * W[k][col] with (k1 - k0) % kKC == 0: each chunk's
+// weights are issued as loads first, so one L2 round trip is paid per chunk, not per weight.
 template <int R>
-__device__ void dense(const MlpLayer &L, const float *inT, float *out, float *part, bool relu, const float *residT,
-                      bool rowmajor, int ldout, const int *onehot_act, int onehot_row0) {
+__device__ __forceinline__ void load_chunk(gfloat_p W, int ldw, int col, int kb, float *w) {
+#pragma unroll
+  for (int j = 0; j < kKC; ++j) w[j] = W[(size_t)(kb + j) * ldw + col];
+}
+
+template <int R>
+__device__ __forceinline__ void fma_chunk(const float *inT, int kb, const float *w, float *acc) {
+#pragma unroll
+  for (int j = 0; j < kKC; ++j) {
+    const float4 a0 = ld4(inT + (kb + j) * R), a1 = ld4(inT + (kb + j) * R + 4);
+    acc[0] = __fmaf_rn(a0.x, w[j], acc[0]); acc[1] = __fmaf_rn(a0.y, w[j], acc[1]);
+    acc[2] = __fmaf_rn(a0.z, w[j], acc[2]); acc[3] = __fmaf_rn(a0.w, w[j], acc[3]);
+    acc[4] = __fmaf_rn(a1.x, w[j], acc[4]); acc[5] = __fmaf_rn(a1.y, w[j], acc[5]);
+    acc[6] = __fmaf_rn(a1.z, w[j], acc[6]); acc[7] = __fmaf_rn(a1.w, w[j], acc[7]);
+  }
+}
+
+// Double-buffered: the next chunk's weight loads are in flight while this chunk's FMAs issue.
+template <int R>
+__device__ __forceinline__ void dot_chunked(gfloat_p W, int ldw, int col, int k0, int k1, const float *inT,
+                                            float *acc) {
+  float wa[kKC], wb[kKC];
+  load_chunk<R>(W, ldw, col, k0, wa);
+  for (int kb = k0; kb < k1; kb += 2 * kKC) {
+    const bool has_b = kb + kKC < k1;
+    if (has_b) load_chunk<R>(W, ldw, col, kb + kKC, wb);
+    fma_chunk<R>(inT, kb, wa, acc);
+    if (!has_b) break;
+    if (kb + 2 * kKC < k1) load_chunk<R>(W, ldw, col, kb + 2 * kKC, wa);
+    fma_chunk<R>(inT, kb + kKC, wb, acc);
+  }
+}
+
+// One network layer on the workgroup's R rows (K % kKC == 0, checked on the host). Called from a
+// loop over the layer schedule, so its code exists once (the loop body must fit the I-cache).
+template <int R>
+__device__ __forceinline__ void dense(const MlpLayer L, const float *inT, float *out, float *part, int relu,
+                                   const float *residT, int rowmajor, int ldout, const int *onehot_act,
+                                   int onehot_row0) {
+  static_assert(R == 8, "dense is written for 8 rows per workgroup");
   const int tid = threadIdx.x;
   const int N = L.N, K = L.K;
+  gfloat_p W = (gfloat_p)L.w;
+  gfloat_p Bv = (gfloat_p)L.b;
   if (N >= kThreads) {
     for (int c = tid; c < N; c += kThreads) {
       float acc[R];
-      const float bias = L.b[c];
+      const float bias = Bv[c];
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[r] = bias;
-      for (int k = 0; k < K; ++k) {
-        const float w = L.w[(size_t)k * L.ldw + c];
-        const float4 a0 = ld4(inT + k * R), a1 = ld4(inT + k * R + 4);
-        acc[0] = __fmaf_rn(a0.x, w, acc[0]); acc[1] = __fmaf_rn(a0.y, w, acc[1]);
-        acc[2] = __fmaf_rn(a0.z, w, acc[2]); acc[3] = __fmaf_rn(a0.w, w, acc[3]);
-        acc[4] = __fmaf_rn(a1.x, w, acc[4]); acc[5] = __fmaf_rn(a1.y, w, acc[5]);
-        acc[6] = __fmaf_rn(a1.z, w, acc[6]); acc[7] = __fmaf_rn(a1.w, w, acc[7]);
-      }
+      dot_chunked<R>(W, L.ldw, c, 0, K, inT, acc);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         float v = acc[r];
@@ -107,51 +146,32 @@ __device__ void dense(const MlpLayer &L, const float *inT, float *out, float *pa
     __syncthreads();
     return;
   }
-  // split K over kThreads / Np lanes per column
+  // split K over up to kThreads / Np lanes per column, whole chunks per lane
   int Np = 1;
   while (Np < N) Np <<= 1;
-  const int splits = kThreads / Np;
+  int splits = min(kThreads / Np, K / kKC);
+  while ((K / kKC) % splits) --splits;  // whole chunks per lane
   const int col = tid % Np, part_id = tid / Np;
-  const int kchunk = (K + splits - 1) / splits;
-  const int k0 = part_id * kchunk, k1 = min(K, k0 + kchunk);
+  const int kchunk = K / splits;  // multiple of kKC
   float acc[R];
+  const bool active = col < N && part_id < splits;
+  const float bias = (active && part_id == 0) ? Bv[col] : 0.0f;
 #pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = 0.0f;
-  if (col < N) {
-    int k = k0;
-    for (; k + 4 <= k1; k += 4) {
-      const float w0 = L.w[(size_t)k * L.ldw + col], w1 = L.w[(size_t)(k + 1) * L.ldw + col];
-      const float w2 = L.w[(size_t)(k + 2) * L.ldw + col], w3 = L.w[(size_t)(k + 3) * L.ldw + col];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float w = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
-        const float4 a0 = ld4(inT + (k + q) * R), a1 = ld4(inT + (k + q) * R + 4);
-        acc[0] = __fmaf_rn(a0.x, w, acc[0]); acc[1] = __fmaf_rn(a0.y, w, acc[1]);
-        acc[2] = __fmaf_rn(a0.z, w, acc[2]); acc[3] = __fmaf_rn(a0.w, w, acc[3]);
-        acc[4] = __fmaf_rn(a1.x, w, acc[4]); acc[5] = __fmaf_rn(a1.y, w, acc[5]);
-        acc[6] = __fmaf_rn(a1.z, w, acc[6]); acc[7] = __fmaf_rn(a1.w, w, acc[7]);
-      }
-    }
-    for (; k < k1; ++k) {
-      const float w = L.w[(size_t)k * L.ldw + col];
-      const float4 a0 = ld4(inT + k * R), a1 = ld4(inT + k * R + 4);
-      acc[0] = __fmaf_rn(a0.x, w, acc[0]); acc[1] = __fmaf_rn(a0.y, w, acc[1]);
-      acc[2] = __fmaf_rn(a0.z, w, acc[2]); acc[3] = __fmaf_rn(a0.w, w, acc[3]);
-      acc[4] = __fmaf_rn(a1.x, w, acc[4]); acc[5] = __fmaf_rn(a1.y, w, acc[5]);
-      acc[6] = __fmaf_rn(a1.z, w, acc[6]); acc[7] = __fmaf_rn(a1.w, w, acc[7]);
-    }
+  for (int r = 0; r < R; ++r) acc[r] = bias;
+  if (active) {
     if (onehot_act && part_id == 0) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] += L.w[(size_t)(onehot_row0 + onehot_act[r]) * L.ldw + col];
+      for (int r = 0; r < R; ++r) acc[r] += W[(size_t)(onehot_row0 + onehot_act[r]) * L.ldw + col];
     }
-  }
+    dot_chunked<R>(W, L.ldw, col, part_id * kchunk, part_id * kchunk + kchunk, inT, acc);
 #pragma unroll
-  for (int r = 0; r < R; ++r) part[(part_id * Np + col) * R + r] = acc[r];
+    for (int r = 0; r < R; ++r) part[(part_id * Np + col) * R + r] = acc[r];
+  }
   __syncthreads();
   for (int e = tid; e < N * R; e += kThreads) {
     const int c = e / R, r = e % R;
-    float v = L.b[c];
-    for (int s = 0; s < splits; ++s) v += part[(s * Np + c) * R + r];
+    float v = part[c * R + r];
+    for (int s = 1; s < splits; ++s) v += part[(s * Np + c) * R + r];
     if (relu) v = fmaxf(v, 0.0f);
     if (residT) v += residT[c * R + r];
     if (rowmajor) out[r * ldout + c] = v; else out[c * R + r] = v;
@@ -209,7 +229,20 @@ __device__ inline void seed_state_parallel(uint32_t seed, const uint32_t *pw, ui
   }
 }
 
-template <int R>
+// Phase stamps (diagnostics only; p.phase == nullptr in production): thread 0 of every
+// workgroup adds the shader-clock cycles spent since the previous stamp to phase[n].
+#define LZM_STAMP(n)                                                              \
+  do {                                                                            \
+    if (p.phase && tid == 0) {                                                    \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();              \
+      atomicAdd(p.phase + (n), now_ - stamp_);                                   \
+      stamp_ = now_;                                                              \
+    }                                                                             \
+  } while (0)
+
+// TL: the workgroup's tree slice (node records, pUCT table, root legal lists) is staged in LDS
+// for the whole search; otherwise the nodes stay in HBM (large action spaces x simulations).
+template <int R, bool TL>
 __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   extern __shared__ float4 smem4[];
   float *smem = reinterpret_cast<float *>(smem4);
@@ -217,6 +250,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   const int B = p.B, A = p.A, H = p.H;
   const int i0 = g * R;
   const int nr = min(R, B - i0);  // roots in this slice
+  unsigned long long stamp_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
 
   __shared__ uint32_t s_z0[31];
   __shared__ int s_players, s_base, s_flag, s_epoch;
@@ -224,31 +258,50 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   __shared__ unsigned long long s_tmask[R];
   __shared__ float s_r[R], s_v[R];
   __shared__ float4 s_mm[R];
+  __shared__ MlpLayer s_L[12];
+  __shared__ int s_step[12][9];
+  __shared__ int s_nsteps, s_stamp_at[4];
 
   // ---- stage the tree slice and per-root state
   TreeView t;
   t.A = A;
   t.cap = p.cap;
-  t.lut = p.lut;
   t.lut_n = p.lut_n;
   t.depth_cap = p.depth_cap;
-  t.legal = p.legal + (size_t)i0 * A;
-  t.nlegal = p.nlegal + i0;
-  t.B = R;
   t.path = reinterpret_cast<int32_t *>(smem + p.off_path);
   t.path_act = reinterpret_cast<int32_t *>(smem + p.off_pact);
   t.pathlen = s_len;
-  if (p.tree_in_lds) {
-    t.stat = reinterpret_cast<NodeStat *>(smem + p.off_stat);
-    t.meta = reinterpret_cast<NodeMeta *>(smem + p.off_meta);
+  if constexpr (TL) {
+    NodeStat *ls = reinterpret_cast<NodeStat *>(smem + p.off_stat);
+    NodeMeta *lm = reinterpret_cast<NodeMeta *>(smem + p.off_meta);
+    float2 *llut = reinterpret_cast<float2 *>(smem + p.off_lut);
+    int32_t *llegal = reinterpret_cast<int32_t *>(smem + p.off_legal);
     for (int e = tid; e < p.cap * R; e += kThreads) {
       const int node = e / R, li = e % R;
       if (li < nr) {
-        t.stat[e] = p.stat[(size_t)node * B + i0 + li];
-        t.meta[e] = p.meta[(size_t)node * B + i0 + li];
+        ls[e] = p.stat[(size_t)node * B + i0 + li];
+        lm[e] = p.meta[(size_t)node * B + i0 + li];
       }
     }
+    for (int e = tid; e < p.lut_n; e += kThreads) llut[e] = p.lut[e];
+    for (int e = tid; e < R * A; e += kThreads) llegal[e] = (e / A < nr) ? p.legal[(size_t)i0 * A + e] : 0;
+    for (int e = tid; e < R; e += kThreads) llegal[R * A + e] = (e < nr) ? p.nlegal[i0 + e] : 0;
+    t.stat = ls;
+    t.meta = lm;
+    t.lut = llut;
+    t.legal = llegal;
+    t.nlegal = llegal + R * A;
+    t.B = R;
+  } else {
+    t.stat = p.stat;
+    t.meta = p.meta;
+    t.lut = p.lut;
+    t.legal = p.legal;
+    t.nlegal = p.nlegal;
+    t.B = B;
   }
+  // tree index of local root li: li in the LDS slice, i0 + li in the HBM batch
+  auto tix = [i0](int li) { return TL ? li : i0 + li; };
   if (tid < R && tid < nr) {
     s_mm[tid] = p.minmax[i0 + tid];
     s_vtp[tid] = p.vtp_in[i0 + tid];
@@ -258,33 +311,62 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     for (int i = 0; i < B; ++i) m = max(m, p.vtp_in[i]);
     s_players = (m == -1) ? 1 : 2;
     s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int l = 0; l < 12; ++l) s_L[l] = p.L[l];
+    // layer schedule: {layer, in, out, relu, resid (-1: none), rowmajor, ldout, one-hot, decode}
+    const int x0 = (int)p.off_x0, x1 = (int)p.off_x1, x2 = (int)p.off_x2, nl = (int)p.off_n, hd = (int)p.off_h,
+              lg = (int)p.off_logit;
+    int n = 0;
+    auto add = [&](int l, int in, int out, int relu, int resid, int rowmajor, int ldout, int onehot, int dec) {
+      int *q = s_step[n++];
+      q[0] = l; q[1] = in; q[2] = out; q[3] = relu; q[4] = resid; q[5] = rowmajor; q[6] = ldout; q[7] = onehot;
+      q[8] = dec;
+    };
+    add(0, x0, x1, 1, -1, 0, 0, 1, 0);                   // fc_dynamics(_1)[0] on [latent; one-hot]
+    add(1, x1, nl, 1, p.res ? x0 : -1, 0, 0, 0, 0);      // [1] (+ latent: res_connection_in_dynamics)
+    int enc = nl;
+    if (p.res) {
+      add(2, nl, x1, 1, -1, 0, 0, 0, 0);                 // fc_dynamics_2
+      add(3, x1, x2, 1, -1, 0, 0, 0, 0);
+      enc = x2;
+    }
+    s_stamp_at[0] = n - 1;
+    add(4, enc, hd, 1, -1, 0, 0, 0, 0);                  // fc_reward_head
+    add(5, hd, lg, 0, -1, 1, p.V + 1, 0, 1);
+    s_stamp_at[1] = n - 1;
+    add(6, nl, x1, 1, -1, 0, 0, 0, 0);                   // fc_prediction_common
+    add(7, x1, x2, 1, -1, 0, 0, 0, 0);
+    s_stamp_at[2] = n - 1;
+    add(8, x2, hd, 1, -1, 0, 0, 0, 0);                   // fc_value_head
+    add(9, hd, lg, 0, -1, 1, p.V + 1, 0, 2);
+    s_stamp_at[3] = n - 1;
+    add(10, x2, hd, 1, -1, 0, 0, 0, 0);                  // fc_policy_head
+    add(11, hd, x1, 0, -1, 1, A, 0, 0);
+    s_nsteps = n;
   }
   __syncthreads();
   const int players = s_players;
   const unsigned long long epoch = (unsigned long long)(uint32_t)s_epoch;
 
+  uint32_t *s_seeds = reinterpret_cast<uint32_t *>(smem + p.off_misc);
+  uint32_t *s_pow = s_seeds + p.S;
+  for (int e = tid; e < p.S; e += kThreads) s_seeds[e] = p.seeds[e];
+  if (!p.fast)
+    for (int e = tid; e < 31; e += kThreads) s_pow[e] = p.pow16807[e];
+  __syncthreads();
+  LZM_STAMP(10);
   float *X0 = smem + p.off_x0, *X1 = smem + p.off_x1, *X2 = smem + p.off_x2, *NL = smem + p.off_n;
   float *HD = smem + p.off_h, *LG = smem + p.off_logit, *PART = smem + p.off_part;
 
   for (int k = 0; k < p.S; ++k) {
-    const uint32_t seed = p.seeds[k];
-    if (!p.fast) seed_state_parallel(seed, p.pow16807, s_z0);
+    const uint32_t seed = s_seeds[k];
+    if (!p.fast) seed_state_parallel(seed, s_pow, s_z0);
     // ---- selection
     if (tid < nr) {
       const int li = tid, i = i0 + li;
-      TreeView tv = t;
-      int ti = li;
-      if (!p.tree_in_lds) {
-        tv.stat = p.stat;
-        tv.meta = p.meta;
-        tv.B = B;
-        tv.legal = p.legal;
-        tv.nlegal = p.nlegal;
-        ti = i;
-        // paths still live in LDS (stride R): copy-in not needed, descend writes them
-      }
+      const TreeView &tv = t;
+      const int ti = tix(li);
       if (p.fast) {
-        auto draw = [&](int level) -> uint32_t {
+        auto draw = [seed, i](int level) -> uint32_t {
           uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)i, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
           return o.x >> 1;
         };
@@ -302,6 +384,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       }
     }
     __syncthreads();
+    LZM_STAMP(0);
     if (!p.fast) {
       // ---- draw offsets: publish this slice's draw count, look back over predecessors
       if (tid == 0) {
@@ -347,15 +430,14 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
           atomicAdd(p.diag + 1, 1);
           int total = 0;
           for (int li = 0; li < nr; ++li) {
-            const int i = i0 + li;
-            TreeView tv = t;
-            int ti = li;
-            if (!p.tree_in_lds) {
-              tv.stat = p.stat; tv.meta = p.meta; tv.B = B; tv.legal = p.legal; tv.nlegal = p.nlegal; ti = i;
-            }
+            const TreeView &tv = t;
+            const int ti = tix(li);
             const int off = base + total;
-            auto draw = [&](int level) -> uint32_t {
-              return glibc_draw(p.coef, p.coef_positions, s_z0, off + level, p.diag);
+            const uint32_t *coef = p.coef;
+            const int npos = p.coef_positions;
+            int32_t *diag = p.diag;
+            auto draw = [coef, npos, diag, off](int level) -> uint32_t {
+              return glibc_draw(coef, npos, s_z0, off + level, diag);
             };
             Descent d = descend_slice<false, false>(tv, ti, li, R, s_mm[li], players, s_vtp[li], p.disc, draw, nullptr);
             s_len[li] = d.len; s_x[li] = d.x; s_act[li] = d.action; s_status[li] = 0;
@@ -373,11 +455,8 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
           int kk = (int)(rr % (uint32_t)__popcll(m));
           for (; kk > 0; --kk) m &= m - 1;
           const int jsel = __ffsll((long long)m) - 1;
-          TreeView tv = t;
-          int ti = li;
-          if (!p.tree_in_lds) {
-            tv.stat = p.stat; tv.meta = p.meta; tv.B = B; tv.legal = p.legal; tv.nlegal = p.nlegal; ti = i0 + li;
-          }
+          const TreeView &tv = t;
+          const int ti = tix(li);
           const int lvl = s_tlevel[li];
           const int parent = tv.path[lvl * R + li];
           const int action = legal_at(tv, ti, parent, jsel);
@@ -395,6 +474,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       p.rec_a[(size_t)k * B + i0 + tid] = s_act[tid];
       p.rec_len[(size_t)k * B + i0 + tid] = s_len[tid];
     }
+    LZM_STAMP(1);
     // ---- gather leaf latents: X0[h][r] = pool[x_r][i0+r][h]
     for (int e = tid; e < H * R; e += kThreads) {
       const int r = e / H, h = e % H;
@@ -403,33 +483,29 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       X0[h * R + r] = v;
     }
     __syncthreads();
+    LZM_STAMP(2);
     // ---- network (recurrent_inference, BN folded): muzero_model_mlp.py:179-204, :420-440
-    dense<R>(p.L[0], X0, X1, PART, true, nullptr, false, 0, s_act, H);         // fc_dynamics(_1) a
-    dense<R>(p.L[1], X1, NL, PART, true, p.res ? X0 : nullptr, false, 0, nullptr, 0);  // b (+ residual)
-    const float *enc = NL;
-    if (p.res) {
-      dense<R>(p.L[2], NL, X1, PART, true, nullptr, false, 0, nullptr, 0);     // fc_dynamics_2
-      dense<R>(p.L[3], X1, X2, PART, true, nullptr, false, 0, nullptr, 0);
-      enc = X2;
+    // One dense() instance walks the layer schedule (s_step): fc_dynamics(_1) (+ one-hot action,
+    // + residual), fc_dynamics_2, reward head (-> decode into s_r), fc_prediction_common, value
+    // head (-> decode into s_v), policy head (-> logits [r][A] in X1).
+    for (int st = 0; st < s_nsteps; ++st) {
+      const int *q = s_step[st];
+      dense<R>(s_L[q[0]], smem + q[1], smem + q[2], PART, q[3], q[4] >= 0 ? smem + q[4] : nullptr, q[5], q[6],
+               q[7] ? s_act : nullptr, H);
+      if (q[8]) {  // decode the support logits just produced (InverseScalarTransform)
+        const int wid = tid >> 6;
+        for (int r = wid; r < nr; r += kThreads / 64) {
+          const float e = wave_expect_lds(LG + r * (p.V + 1), p.V);
+          if ((tid & 63) == 0) (q[8] == 1 ? s_r : s_v)[r] = h_inverse(e);
+        }
+        __syncthreads();
+      }
+      if (st == s_stamp_at[0]) LZM_STAMP(3);
+      if (st == s_stamp_at[1]) LZM_STAMP(4);
+      if (st == s_stamp_at[2]) LZM_STAMP(5);
+      if (st == s_stamp_at[3]) LZM_STAMP(6);
     }
-    dense<R>(p.L[4], enc, HD, PART, true, nullptr, false, 0, nullptr, 0);      // reward head
-    dense<R>(p.L[5], HD, LG, PART, false, nullptr, true, p.V + 1, nullptr, 0);
-    const int wid = tid >> 6;
-    for (int r = wid; r < nr; r += kThreads / 64) {
-      const float e = wave_expect_lds(LG + r * (p.V + 1), p.V);
-      if ((tid & 63) == 0) s_r[r] = h_inverse(e);
-    }
-    __syncthreads();
-    dense<R>(p.L[6], NL, X1, PART, true, nullptr, false, 0, nullptr, 0);       // prediction common
-    dense<R>(p.L[7], X1, X2, PART, true, nullptr, false, 0, nullptr, 0);
-    dense<R>(p.L[8], X2, HD, PART, true, nullptr, false, 0, nullptr, 0);       // value head
-    dense<R>(p.L[9], HD, LG, PART, false, nullptr, true, p.V + 1, nullptr, 0);
-    for (int r = wid; r < nr; r += kThreads / 64) {
-      const float e = wave_expect_lds(LG + r * (p.V + 1), p.V);
-      if ((tid & 63) == 0) s_v[r] = h_inverse(e);
-    }
-    dense<R>(p.L[10], X2, HD, PART, true, nullptr, false, 0, nullptr, 0);      // policy head
-    dense<R>(p.L[11], HD, X1, PART, false, nullptr, true, A, nullptr, 0);      // logits [r][A] in X1
+    LZM_STAMP(7);
     // ---- file the new latents (mcts_ctree.py:305): pool[k+1][i][h] = NL[h][r]
     for (int e = tid; e < H * R; e += kThreads) {
       const int r = e / H, h = e % H;
@@ -440,14 +516,12 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       p.rec_dec[((size_t)k * B + i0 + tid) * 2 + 1] = s_v[tid];
       for (int a = 0; a < A; ++a) p.rec_logits[((size_t)k * B + i0 + tid) * A + a] = X1[tid * A + a];
     }
+    LZM_STAMP(8);
     // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500)
     if (tid < nr) {
       const int li = tid;
-      TreeView tv = t;
-      int ti = li;
-      if (!p.tree_in_lds) {
-        tv.stat = p.stat; tv.meta = p.meta; tv.B = B; tv.legal = p.legal; tv.nlegal = p.nlegal; ti = i0 + li;
-      }
+      const TreeView &tv = t;
+      const int ti = tix(li);
       const int len = s_len[li];
       // best_action along the final path (cnode.cpp:806)
       for (int l = 0; l < len; ++l) tv.meta[nidx(tv, tv.path[l * R + li], ti)].best = tv.path_act[l * R + li];
@@ -459,9 +533,11 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       backup_slice<false>(tv, ti, li, R, &s_mm[li], vtp, s_v[li], p.disc);
     }
     __syncthreads();
+    LZM_STAMP(9);
   }
   // ---- write back the slice (tree, min-max, last paths)
-  if (p.tree_in_lds) {
+  LZM_STAMP(11);
+  if constexpr (TL) {
     for (int e = tid; e < p.cap * R; e += kThreads) {
       const int node = e / R, li = e % R;
       if (li < nr) {

@@ -1,0 +1,54 @@
+"""Diagnostic: per-phase shader-clock cycles of the fused search kernel (LZM_PHASE_TIMING=1).
+
+    LZM_PHASE_TIMING=1 python tools/phase_timing.py [--envs 256] [--sims 50] [--zero-heads]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("LZM_PHASE_TIMING", "1")
+
+import bench  # noqa: E402
+from lightzero_amd import _lib  # noqa: E402
+
+NAMES = ["select", "offsets+lookback", "gather", "dynamics", "reward head+decode", "pred trunk",
+         "value head+decode", "policy head", "file latents", "expand+backup", "stage-in", "write-back"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=256)
+    ap.add_argument("--sims", type=int, default=50)
+    ap.add_argument("--rng", default="glibc")
+    ap.add_argument("--zero-heads", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    model = bench.build_model(dev, a.zero_heads, 0)
+    step = bench.GpuStep(a.envs, a.sims, model, dev, a.rng, 0, 1)
+    step()
+    torch.cuda.synchronize()
+    from lightzero_amd.tree import POOL
+    t = next(iter(POOL._free.values()))[0]
+    buf = (ctypes.c_uint64 * 16)()
+    _lib.load().lzm_debug_phase_cycles(t.h, buf, 1)
+    n = 3
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    _lib.load().lzm_debug_phase_cycles(t.h, buf, 0)
+    G = (a.envs + 7) // 8
+    per = np.array(buf[:12], dtype=np.float64) / (n * G)
+    tot = per.sum()
+    print(f"per workgroup per search (cycles), G={G}, sims={a.sims}:")
+    for name, c in zip(NAMES, per):
+        print(f"  {name:20s} {c:12.0f}  per-sim {c / a.sims:9.0f}  {100 * c / tot:5.1f}%")
+    print(f"  total {tot:.0f} cycles = {tot / 2.1e3:.0f} us at 2.1 GHz")
+
+
+if __name__ == "__main__":
+    main()
