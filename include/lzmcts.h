@@ -130,7 +130,9 @@ int lzm_get_trajectories(lzm_handle *h, int32_t *out, int tmax, void *stream);
  * (dynamics + reward head + prediction heads, BatchNorm folded into the Linears), support decode
  * (InverseScalarTransform, softmax always applied: the heads are Linear logits), expansion and
  * backup. Roots must be prepared (lzm_roots_prepare) and minmax initialised (lzm_minmax_init).
- * weights: device float buffer, lzm_mlp_packed_floats() floats, layers in the order
+ * weights: the kernel-layout buffer written by lzm_mlp_prepare (lzm_mlp_kernel_floats() floats,
+ * 16-byte aligned). lzm_mlp_prepare reads the packed network: lzm_mlp_packed_floats() floats,
+ * layers in the order
  *   fc_dynamics(_1)[0] (K = hidden + actions: latent rows then one-hot action rows),
  *   fc_dynamics(_1)[1], [fc_dynamics_2[0], fc_dynamics_2[1] if res_dynamics],
  *   fc_reward_head[0] (hidden -> head_hidden), fc_reward_head[1] (head_hidden -> support),
@@ -142,6 +144,12 @@ int lzm_get_trajectories(lzm_handle *h, int32_t *out, int tmax, void *stream);
  * rec_* (nullable, [S][B] / [S][B][2] / [S][B][actions]): per-simulation x, last action,
  * search_len, decoded {reward, value} and policy logits. */
 int64_t lzm_mlp_packed_floats(int hidden, int actions, int head_hidden, int support, int res_dynamics);
+/* Kernel layout: each layer's weights in the order the search kernel's lanes stream them (one
+ * contiguous 1 KiB dwordx4 read per wave-instruction), K zero-padded to a multiple of 16, then its
+ * bias. Asynchronous on `stream`; re-run whenever the network's parameters change. */
+int64_t lzm_mlp_kernel_floats(int hidden, int actions, int head_hidden, int support, int res_dynamics);
+int lzm_mlp_prepare(int hidden, int actions, int head_hidden, int support, int res_dynamics, const float *packed,
+                    float *out, void *stream);
 int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int res_dynamics, const float *weights,
                    int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
                    const uint32_t *seeds, const int32_t *virtual_to_play, float *latent_pool, int32_t *rec_x,
@@ -160,7 +168,8 @@ int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream);
  * runs with LZM_PHASE_TIMING=1 (synchronous; reset != 0 clears the counters). Phases: 0 select,
  * 1 draw offsets + look-back, 2 leaf gather, 3 dynamics, 4 reward head + decode, 5 prediction
  * trunk, 6 value head + decode, 7 policy head, 8 latent filing, 9 expand + backup, 10 stage-in,
- * 11 write-back. */
+ * 11 write-back; 16 + 4 * step + j: network schedule step `step`, j = 0 FMAs + prefetch issue,
+ * 1 first barrier, 2 reduction + barrier, 3 decode. out_host holds 64 counters. */
 int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset);
 int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*/, int n, void *stream);
 

@@ -52,6 +52,8 @@ SIGNATURES = {
     "lzm_get_trajectories": [_vp, _vp, _i, _vp],
     "lzm_last_traverse_passes": [_vp, _vp, _vp],
     "lzm_mlp_packed_floats": [_i, _i, _i, _i, _i],
+    "lzm_mlp_kernel_floats": [_i, _i, _i, _i, _i],
+    "lzm_mlp_prepare": [_i, _i, _i, _i, _i, _vp, _vp, _vp],
     "lzm_search_mlp": [_vp, _i, _i, _i, _i, _vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_diagnostics": [_vp, _vp, _vp],
     "lzm_debug_expf": [_vp, _vp, _i64, _vp],
@@ -59,7 +61,8 @@ SIGNATURES = {
     "lzm_debug_philox": [_vp, _vp, _i, _vp],
     "lzm_debug_phase_cycles": [_vp, _vp, _i],
 }
-_RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64}
+_RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
+            "lzm_mlp_kernel_floats": ctypes.c_int64}
 
 _lib = None
 

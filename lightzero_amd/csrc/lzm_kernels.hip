@@ -568,7 +568,7 @@ struct lzm_handle {
   int flag_sims = 0;
   uint32_t *epoch = nullptr;               // [2] launch epoch, done counter
   int32_t *search_diag = nullptr;          // [2]
-  unsigned long long *phase = nullptr;     // [16] diagnostic phase cycles (LZM_PHASE_TIMING=1)
+  unsigned long long *phase = nullptr;     // [64] diagnostic phase cycles (LZM_PHASE_TIMING=1)
 };
 
 // Jump matrices of glibc random_r: row m of J_first expresses z[344+m] (the m-th rand()
@@ -1011,12 +1011,34 @@ int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream) {
 // ---------------------------------------------------------------- fused whole-search (MLP)
 namespace {
 
-// Layer shapes of the packed MuZeroModelMLP recurrent network (lzm_search_mlp.h order).
+// Layer shapes of the packed MuZeroModelMLP recurrent network (lzm_search_mlp.h order): krows
+// input rows in the packed (torch-transposed) layout, K = krows rounded up to kKC in the kernel's.
 struct LayerShape {
   int krows, K, N;
 };
+bool layer_used(int l, int res_dynamics) { return res_dynamics || (l != 2 && l != 3); }
+// float offset of each layer's weights / bias in the kernel layout (16-B aligned), total size
+size_t kernel_layout(const LayerShape *s, int res_dynamics, size_t *w_off, size_t *b_off) {
+  size_t off = 0;
+  for (int l = 0; l < 12; ++l) {
+    w_off[l] = b_off[l] = off;
+    if (!layer_used(l, res_dynamics)) continue;
+    off += swz_floats(s[l].K, s[l].N);
+    b_off[l] = off;
+    off = (off + s[l].N + 3) & ~(size_t)3;
+  }
+  return off;
+}
+
+__global__ void mlp_swizzle_kernel(const float *src, int krows, int K, int N, float *dst, size_t n) {
+  const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  int k, col;
+  swz_source(K, N, d, &k, &col);
+  dst[d] = (col < N && k < krows) ? src[(size_t)k * N + col] : 0.0f;
+}
 void mlp_shapes(int H, int A, int F, int V, LayerShape *s) {
-  s[0] = {H + A, H, H};  // fc_dynamics(_1)[0]: input [latent; one-hot action]
+  s[0] = {H + A, (H + A + kKC - 1) / kKC * kKC, H};  // fc_dynamics(_1)[0]: [latent; one-hot action]
   s[1] = {H, H, H};
   s[2] = {H, H, H};      // fc_dynamics_2 (res_connection_in_dynamics)
   s[3] = {H, H, H};
@@ -1078,14 +1100,48 @@ int ensure_flags(lzm_handle *h, int sims, int G) {
   if (h->flag_sims >= sims) return LZM_OK;
   dfree(h->lb_flags);
   h->lb_flags = nullptr;
-  const size_t n = (size_t)sims * G;
+  const size_t n = (size_t)sims * std::max(G, h->B);  // any roots-per-workgroup choice fits
   LZM_HIP(hipMalloc(&h->lb_flags, n * sizeof(unsigned long long)));
   LZM_HIP(hipMemset(h->lb_flags, 0, n * sizeof(unsigned long long)));  // epoch 0 never matches
   h->flag_sims = sims;
   return LZM_OK;
 }
 
-constexpr int kRoots = 8;  // roots per workgroup in the fused search
+// Roots per workgroup in the fused search: the smallest of 1, 2, 4, 8 that keeps the grid within
+// one workgroup per CU (each simulation is a latency chain per workgroup, so spreading the batch
+// over more CUs shortens it; fewer, fuller workgroups amortise each weight read over more rows).
+// LZM_ROOTS_PER_WG overrides (experiments).
+int roots_per_wg(int B) {
+  const char *e = getenv("LZM_ROOTS_PER_WG");
+  if (e) {
+    const int r = atoi(e);
+    if (r == 1 || r == 2 || r == 4 || r == 8) return r;
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  for (int r = 1; r < 8; r *= 2)
+    if ((B + r - 1) / r <= cus) return r;
+  return 8;
+}
+
+template <int R, bool TL>
+hipError_t launch_search(const SearchArgs &p, int G, size_t lds, hipStream_t stream) {
+  hipError_t e = hipFuncSetAttribute((const void *)search_mlp_kernel<R, TL>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((search_mlp_kernel<R, TL>), dim3(G), dim3(kThreads), lds, stream, p);
+  return hipGetLastError();
+}
+
+template <int R>
+hipError_t launch_search_r(const SearchArgs &p, int G, size_t lds, hipStream_t stream) {
+  return p.tree_in_lds ? launch_search<R, true>(p, G, lds, stream) : launch_search<R, false>(p, G, lds, stream);
+}
 constexpr size_t kMaxLds = 160 * 1024 - 1024;
 
 size_t round4(size_t x) { return (x + 3) & ~(size_t)3; }
@@ -1106,6 +1162,40 @@ int64_t lzm_mlp_packed_floats(int hidden, int actions, int head_hidden, int supp
   return n;
 }
 
+int64_t lzm_mlp_kernel_floats(int hidden, int actions, int head_hidden, int support, int res_dynamics) {
+  if (hidden <= 0 || actions <= 0 || head_hidden <= 0 || support <= 0) return -1;
+  LayerShape s[12];
+  mlp_shapes(hidden, actions, head_hidden, support, s);
+  size_t w_off[12], b_off[12];
+  return (int64_t)kernel_layout(s, res_dynamics, w_off, b_off);
+}
+
+int lzm_mlp_prepare(int hidden, int actions, int head_hidden, int support, int res_dynamics, const float *packed,
+                    float *out, void *stream) {
+  if (!packed || !out || hidden <= 0 || actions <= 0 || head_hidden <= 0 || support <= 0 ||
+      hidden % kKC != 0 || head_hidden % kKC != 0) {
+    set_err("lzm_mlp_prepare: bad arguments (hidden and head widths must be multiples of 16)");
+    return LZM_ERR_ARG;
+  }
+  LayerShape s[12];
+  mlp_shapes(hidden, actions, head_hidden, support, s);
+  size_t w_off[12], b_off[12];
+  kernel_layout(s, res_dynamics, w_off, b_off);
+  size_t src = 0;
+  for (int l = 0; l < 12; ++l) {
+    if (!layer_used(l, res_dynamics)) continue;
+    const size_t n = swz_floats(s[l].K, s[l].N);
+    hipLaunchKernelGGL(mlp_swizzle_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       packed + src, s[l].krows, s[l].K, s[l].N, out + w_off[l], n);
+    LZM_CHECK_LAUNCH();
+    src += (size_t)s[l].krows * s[l].N;
+    LZM_HIP(hipMemcpyAsync(out + b_off[l], packed + src, (size_t)s[l].N * sizeof(float), hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    src += s[l].N;
+  }
+  return LZM_OK;
+}
+
 int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int res_dynamics, const float *weights,
                    int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
                    const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, int32_t *rec_x, int32_t *rec_a,
@@ -1114,12 +1204,17 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     set_err("lzm_search_mlp: null argument or no simulations");
     return LZM_ERR_ARG;
   }
+  if ((uintptr_t)weights & 15) {
+    set_err("lzm_search_mlp: weights must be 16-byte aligned (lzm_mlp_prepare output)");
+    return LZM_ERR_ARG;
+  }
   if (h->flags & LZM_TREE_EZ) {
     set_err("lzm_search_mlp: MuZero trees only");
     return LZM_ERR_ARG;
   }
   const int H = hidden, F = head_hidden, V = support, A = h->A, S = num_simulations;
-  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || A > H || H % kKC != 0 || F % kKC != 0) {
+  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || V > 2 * kThreads || A > H || H % kKC != 0 ||
+      F % kKC != 0) {
     set_err("lzm_search_mlp: unsupported network shape (hidden and head widths must be multiples of 16)");
     return LZM_ERR_ARG;
   }
@@ -1129,7 +1224,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   }
   int rc = fill_lut(h, pb_c_base, pb_c_init);
   if (rc != LZM_OK) return rc;
-  const int R = kRoots;
+  const int R = roots_per_wg(h->B);
   const int G = (h->B + R - 1) / R;
   const bool fast = (h->flags & LZM_RNG_FAST) != 0;
   if (!fast) {
@@ -1149,25 +1244,21 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   {
     LayerShape s[12];
     mlp_shapes(H, A, F, V, s);
-    size_t off = 0;
+    size_t w_off[12], b_off[12];
+    kernel_layout(s, res_dynamics, w_off, b_off);
     for (int l = 0; l < 12; ++l) {
-      if (!res_dynamics && (l == 2 || l == 3)) {
-        p.L[l] = MlpLayer{nullptr, nullptr, 0, 0, 0};
+      if (!layer_used(l, res_dynamics)) {
+        p.L[l] = MlpLayer{nullptr, nullptr, 0, 0};
         continue;
       }
-      p.L[l].w = weights + off;
-      p.L[l].b = weights + off + (size_t)s[l].krows * s[l].N;
-      p.L[l].K = s[l].K;
-      p.L[l].N = s[l].N;
-      p.L[l].ldw = s[l].N;
-      off += (size_t)s[l].krows * s[l].N + s[l].N;
+      p.L[l] = MlpLayer{weights + w_off[l], weights + b_off[l], s[l].K, s[l].N};
     }
   }
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
   p.flags = h->lb_flags; p.epoch = h->epoch; p.diag = h->search_diag; p.fast = fast ? 1 : 0;
   if (!h->phase && getenv("LZM_PHASE_TIMING") && atoi(getenv("LZM_PHASE_TIMING")) > 0) {
-    LZM_HIP(hipMalloc(&h->phase, 16 * sizeof(unsigned long long)));
-    LZM_HIP(hipMemset(h->phase, 0, 16 * sizeof(unsigned long long)));
+    LZM_HIP(hipMalloc(&h->phase, 64 * sizeof(unsigned long long)));
+    LZM_HIP(hipMemset(h->phase, 0, 64 * sizeof(unsigned long long)));
   }
   p.phase = h->phase;
   p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
@@ -1181,28 +1272,29 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.off_legal = o; if (p.tree_in_lds) o += round4((size_t)R * A + R);
   p.off_path = o; o += round4((size_t)h->depth_cap * R);
   p.off_pact = o; o += round4((size_t)h->depth_cap * R);
-  p.off_x0 = o; o += round4((size_t)H * R);
-  p.off_x1 = o; o += round4((size_t)H * R);
-  p.off_x2 = o; o += round4((size_t)H * R);
-  p.off_n = o; o += round4((size_t)H * R);
-  p.off_h = o; o += round4((size_t)F * R);
-  p.off_logit = o; o += round4((size_t)(V + 1) * R);
-  p.off_part = o; o += round4((size_t)kThreads * R);
+  // transposed activations [k][r], 4-float pad per kKC rows (tpos in lzm_search_mlp.h)
+  auto tfl = [R](int K) { return (size_t)((K + kKC - 1) / kKC) * (kKC * R + 4); };
+  p.off_x0 = o; o += round4(tfl(p.L[0].K));  // [latent; one-hot] rows, zero-padded
+  p.off_x1 = o; o += round4(tfl(H));          // also the policy logits [r][A]
+  p.off_x2 = o; o += round4(tfl(H));
+  p.off_n = o; o += round4(tfl(H));
+  p.off_h = o; o += round4(tfl(F));
+  p.off_logit = o; if (V < kThreads) o += round4((size_t)(V + 1) * R);  // wide supports decode from registers
+  p.off_part = o;  // (unused: split-K partials meet through DPP)
   p.off_misc = o; o += round4((size_t)S + 32);  // staged seeds[S] + 16807^i table
   const size_t lds = o * sizeof(float);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_mlp: %zu B of LDS needed (network too wide)", lds);
     return LZM_ERR_ARG;
   }
-  if (p.tree_in_lds) {
-    LZM_HIP(hipFuncSetAttribute((const void *)search_mlp_kernel<kRoots, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((search_mlp_kernel<kRoots, true>), dim3(G), dim3(kThreads), lds, (hipStream_t)stream, p);
-  } else {
-    LZM_HIP(hipFuncSetAttribute((const void *)search_mlp_kernel<kRoots, false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((search_mlp_kernel<kRoots, false>), dim3(G), dim3(kThreads), lds, (hipStream_t)stream, p);
+  hipError_t e;
+  switch (R) {
+    case 1: e = launch_search_r<1>(p, G, lds, (hipStream_t)stream); break;
+    case 2: e = launch_search_r<2>(p, G, lds, (hipStream_t)stream); break;
+    case 4: e = launch_search_r<4>(p, G, lds, (hipStream_t)stream); break;
+    default: e = launch_search_r<8>(p, G, lds, (hipStream_t)stream); break;
   }
+  LZM_HIP(e);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
@@ -1210,12 +1302,12 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
 int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset) {
   if (!h || !out_host) return LZM_ERR_ARG;
   if (!h->phase) {
-    memset(out_host, 0, 16 * sizeof(uint64_t));
+    memset(out_host, 0, 64 * sizeof(uint64_t));
     return LZM_OK;
   }
   LZM_HIP(hipDeviceSynchronize());
-  LZM_HIP(hipMemcpy(out_host, h->phase, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  if (reset) LZM_HIP(hipMemset(h->phase, 0, 16 * sizeof(unsigned long long)));
+  LZM_HIP(hipMemcpy(out_host, h->phase, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (reset) LZM_HIP(hipMemset(h->phase, 0, 64 * sizeof(unsigned long long)));
   return LZM_OK;
 }
 

@@ -32,9 +32,9 @@ namespace lzm {
 constexpr int kThreads = 512;  // 8 waves: two per SIMD, so one's memory wait hides under the other's FMAs
 
 struct MlpLayer {
-  const float *w;  // [K][ldw] (input-major), zero-padded columns
-  const float *b;  // [ldw]
-  int K, N, ldw;
+  const float *w;  // kernel (swizzled) layout, see swz_source
+  const float *b;  // [N]
+  int K, N;        // K: inputs rounded up to kKC (zero rows)
 };
 
 struct SearchArgs {
@@ -76,107 +76,343 @@ struct SearchArgs {
 // ------------------------------------------------------------------------------ LDS helpers
 __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
 
-// out_T[n][r] (or out[r][n] when rowmajor) = act(in_T . W + b (+ W[H+a_r] one-hot row)) (+ resid_T)
-// Each weight element is read from L2 by exactly one lane: a lane owns one output column for all
-// R rows; spare lanes split K and reduce through LDS partials.
-constexpr int kKC = 16;  // weights held in registers per lane before the FMAs that use them
-typedef const __attribute__((address_space(1))) float *gfloat_p;  // global (not flat) loads
-
-// acc[r] += sum_{k in [k0, k1)} inT[k][r] * W[k][col] with (k1 - k0) % kKC == 0: each chunk's
-// weights are issued as loads first, so one L2 round trip is paid per chunk, not per weight.
+// Dense layers: out_T[n][r] (or out[r][n] when rowmajor) = act(in_T . W + b) (+ resid_T).
+// A lane owns one output column for all R rows over a range of K; when a layer has fewer columns
+// than lanes, `splits` lanes share a column (whole kKC-chunks each) and reduce through LDS.
+// Each weight is read from L2 once per workgroup per simulation.
+constexpr int kKC = 16;        // K-chunk: weights a lane holds in registers per group of FMAs
+// chunks per lane loaded one step ahead (pre_chunks * kKC registers): fewer for wider R, whose
+// accumulators and input reads need the registers
 template <int R>
-__device__ __forceinline__ void load_chunk(gfloat_p W, int ldw, int col, int kb, float *w) {
-#pragma unroll
-  for (int j = 0; j < kKC; ++j) w[j] = W[(size_t)(kb + j) * ldw + col];
+constexpr int pre_chunks() { return R <= 2 ? 3 : 2; }
+typedef const __attribute__((address_space(1))) float *gfloat_p;    // global (not flat) loads
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) f32x4 *gfloat4_p;  // dwordx4 global loads
+
+// Lane split of a layer with K inputs (K % kKC == 0) and N outputs, shared by the kernel and the
+// host-side weight swizzle. splits == 0: wide layer (N >= kThreads), lane tid owns columns
+// tid, tid + kThreads, ... over all K. Otherwise `splits` (a power of two <= 16) adjacent lanes
+// share a column: lane = col * splits + part, col < Np (N rounded up to a power of two; columns
+// >= N compute zeros), part p owns chunks [p * cpl, p * cpl + cpl) of K (chunks past K / kKC are
+// skipped), and the partial sums meet through DPP lane exchanges, not LDS.
+struct Split {
+  int Np, splits, cpl, log2s;
+};
+__host__ __device__ inline Split layer_split(int K, int N) {
+  Split s;
+  const int nc = K / kKC;
+  if (N >= kThreads) {
+    s.Np = N; s.splits = 0; s.cpl = nc; s.log2s = 0;
+    return s;
+  }
+  int Np = 1;
+  while (Np < N) Np <<= 1;
+  int sp = 1, lg = 0;
+  while (sp < 16 && sp * 2 * Np <= kThreads && sp < nc) {
+    sp *= 2;
+    ++lg;
+  }
+  s.Np = Np; s.splits = sp; s.cpl = (nc + sp - 1) / sp; s.log2s = lg;
+  return s;
 }
 
+// Kernel weight layout ("swizzled"): lane order, so that every wave-instruction of a layer's
+// weight stream is one contiguous 1 KiB dwordx4 load. Split layer: float4 index
+// (j * 4 + q) * (Np * splits) + lane holds W[k .. k+3][col], col = lane >> log2s,
+// k = ((lane & (splits - 1)) * cpl + j) * kKC + 4q (zeros for col >= N or k >= K). Wide layer:
+// round u (columns u * kThreads + lane, lane < n_u = min(kThreads, N - u * kThreads)) starts at
+// float u * kThreads * K and holds float4 (j * 4 + q) * n_u + lane = W[j * kKC + 4q .. +3][col].
+__host__ __device__ inline size_t swz_floats(int K, int N) {
+  const Split s = layer_split(K, N);
+  return s.splits ? (size_t)s.cpl * kKC * s.Np * s.splits : (size_t)K * N;
+}
+// Source (k, col) of kernel-layout float d of a layer; col >= N or k >= K marks padding.
+__host__ __device__ inline void swz_source(int K, int N, size_t d, int *k, int *col) {
+  const Split s = layer_split(K, N);
+  const int e = (int)(d & 3);
+  size_t f4 = d >> 2;
+  if (s.splits) {
+    const size_t nl = (size_t)s.Np * s.splits;
+    const int lane = (int)(f4 % nl);
+    const int q = (int)((f4 / nl) & 3);
+    const int j = (int)(f4 / nl / 4);
+    *col = lane >> s.log2s;
+    *k = ((lane & (s.splits - 1)) * s.cpl + j) * kKC + 4 * q + e;
+  } else {
+    const size_t round = (size_t)kThreads * K;
+    const int u = (int)(d / round);
+    f4 = (d - (size_t)u * round) >> 2;
+    const int nu = N - u * kThreads < kThreads ? N - u * kThreads : kThreads;
+    const int lane = (int)(f4 % nu);
+    const int q = (int)((f4 / nu) & 3);
+    const int j = (int)(f4 / nu / 4);
+    *col = u * kThreads + lane;
+    *k = j * kKC + 4 * q + e;
+  }
+}
+
+// One entry of the layer schedule (LDS float offsets of input / output / residual).
+struct Step {
+  int layer, in, out, relu, resid, rowmajor, ldout, decode, Np, splits, cpl, log2s;
+};
+
+// chunk j of this lane: 4 float4 loads, lane stride nl (float4 units)
+__device__ __forceinline__ void load_chunk(gfloat4_p base, int nl, int lane, int j, float *w) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 v = base[(size_t)(j * 4 + q) * nl + lane];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+}
+
+// Activations in LDS are transposed, [k][r], with a 4-float pad after every kKC rows of k: the
+// lanes of a wave that split K read chunks a multiple of kKC apart, and the pad puts those reads
+// on different banks.
+template <int R>
+__device__ __forceinline__ int tpos(int k, int r) { return (k / kKC) * (kKC * R + 4) + (k % kKC) * R + r; }
+
+// acc[r] += sum_{j < kKC} inT[kb + j][r] * w[j], k ascending (one fmaf per term). Inputs are
+// broadcast LDS reads: one float4 covers 4 / R consecutive k for R < 4, or half a k for R = 8.
 template <int R>
 __device__ __forceinline__ void fma_chunk(const float *inT, int kb, const float *w, float *acc) {
+  static_assert(R == 1 || R == 2 || R == 4 || R == 8, "rows per workgroup: 1, 2, 4 or 8");
+  const float *cb = inT + tpos<R>(kb, 0);  // kb % kKC == 0: the chunk is contiguous
+  if constexpr (R == 8) {
 #pragma unroll
-  for (int j = 0; j < kKC; ++j) {
-    const float4 a0 = ld4(inT + (kb + j) * R), a1 = ld4(inT + (kb + j) * R + 4);
-    acc[0] = __fmaf_rn(a0.x, w[j], acc[0]); acc[1] = __fmaf_rn(a0.y, w[j], acc[1]);
-    acc[2] = __fmaf_rn(a0.z, w[j], acc[2]); acc[3] = __fmaf_rn(a0.w, w[j], acc[3]);
-    acc[4] = __fmaf_rn(a1.x, w[j], acc[4]); acc[5] = __fmaf_rn(a1.y, w[j], acc[5]);
-    acc[6] = __fmaf_rn(a1.z, w[j], acc[6]); acc[7] = __fmaf_rn(a1.w, w[j], acc[7]);
+    for (int j = 0; j < kKC; ++j) {
+      const float4 a0 = ld4(cb + j * R), a1 = ld4(cb + j * R + 4);
+      acc[0] = __fmaf_rn(a0.x, w[j], acc[0]); acc[1] = __fmaf_rn(a0.y, w[j], acc[1]);
+      acc[2] = __fmaf_rn(a0.z, w[j], acc[2]); acc[3] = __fmaf_rn(a0.w, w[j], acc[3]);
+      acc[4] = __fmaf_rn(a1.x, w[j], acc[4]); acc[5] = __fmaf_rn(a1.y, w[j], acc[5]);
+      acc[6] = __fmaf_rn(a1.z, w[j], acc[6]); acc[7] = __fmaf_rn(a1.w, w[j], acc[7]);
+    }
+  } else if constexpr (R == 4) {
+#pragma unroll
+    for (int j = 0; j < kKC; ++j) {
+      const float4 a = ld4(cb + j * R);
+      acc[0] = __fmaf_rn(a.x, w[j], acc[0]); acc[1] = __fmaf_rn(a.y, w[j], acc[1]);
+      acc[2] = __fmaf_rn(a.z, w[j], acc[2]); acc[3] = __fmaf_rn(a.w, w[j], acc[3]);
+    }
+  } else if constexpr (R == 2) {
+#pragma unroll
+    for (int j = 0; j < kKC; j += 2) {
+      const float4 a = ld4(cb + j * R);  // k = j: (x, y), k = j + 1: (z, w)
+      acc[0] = __fmaf_rn(a.x, w[j], acc[0]); acc[1] = __fmaf_rn(a.y, w[j], acc[1]);
+      acc[0] = __fmaf_rn(a.z, w[j + 1], acc[0]); acc[1] = __fmaf_rn(a.w, w[j + 1], acc[1]);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kKC; j += 4) {
+      const float4 a = ld4(cb + j);
+      acc[0] = __fmaf_rn(a.x, w[j], acc[0]); acc[0] = __fmaf_rn(a.y, w[j + 1], acc[0]);
+      acc[0] = __fmaf_rn(a.z, w[j + 2], acc[0]); acc[0] = __fmaf_rn(a.w, w[j + 3], acc[0]);
+    }
   }
 }
 
-// Double-buffered: the next chunk's weight loads are in flight while this chunk's FMAs issue.
+// Issue this lane's first kPreChunks weight chunks (and its bias) of a schedule step. Called right
+// after the previous step's FMAs, so the L2 round trip overlaps that step's barrier, reduction and
+// decode (and, for the first step of a simulation, the whole tree phase). Every register is
+// (re)defined on every path, so no stale value stays live across the schedule loop.
 template <int R>
-__device__ __forceinline__ void dot_chunked(gfloat_p W, int ldw, int col, int k0, int k1, const float *inT,
-                                            float *acc) {
-  float wa[kKC], wb[kKC];
-  load_chunk<R>(W, ldw, col, k0, wa);
-  for (int kb = k0; kb < k1; kb += 2 * kKC) {
-    const bool has_b = kb + kKC < k1;
-    if (has_b) load_chunk<R>(W, ldw, col, kb + kKC, wb);
-    fma_chunk<R>(inT, kb, wa, acc);
-    if (!has_b) break;
-    if (kb + 2 * kKC < k1) load_chunk<R>(W, ldw, col, kb + 2 * kKC, wa);
-    fma_chunk<R>(inT, kb + kKC, wb, acc);
-  }
-}
-
-// One network layer on the workgroup's R rows (K % kKC == 0, checked on the host). Called from a
-// loop over the layer schedule, so its code exists once (the loop body must fit the I-cache).
-template <int R>
-__device__ __forceinline__ void dense(const MlpLayer L, const float *inT, float *out, float *part, int relu,
-                                   const float *residT, int rowmajor, int ldout, const int *onehot_act,
-                                   int onehot_row0) {
-  static_assert(R == 8, "dense is written for 8 rows per workgroup");
+__device__ __forceinline__ void prefetch_step(const MlpLayer L, const Step &s, float *w, float &bias) {
+  constexpr int kPreChunks = pre_chunks<R>();
   const int tid = threadIdx.x;
-  const int N = L.N, K = L.K;
-  gfloat_p W = (gfloat_p)L.w;
-  gfloat_p Bv = (gfloat_p)L.b;
-  if (N >= kThreads) {
-    for (int c = tid; c < N; c += kThreads) {
-      float acc[R];
-      const float bias = Bv[c];
+  const int nl = s.splits ? s.Np * s.splits : (L.N < kThreads ? L.N : kThreads);
+  const bool active = tid < nl;
+  const int nc = L.K / kKC;
+  const int c0 = s.splits ? (tid & (s.splits - 1)) * s.cpl : 0;
+  const int n = active ? min(s.cpl, nc - c0) : 0;
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = bias;
-      dot_chunked<R>(W, L.ldw, c, 0, K, inT, acc);
+  for (int c = 0; c < kPreChunks; ++c) {
+    if (c < n) {
+      load_chunk((gfloat4_p)L.w, nl, tid, c, w + c * kKC);
+    } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        float v = acc[r];
-        if (relu) v = fmaxf(v, 0.0f);
-        if (rowmajor) out[r * ldout + c] = v; else out[c * R + r] = v;
+      for (int j = 0; j < kKC; ++j) w[c * kKC + j] = 0.0f;
+    }
+  }
+  const int col = s.splits ? tid >> s.log2s : tid;
+  const bool lead = s.splits ? (tid & (s.splits - 1)) == 0 : true;  // adds the bias
+  bias = (active && lead && col < L.N) ? ((gfloat_p)L.b)[col] : 0.0f;
+}
+
+// acc += chunks [j0, j1) of this lane streamed from L2, double-buffered.
+template <int R>
+__device__ __forceinline__ void dot_stream(gfloat4_p base, int nl, int lane, int j0, int j1, int kofs,
+                                           const float *inT, float *acc) {
+  float wa[kKC], wb[kKC];
+  load_chunk(base, nl, lane, j0, wa);
+  for (int j = j0; j < j1; j += 2) {
+    const bool has_b = j + 1 < j1;
+    if (has_b) load_chunk(base, nl, lane, j + 1, wb);
+    fma_chunk<R>(inT, kofs + j * kKC, wa, acc);
+    if (!has_b) break;
+    if (j + 2 < j1) load_chunk(base, nl, lane, j + 2, wa);
+    fma_chunk<R>(inT, kofs + (j + 1) * kKC, wb, acc);
+  }
+}
+
+// acc += this lane's cnt chunks (k from kofs): the first pre_chunks from the prefetched w, the
+// rest streamed.
+template <int R>
+__device__ __forceinline__ void dot_lane(gfloat4_p base, int nl, int lane, int cnt, int kofs, const float *inT,
+                                         const float *w, float *acc) {
+  constexpr int kPreChunks = pre_chunks<R>();
+  if (cnt > 0) fma_chunk<R>(inT, kofs, w, acc);
+  if (cnt > 1) fma_chunk<R>(inT, kofs + kKC, w + kKC, acc);
+  if (kPreChunks > 2 && cnt > 2) fma_chunk<R>(inT, kofs + 2 * kKC, w + 2 * kKC, acc);
+  if (cnt > kPreChunks) dot_stream<R>(base, nl, lane, kPreChunks, cnt, kofs, inT, acc);
+}
+
+// DPP lane exchange inside a row of 16 lanes.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over each group of 2^log2s adjacent lanes (every lane of a group gets its group's sum):
+// quad_perm xor 1, xor 2, then row_half_mirror and row_mirror pair the quads and half-rows.
+template <int R>
+__device__ __forceinline__ void group_sum(float *acc, int log2s) {
+  if (log2s >= 1) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += dpp_f<0xB1>(acc[r]);
+  }
+  if (log2s >= 2) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += dpp_f<0x4E>(acc[r]);
+  }
+  if (log2s >= 3) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += dpp_f<0x141>(acc[r]);
+  }
+  if (log2s >= 4) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] += dpp_f<0x140>(acc[r]);
+  }
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+constexpr int kWaves = kThreads / 64;
+
+// out column c of a step: activation, residual, layout
+template <int R>
+__device__ __forceinline__ void store_col(const Step &s, float *out, const float *residT, int c, const float *v) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float x = v[r];
+    if (s.relu) x = fmaxf(x, 0.0f);
+    if (residT) x += residT[tpos<R>(c, r)];
+    if (s.rowmajor) out[r * s.ldout + c] = x; else out[tpos<R>(c, r)] = x;
+  }
+}
+
+// One schedule step: out = act(in . W + b) (+ resid) for the workgroup's R rows, from the lane's
+// prefetched weights `w`/`bias`; right after its FMAs it issues the next step's prefetch into the
+// same registers. Wide layers with `decode` never store their logits: the categorical support
+// expectation (scaling_transform.py:118-121: softmax, then sum p_j * (j - (V-1)/2)) is reduced
+// across the workgroup from registers and h^-1 applied (InverseScalarTransform), into dec_out[r].
+// `red`: 3 * kWaves * R floats of LDS. The caller's barrier follows.
+template <int R>
+__device__ __forceinline__ void dense_step(const MlpLayer L, const Step &s, float *smem_f, float *w, float &bias,
+                                          float *red, float *dec_out, int nr, const MlpLayer Ln, const Step &sn) {
+  const int tid = threadIdx.x;
+  const int N = L.N;
+  const float *inT = smem_f + s.in;
+  float *out = smem_f + s.out;
+  const float *residT = s.resid >= 0 ? smem_f + s.resid : nullptr;
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = bias;
+  if (s.splits == 0) {
+    // wide layer (N >= kThreads): column tid from the prefetched registers, later rounds streamed
+    dot_lane<R>((gfloat4_p)L.w, kThreads, tid, s.cpl, 0, inT, w, acc);
+    float lg1[R];
+    bool has1 = false;
+    for (int u = 1; u * kThreads < N; ++u) {
+      const int c = u * kThreads + tid;
+      const int nu = N - u * kThreads < kThreads ? N - u * kThreads : kThreads;
+      if (c < N) {
+        float a2[R];
+        const float b = ((gfloat_p)L.b)[c];
+#pragma unroll
+        for (int r = 0; r < R; ++r) a2[r] = b;
+        dot_stream<R>((gfloat4_p)(L.w + (size_t)u * kThreads * L.K), nu, tid, 0, s.cpl, 0, inT, a2);
+        if (s.decode) {
+#pragma unroll
+          for (int r = 0; r < R; ++r) lg1[r] = a2[r];
+          has1 = true;
+        } else {
+          store_col<R>(s, out, residT, c, a2);
+        }
+      }
+    }
+    prefetch_step<R>(Ln, sn, w, bias);
+    if (!s.decode) {
+      store_col<R>(s, out, residT, tid, acc);
+      return;
+    }
+    // ---- fused support decode (N <= 2 * kThreads, checked on the host)
+    const int wid = tid >> 6, lane = tid & 63;
+    float m[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      m[r] = wave_max(has1 ? fmaxf(acc[r], lg1[r]) : acc[r]);
+      if (lane == 0) red[wid * R + r] = m[r];
+    }
+    __syncthreads();
+    const float half = (float)((N - 1) / 2);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float M = red[r];
+      for (int q = 1; q < kWaves; ++q) M = fmaxf(M, red[q * R + r]);
+      const float e0 = expf(acc[r] - M);
+      float se = e0, sj = e0 * ((float)tid - half);
+      if (has1) {
+        const float e1 = expf(lg1[r] - M);
+        se += e1;
+        sj += e1 * ((float)(tid + kThreads) - half);
+      }
+      se = wave_sum(se);
+      sj = wave_sum(sj);
+      if (lane == 0) {
+        red[(kWaves + wid) * R + r] = se;
+        red[(2 * kWaves + wid) * R + r] = sj;
       }
     }
     __syncthreads();
+    if (tid < nr) {
+      float se = 0.0f, sj = 0.0f;
+      for (int q = 0; q < kWaves; ++q) {
+        se += red[(kWaves + q) * R + tid];
+        sj += red[(2 * kWaves + q) * R + tid];
+      }
+      dec_out[tid] = h_inverse(sj / se);
+    }
     return;
   }
-  // split K over up to kThreads / Np lanes per column, whole chunks per lane
-  int Np = 1;
-  while (Np < N) Np <<= 1;
-  int splits = min(kThreads / Np, K / kKC);
-  while ((K / kKC) % splits) --splits;  // whole chunks per lane
-  const int col = tid % Np, part_id = tid / Np;
-  const int kchunk = K / splits;  // multiple of kKC
-  float acc[R];
-  const bool active = col < N && part_id < splits;
-  const float bias = (active && part_id == 0) ? Bv[col] : 0.0f;
-#pragma unroll
-  for (int r = 0; r < R; ++r) acc[r] = bias;
-  if (active) {
-    if (onehot_act && part_id == 0) {
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] += W[(size_t)(onehot_row0 + onehot_act[r]) * L.ldw + col];
-    }
-    dot_chunked<R>(W, L.ldw, col, part_id * kchunk, part_id * kchunk + kchunk, inT, acc);
-#pragma unroll
-    for (int r = 0; r < R; ++r) part[(part_id * Np + col) * R + r] = acc[r];
+  // split layer: groups of `splits` adjacent lanes per column, partial sums meet through DPP
+  const int nl = s.Np << s.log2s;
+  const int part = tid & (s.splits - 1), col = tid >> s.log2s;
+  const int c0 = part * s.cpl;
+  const int cnt = min(s.cpl, L.K / kKC - c0);
+  if (tid < nl) dot_lane<R>((gfloat4_p)L.w, nl, tid, cnt, c0 * kKC, inT, w, acc);
+  prefetch_step<R>(Ln, sn, w, bias);
+  if (tid < nl) {
+    group_sum<R>(acc, s.log2s);
+    if (part == 0 && col < N) store_col<R>(s, out, residT, col, acc);
   }
-  __syncthreads();
-  for (int e = tid; e < N * R; e += kThreads) {
-    const int c = e / R, r = e % R;
-    float v = part[c * R + r];
-    for (int s = 1; s < splits; ++s) v += part[(s * Np + c) * R + r];
-    if (relu) v = fmaxf(v, 0.0f);
-    if (residT) v += residT[c * R + r];
-    if (rowmajor) out[r * ldout + c] = v; else out[c * R + r] = v;
-  }
-  __syncthreads();
 }
 
 // Expectation of the categorical support of one row by one wave (scaling_transform.py:118-121).
@@ -230,13 +466,23 @@ __device__ inline void seed_state_parallel(uint32_t seed, const uint32_t *pw, ui
 }
 
 // Phase stamps (diagnostics only; p.phase == nullptr in production): thread 0 of every
-// workgroup adds the shader-clock cycles spent since the previous stamp to phase[n].
+// workgroup adds the shader-clock cycles spent since the previous stamp to s_phase[n] (LDS), and
+// flushes them into phase[] once at the end (no global atomics inside the timed phases).
 #define LZM_STAMP(n)                                                              \
   do {                                                                            \
     if (p.phase && tid == 0) {                                                    \
       const unsigned long long now_ = __builtin_amdgcn_s_memtime();              \
-      atomicAdd(p.phase + (n), now_ - stamp_);                                   \
+      s_phase[n] += now_ - stamp_;                                                \
       stamp_ = now_;                                                              \
+    }                                                                             \
+  } while (0)
+
+#define LZM_SUBSTAMP(n)                                                           \
+  do {                                                                            \
+    if (p.phase && tid == 0) {                                                    \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();              \
+      s_phase[n] += now_ - sub_;                                                  \
+      sub_ = now_;                                                                \
     }                                                                             \
   } while (0)
 
@@ -259,8 +505,11 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   __shared__ float s_r[R], s_v[R];
   __shared__ float4 s_mm[R];
   __shared__ MlpLayer s_L[12];
-  __shared__ int s_step[12][9];
+  __shared__ Step s_step[12];
   __shared__ int s_nsteps, s_stamp_at[4];
+  __shared__ unsigned long long s_phase[64];
+  __shared__ float s_red[3 * kWaves * R];
+  if (p.phase && tid < 64) s_phase[tid] = 0ull;
 
   // ---- stage the tree slice and per-root state
   TreeView t;
@@ -312,35 +561,37 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     s_players = (m == -1) ? 1 : 2;
     s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int l = 0; l < 12; ++l) s_L[l] = p.L[l];
-    // layer schedule: {layer, in, out, relu, resid (-1: none), rowmajor, ldout, one-hot, decode}
+    // layer schedule (LDS float offsets); layer 0 reads [latent; one-hot action] from X0
     const int x0 = (int)p.off_x0, x1 = (int)p.off_x1, x2 = (int)p.off_x2, nl = (int)p.off_n, hd = (int)p.off_h,
               lg = (int)p.off_logit;
     int n = 0;
-    auto add = [&](int l, int in, int out, int relu, int resid, int rowmajor, int ldout, int onehot, int dec) {
-      int *q = s_step[n++];
-      q[0] = l; q[1] = in; q[2] = out; q[3] = relu; q[4] = resid; q[5] = rowmajor; q[6] = ldout; q[7] = onehot;
-      q[8] = dec;
+    auto add = [&](int l, int in, int out, int relu, int resid, int rowmajor, int ldout, int dec) {
+      Step &q = s_step[n++];
+      q.layer = l; q.in = in; q.out = out; q.relu = relu; q.resid = resid; q.rowmajor = rowmajor; q.ldout = ldout;
+      q.decode = dec;
+      const Split sp = layer_split(p.L[l].K, p.L[l].N);
+      q.Np = sp.Np; q.splits = sp.splits; q.cpl = sp.cpl; q.log2s = sp.log2s;
     };
-    add(0, x0, x1, 1, -1, 0, 0, 1, 0);                   // fc_dynamics(_1)[0] on [latent; one-hot]
-    add(1, x1, nl, 1, p.res ? x0 : -1, 0, 0, 0, 0);      // [1] (+ latent: res_connection_in_dynamics)
+    add(0, x0, x1, 1, -1, 0, 0, 0);                   // fc_dynamics(_1)[0]
+    add(1, x1, nl, 1, p.res ? x0 : -1, 0, 0, 0);      // [1] (+ latent: res_connection_in_dynamics)
     int enc = nl;
     if (p.res) {
-      add(2, nl, x1, 1, -1, 0, 0, 0, 0);                 // fc_dynamics_2
-      add(3, x1, x2, 1, -1, 0, 0, 0, 0);
+      add(2, nl, x1, 1, -1, 0, 0, 0);                 // fc_dynamics_2
+      add(3, x1, x2, 1, -1, 0, 0, 0);
       enc = x2;
     }
     s_stamp_at[0] = n - 1;
-    add(4, enc, hd, 1, -1, 0, 0, 0, 0);                  // fc_reward_head
-    add(5, hd, lg, 0, -1, 1, p.V + 1, 0, 1);
+    add(4, enc, hd, 1, -1, 0, 0, 0);                  // fc_reward_head
+    add(5, hd, lg, 0, -1, 1, p.V + 1, 1);
     s_stamp_at[1] = n - 1;
-    add(6, nl, x1, 1, -1, 0, 0, 0, 0);                   // fc_prediction_common
-    add(7, x1, x2, 1, -1, 0, 0, 0, 0);
+    add(6, nl, x1, 1, -1, 0, 0, 0);                   // fc_prediction_common
+    add(7, x1, x2, 1, -1, 0, 0, 0);
     s_stamp_at[2] = n - 1;
-    add(8, x2, hd, 1, -1, 0, 0, 0, 0);                   // fc_value_head
-    add(9, hd, lg, 0, -1, 1, p.V + 1, 0, 2);
+    add(8, x2, hd, 1, -1, 0, 0, 0);                   // fc_value_head
+    add(9, hd, lg, 0, -1, 1, p.V + 1, 2);
     s_stamp_at[3] = n - 1;
-    add(10, x2, hd, 1, -1, 0, 0, 0, 0);                  // fc_policy_head
-    add(11, hd, x1, 0, -1, 1, A, 0, 0);
+    add(10, x2, hd, 1, -1, 0, 0, 0);                  // fc_policy_head
+    add(11, hd, x1, 0, -1, 1, A, 0);
     s_nsteps = n;
   }
   __syncthreads();
@@ -354,8 +605,11 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     for (int e = tid; e < 31; e += kThreads) s_pow[e] = p.pow16807[e];
   __syncthreads();
   LZM_STAMP(10);
-  float *X0 = smem + p.off_x0, *X1 = smem + p.off_x1, *X2 = smem + p.off_x2, *NL = smem + p.off_n;
-  float *HD = smem + p.off_h, *LG = smem + p.off_logit, *PART = smem + p.off_part;
+  float *X0 = smem + p.off_x0, *X1 = smem + p.off_x1, *NL = smem + p.off_n;
+  float *LG = smem + p.off_logit;
+  // this lane's weights for the next schedule step, loaded one step ahead (prefetch_step)
+  float wpre[pre_chunks<R>() * kKC], bpre = 0.0f;
+  prefetch_step<R>(s_L[s_step[0].layer], s_step[0], wpre, bpre);
 
   for (int k = 0; k < p.S; ++k) {
     const uint32_t seed = s_seeds[k];
@@ -480,7 +734,12 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       const int r = e / H, h = e % H;
       float v = 0.0f;
       if (r < nr) v = p.pool[((size_t)max(s_x[r], 0) * B + i0 + r) * H + h];
-      X0[h * R + r] = v;
+      X0[tpos<R>(h, r)] = v;
+    }
+    // one-hot action rows H .. K0 (layer 0's zero-padded input; muzero_model_mlp.py:188-190)
+    for (int e = tid; e < (s_L[0].K - H) * R; e += kThreads) {
+      const int a = e / R, r = e % R;
+      X0[tpos<R>(H + a, r)] = (r < nr && s_act[r] == a) ? 1.0f : 0.0f;
     }
     __syncthreads();
     LZM_STAMP(2);
@@ -489,17 +748,23 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     // + residual), fc_dynamics_2, reward head (-> decode into s_r), fc_prediction_common, value
     // head (-> decode into s_v), policy head (-> logits [r][A] in X1).
     for (int st = 0; st < s_nsteps; ++st) {
-      const int *q = s_step[st];
-      dense<R>(s_L[q[0]], smem + q[1], smem + q[2], PART, q[3], q[4] >= 0 ? smem + q[4] : nullptr, q[5], q[6],
-               q[7] ? s_act : nullptr, H);
-      if (q[8]) {  // decode the support logits just produced (InverseScalarTransform)
+      const Step q = s_step[st];
+      const MlpLayer L = s_L[q.layer];
+      unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
+      const int nx = (st + 1 < s_nsteps) ? st + 1 : 0;  // after the last step: the next simulation's first
+      dense_step<R>(L, q, smem, wpre, bpre, s_red, q.decode == 1 ? s_r : s_v, nr, s_L[s_step[nx].layer], s_step[nx]);
+      LZM_SUBSTAMP(16 + 4 * st);
+      __syncthreads();
+      LZM_SUBSTAMP(17 + 4 * st);
+      if (q.decode && q.splits) {  // narrow support (< kThreads): logits were stored to LG, one wave per row
         const int wid = tid >> 6;
-        for (int r = wid; r < nr; r += kThreads / 64) {
+        for (int r = wid; r < nr; r += kWaves) {
           const float e = wave_expect_lds(LG + r * (p.V + 1), p.V);
-          if ((tid & 63) == 0) (q[8] == 1 ? s_r : s_v)[r] = h_inverse(e);
+          if ((tid & 63) == 0) (q.decode == 1 ? s_r : s_v)[r] = h_inverse(e);
         }
         __syncthreads();
       }
+      LZM_SUBSTAMP(18 + 4 * st);
       if (st == s_stamp_at[0]) LZM_STAMP(3);
       if (st == s_stamp_at[1]) LZM_STAMP(4);
       if (st == s_stamp_at[2]) LZM_STAMP(5);
@@ -509,7 +774,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     // ---- file the new latents (mcts_ctree.py:305): pool[k+1][i][h] = NL[h][r]
     for (int e = tid; e < H * R; e += kThreads) {
       const int r = e / H, h = e % H;
-      if (r < nr) p.pool[((size_t)(k + 1) * B + i0 + r) * H + h] = NL[h * R + r];
+      if (r < nr) p.pool[((size_t)(k + 1) * B + i0 + r) * H + h] = NL[tpos<R>(h, r)];
     }
     if (p.rec_dec && tid < nr) {
       p.rec_dec[((size_t)k * B + i0 + tid) * 2] = s_r[tid];
@@ -559,6 +824,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   }
   // epoch advance by the last workgroup to finish (the next launch reads the new epoch)
   __syncthreads();
+  if (p.phase && tid < 64 && s_phase[tid]) atomicAdd(p.phase + tid, s_phase[tid]);
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const uint32_t done = atomicAdd(p.epoch + 1, 1u);

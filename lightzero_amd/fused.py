@@ -115,8 +115,18 @@ def pack_muzero_mlp(model, device):
     return flat, dims
 
 
+def prepare_kernel_weights(flat, dims):
+    """Packed network -> the search kernel's lane-order layout (lzm_mlp_prepare, on the current stream)."""
+    args = (dims["hidden"], dims["actions"], dims["head_hidden"], dims["support"], int(dims["res"]))
+    n = _lib.load().lzm_mlp_kernel_floats(*args)
+    out = torch.empty(n, dtype=torch.float32, device=flat.device)
+    _lib.call("lzm_mlp_prepare", *args, _lib.ptr(flat), _lib.ptr(out), _lib.stream_ptr())
+    return out
+
+
 class PackedCache:
-    """Re-packs only when the model's parameters or buffers change (tensor version counters)."""
+    """Kernel-layout weights of a model; re-packs only when the model's parameters or buffers
+    change (tensor version counters)."""
 
     def __init__(self):
         self.key = None
@@ -126,6 +136,7 @@ class PackedCache:
         ver = tuple(t._version for t in list(model.parameters()) + list(model.buffers()))
         key = (id(model), str(device), ver)
         if key != self.key:
-            self.value = pack_muzero_mlp(model, device)
+            flat, dims = pack_muzero_mlp(model, device)
+            self.value = (prepare_kernel_weights(flat, dims), dims)
             self.key = key
         return self.value

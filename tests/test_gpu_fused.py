@@ -38,11 +38,11 @@ def make_model(A, H, zero_heads, seed=0, support_scale=300):
     return m.to(DEV).eval()
 
 
-def fused_search(B, S, A, H, zero_heads, players, fast, seed):
+def fused_search(B, S, A, H, zero_heads, players, fast, seed, support_scale=300):
     from lightzero_amd.mcts_ctree import MuZeroMCTSCtree
     from lightzero_amd.tree import SequentialSeeds, set_seed_source
     from lightzero_amd.utils import EasyDict
-    model = make_model(A, H, zero_heads, seed)
+    model = make_model(A, H, zero_heads, seed, support_scale)
     rng = np.random.default_rng(seed)
     obs = torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32)).to(DEV)
     with torch.no_grad():
@@ -51,7 +51,7 @@ def fused_search(B, S, A, H, zero_heads, players, fast, seed):
     noises = rng.dirichlet([0.3] * A, size=B).astype(np.float32)
     to_play = [-1] * B if players == 1 else rng.integers(1, 3, size=B).tolist()
     cfg = EasyDict(dict(num_simulations=S, discount_factor=float(DISC), device=DEV,
-                        model=dict(support_scale=300, categorical_distribution=True)))
+                        model=dict(support_scale=support_scale, categorical_distribution=True)))
     cls = MuZeroMCTSCtree
     old = cls.rng_mode
     cls.rng_mode = "philox" if fast else "glibc"
@@ -88,9 +88,25 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", CASES, ids=lambda c: "b{}_s{}_a{}_h{}_{}_p{}_{}".format(
-    c[0], c[1], c[2], c[3], "zero" if c[4] else "rand", c[5], "philox" if c[6] else "glibc"))
+def _case_id(c):
+    return "b{}_s{}_a{}_h{}_{}_p{}_{}".format(c[0], c[1], c[2], c[3], "zero" if c[4] else "rand", c[5],
+                                              "philox" if c[6] else "glibc")
+
+
+@pytest.mark.parametrize("case", CASES, ids=_case_id)
 def test_fused_tree_exact_given_network_outputs(case):
+    check_tree_exact(case)
+
+
+# every roots-per-workgroup variant of the kernel (the library picks one from the batch size)
+@pytest.mark.parametrize("roots", [1, 2, 4, 8])
+@pytest.mark.parametrize("case", [CASES[0], CASES[2], CASES[3], CASES[5]], ids=_case_id)
+def test_fused_roots_per_workgroup(case, roots, monkeypatch):
+    monkeypatch.setenv("LZM_ROOTS_PER_WG", str(roots))
+    check_tree_exact(case)
+
+
+def check_tree_exact(case):
     B, S, A, H, zero, players, fast = case
     r = fused_search(B, S, A, H, zero, players, fast, seed=B + S + A)
     rec = r["rec"]
@@ -109,10 +125,11 @@ def test_fused_tree_exact_given_network_outputs(case):
     assert np.array_equal(r["traj"], ot.trajectories(S + 2))
 
 
-@pytest.mark.parametrize("H,A", [(128, 2), (64, 9)])
-def test_fused_network_matches_torch_module(H, A):
+# support 601 decodes from registers across the workgroup; support 21 (< 512 lanes) through LDS
+@pytest.mark.parametrize("H,A,scale", [(128, 2, 300), (64, 9, 300), (64, 3, 10)])
+def test_fused_network_matches_torch_module(H, A, scale):
     B, S = 128, 20
-    r = fused_search(B, S, A, H, False, 1, False, seed=3)
+    r = fused_search(B, S, A, H, False, 1, False, seed=3, support_scale=scale)
     rec, pool, model = r["rec"], r["pool"], r["model"]
     idx = torch.arange(B, device=DEV)
     with torch.no_grad():
@@ -124,10 +141,10 @@ def test_fused_network_matches_torch_module(H, A):
             torch.testing.assert_close(torch.from_numpy(rec["policy_logits"][k]).to(DEV), out.policy_logits,
                                        rtol=1e-4, atol=1e-5)
             dec = torch.from_numpy(rec["decoded"][k]).to(DEV)
-            torch.testing.assert_close(dec[:, 0], torch_inverse_scalar_transform(out.reward, 300).squeeze(1),
-                                       rtol=1e-4, atol=1e-5 * 300)
-            torch.testing.assert_close(dec[:, 1], torch_inverse_scalar_transform(out.value, 300).squeeze(1),
-                                       rtol=1e-4, atol=1e-5 * 300)
+            torch.testing.assert_close(dec[:, 0], torch_inverse_scalar_transform(out.reward, scale).squeeze(1),
+                                       rtol=1e-4, atol=1e-5 * scale)
+            torch.testing.assert_close(dec[:, 1], torch_inverse_scalar_transform(out.value, scale).squeeze(1),
+                                       rtol=1e-4, atol=1e-5 * scale)
 
 
 def test_fused_pack_rejects_unsupported_models():

@@ -1,6 +1,6 @@
 """Diagnostic: per-phase shader-clock cycles of the fused search kernel (LZM_PHASE_TIMING=1).
 
-    LZM_PHASE_TIMING=1 python tools/phase_timing.py [--envs 256] [--sims 50] [--zero-heads]
+    LZM_PHASE_TIMING=1 python tools/phase_timing.py [--envs 256] [--sims 50] [--zero-heads] [--roots R]
 """
 import argparse
 import ctypes
@@ -26,7 +26,11 @@ def main():
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--rng", default="glibc")
     ap.add_argument("--zero-heads", action="store_true")
+    ap.add_argument("--roots", type=int, default=0, help="roots per workgroup (0: library's choice)")
     a = ap.parse_args()
+    if a.roots:
+        os.environ["LZM_ROOTS_PER_WG"] = str(a.roots)
+    R = a.roots or next(r for r in (1, 2, 4, 8) if -(-a.envs // r) <= 256 or r == 8)
     dev = torch.device("cuda", 0)
     model = bench.build_model(dev, a.zero_heads, 0)
     step = bench.GpuStep(a.envs, a.sims, model, dev, a.rng, 0, 1)
@@ -34,20 +38,25 @@ def main():
     torch.cuda.synchronize()
     from lightzero_amd.tree import POOL
     t = next(iter(POOL._free.values()))[0]
-    buf = (ctypes.c_uint64 * 16)()
+    buf = (ctypes.c_uint64 * 64)()
     _lib.load().lzm_debug_phase_cycles(t.h, buf, 1)
     n = 3
     for _ in range(n):
         step()
     torch.cuda.synchronize()
     _lib.load().lzm_debug_phase_cycles(t.h, buf, 0)
-    G = (a.envs + 7) // 8
+    G = -(-a.envs // R)
     per = np.array(buf[:12], dtype=np.float64) / (n * G)
     tot = per.sum()
-    print(f"per workgroup per search (cycles), G={G}, sims={a.sims}:")
+    print(f"per workgroup per search (cycles), R={R}, G={G}, sims={a.sims}:")
     for name, c in zip(NAMES, per):
         print(f"  {name:20s} {c:12.0f}  per-sim {c / a.sims:9.0f}  {100 * c / tot:5.1f}%")
     print(f"  total {tot:.0f} cycles = {tot / 2.1e3:.0f} us at 2.1 GHz")
+    sub = np.array(buf[16:64], dtype=np.float64).reshape(12, 4) / (n * G * a.sims)
+    print("per schedule step, per simulation (cycles): fma+prefetch, barrier, reduce+barrier, decode")
+    for st in range(12):
+        if sub[st].sum() > 0:
+            print(f"  step {st:2d}  " + "  ".join(f"{c:8.0f}" for c in sub[st]))
 
 
 if __name__ == "__main__":
