@@ -168,8 +168,8 @@ int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream);
  * runs with LZM_PHASE_TIMING=1 (synchronous; reset != 0 clears the counters). Phases: 0 select,
  * 1 draw offsets + look-back, 2 leaf gather, 3 dynamics, 4 reward head + decode, 5 prediction
  * trunk, 6 value head + decode, 7 policy head, 8 latent filing, 9 expand + backup, 10 stage-in,
- * 11 write-back; 16 + 4 * step + j: network schedule step `step`, j = 0 FMAs + prefetch issue,
- * 1 first barrier, 2 reduction + barrier, 3 decode. out_host holds 64 counters. */
+ * 11 write-back; 16 + 4 * step + j: network schedule step `step`, j = 0 step body (FMAs, weight
+ * prefetch, reduction, store, support decode), 1 barrier. out_host holds 64 counters. */
 int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset);
 int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*/, int n, void *stream);
 

@@ -1146,6 +1146,49 @@ constexpr size_t kMaxLds = 160 * 1024 - 1024;
 
 size_t round4(size_t x) { return (x + 3) & ~(size_t)3; }
 
+// The recurrent network as a schedule of dense steps (LDS activation buffers by float offset):
+// fc_dynamics(_1) on [latent; one-hot] (+ latent residual), fc_dynamics_2, reward head (decoded),
+// fc_prediction_common, value head (decoded), policy head (logits [r][A] in X1)
+// (muzero_model_mlp.py:179-204, :420-440). Even length (two weight-prefetch buffers alternate).
+void build_schedule(SearchArgs &p, const LayerShape *s, const size_t *w_off, const size_t *b_off, const float *weights,
+                    int res, int A, int V) {
+  const int x0 = (int)p.off_x0, x1 = (int)p.off_x1, x2 = (int)p.off_x2, nl = (int)p.off_n, hd = (int)p.off_h,
+            lg = (int)p.off_logit;
+  int n = 0;
+  auto add = [&](int l, int in, int out, int relu, int resid, int rowmajor, int ldout, int dec) {
+    StepRec &q = p.sched[n++];
+    q.w = weights + w_off[l];
+    q.b = weights + b_off[l];
+    q.K = s[l].K;
+    q.N = s[l].N;
+    q.wbytes = (int)(swz_floats(s[l].K, s[l].N) * sizeof(float));
+    q.in = in; q.out = out; q.relu = relu; q.resid = resid; q.rowmajor = rowmajor; q.ldout = ldout; q.decode = dec;
+    const Split sp = layer_split(s[l].K, s[l].N);
+    q.Np = sp.Np; q.splits = sp.splits; q.cpl = sp.cpl; q.log2s = sp.log2s;
+  };
+  add(0, x0, x1, 1, -1, 0, 0, 0);                // fc_dynamics(_1)[0]
+  add(1, x1, nl, 1, res ? x0 : -1, 0, 0, 0);     // [1] (+ latent: res_connection_in_dynamics)
+  int enc = nl;
+  if (res) {
+    add(2, nl, x1, 1, -1, 0, 0, 0);              // fc_dynamics_2
+    add(3, x1, x2, 1, -1, 0, 0, 0);
+    enc = x2;
+  }
+  p.stamp_at[0] = n - 1;
+  add(4, enc, hd, 1, -1, 0, 0, 0);               // fc_reward_head
+  add(5, hd, lg, 0, -1, 1, V + 1, 1);
+  p.stamp_at[1] = n - 1;
+  add(6, nl, x1, 1, -1, 0, 0, 0);                // fc_prediction_common
+  add(7, x1, x2, 1, -1, 0, 0, 0);
+  p.stamp_at[2] = n - 1;
+  add(8, x2, hd, 1, -1, 0, 0, 0);                // fc_value_head
+  add(9, hd, lg, 0, -1, 1, V + 1, 2);
+  p.stamp_at[3] = n - 1;
+  add(10, x2, hd, 1, -1, 0, 0, 0);               // fc_policy_head
+  add(11, hd, x1, 0, -1, 1, A, 0);
+  p.nsteps = n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1213,7 +1256,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     return LZM_ERR_ARG;
   }
   const int H = hidden, F = head_hidden, V = support, A = h->A, S = num_simulations;
-  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || V > 2 * kThreads || A > H || H % kKC != 0 ||
+  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || V > kMaxRounds * kThreads || A > H || H % kKC != 0 ||
       F % kKC != 0) {
     set_err("lzm_search_mlp: unsupported network shape (hidden and head widths must be multiples of 16)");
     return LZM_ERR_ARG;
@@ -1236,6 +1279,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
 
   SearchArgs p;
   memset(&p, 0, sizeof(p));
+  LayerShape shp[12];
+  size_t lay_w[12], lay_b[12];
   p.stat = h->stat; p.meta = h->meta; p.legal = h->legal; p.nlegal = h->nlegal;
   p.path = h->path; p.path_act = h->path_act; p.pathlen = h->pathlen; p.lut = h->lut;
   p.B = h->B; p.A = A; p.cap = h->cap; p.lut_n = h->lut_n; p.depth_cap = h->depth_cap;
@@ -1244,15 +1289,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   {
     LayerShape s[12];
     mlp_shapes(H, A, F, V, s);
-    size_t w_off[12], b_off[12];
-    kernel_layout(s, res_dynamics, w_off, b_off);
-    for (int l = 0; l < 12; ++l) {
-      if (!layer_used(l, res_dynamics)) {
-        p.L[l] = MlpLayer{nullptr, nullptr, 0, 0};
-        continue;
-      }
-      p.L[l] = MlpLayer{weights + w_off[l], weights + b_off[l], s[l].K, s[l].N};
-    }
+    kernel_layout(s, res_dynamics, lay_w, lay_b);
+    for (int l = 0; l < 12; ++l) shp[l] = s[l];
   }
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
   p.flags = h->lb_flags; p.epoch = h->epoch; p.diag = h->search_diag; p.fast = fast ? 1 : 0;
@@ -1261,6 +1299,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     LZM_HIP(hipMemset(h->phase, 0, 64 * sizeof(unsigned long long)));
   }
   p.phase = h->phase;
+  p.diag_mode = getenv("LZM_DIAG_MODE") ? atoi(getenv("LZM_DIAG_MODE")) : 0;  // timing experiments only
   p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
   // dynamic LDS plan (float offsets, 16-B aligned)
   size_t o = 0;
@@ -1270,11 +1309,15 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.off_meta = o; if (p.tree_in_lds) o += tree_floats;
   p.off_lut = o; if (p.tree_in_lds) o += round4((size_t)2 * h->lut_n);
   p.off_legal = o; if (p.tree_in_lds) o += round4((size_t)R * A + R);
+  p.off_val = o; if (p.tree_in_lds) o += round4((size_t)h->cap * R);
+  // pUCT visit table rows: all of lut when the triangle fits 32 KB (descent falls back to dividing)
+  p.pbt_rows = (p.tree_in_lds && (size_t)h->lut_n * (h->lut_n + 1) / 2 <= 8192) ? h->lut_n : 0;
+  p.off_pbt = o; o += round4((size_t)p.pbt_rows * (p.pbt_rows + 1) / 2);
   p.off_path = o; o += round4((size_t)h->depth_cap * R);
   p.off_pact = o; o += round4((size_t)h->depth_cap * R);
   // transposed activations [k][r], 4-float pad per kKC rows (tpos in lzm_search_mlp.h)
   auto tfl = [R](int K) { return (size_t)((K + kKC - 1) / kKC) * (kKC * R + 4); };
-  p.off_x0 = o; o += round4(tfl(p.L[0].K));  // [latent; one-hot] rows, zero-padded
+  p.off_x0 = o; o += round4(tfl(shp[0].K));  // [latent; one-hot] rows, zero-padded
   p.off_x1 = o; o += round4(tfl(H));          // also the policy logits [r][A]
   p.off_x2 = o; o += round4(tfl(H));
   p.off_n = o; o += round4(tfl(H));
@@ -1283,6 +1326,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.off_part = o;  // (unused: split-K partials meet through DPP)
   p.off_misc = o; o += round4((size_t)S + 32);  // staged seeds[S] + 16807^i table
   const size_t lds = o * sizeof(float);
+  build_schedule(p, shp, lay_w, lay_b, weights, res_dynamics, A, V);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_mlp: %zu B of LDS needed (network too wide)", lds);
     return LZM_ERR_ARG;

@@ -29,12 +29,23 @@
 
 namespace lzm {
 
-constexpr int kThreads = 512;  // 8 waves: two per SIMD, so one's memory wait hides under the other's FMAs
+#ifndef LZM_SEARCH_THREADS
+#define LZM_SEARCH_THREADS 512
+#endif
+// Threads per search workgroup: two waves per SIMD. With fewer lanes the wide layers need more
+// K-chunks per lane than the two-step prefetch holds in registers.
+constexpr int kThreads = LZM_SEARCH_THREADS;
 
-struct MlpLayer {
-  const float *w;  // kernel (swizzled) layout, see swz_source
-  const float *b;  // [N]
-  int K, N;        // K: inputs rounded up to kKC (zero rows)
+
+// One step of the network schedule, built on the host and read from the kernel arguments (scalar
+// loads, no LDS round trips): the layer (kernel layout, see swz_source), its lane split, and the LDS
+// float offsets of its input, output and residual.
+struct StepRec {
+  const float *w;  // lane-order weights, wbytes bytes
+  const float *b;  // bias [N]
+  int K, N, wbytes;  // K: inputs rounded up to kKC (zero rows)
+  int in, out, relu, resid, rowmajor, ldout, decode;  // resid < 0: none; decode 1 reward, 2 value
+  int Np, splits, cpl, log2s;                        // layer_split(K, N)
 };
 
 struct SearchArgs {
@@ -53,7 +64,6 @@ struct SearchArgs {
   float4 *minmax;         // [B]
   float *pool;            // [S+1][B][H]
   // network
-  MlpLayer L[12];
   int H, F, V, res;
   // parity-mode draw table and look-back
   const uint32_t *coef;  // [P][31]
@@ -67,10 +77,15 @@ struct SearchArgs {
   // optional per-simulation record (tests / tracing), may be null
   int32_t *rec_x, *rec_a, *rec_len;
   float *rec_dec, *rec_logits;
+  // network schedule (host-built)
+  StepRec sched[12];
+  int nsteps, stamp_at[4];
+  int diag_mode;  // timing experiments only (LZM_DIAG_MODE): 1 or 3 weight loads out of range, 2 no dense FMAs
   // dynamic LDS layout (float offsets)
   int tree_in_lds;
   size_t off_stat, off_meta, off_lut, off_legal, off_path, off_pact, off_x0, off_x1, off_x2, off_n, off_h, off_logit, off_part,
-      off_misc;
+      off_misc, off_val, off_pbt;
+  int pbt_rows;  // rows N of the pUCT visit table in LDS (0: none)
 };
 
 // ------------------------------------------------------------------------------ LDS helpers
@@ -81,10 +96,13 @@ __device__ inline float4 ld4(const float *p) { return *reinterpret_cast<const fl
 // than lanes, `splits` lanes share a column (whole kKC-chunks each) and reduce through LDS.
 // Each weight is read from L2 once per workgroup per simulation.
 constexpr int kKC = 16;        // K-chunk: weights a lane holds in registers per group of FMAs
-// chunks per lane loaded one step ahead (pre_chunks * kKC registers): fewer for wider R, whose
-// accumulators and input reads need the registers
+// Weight chunks per lane prefetched two schedule steps ahead into two register buffers: buffer A
+// serves the even steps (including step 0, the widest: [latent; one-hot] rows), buffer B the odd
+// ones. Wider R keeps fewer, its accumulators and input reads need the registers.
 template <int R>
-constexpr int pre_chunks() { return R <= 2 ? 3 : 2; }
+constexpr int pre_a() { return R == 1 ? 3 : (R == 2 ? 2 : 1); }
+template <int R>
+constexpr int pre_b() { return R == 1 ? 2 : 1; }
 typedef const __attribute__((address_space(1))) float *gfloat_p;    // global (not flat) loads
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) f32x4 *gfloat4_p;  // dwordx4 global loads
@@ -151,10 +169,6 @@ __host__ __device__ inline void swz_source(int K, int N, size_t d, int *k, int *
   }
 }
 
-// One entry of the layer schedule (LDS float offsets of input / output / residual).
-struct Step {
-  int layer, in, out, relu, resid, rowmajor, ldout, decode, Np, splits, cpl, log2s;
-};
 
 // chunk j of this lane: 4 float4 loads, lane stride nl (float4 units)
 __device__ __forceinline__ void load_chunk(gfloat4_p base, int nl, int lane, int j, float *w) {
@@ -171,7 +185,7 @@ __device__ __forceinline__ void load_chunk(gfloat4_p base, int nl, int lane, int
 template <int R>
 __device__ __forceinline__ int tpos(int k, int r) { return (k / kKC) * (kKC * R + 4) + (k % kKC) * R + r; }
 
-// acc[r] += sum_{j < kKC} inT[kb + j][r] * w[j], k ascending (one fmaf per term). Inputs are
+// acc[r] += sum_{j < kKC} inT[kb + j][r] * w[j] (R >= 2: k ascending, one fmaf per term). Inputs are
 // broadcast LDS reads: one float4 covers 4 / R consecutive k for R < 4, or half a k for R = 8.
 template <int R>
 __device__ __forceinline__ void fma_chunk(const float *inT, int kb, const float *w, float *acc) {
@@ -201,12 +215,15 @@ __device__ __forceinline__ void fma_chunk(const float *inT, int kb, const float 
       acc[0] = __fmaf_rn(a.z, w[j + 1], acc[0]); acc[1] = __fmaf_rn(a.w, w[j + 1], acc[1]);
     }
   } else {
+    // R = 1: four independent chains (k mod 4) instead of one 16-deep dependent chain
+    float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < kKC; j += 4) {
       const float4 a = ld4(cb + j);
-      acc[0] = __fmaf_rn(a.x, w[j], acc[0]); acc[0] = __fmaf_rn(a.y, w[j + 1], acc[0]);
-      acc[0] = __fmaf_rn(a.z, w[j + 2], acc[0]); acc[0] = __fmaf_rn(a.w, w[j + 3], acc[0]);
+      a4[0] = __fmaf_rn(a.x, w[j], a4[0]); a4[1] = __fmaf_rn(a.y, w[j + 1], a4[1]);
+      a4[2] = __fmaf_rn(a.z, w[j + 2], a4[2]); a4[3] = __fmaf_rn(a.w, w[j + 3], a4[3]);
     }
+    acc[0] += (a4[0] + a4[1]) + (a4[2] + a4[3]);
   }
 }
 
@@ -214,27 +231,46 @@ __device__ __forceinline__ void fma_chunk(const float *inT, int kb, const float 
 // after the previous step's FMAs, so the L2 round trip overlaps that step's barrier, reduction and
 // decode (and, for the first step of a simulation, the whole tree phase). Every register is
 // (re)defined on every path, so no stale value stays live across the schedule loop.
-template <int R>
-__device__ __forceinline__ void prefetch_step(const MlpLayer L, const Step &s, float *w, float &bias) {
-  constexpr int kPreChunks = pre_chunks<R>();
+// Buffer descriptor over `bytes` bytes at p, built from provably wave-uniform values.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *p, int bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+constexpr int kOOR = 0x7fffffff;  // out-of-range buffer offset: the load returns 0, no request
+
+template <int kPreChunks>
+__device__ __forceinline__ void prefetch_step(const StepRec &s, float *w, float &bias, bool diag_no_loads = false,
+                                              bool diag_skip = false) {
+  // Branch-free: every lane issues the same kPreChunks * 4 + 1 buffer loads; lanes (or chunks)
+  // without data use an out-of-range offset, which returns zeros without a memory request. A fixed
+  // load count per step lets s_waitcnt vmcnt wait for exactly the loads a step consumes while the
+  // next step's stay in flight.
   const int tid = threadIdx.x;
-  const int nl = s.splits ? s.Np * s.splits : (L.N < kThreads ? L.N : kThreads);
+  const int nl = s.splits ? s.Np * s.splits : (s.N < kThreads ? s.N : kThreads);
   const bool active = tid < nl;
-  const int nc = L.K / kKC;
+  const int nc = s.K / kKC;
   const int c0 = s.splits ? (tid & (s.splits - 1)) * s.cpl : 0;
   const int n = active ? min(s.cpl, nc - c0) : 0;
+  const __amdgpu_buffer_rsrc_t rw = wave_rsrc(s.w, diag_no_loads ? 0 : s.wbytes);
 #pragma unroll
   for (int c = 0; c < kPreChunks; ++c) {
-    if (c < n) {
-      load_chunk((gfloat4_p)L.w, nl, tid, c, w + c * kKC);
-    } else {
+    // no branch around the loads, even for chunk slots no lane has: a branch makes the load count
+    // path-dependent and the compiler then drains vmcnt conservatively (measured slower)
 #pragma unroll
-      for (int j = 0; j < kKC; ++j) w[c * kKC + j] = 0.0f;
+    for (int q = 0; q < 4; ++q) {
+      const int off = (c < n && !diag_skip) ? ((c * 4 + q) * nl + tid) * 16 : kOOR;
+      const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0);
+      w[c * kKC + 4 * q] = v.x; w[c * kKC + 4 * q + 1] = v.y; w[c * kKC + 4 * q + 2] = v.z;
+      w[c * kKC + 4 * q + 3] = v.w;
     }
   }
   const int col = s.splits ? tid >> s.log2s : tid;
   const bool lead = s.splits ? (tid & (s.splits - 1)) == 0 : true;  // adds the bias
-  bias = (active && lead && col < L.N) ? ((gfloat_p)L.b)[col] : 0.0f;
+  const __amdgpu_buffer_rsrc_t rb = wave_rsrc(s.b, s.N * 4);
+  bias = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rb, (active && lead && col < s.N) ? col * 4 : kOOR, 0, 0));
 }
 
 // acc += chunks [j0, j1) of this lane streamed from L2, double-buffered.
@@ -255,21 +291,16 @@ __device__ __forceinline__ void dot_stream(gfloat4_p base, int nl, int lane, int
 
 // acc += this lane's cnt chunks (k from kofs): the first pre_chunks from the prefetched w, the
 // rest streamed.
-template <int R>
+template <int R, int kPreChunks>
 __device__ __forceinline__ void dot_lane(gfloat4_p base, int nl, int lane, int cnt, int kofs, const float *inT,
                                          const float *w, float *acc) {
-  constexpr int kPreChunks = pre_chunks<R>();
   if (cnt > 0) fma_chunk<R>(inT, kofs, w, acc);
-  if (cnt > 1) fma_chunk<R>(inT, kofs + kKC, w + kKC, acc);
+  if (kPreChunks > 1 && cnt > 1) fma_chunk<R>(inT, kofs + kKC, w + kKC, acc);
   if (kPreChunks > 2 && cnt > 2) fma_chunk<R>(inT, kofs + 2 * kKC, w + 2 * kKC, acc);
+  static_assert(kPreChunks >= 1 && kPreChunks <= 3, "prefetch depth");
   if (cnt > kPreChunks) dot_stream<R>(base, nl, lane, kPreChunks, cnt, kofs, inT, acc);
 }
 
-// DPP lane exchange inside a row of 16 lanes.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
-}
 
 // Sum over each group of 2^log2s adjacent lanes (every lane of a group gets its group's sum):
 // quad_perm xor 1, xor 2, then row_half_mirror and row_mirror pair the quads and half-rows.
@@ -293,22 +324,23 @@ __device__ __forceinline__ void group_sum(float *acc, int log2s) {
   }
 }
 
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v = fmaxf(v, __shfl_xor(v, d, 64));
-  return v;
-}
+__device__ __forceinline__ float wave_max(float v) { return wave_max_dpp(v); }
+// sum over the wave (rows of 16 by DPP, then the four row sums by readlane); every lane gets it
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
+  v += dpp_f<0xB1>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0x141>(v);
+  v += dpp_f<0x140>(v);
+  return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
 }
 
 constexpr int kWaves = kThreads / 64;
+// column rounds of a wide layer whose support is decoded in registers (supports up to 1024)
+constexpr int kMaxRounds = (1024 + kThreads - 1) / kThreads;
 
 // out column c of a step: activation, residual, layout
 template <int R>
-__device__ __forceinline__ void store_col(const Step &s, float *out, const float *residT, int c, const float *v) {
+__device__ __forceinline__ void store_col(const StepRec &s, float *out, const float *residT, int c, const float *v) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     float x = v[r];
@@ -319,16 +351,16 @@ __device__ __forceinline__ void store_col(const Step &s, float *out, const float
 }
 
 // One schedule step: out = act(in . W + b) (+ resid) for the workgroup's R rows, from the lane's
-// prefetched weights `w`/`bias`; right after its FMAs it issues the next step's prefetch into the
-// same registers. Wide layers with `decode` never store their logits: the categorical support
+// prefetched weights `w`/`bias` (P chunks); right after its FMAs it issues the prefetch of step
+// `sn` (two steps on) into the same registers. Wide layers with `decode` never store their logits: the categorical support
 // expectation (scaling_transform.py:118-121: softmax, then sum p_j * (j - (V-1)/2)) is reduced
 // across the workgroup from registers and h^-1 applied (InverseScalarTransform), into dec_out[r].
 // `red`: 3 * kWaves * R floats of LDS. The caller's barrier follows.
-template <int R>
-__device__ __forceinline__ void dense_step(const MlpLayer L, const Step &s, float *smem_f, float *w, float &bias,
-                                          float *red, float *dec_out, int nr, const MlpLayer Ln, const Step &sn) {
+template <int R, int P>
+__device__ __forceinline__ void dense_step(const StepRec &s, float *smem_f, float *w, float &bias, float *red,
+                                          float *dec_out, int nr, const StepRec &sn, int diag = 0) {
   const int tid = threadIdx.x;
-  const int N = L.N;
+  const int N = s.N;
   const float *inT = smem_f + s.in;
   float *out = smem_f + s.out;
   const float *residT = s.resid >= 0 ? smem_f + s.resid : nullptr;
@@ -337,39 +369,47 @@ __device__ __forceinline__ void dense_step(const MlpLayer L, const Step &s, floa
   for (int r = 0; r < R; ++r) acc[r] = bias;
   if (s.splits == 0) {
     // wide layer (N >= kThreads): column tid from the prefetched registers, later rounds streamed
-    dot_lane<R>((gfloat4_p)L.w, kThreads, tid, s.cpl, 0, inT, w, acc);
-    float lg1[R];
-    bool has1 = false;
-    for (int u = 1; u * kThreads < N; ++u) {
-      const int c = u * kThreads + tid;
-      const int nu = N - u * kThreads < kThreads ? N - u * kThreads : kThreads;
-      if (c < N) {
-        float a2[R];
-        const float b = ((gfloat_p)L.b)[c];
+    if (diag != 2) dot_lane<R, P>((gfloat4_p)s.w, kThreads, tid, s.cpl, 0, inT, w, acc);
+    // later column rounds (logits kept in registers when decoding; unrolled: static indices)
+    float lg[kMaxRounds][R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) a2[r] = b;
-        dot_stream<R>((gfloat4_p)(L.w + (size_t)u * kThreads * L.K), nu, tid, 0, s.cpl, 0, inT, a2);
-        if (s.decode) {
+    for (int r = 0; r < R; ++r) lg[0][r] = acc[r];
 #pragma unroll
-          for (int r = 0; r < R; ++r) lg1[r] = a2[r];
-          has1 = true;
-        } else {
-          store_col<R>(s, out, residT, c, a2);
+    for (int u = 1; u < kMaxRounds; ++u) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) lg[u][r] = -INFINITY;
+      if (u * kThreads < N) {
+        const int c = u * kThreads + tid;
+        const int nu = N - u * kThreads < kThreads ? N - u * kThreads : kThreads;
+        if (c < N) {
+          float a2[R];
+          const float b = ((gfloat_p)s.b)[c];
+#pragma unroll
+          for (int r = 0; r < R; ++r) a2[r] = b;
+          dot_stream<R>((gfloat4_p)(s.w + (size_t)u * kThreads * s.K), nu, tid, 0, s.cpl, 0, inT, a2);
+          if (s.decode) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) lg[u][r] = a2[r];
+          } else {
+            store_col<R>(s, out, residT, c, a2);
+          }
         }
       }
     }
-    prefetch_step<R>(Ln, sn, w, bias);
+    prefetch_step<P>(sn, w, bias, diag == 1, diag == 3);
     if (!s.decode) {
       store_col<R>(s, out, residT, tid, acc);
       return;
     }
-    // ---- fused support decode (N <= 2 * kThreads, checked on the host)
+    // ---- fused support decode (N <= kMaxRounds * kThreads, checked on the host)
     const int wid = tid >> 6, lane = tid & 63;
-    float m[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      m[r] = wave_max(has1 ? fmaxf(acc[r], lg1[r]) : acc[r]);
-      if (lane == 0) red[wid * R + r] = m[r];
+      float m = lg[0][r];
+#pragma unroll
+      for (int u = 1; u < kMaxRounds; ++u) m = fmaxf(m, lg[u][r]);
+      m = wave_max(m);
+      if (lane == 0) red[wid * R + r] = m;
     }
     __syncthreads();
     const float half = (float)((N - 1) / 2);
@@ -377,12 +417,14 @@ __device__ __forceinline__ void dense_step(const MlpLayer L, const Step &s, floa
     for (int r = 0; r < R; ++r) {
       float M = red[r];
       for (int q = 1; q < kWaves; ++q) M = fmaxf(M, red[q * R + r]);
-      const float e0 = expf(acc[r] - M);
-      float se = e0, sj = e0 * ((float)tid - half);
-      if (has1) {
-        const float e1 = expf(lg1[r] - M);
-        se += e1;
-        sj += e1 * ((float)(tid + kThreads) - half);
+      float se = 0.0f, sj = 0.0f;
+#pragma unroll
+      for (int u = 0; u < kMaxRounds; ++u) {
+        if (u * kThreads + tid < N) {
+          const float e = expf(lg[u][r] - M);
+          se += e;
+          sj += e * ((float)(u * kThreads + tid) - half);
+        }
       }
       se = wave_sum(se);
       sj = wave_sum(sj);
@@ -400,15 +442,15 @@ __device__ __forceinline__ void dense_step(const MlpLayer L, const Step &s, floa
       }
       dec_out[tid] = h_inverse(sj / se);
     }
-    return;
+      return;
   }
   // split layer: groups of `splits` adjacent lanes per column, partial sums meet through DPP
   const int nl = s.Np << s.log2s;
   const int part = tid & (s.splits - 1), col = tid >> s.log2s;
   const int c0 = part * s.cpl;
-  const int cnt = min(s.cpl, L.K / kKC - c0);
-  if (tid < nl) dot_lane<R>((gfloat4_p)L.w, nl, tid, cnt, c0 * kKC, inT, w, acc);
-  prefetch_step<R>(Ln, sn, w, bias);
+  const int cnt = min(s.cpl, s.K / kKC - c0);
+  if (tid < nl && diag != 2) dot_lane<R, P>((gfloat4_p)s.w, nl, tid, cnt, c0 * kKC, inT, w, acc);
+  prefetch_step<P>(sn, w, bias, diag == 1, diag == 3);
   if (tid < nl) {
     group_sum<R>(acc, s.log2s);
     if (part == 0 && col < N) store_col<R>(s, out, residT, col, acc);
@@ -504,9 +546,6 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   __shared__ unsigned long long s_tmask[R];
   __shared__ float s_r[R], s_v[R];
   __shared__ float4 s_mm[R];
-  __shared__ MlpLayer s_L[12];
-  __shared__ Step s_step[12];
-  __shared__ int s_nsteps, s_stamp_at[4];
   __shared__ unsigned long long s_phase[64];
   __shared__ float s_red[3 * kWaves * R];
   if (p.phase && tid < 64) s_phase[tid] = 0ull;
@@ -533,6 +572,19 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       }
     }
     for (int e = tid; e < p.lut_n; e += kThreads) llut[e] = p.lut[e];
+    // caches replacing the descent's divisions (bit-identical: same operands, same IEEE division)
+    float *lval = smem + p.off_val;
+    for (int e = tid; e < p.cap * R; e += kThreads) {
+      const int node = e / R, li = e % R;
+      lval[e] = li < nr ? node_value(p.stat[(size_t)node * B + i0 + li]) : 0.0f;
+    }
+    float *lpbt = smem + p.off_pbt;
+    for (int n = 0; n < p.pbt_rows; ++n) {
+      const float y = p.lut[n].y;
+      for (int v = tid; v <= n; v += kThreads) lpbt[n * (n + 1) / 2 + v] = y / (float)(v + 1);
+    }
+    t.val = lval;
+    t.pbt = p.pbt_rows ? lpbt : nullptr;
     for (int e = tid; e < R * A; e += kThreads) llegal[e] = (e / A < nr) ? p.legal[(size_t)i0 * A + e] : 0;
     for (int e = tid; e < R; e += kThreads) llegal[R * A + e] = (e < nr) ? p.nlegal[i0 + e] : 0;
     t.stat = ls;
@@ -560,39 +612,6 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     for (int i = 0; i < B; ++i) m = max(m, p.vtp_in[i]);
     s_players = (m == -1) ? 1 : 2;
     s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int l = 0; l < 12; ++l) s_L[l] = p.L[l];
-    // layer schedule (LDS float offsets); layer 0 reads [latent; one-hot action] from X0
-    const int x0 = (int)p.off_x0, x1 = (int)p.off_x1, x2 = (int)p.off_x2, nl = (int)p.off_n, hd = (int)p.off_h,
-              lg = (int)p.off_logit;
-    int n = 0;
-    auto add = [&](int l, int in, int out, int relu, int resid, int rowmajor, int ldout, int dec) {
-      Step &q = s_step[n++];
-      q.layer = l; q.in = in; q.out = out; q.relu = relu; q.resid = resid; q.rowmajor = rowmajor; q.ldout = ldout;
-      q.decode = dec;
-      const Split sp = layer_split(p.L[l].K, p.L[l].N);
-      q.Np = sp.Np; q.splits = sp.splits; q.cpl = sp.cpl; q.log2s = sp.log2s;
-    };
-    add(0, x0, x1, 1, -1, 0, 0, 0);                   // fc_dynamics(_1)[0]
-    add(1, x1, nl, 1, p.res ? x0 : -1, 0, 0, 0);      // [1] (+ latent: res_connection_in_dynamics)
-    int enc = nl;
-    if (p.res) {
-      add(2, nl, x1, 1, -1, 0, 0, 0);                 // fc_dynamics_2
-      add(3, x1, x2, 1, -1, 0, 0, 0);
-      enc = x2;
-    }
-    s_stamp_at[0] = n - 1;
-    add(4, enc, hd, 1, -1, 0, 0, 0);                  // fc_reward_head
-    add(5, hd, lg, 0, -1, 1, p.V + 1, 1);
-    s_stamp_at[1] = n - 1;
-    add(6, nl, x1, 1, -1, 0, 0, 0);                   // fc_prediction_common
-    add(7, x1, x2, 1, -1, 0, 0, 0);
-    s_stamp_at[2] = n - 1;
-    add(8, x2, hd, 1, -1, 0, 0, 0);                   // fc_value_head
-    add(9, hd, lg, 0, -1, 1, p.V + 1, 2);
-    s_stamp_at[3] = n - 1;
-    add(10, x2, hd, 1, -1, 0, 0, 0);                  // fc_policy_head
-    add(11, hd, x1, 0, -1, 1, A, 0);
-    s_nsteps = n;
   }
   __syncthreads();
   const int players = s_players;
@@ -608,33 +627,38 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   float *X0 = smem + p.off_x0, *X1 = smem + p.off_x1, *NL = smem + p.off_n;
   float *LG = smem + p.off_logit;
   // this lane's weights for the next schedule step, loaded one step ahead (prefetch_step)
-  float wpre[pre_chunks<R>() * kKC], bpre = 0.0f;
-  prefetch_step<R>(s_L[s_step[0].layer], s_step[0], wpre, bpre);
+  // weight prefetch buffers: A for even schedule steps, B for odd (schedules have an even length)
+  float wA[pre_a<R>() * kKC], bA = 0.0f, wB[pre_b<R>() * kKC], bB = 0.0f;
+  prefetch_step<pre_a<R>()>(p.sched[0], wA, bA);
+  prefetch_step<pre_b<R>()>(p.sched[1], wB, bB);
 
   for (int k = 0; k < p.S; ++k) {
     const uint32_t seed = s_seeds[k];
     if (!p.fast) seed_state_parallel(seed, s_pow, s_z0);
-    // ---- selection
-    if (tid < nr) {
-      const int li = tid, i = i0 + li;
+    // ---- selection: wave w walks roots w, w + kWaves, ... (one lane per child, descend_wave)
+    for (int li = tid >> 6; li < nr; li += kWaves) {
+      const int i = i0 + li;
       const TreeView &tv = t;
       const int ti = tix(li);
+      const bool lead = (tid & 63) == 0;
       if (p.fast) {
         auto draw = [seed, i](int level) -> uint32_t {
           uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)i, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
           return o.x >> 1;
         };
-        Descent d = descend_slice<false, false>(tv, ti, li, R, s_mm[li], players, s_vtp[li], p.disc, draw, nullptr);
-        s_len[li] = d.len; s_x[li] = d.x; s_act[li] = d.action; s_status[li] = 0;
+        Descent d = descend_wave<false, false>(tv, ti, li, R, s_mm[li], players, s_vtp[li], p.disc, draw, nullptr);
+        if (lead) { s_len[li] = d.len; s_x[li] = d.x; s_act[li] = d.action; s_status[li] = 0; }
       } else {
         // classification pass: no draw values needed unless a tie involves an expanded child
         TieInfo ti_info;
         auto nodraw = [](int) -> uint32_t { return 0u; };
-        Descent d = descend_slice<false, true>(tv, ti, li, R, s_mm[li], players, s_vtp[li], p.disc, nodraw, &ti_info);
-        s_len[li] = d.len; s_x[li] = d.x; s_act[li] = d.action;
-        s_status[li] = ti_info.status;
-        s_tlevel[li] = ti_info.level;
-        s_tmask[li] = ti_info.mask;
+        Descent d = descend_wave<false, true>(tv, ti, li, R, s_mm[li], players, s_vtp[li], p.disc, nodraw, &ti_info);
+        if (lead) {
+          s_len[li] = d.len; s_x[li] = d.x; s_act[li] = d.action;
+          s_status[li] = ti_info.status;
+          s_tlevel[li] = ti_info.level;
+          s_tmask[li] = ti_info.mask;
+        }
       }
     }
     __syncthreads();
@@ -737,39 +761,47 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       X0[tpos<R>(h, r)] = v;
     }
     // one-hot action rows H .. K0 (layer 0's zero-padded input; muzero_model_mlp.py:188-190)
-    for (int e = tid; e < (s_L[0].K - H) * R; e += kThreads) {
+    for (int e = tid; e < (p.sched[0].K - H) * R; e += kThreads) {
       const int a = e / R, r = e % R;
       X0[tpos<R>(H + a, r)] = (r < nr && s_act[r] == a) ? 1.0f : 0.0f;
     }
     __syncthreads();
     LZM_STAMP(2);
     // ---- network (recurrent_inference, BN folded): muzero_model_mlp.py:179-204, :420-440
-    // One dense() instance walks the layer schedule (s_step): fc_dynamics(_1) (+ one-hot action,
+    // The schedule (p.sched) walks: fc_dynamics(_1) (+ one-hot action,
     // + residual), fc_dynamics_2, reward head (-> decode into s_r), fc_prediction_common, value
     // head (-> decode into s_v), policy head (-> logits [r][A] in X1).
-    for (int st = 0; st < s_nsteps; ++st) {
-      const Step q = s_step[st];
-      const MlpLayer L = s_L[q.layer];
-      unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
-      const int nx = (st + 1 < s_nsteps) ? st + 1 : 0;  // after the last step: the next simulation's first
-      dense_step<R>(L, q, smem, wpre, bpre, s_red, q.decode == 1 ? s_r : s_v, nr, s_L[s_step[nx].layer], s_step[nx]);
-      LZM_SUBSTAMP(16 + 4 * st);
-      __syncthreads();
-      LZM_SUBSTAMP(17 + 4 * st);
-      if (q.decode && q.splits) {  // narrow support (< kThreads): logits were stored to LG, one wave per row
-        const int wid = tid >> 6;
-        for (int r = wid; r < nr; r += kWaves) {
-          const float e = wave_expect_lds(LG + r * (p.V + 1), p.V);
-          if ((tid & 63) == 0) (q.decode == 1 ? s_r : s_v)[r] = h_inverse(e);
-        }
-        __syncthreads();
-      }
-      LZM_SUBSTAMP(18 + 4 * st);
-      if (st == s_stamp_at[0]) LZM_STAMP(3);
-      if (st == s_stamp_at[1]) LZM_STAMP(4);
-      if (st == s_stamp_at[2]) LZM_STAMP(5);
-      if (st == s_stamp_at[3]) LZM_STAMP(6);
+    // schedule, unrolled by two so each register buffer has a fixed place in the instruction
+    // stream: even steps consume buffer A, odd steps B; each refills its buffer for two steps on
+    // (wrapping into the next simulation's first two steps)
+#define LZM_NET_STEP(ST, W, BIAS, P)                                                                  \
+  do {                                                                                               \
+    const int st_ = (ST);                                                                            \
+    const StepRec &q = p.sched[st_];                                                                 \
+    unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;                         \
+    const int nx = st_ + 2 < p.nsteps ? st_ + 2 : st_ + 2 - p.nsteps;                               \
+    float *dec = q.decode == 1 ? s_r : s_v;                                                          \
+    dense_step<R, P>(q, smem, W, BIAS, s_red, dec, nr, p.sched[nx], p.diag_mode);                    \
+    LZM_SUBSTAMP(16 + 4 * st_);                                                                      \
+    __syncthreads();                                                                                 \
+    LZM_SUBSTAMP(17 + 4 * st_);                                                                      \
+    if (q.decode && q.splits) { /* narrow support (< kThreads): logits in LG, one wave per row */    \
+      for (int r = tid >> 6; r < nr; r += kWaves) {                                                  \
+        const float e = wave_expect_lds(LG + r * (p.V + 1), p.V);                                    \
+        if ((tid & 63) == 0) dec[r] = h_inverse(e);                                                  \
+      }                                                                                              \
+      __syncthreads();                                                                               \
+    }                                                                                                \
+    if (st_ == p.stamp_at[0]) LZM_STAMP(3);                                                          \
+    if (st_ == p.stamp_at[1]) LZM_STAMP(4);                                                          \
+    if (st_ == p.stamp_at[2]) LZM_STAMP(5);                                                          \
+    if (st_ == p.stamp_at[3]) LZM_STAMP(6);                                                          \
+  } while (0)
+    for (int st = 0; st < p.nsteps; st += 2) {
+      LZM_NET_STEP(st, wA, bA, pre_a<R>());
+      LZM_NET_STEP(st + 1, wB, bB, pre_b<R>());
     }
+#undef LZM_NET_STEP
     LZM_STAMP(7);
     // ---- file the new latents (mcts_ctree.py:305): pool[k+1][i][h] = NL[h][r]
     for (int e = tid; e < H * R; e += kThreads) {

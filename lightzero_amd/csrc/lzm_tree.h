@@ -44,6 +44,11 @@ struct TreeView {
   int32_t *pathlen;       // [B] edges of the last path
   const float2 *lut;      // [N] {log((N+base+1)/base)+init, sqrt(N)}
   int B, A, cap, lut_n, depth_cap;
+  // optional caches (the fused search keeps them in LDS; null elsewhere), bit-identical to the
+  // divisions they replace: val[node * B + i] = node_value(stat) kept current by expand/backup;
+  // pbt[N * (N + 1) / 2 + v] = lut[N].y / (v + 1) for child visits v <= N.
+  float *val = nullptr;
+  const float *pbt = nullptr;
 };
 
 __device__ inline size_t nidx(const TreeView &t, int node, int i) { return (size_t)node * t.B + i; }
@@ -112,7 +117,8 @@ __device__ inline Descent descend_slice(const TreeView &t, int i, int li, int ps
       if (c.visit > 0) {
         float tr = c.reward;
         if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
-        float qsa = tr + disc * node_value(c);
+        const float cv = t.val ? t.val[nidx(t, base + a, i)] : node_value(c);
+        float qsa = tr + disc * cv;
         total_q += qsa;
         total_v += 1;
       }
@@ -134,7 +140,7 @@ __device__ inline Descent descend_slice(const TreeView &t, int i, int li, int ps
       const int a = legal_at(t, i, node, j);
       const NodeStat c = t.stat[nidx(t, base + a, i)];
       float pb_c = L.x;
-      pb_c *= (L.y / (float)(c.visit + 1));
+      pb_c *= (t.pbt && c.visit <= N) ? t.pbt[N * (N + 1) / 2 + c.visit] : (L.y / (float)(c.visit + 1));
       const float prior_score = pb_c * c.prior;
       float vs;
       if (c.visit == 0) {
@@ -142,10 +148,11 @@ __device__ inline Descent descend_slice(const TreeView &t, int i, int li, int ps
       } else {
         float tr = c.reward;
         if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
+        const float cv = t.val ? t.val[nidx(t, base + a, i)] : node_value(c);
         if (players == 1)
-          vs = tr + disc * node_value(c);
+          vs = tr + disc * cv;
         else
-          vs = tr + disc * (-node_value(c));
+          vs = tr + disc * (-cv);
       }
       vs = mm_normalize(mm, vs);
       if (vs < 0) vs = 0;
@@ -207,6 +214,133 @@ __device__ inline Descent descend(const TreeView &t, int i, float4 mm, int playe
   return descend_slice<EZ, false>(t, i, i, t.B, mm, players, vtp, disc, draw, nullptr);
 }
 
+// DPP lane exchange inside a row of 16 lanes.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+// max over the wave (rows of 16 by DPP, then the four row results by readlane)
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
+
+// descend_slice with one whole wave per root, lane j scoring child j (legal position j), so a
+// level costs one round of child reads instead of a serial chain. Bit-identical to the serial
+// walk: the visited-children sum of compute_mean_q runs in child order (readlane loop), and the
+// order-dependent tie list of cselect_child (running max, reset on a strictly larger score, append
+// within 1e-6 of the running max) equals {r} + {j > r : score_j >= M - 1e-6}, where M is the
+// maximum score and r its first position: the running max only ever resets at the first position
+// reaching a new maximum, so the last reset is at r and from then on the running max is M.
+// Every lane returns the same Descent; lane 0 writes the path. All 64 lanes must call it.
+template <bool EZ, bool CLASSIFY, typename Draw>
+__device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps, float4 mm, int players, int vtp,
+                                       float disc, Draw draw, TieInfo *tie) {
+  const int lane = threadIdx.x & 63;
+  int node = 0, is_root = 1, len = 0, last_action = -1, parent = 0;
+  float parent_q = 0.0f;
+  NodeStat s = t.stat[nidx(t, 0, i)];
+  NodeMeta m = t.meta[nidx(t, 0, i)];
+  if (lane == 0) t.path[li] = 0;
+  if (CLASSIFY) tie->status = 0;
+  while (m.latent >= 0 && len < t.depth_cap - 1) {
+    const int n = legal_n(t, i, node);
+    const int base = 1 + t.A * m.latent;
+    const float pvp = s.reward;
+    const int preset = m.is_reset;
+    const bool valid = lane < n;
+    const int a = valid ? legal_at(t, i, node, lane) : 0;
+    NodeStat c;
+    float cv = 0.0f;
+    if (valid) {
+      c = t.stat[nidx(t, base + a, i)];
+      cv = t.val ? t.val[nidx(t, base + a, i)] : node_value(c);
+    } else {
+      c.visit = 0; c.value_sum = 0.0f; c.prior = 0.0f; c.reward = 0.0f;
+    }
+    float tr = c.reward;
+    if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
+    // compute_mean_q: visited children in legal order
+    const float qsa = tr + disc * cv;
+    uint64_t vis = __ballot(valid && c.visit > 0);
+    float total_q = 0.0f;
+    const int total_v = __popcll(vis);
+    for (uint64_t q = vis; q; q &= q - 1) total_q += readlane_f(qsa, __ffsll((long long)q) - 1);
+    float mean_q;
+    if (is_root && total_v > 0)
+      mean_q = total_q / (float)total_v;
+    else
+      mean_q = (parent_q + total_q) / (float)(total_v + 1);
+    is_root = 0;
+    parent_q = mean_q;
+    // cselect_child / cucb_score, every child at once
+    int N = s.visit - 1;
+    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
+    const float2 L = t.lut[N];
+    float pb_c = L.x;
+    pb_c *= (t.pbt && c.visit <= N) ? t.pbt[N * (N + 1) / 2 + c.visit] : (L.y / (float)(c.visit + 1));
+    const float prior_score = pb_c * c.prior;
+    float vs;
+    if (c.visit == 0)
+      vs = mean_q;
+    else
+      vs = (players == 1) ? tr + disc * cv : tr + disc * (-cv);
+    vs = mm_normalize(mm, vs);
+    if (vs < 0) vs = 0;
+    if (vs > 1) vs = 1;
+    const float score = prior_score + vs;
+    const float M = wave_max_dpp(valid ? score : -INFINITY);
+    const int r = __ffsll((long long)__ballot(valid && score == M)) - 1;
+    const uint64_t mask = __ballot(valid && lane > r && score >= M - 0.000001f) | (1ull << r);
+    const int nl = __popcll(mask);
+    if (CLASSIFY && nl > 1) {
+      const bool leaf_child = !((mask >> lane) & 1ull) || t.meta[nidx(t, base + a, i)].latent < 0;
+      const bool all_leaves = __ballot(!leaf_child) == 0ull;
+      if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+      tie->status = all_leaves ? 1 : 2;
+      tie->level = len;
+      tie->mask = mask;
+      Descent d;
+      d.len = len + 1;
+      d.x = m.latent;
+      d.action = -1;
+      d.vtp = vtp;
+      d.leaf = -1;
+      return d;
+    }
+    const uint32_t rr = CLASSIFY ? 0u : draw(len);
+    int k = (int)(rr % (uint32_t)nl);
+    uint64_t mm_ = mask;
+    for (; k > 0; --k) mm_ &= mm_ - 1;
+    const int jsel = __ffsll((long long)mm_) - 1;
+    const int action = __builtin_amdgcn_readlane(a, jsel);
+    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+    parent = node;
+    node = base + action;
+    last_action = action;
+    if (lane == 0) {
+      t.path_act[(size_t)len * ps + li] = action;
+      t.path[(size_t)(len + 1) * ps + li] = node;
+    }
+    ++len;
+    s = t.stat[nidx(t, node, i)];
+    m = t.meta[nidx(t, node, i)];
+  }
+  Descent d;
+  d.len = len;
+  d.x = t.meta[nidx(t, parent, i)].latent;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
 
 // CNode::expand of a non-root leaf (cnode.cpp:83-147): all A actions legal, masked-softmax
 // priors with glibc expf, sequential sum; children reset to CNode(prior, {}).
@@ -238,6 +372,7 @@ __device__ inline void expand_leaf(const TreeView &t, int i, int leaf, int to_pl
     cm.best = -1;
     cm.is_reset = 0;
     t.meta[nidx(t, base + a, i)] = cm;
+    if (t.val) t.val[nidx(t, base + a, i)] = 0.0f;
   }
 }
 
@@ -260,6 +395,7 @@ __device__ inline void backup_slice(const TreeView &t, int i, int li, int ps, fl
     s.visit += 1;
     t.stat[nidx(t, node, i)] = s;
     const float v = node_value(s);
+    if (t.val) t.val[nidx(t, node, i)] = v;
     if (!EZ) {
       const float tr = s.reward;
       float q;
