@@ -12,8 +12,10 @@ independent trees: weak scaling, no collective in the data path). value = all ra
 slowest rank's time.
 
 Extra objects on the JSON line:
-  roofline     - dominant HIP kernel of the step, algorithmic bytes per launch / its live
-                 HIP-event duration vs the HBM peak (profiles/ holds the matching rocprof stats)
+  roofline     - dominant HIP kernel of the step: algorithmic work per launch / its live HIP-event
+                 duration vs the peak (fused: fp32 FLOPs vs the dense fp32 peak, plus the L2 weight
+                 stream; generic: bytes vs HBM); traffic = PMC HBM bytes per launch from the committed
+                 profile (profiles/pmc_latest.json); profiles/ holds the matching rocprof stats
   cpu_baseline - the oracle's CPU restatement of the reference ctree driving the same network on
                  the host cores (the reference's architecture with device='cpu'), bounded sample.
 """
@@ -32,6 +34,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (matrix = vector rate on gfx950, MI355X_MICROARCH.md)
+L2_PEAK_TBS = 34.5  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -157,6 +160,52 @@ def mlp_flops_per_sim(H, A, F, V, res=True):
     return 2 * mac
 
 
+def shard_seed(rank):
+    """Each rank searches its own envs: per-rank synthetic inputs and traverse seeds."""
+    return 1000 + rank
+
+
+def slowest_rank_seconds(elapsed, world, device):
+    """The job's time is the slowest rank's (max-reduce; the only collective: envs are
+    independent trees, nothing crosses ranks in the data path)."""
+    if world == 1:
+        return elapsed
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def whole_job_rate(B, S, steps, world, seconds):
+    """Simulations of all ranks (B envs x S sims per rank per step) per second."""
+    return world * B * S * steps / seconds
+
+
+def roots_per_workgroup(B, device):
+    """The library's choice (lzm_kernels.hip roots_per_wg): smallest of 1, 2, 4, 8 that fits one
+    workgroup per CU; LZM_ROOTS_PER_WG overrides."""
+    env = os.environ.get("LZM_ROOTS_PER_WG")
+    if env in ("1", "2", "4", "8"):
+        return int(env)
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    return next((r for r in (1, 2, 4) if -(-B // r) <= cus), 8)
+
+
+def _lib_kernel_floats(H=128, A=2, F=32, V=601, res=1):
+    from lightzero_amd import _lib
+    return int(_lib.load().lzm_mlp_kernel_floats(H, A, F, V, res))
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch from the committed PMC pass (profiles/pmc_latest.json, written by
+    tools/profile_round.sh on the GPU box): 2 x FETCH_SIZE + WRITE_SIZE, or None."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    return d.get("traffic_bytes") if kernel.split("<")[0] in d.get("kernel", "") else None
+
+
 def algorithmic_bytes(B, A, H, V, dbar):
     """Bytes each kernel must move per launch (this layout: 16-B node records).
     traverse: per level the parent's stat+meta records (32 B) and A child stat records (16 A),
@@ -221,7 +270,7 @@ def main():
     torch.cuda.set_device(device)
     B, S = args.envs, args.sims
     model = build_model(device, args.zero_heads, seed=0)
-    step = GpuStep(B, S, model, device, args.rng, args.graph, seed=1000 + rank, fused=args.path == "fused")
+    step = GpuStep(B, S, model, device, args.rng, args.graph, seed=shard_seed(rank), fused=args.path == "fused")
 
     for _ in range(args.warmup):
         step()
@@ -235,13 +284,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    sims = world * B * S * args.steps
-    value = sims / el
+    el = slowest_rank_seconds(time.perf_counter() - t0, world, device)
+    value = whole_job_rate(B, S, args.steps, world, el)
 
     # sanity: every root received exactly S visits
     dsum = step.last[0].sum(dim=1)
@@ -252,16 +296,24 @@ def main():
     if rank == 0:
         ms, dbar = kernel_timing(step)
         if "search_mlp" in ms:
-            # fused whole-search kernel: one launch = B x S simulations; fp32 FMA network dominates
+            # fused whole-search kernel: one launch = B x S simulations; its algorithmic work is the
+            # fp32 network (the launch is a chain of S dependent simulations, so neither
+            # peak bounds it; the L2 weight stream is reported beside)
             flops = B * S * mlp_flops_per_sim(128, 2, 32, 601)
             hbm = B * (S * 8 * 128 + 2 * 32 * (1 + 2 * (S + 1)))  # latent gather+file per sim, tree slice in/out
             sec = ms["search_mlp"] * 1e-3
             achieved = flops / sec / 1e12
+            R = roots_per_workgroup(B, device)
+            wbytes = 4 * _lib_kernel_floats()
+            l2 = -(-B // R) * S * wbytes  # every workgroup streams the kernel-layout weights once per simulation
             roofline = {"bound": "mfma", "kernel": "search_mlp_kernel", "achieved": round(achieved, 3),
                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-                        "traffic": None, "alg_flops_per_launch": int(flops), "alg_hbm_bytes_per_launch": int(hbm),
-                        "hbm_achieved_GBs": round(hbm / sec / 1e9, 2), "launch_us": round(ms["search_mlp"] * 1e3, 1),
-                        "sims_per_launch": B * S, "mean_search_len": round(dbar, 3)}
+                        "traffic": pmc_traffic("search_mlp_kernel"), "alg_flops_per_launch": int(flops),
+                        "alg_hbm_bytes_per_launch": int(hbm), "hbm_achieved_GBs": round(hbm / sec / 1e9, 2),
+                        "l2_weight_bytes_per_launch": int(l2), "l2_achieved_TBs": round(l2 / sec / 1e12, 3),
+                        "l2_peak_TBs": L2_PEAK_TBS, "roots_per_workgroup": R,
+                        "launch_us": round(ms["search_mlp"] * 1e3, 1), "sims_per_launch": B * S,
+                        "mean_search_len": round(dbar, 3)}
         else:
             byt = algorithmic_bytes(B, 2, 128, 601, dbar)
             dom = max(ms, key=lambda k: ms[k])
