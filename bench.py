@@ -49,6 +49,9 @@ def parse():
                    help="fused: one lzm_search_mlp launch per search; generic: HIP tree kernels around the "
                         "PyTorch network (any model)")
     p.add_argument("--graph", type=int, default=1, help="generic path: replay each search as one HIP graph")
+    p.add_argument("--step", choices=["graph", "python"], default="graph",
+                   help="graph: the collect-time search pass as one HIP graph (lightzero_amd.collect."
+                        "DeviceSearchStep); python: the same sequence driven call by call from Python")
     p.add_argument("--cpu-baseline-secs", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--zero-heads", action="store_true", help="reference zero-init last layers (all-tie search)")
@@ -71,8 +74,29 @@ def build_model(device, zero_heads, seed):
     return m.to(device).eval()
 
 
+class GraphStep:
+    """One collect-time search pass (muzero.py:617-690) as one HIP graph (DeviceSearchStep):
+    initial_inference -> Roots.prepare (noise) -> fused search -> distributions / values; the
+    traverse seeds advance on the device every replay."""
+
+    def __init__(self, B, S, model, device, rng_mode, seed):
+        from lightzero_amd.collect import DeviceSearchStep
+        rng = np.random.default_rng(seed)
+        self.B, self.S = B, S
+        self.step = DeviceSearchStep(model, B, S, [[0, 1]] * B, (4,), device, noise_weight=0.25, seed=seed,
+                                     rng_mode=rng_mode, graph=True)
+        self.step.set_inputs(obs=torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32)).to(device),
+                             noises=torch.from_numpy(rng.dirichlet([0.3, 0.3], size=B).astype(np.float32)).to(device))
+        self.mcts = self.step.mcts
+        self.last = None
+
+    def __call__(self):
+        out = self.step.step()
+        self.last = (out["distributions"], out["values"], None)
+
+
 class GpuStep:
-    """One collect-time search pass (muzero.py:660-690) on the GPU drop-in."""
+    """One collect-time search pass (muzero.py:660-690) on the GPU drop-in, driven from Python."""
 
     def __init__(self, B, S, model, device, rng_mode, graph, seed, fused=True):
         from lightzero_amd.mcts_ctree import MuZeroMCTSCtree
@@ -132,9 +156,11 @@ def kernel_timing(step, n_search=3):
     for n in names:
         setattr(mc.DeviceTree, n, timed(n, orig[n]))
     mcts.record = True
+    # a graph replay runs no Python: time the captured body eagerly (same kernels, same inputs)
+    run = step.step._body if isinstance(step, GraphStep) else step
     try:
         for _ in range(n_search):
-            step()
+            run()
             if mcts.last_record is not None and not acc["traverse"]:
                 depth.append(mcts.last_record.search_len.clone())
         torch.cuda.synchronize()
@@ -270,7 +296,10 @@ def main():
     torch.cuda.set_device(device)
     B, S = args.envs, args.sims
     model = build_model(device, args.zero_heads, seed=0)
-    step = GpuStep(B, S, model, device, args.rng, args.graph, seed=shard_seed(rank), fused=args.path == "fused")
+    if args.path == "fused" and args.step == "graph":
+        step = GraphStep(B, S, model, device, args.rng, seed=shard_seed(rank))
+    else:
+        step = GpuStep(B, S, model, device, args.rng, args.graph, seed=shard_seed(rank), fused=args.path == "fused")
 
     for _ in range(args.warmup):
         step()
@@ -338,7 +367,8 @@ def main():
                 "config": {"workload": "CartPole-v0 MuZero search, MuZeroModelMLP (latent 128, support 601), "
                                        f"{B} envs x {S} sims per GPU",
                            "global_batch": world * B, "num_simulations": S, "rng": args.rng,
-                           "path": args.path, "hip_graph": bool(args.graph) and args.path == "generic",
+                           "path": args.path,
+                           "hip_graph": (args.step == "graph") if args.path == "fused" else bool(args.graph),
                            "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
                 "roofline": roofline, "cpu_baseline": cpu}

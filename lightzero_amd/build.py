@@ -9,9 +9,13 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("LZM_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no fused multiply-add anywhere in the tree kernels, so every fp32
 # expression rounds like the reference's SSE build; division and sqrt stay IEEE (HIP default).
-FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-Wall", f"--offload-arch={ARCH}"]
+# -fno-slp-vectorize: no v_pk_fma_f32 pairing in the fused search's dense layers — its operand
+# pairs cost ~3 v_mov each (measured: ~370 -> ~75 moves per network step).
+FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC", "-shared", "-Wall",
+         f"--offload-arch={ARCH}"]
 SOURCES = [os.path.join(HERE, "csrc", "lzm_kernels.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", "lzm_numerics.h"), os.path.join(REPO, "include", "lzmcts.h")]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", h) for h in ("lzm_numerics.h", "lzm_tree.h", "lzm_search_mlp.h")] + [
+    os.path.join(REPO, "include", "lzmcts.h")]
 OUT = os.path.join(HERE, "liblzmcts.so")
 
 

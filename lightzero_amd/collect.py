@@ -1,0 +1,100 @@
+"""Device-resident collect-time search step (first piece).
+
+MuZeroPolicy._forward_collect (lzero/policy/muzero.py:617-690) runs, per env step:
+initial_inference -> Roots.prepare (Dirichlet-mixed root priors) -> MuZeroMCTSCtree.search ->
+get_distributions / get_values. `DeviceSearchStep` runs exactly that sequence on device tensors
+and captures it as ONE HIP graph, so a step costs one graph launch: no Python glue, no host copies
+between the network, the root preparation and the fused search. The traverse seeds (the
+reference's per-call srand(tv_usec) values) are derived on the device from a replay counter,
+usec_k = (1000003 * seed + n) mod 10^6 for the n-th traverse of the run (the SequentialSeeds rule
+of tests and bench), so every replay is a fresh search.
+
+Inputs are static device buffers the caller refills before `step()` (obs, Dirichlet noises,
+to_play); outputs are static device tensors overwritten by each step (visit counts per legal
+action, root values, root latents and policy logits).
+"""
+import torch
+
+from .mcts_ctree import MuZeroMCTSCtree
+from .utils import EasyDict
+
+
+class DeviceSearchStep:
+    def __init__(self, model, num_envs, num_simulations, legal_actions, obs_shape, device, noise_weight=0.25,
+                 discount_factor=0.997, support_scale=300, seed=0, rng_mode="glibc", graph=True, cfg_extra=None):
+        self.model = model.eval()
+        self.B, self.S = int(num_envs), int(num_simulations)
+        self.device = torch.device(device)
+        self.noise_weight = float(noise_weight)
+        cfg = dict(num_simulations=self.S, discount_factor=float(discount_factor), device=self.device,
+                   model=dict(support_scale=int(support_scale), categorical_distribution=True))
+        cfg.update(cfg_extra or {})
+        self.mcts_cls = MuZeroMCTSCtree
+        self.rng_mode = rng_mode
+        self.mcts = MuZeroMCTSCtree(EasyDict(cfg))
+        self.legal = [list(l) for l in legal_actions]
+        self.A = max(len(l) for l in self.legal)
+        dev = self.device
+        self.obs = torch.zeros((self.B,) + tuple(obs_shape), dtype=torch.float32, device=dev)
+        self.noises = torch.zeros((self.B, self.A), dtype=torch.float32, device=dev)
+        self.to_play = torch.full((self.B,), -1, dtype=torch.int32, device=dev)
+        self.rewards = torch.zeros(self.B, dtype=torch.float32, device=dev)
+        self._count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._base = (1000003 * int(seed)) % 1000000
+        self._ar = torch.arange(self.S, dtype=torch.int64, device=dev)
+        self.graph = None
+        self.use_graph = bool(graph)
+        self.roots = None
+        self.out = None
+
+    def set_inputs(self, obs=None, noises=None, to_play=None):
+        if obs is not None:
+            self.obs.copy_(obs)
+        if noises is not None:
+            self.noises.copy_(noises)
+        if to_play is not None:
+            self.to_play.copy_(to_play)
+
+    def _body(self):
+        with torch.no_grad():
+            old = self.mcts_cls.rng_mode
+            self.mcts_cls.rng_mode = self.rng_mode
+            try:
+                if self.roots is None:
+                    self.roots = self.mcts_cls.roots(self.B, self.legal)
+                out = self.model.initial_inference(self.obs)
+                seeds = ((self._base + self._count * self.S + self._ar) % 1000000).to(torch.int32)
+                self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
+                                          self.to_play)
+                self.mcts.search(self.roots, self.model, out.latent_state, self.to_play, seeds=seeds)
+                t = self.roots.tree
+                dist, values = t.distributions(), t.values()
+                self._count.add_(1)
+                return dict(distributions=dist, values=values, latent_state=out.latent_state,
+                            policy_logits=out.policy_logits)
+            finally:
+                self.mcts_cls.rng_mode = old
+
+    def step(self):
+        """One collect-time search pass over the current inputs; returns the static output dict."""
+        if not self.use_graph:
+            self.out = self._body()
+            return self.out
+        if self.graph is None:
+            # warm-up outside capture: allocations (tree handle, glibc tables, packed weights,
+            # torch workspaces) happen here, so the captured body is launch-only
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    self._body()
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._count.zero_()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = self._body()
+        self.graph.replay()
+        return self.out
+
+    def reset_seed_counter(self):
+        self._count.zero_()

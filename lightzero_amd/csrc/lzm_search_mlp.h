@@ -364,14 +364,16 @@ __device__ __forceinline__ void dense_step(const StepRec &s, float *smem_f, floa
   const float *inT = smem_f + s.in;
   float *out = smem_f + s.out;
   const float *residT = s.resid >= 0 ? smem_f + s.resid : nullptr;
+  const bool wide = s.splits == 0;
   float acc[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) acc[r] = bias;
-  if (s.splits == 0) {
-    // wide layer (N >= kThreads): column tid from the prefetched registers, later rounds streamed
+  float lg[kMaxRounds][R];  // wide + decode: logits of this lane's column rounds, static indices
+  const int nl = wide ? kThreads : (s.Np << s.log2s);
+  const int part = wide ? 0 : tid & (s.splits - 1), col = wide ? tid : tid >> s.log2s;
+  // ---- FMAs (the prefetched registers are only read here)
+  if (wide) {
     if (diag != 2) dot_lane<R, P>((gfloat4_p)s.w, kThreads, tid, s.cpl, 0, inT, w, acc);
-    // later column rounds (logits kept in registers when decoding; unrolled: static indices)
-    float lg[kMaxRounds][R];
 #pragma unroll
     for (int r = 0; r < R; ++r) lg[0][r] = acc[r];
 #pragma unroll
@@ -396,64 +398,65 @@ __device__ __forceinline__ void dense_step(const StepRec &s, float *smem_f, floa
         }
       }
     }
-    prefetch_step<P>(sn, w, bias, diag == 1, diag == 3);
-    if (!s.decode) {
-      store_col<R>(s, out, residT, tid, acc);
-      return;
-    }
-    // ---- fused support decode (N <= kMaxRounds * kThreads, checked on the host)
-    const int wid = tid >> 6, lane = tid & 63;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float m = lg[0][r];
-#pragma unroll
-      for (int u = 1; u < kMaxRounds; ++u) m = fmaxf(m, lg[u][r]);
-      m = wave_max(m);
-      if (lane == 0) red[wid * R + r] = m;
-    }
-    __syncthreads();
-    const float half = (float)((N - 1) / 2);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      float M = red[r];
-      for (int q = 1; q < kWaves; ++q) M = fmaxf(M, red[q * R + r]);
-      float se = 0.0f, sj = 0.0f;
-#pragma unroll
-      for (int u = 0; u < kMaxRounds; ++u) {
-        if (u * kThreads + tid < N) {
-          const float e = expf(lg[u][r] - M);
-          se += e;
-          sj += e * ((float)(u * kThreads + tid) - half);
-        }
-      }
-      se = wave_sum(se);
-      sj = wave_sum(sj);
-      if (lane == 0) {
-        red[(kWaves + wid) * R + r] = se;
-        red[(2 * kWaves + wid) * R + r] = sj;
-      }
-    }
-    __syncthreads();
-    if (tid < nr) {
-      float se = 0.0f, sj = 0.0f;
-      for (int q = 0; q < kWaves; ++q) {
-        se += red[(kWaves + q) * R + tid];
-        sj += red[(2 * kWaves + q) * R + tid];
-      }
-      dec_out[tid] = h_inverse(sj / se);
-    }
-      return;
+  } else {
+    const int cnt = min(s.cpl, s.K / kKC - part * s.cpl);
+    if (tid < nl && diag != 2) dot_lane<R, P>((gfloat4_p)s.w, nl, tid, cnt, part * s.cpl * kKC, inT, w, acc);
   }
-  // split layer: groups of `splits` adjacent lanes per column, partial sums meet through DPP
-  const int nl = s.Np << s.log2s;
-  const int part = tid & (s.splits - 1), col = tid >> s.log2s;
-  const int c0 = part * s.cpl;
-  const int cnt = min(s.cpl, s.K / kKC - c0);
-  if (tid < nl && diag != 2) dot_lane<R, P>((gfloat4_p)s.w, nl, tid, cnt, c0 * kKC, inT, w, acc);
+  // ---- the next-but-one step's weights: ONE definition point of the register buffer per step, so
+  // the loop-carried registers need no copies at control-flow joins
   prefetch_step<P>(sn, w, bias, diag == 1, diag == 3);
-  if (tid < nl) {
-    group_sum<R>(acc, s.log2s);
-    if (part == 0 && col < N) store_col<R>(s, out, residT, col, acc);
+  // ---- epilogue
+  if (!wide) {
+    if (tid < nl) {
+      group_sum<R>(acc, s.log2s);
+      if (part == 0 && col < N) store_col<R>(s, out, residT, col, acc);
+    }
+    return;
+  }
+  if (!s.decode) {
+    store_col<R>(s, out, residT, tid, acc);
+    return;
+  }
+  // fused support decode (N <= kMaxRounds * kThreads, checked on the host)
+  const int wid = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float m = lg[0][r];
+#pragma unroll
+    for (int u = 1; u < kMaxRounds; ++u) m = fmaxf(m, lg[u][r]);
+    m = wave_max(m);
+    if (lane == 0) red[wid * R + r] = m;
+  }
+  __syncthreads();
+  const float half = (float)((N - 1) / 2);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float M = red[r];
+    for (int q = 1; q < kWaves; ++q) M = fmaxf(M, red[q * R + r]);
+    float se = 0.0f, sj = 0.0f;
+#pragma unroll
+    for (int u = 0; u < kMaxRounds; ++u) {
+      if (u * kThreads + tid < N) {
+        const float e = expf(lg[u][r] - M);
+        se += e;
+        sj += e * ((float)(u * kThreads + tid) - half);
+      }
+    }
+    se = wave_sum(se);
+    sj = wave_sum(sj);
+    if (lane == 0) {
+      red[(kWaves + wid) * R + r] = se;
+      red[(2 * kWaves + wid) * R + r] = sj;
+    }
+  }
+  __syncthreads();
+  if (tid < nr) {
+    float se = 0.0f, sj = 0.0f;
+    for (int q = 0; q < kWaves; ++q) {
+      se += red[(kWaves + q) * R + tid];
+      sj += red[(2 * kWaves + q) * R + tid];
+    }
+    dec_out[tid] = h_inverse(sj / se);
   }
 }
 

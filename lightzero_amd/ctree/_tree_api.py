@@ -122,19 +122,20 @@ class _RootsBase:
         B = self.root_num
         A = logits.shape[-1]
         t = self._acquire(A, logits.device)
-        rows = self.legal_actions_list[:B]
-        if all(len(l) == A for l in rows):
-            legal = np.asarray(rows, dtype=np.int32).reshape(B, A)
-            count = np.full(B, A, np.int32)
-        else:
+        dev = logits.device
+        key = (A, str(dev))
+        if getattr(self, "_legal_dev_key", None) != key:
+            # the legal lists are fixed per Roots object: upload once (no host copy on later calls,
+            # so the call can be captured in a HIP graph)
+            rows = self.legal_actions_list[:B]
             legal = np.full((B, A), -1, np.int32)
             count = np.zeros(B, np.int32)
             for i, l in enumerate(rows):
                 legal[i, :len(l)] = l
                 count[i] = len(l)
-        dev = logits.device
-        legal = torch.from_numpy(legal).to(dev)
-        count = torch.from_numpy(count).to(dev)
+            self._legal_dev = (torch.from_numpy(legal).to(dev), torch.from_numpy(count).to(dev))
+            self._legal_dev_key = key
+        legal, count = self._legal_dev
         t.prepare(legal, count,
                   None if noises is None else noises.to(dev, torch.float32).contiguous(), _f32(root_noise_weight),
                   rewards.to(dev, torch.float32).contiguous(), logits.to(dev, torch.float32).contiguous(),

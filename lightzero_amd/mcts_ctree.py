@@ -165,7 +165,10 @@ class MuZeroMCTSCtree(object):
                               out_decoded=None if rec is None else rec.decoded[k])
 
     def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
-               to_play_batch: Union[int, List[Any]]) -> None:
+               to_play_batch: Union[int, List[Any]], seeds: torch.Tensor = None) -> None:
+        """seeds (not in the reference): optional device int32 [num_simulations] traverse seeds
+        (the srand(tv_usec) values, uint32 bits) instead of the host seed source — keeps the call
+        free of host copies (HIP-graph capture, lightzero_amd.collect)."""
         with torch.no_grad():
             model.eval()
             t = roots.tree
@@ -181,7 +184,7 @@ class MuZeroMCTSCtree(object):
             buf = self._buf.get(B, S, shape, dev)
             buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
-            buf.seeds.copy_(_seeds(S, dev))
+            buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
             rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
             if rec is not None:
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
