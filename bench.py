@@ -151,7 +151,7 @@ def kernel_timing(step, n_search=3):
                 depth.append(self.search_len.clone())
         return w
 
-    use_graph = mcts._cfg.use_hip_graph
+    use_graph = mcts._cfg.get("use_hip_graph", False)
     mcts._cfg.use_hip_graph = False
     for n in names:
         setattr(mc.DeviceTree, n, timed(n, orig[n]))

@@ -817,20 +817,18 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       for (int a = 0; a < A; ++a) p.rec_logits[((size_t)k * B + i0 + tid) * A + a] = X1[tid * A + a];
     }
     LZM_STAMP(8);
-    // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500)
-    if (tid < nr) {
-      const int li = tid;
+    // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500): wave w takes root w, one lane
+    // per child (expand) and per path level (backup)
+    for (int li = tid >> 6; li < nr; li += kWaves) {
       const TreeView &tv = t;
       const int ti = tix(li);
       const int len = s_len[li];
-      // best_action along the final path (cnode.cpp:806)
-      for (int l = 0; l < len; ++l) tv.meta[nidx(tv, tv.path[l * R + li], ti)].best = tv.path_act[l * R + li];
       const int leaf = tv.path[len * R + li];
       int vtp = s_vtp[li];
       if (players > 1)
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
-      expand_leaf(tv, ti, leaf, vtp, k + 1, s_r[li], X1 + li * A, 0, false);
-      backup_slice<false>(tv, ti, li, R, &s_mm[li], vtp, s_v[li], p.disc);
+      expand_wave(tv, ti, leaf, vtp, k + 1, s_r[li], X1 + li * A);
+      backup_wave(tv, ti, li, R, &s_mm[li], vtp, s_v[li], p.disc);
     }
     __syncthreads();
     LZM_STAMP(9);

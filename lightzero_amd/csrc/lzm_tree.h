@@ -435,6 +435,104 @@ __device__ inline void backup(const TreeView &t, int i, float4 *mm_ptr, int to_p
   backup_slice<EZ>(t, i, i, t.B, mm_ptr, to_play, value, disc);
 }
 
+// expand_leaf with one lane per child (MuZero; all 64 lanes of the wave call it, A <= 64).
+// Bit-identical: pmax is a max (order-free), the prior denominator is summed in action order by a
+// readlane chain, every other quantity is per child.
+__device__ inline void expand_wave(const TreeView &t, int i, int leaf, int to_play, int latent, float reward,
+                                   const float *logits) {
+  const int lane = threadIdx.x & 63;
+  const int A = t.A;
+  if (lane == 0) {
+    NodeMeta m = t.meta[nidx(t, leaf, i)];
+    m.latent = latent;
+    m.to_play = to_play;
+    t.meta[nidx(t, leaf, i)] = m;
+    t.stat[nidx(t, leaf, i)].reward = reward;
+  }
+  const bool act = lane < A;
+  const float lg = act ? logits[lane] : -INFINITY;
+  const float pmax = fmaxf(kFloatMin, wave_max_dpp(lg));
+  const float e = act ? glibc_expf(lg - pmax) : 0.0f;
+  float sum = 0.0f;
+  for (int a = 0; a < A; ++a) sum += readlane_f(e, a);
+  if (act) {
+    const int c = 1 + A * latent + lane;
+    NodeStat cs;
+    cs.visit = 0;
+    cs.value_sum = 0.0f;
+    cs.prior = e / sum;
+    cs.reward = 0.0f;
+    t.stat[nidx(t, c, i)] = cs;
+    NodeMeta cm;
+    cm.latent = -1;
+    cm.to_play = 0;
+    cm.best = -1;
+    cm.is_reset = 0;
+    t.meta[nidx(t, c, i)] = cm;
+    if (t.val) t.val[nidx(t, c, i)] = 0.0f;
+  }
+}
+
+// backup_slice<false> with one lane per path level (all 64 lanes call it). The bootstrap value is
+// the only serial quantity: it runs leaf to root in registers (readlane chain, the reference's
+// exact operation order), then every level updates its node, value cache and q in parallel; the
+// min-max update is an order-free max / min (exact). Paths longer than 64 levels take several
+// rounds. Also writes best_action along the path (cnode.cpp:806).
+__device__ inline void backup_wave(const TreeView &t, int i, int li, int ps, float4 *mm_ptr, int to_play, float value,
+                                   float disc) {
+  const int lane = threadIdx.x & 63;
+  const int len = t.pathlen[li];
+  for (int l = lane; l < len; l += 64)
+    t.meta[nidx(t, t.path[(size_t)l * ps + li], i)].best = t.path_act[(size_t)l * ps + li];
+  float b = value;  // wave-uniform chain value
+  float qmax = -INFINITY, qmin = INFINITY;
+  for (int g0 = len; g0 >= 0; g0 -= 64) {
+    const int l = g0 - lane;  // lane j holds level g0 - j (leaf-most first)
+    const bool act = l >= 0;
+    int node = 0, ntp = 0;
+    NodeStat s;
+    s.visit = 0; s.value_sum = 0.0f; s.prior = 0.0f; s.reward = 0.0f;
+    if (act) {
+      node = t.path[(size_t)l * ps + li];
+      s = t.stat[nidx(t, node, i)];
+      ntp = t.meta[nidx(t, node, i)].to_play;
+    }
+    const int nlev = g0 + 1 < 64 ? g0 + 1 : 64;
+    float bl = 0.0f;
+    for (int j = 0; j < nlev; ++j) {
+      if (lane == j) bl = b;
+      const float tr = readlane_f(s.reward, j);
+      if (to_play == -1) {
+        b = tr + disc * b;
+      } else {
+        const int nj = __builtin_amdgcn_readlane(ntp, j);
+        b = (nj == to_play) ? (-tr + disc * b) : (tr + disc * b);
+      }
+    }
+    if (act) {
+      if (to_play == -1 || ntp == to_play)
+        s.value_sum += bl;
+      else
+        s.value_sum += -bl;
+      s.visit += 1;
+      t.stat[nidx(t, node, i)] = s;
+      const float v = node_value(s);
+      if (t.val) t.val[nidx(t, node, i)] = v;
+      const float q = (to_play == -1) ? s.reward + disc * v : s.reward + disc * -v;
+      qmax = fmaxf(qmax, q);
+      qmin = fminf(qmin, q);
+    }
+  }
+  qmax = wave_max_dpp(qmax);
+  qmin = -wave_max_dpp(-qmin);
+  if (lane == 0) {
+    float4 mm = *mm_ptr;
+    if (qmax > mm.x) mm.x = qmax;
+    if (qmin < mm.y) mm.y = qmin;
+    *mm_ptr = mm;
+  }
+}
+
 // h^-1 of InverseScalarTransform (scaling_transform.py:123-127), eps = 0.001.
 __device__ inline float h_inverse(float value) {
   const float eps = 0.001f;
