@@ -12,7 +12,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblzmcts.so")
+LIB_PATH = os.environ.get("LZM_LIB") or os.path.join(HERE, "liblzmcts.so")  # override: build experiments
 
 LZM_OK = 0
 LZM_ERR_ARG = -1

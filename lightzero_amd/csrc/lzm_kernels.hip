@@ -1017,25 +1017,71 @@ struct LayerShape {
   int krows, K, N;
 };
 bool layer_used(int l, int res_dynamics) { return res_dynamics || (l != 2 && l != 3); }
-// float offset of each layer's weights / bias in the kernel layout (16-B aligned), total size
-size_t kernel_layout(const LayerShape *s, int res_dynamics, size_t *w_off, size_t *b_off) {
+
+// Kernel layers: the packed layers as the search kernel runs them. Two pairs are merged, each
+// into one layer with columns [src0 | src1] over the same K: the value and policy head hiddens
+// (fc_value_head[0] | fc_policy_head[0], same input) and the value and policy head outputs
+// (fc_value_head[1] | fc_policy_head[1], inputs the two halves of that merged hidden) — fewer
+// dependent steps per simulation, and fuller lanes.
+struct KLayer {
+  int src0, src1;  // packed layer indices (src1 < 0: single source)
+  int K, N, N0;    // N0: columns taken from src0
+};
+int kernel_layers(const LayerShape *s, int res, KLayer *kl) {
+  int n = 0;
+  auto one = [&](int l) { kl[n++] = KLayer{l, -1, s[l].K, s[l].N, s[l].N}; };
+  auto two = [&](int a, int b) { kl[n++] = KLayer{a, b, s[a].K, s[a].N + s[b].N, s[a].N}; };
+  one(0);
+  one(1);
+  if (res) {
+    one(2);
+    one(3);
+  }
+  one(4);
+  one(5);
+  one(6);
+  one(7);
+  two(8, 10);
+  two(9, 11);
+  return n;
+}
+// float offsets of each packed layer (weights [krows][N], then bias [N]) in the packed buffer
+void packed_offsets(const LayerShape *s, int res, size_t *w, size_t *b) {
   size_t off = 0;
   for (int l = 0; l < 12; ++l) {
-    w_off[l] = b_off[l] = off;
-    if (!layer_used(l, res_dynamics)) continue;
-    off += swz_floats(s[l].K, s[l].N);
+    w[l] = b[l] = off;
+    if (!layer_used(l, res)) continue;
+    off += (size_t)s[l].krows * s[l].N;
+    b[l] = off;
+    off += s[l].N;
+  }
+}
+// float offset of each kernel layer's weights / bias in the kernel layout (16-B aligned), total
+size_t kernel_layout(const KLayer *kl, int nk, size_t *w_off, size_t *b_off) {
+  size_t off = 0;
+  for (int l = 0; l < nk; ++l) {
+    w_off[l] = off;
+    off += swz_floats(kl[l].K, kl[l].N);
     b_off[l] = off;
-    off = (off + s[l].N + 3) & ~(size_t)3;
+    off = (off + kl[l].N + 3) & ~(size_t)3;
   }
   return off;
 }
 
-__global__ void mlp_swizzle_kernel(const float *src, int krows, int K, int N, float *dst, size_t n) {
+// kernel-layout float d <- packed (k, col): col < N0 from src0 [krows0][N0], else src1 [krows1][N - N0]
+__global__ void mlp_swizzle_kernel(const float *src0, int krows0, const float *src1, int krows1, int K, int N, int N0,
+                                   float *dst, size_t n) {
   const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n) return;
   int k, col;
   swz_source(K, N, d, &k, &col);
-  dst[d] = (col < N && k < krows) ? src[(size_t)k * N + col] : 0.0f;
+  float v = 0.0f;
+  if (col < N0) {
+    if (k < krows0) v = src0[(size_t)k * N0 + col];
+  } else if (col < N) {
+    if (k < krows1) v = src1[(size_t)k * (N - N0) + (col - N0)];
+  }
+  dst[d] = v;
 }
 void mlp_shapes(int H, int A, int F, int V, LayerShape *s) {
   s[0] = {H + A, (H + A + kKC - 1) / kKC * kKC, H};  // fc_dynamics(_1)[0]: [latent; one-hot action]
@@ -1146,49 +1192,56 @@ constexpr size_t kMaxLds = 160 * 1024 - 1024;
 
 size_t round4(size_t x) { return (x + 3) & ~(size_t)3; }
 
-// The recurrent network as a schedule of dense steps (LDS activation buffers by float offset):
-// fc_dynamics(_1) on [latent; one-hot] (+ latent residual), fc_dynamics_2, reward head (decoded),
-// fc_prediction_common, value head (decoded), policy head (logits [r][A] in X1)
+// The recurrent network as a schedule of dense steps over the kernel layers (LDS activation
+// buffers by float offset): fc_dynamics(_1) on [latent; one-hot] (+ latent residual),
+// fc_dynamics_2, reward head (decoded), fc_prediction_common, [value | policy] head hidden,
+// [value | policy] head output: value decoded, policy logits [r][A] into X1
 // (muzero_model_mlp.py:179-204, :420-440). Even length (two weight-prefetch buffers alternate).
-void build_schedule(SearchArgs &p, const LayerShape *s, const size_t *w_off, const size_t *b_off, const float *weights,
-                    int res, int A, int V) {
+void build_schedule(SearchArgs &p, const KLayer *kl, int nk, const size_t *w_off, const size_t *b_off,
+                    const float *weights, int res, int A, int V, int F, int R) {
   const int x0 = (int)p.off_x0, x1 = (int)p.off_x1, x2 = (int)p.off_x2, nl = (int)p.off_n, hd = (int)p.off_h,
             lg = (int)p.off_logit;
-  int n = 0;
-  auto add = [&](int l, int in, int out, int relu, int resid, int rowmajor, int ldout, int dec) {
+  int n = 0, l = 0;
+  auto add = [&](int in, int out, int relu, int resid, int rowmajor, int ldout, int dec) -> StepRec & {
+    const KLayer &k = kl[l];
     StepRec &q = p.sched[n++];
     q.w = weights + w_off[l];
     q.b = weights + b_off[l];
-    q.K = s[l].K;
-    q.N = s[l].N;
-    q.wbytes = (int)(swz_floats(s[l].K, s[l].N) * sizeof(float));
+    q.K = k.K;
+    q.N = k.N;
+    q.wbytes = (int)(swz_floats(k.K, k.N) * sizeof(float));
     q.in = in; q.out = out; q.relu = relu; q.resid = resid; q.rowmajor = rowmajor; q.ldout = ldout; q.decode = dec;
-    const Split sp = layer_split(s[l].K, s[l].N);
+    q.ncol1 = k.N;  // columns routed like the first source (all, unless set below)
+    q.in2 = in; q.out2 = out; q.rowmajor2 = rowmajor; q.ldout2 = ldout;
+    const Split sp = layer_split(k.K, k.N);
     q.Np = sp.Np; q.splits = sp.splits; q.cpl = sp.cpl; q.log2s = sp.log2s;
+    ++l;
+    return q;
   };
-  add(0, x0, x1, 1, -1, 0, 0, 0);                // fc_dynamics(_1)[0]
-  add(1, x1, nl, 1, res ? x0 : -1, 0, 0, 0);     // [1] (+ latent: res_connection_in_dynamics)
+  add(x0, x1, 1, -1, 0, 0, 0);                  // fc_dynamics(_1)[0]
+  add(x1, nl, 1, res ? x0 : -1, 0, 0, 0);       // [1] (+ latent: res_connection_in_dynamics)
   int enc = nl;
   if (res) {
-    add(2, nl, x1, 1, -1, 0, 0, 0);              // fc_dynamics_2
-    add(3, x1, x2, 1, -1, 0, 0, 0);
+    add(nl, x1, 1, -1, 0, 0, 0);                // fc_dynamics_2
+    add(x1, x2, 1, -1, 0, 0, 0);
     enc = x2;
   }
   p.stamp_at[0] = n - 1;
-  add(4, enc, hd, 1, -1, 0, 0, 0);               // fc_reward_head
-  add(5, hd, lg, 0, -1, 1, V + 1, 1);
+  add(enc, hd, 1, -1, 0, 0, 0);                 // fc_reward_head
+  add(hd, lg, 0, -1, 1, V + 1, 1);
   p.stamp_at[1] = n - 1;
-  add(6, nl, x1, 1, -1, 0, 0, 0);                // fc_prediction_common
-  add(7, x1, x2, 1, -1, 0, 0, 0);
+  add(nl, x1, 1, -1, 0, 0, 0);                  // fc_prediction_common
+  add(x1, x2, 1, -1, 0, 0, 0);
   p.stamp_at[2] = n - 1;
-  add(8, x2, hd, 1, -1, 0, 0, 0);                // fc_value_head
-  add(9, hd, lg, 0, -1, 1, V + 1, 2);
+  add(x2, hd, 1, -1, 0, 0, 0);                  // [fc_value_head[0] | fc_policy_head[0]]: 2F rows of hd
+  StepRec &o = add(hd, lg, 0, -1, 1, V + 1, 2);  // [fc_value_head[1] | fc_policy_head[1]]
+  o.ncol1 = V;                                  // value support columns, decoded
+  o.in2 = hd + F / kKC * (kKC * R + 4);         // policy columns read the policy half of hd
+  o.out2 = x1; o.rowmajor2 = 1; o.ldout2 = A;   // logits [r][A]
   p.stamp_at[3] = n - 1;
-  add(10, x2, hd, 1, -1, 0, 0, 0);               // fc_policy_head
-  add(11, hd, x1, 0, -1, 1, A, 0);
   p.nsteps = n;
+  (void)nk;
 }
-
 }  // namespace
 
 extern "C" {
@@ -1209,8 +1262,10 @@ int64_t lzm_mlp_kernel_floats(int hidden, int actions, int head_hidden, int supp
   if (hidden <= 0 || actions <= 0 || head_hidden <= 0 || support <= 0) return -1;
   LayerShape s[12];
   mlp_shapes(hidden, actions, head_hidden, support, s);
+  KLayer kl[12];
+  const int nk = kernel_layers(s, res_dynamics, kl);
   size_t w_off[12], b_off[12];
-  return (int64_t)kernel_layout(s, res_dynamics, w_off, b_off);
+  return (int64_t)kernel_layout(kl, nk, w_off, b_off);
 }
 
 int lzm_mlp_prepare(int hidden, int actions, int head_hidden, int support, int res_dynamics, const float *packed,
@@ -1222,19 +1277,25 @@ int lzm_mlp_prepare(int hidden, int actions, int head_hidden, int support, int r
   }
   LayerShape s[12];
   mlp_shapes(hidden, actions, head_hidden, support, s);
+  size_t pw[12], pb[12];
+  packed_offsets(s, res_dynamics, pw, pb);
+  KLayer kl[12];
+  const int nk = kernel_layers(s, res_dynamics, kl);
   size_t w_off[12], b_off[12];
-  kernel_layout(s, res_dynamics, w_off, b_off);
-  size_t src = 0;
-  for (int l = 0; l < 12; ++l) {
-    if (!layer_used(l, res_dynamics)) continue;
-    const size_t n = swz_floats(s[l].K, s[l].N);
+  kernel_layout(kl, nk, w_off, b_off);
+  for (int l = 0; l < nk; ++l) {
+    const KLayer &q = kl[l];
+    const size_t n = swz_floats(q.K, q.N);
+    const int s1 = q.src1 >= 0 ? q.src1 : q.src0;
     hipLaunchKernelGGL(mlp_swizzle_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       packed + src, s[l].krows, s[l].K, s[l].N, out + w_off[l], n);
+                       packed + pw[q.src0], s[q.src0].krows, packed + pw[s1], s[s1].krows, q.K, q.N, q.N0,
+                       out + w_off[l], n);
     LZM_CHECK_LAUNCH();
-    src += (size_t)s[l].krows * s[l].N;
-    LZM_HIP(hipMemcpyAsync(out + b_off[l], packed + src, (size_t)s[l].N * sizeof(float), hipMemcpyDeviceToDevice,
-                           (hipStream_t)stream));
-    src += s[l].N;
+    LZM_HIP(hipMemcpyAsync(out + b_off[l], packed + pb[q.src0], (size_t)q.N0 * sizeof(float),
+                           hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    if (q.src1 >= 0)
+      LZM_HIP(hipMemcpyAsync(out + b_off[l] + q.N0, packed + pb[q.src1], (size_t)(q.N - q.N0) * sizeof(float),
+                             hipMemcpyDeviceToDevice, (hipStream_t)stream));
   }
   return LZM_OK;
 }
@@ -1256,7 +1317,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     return LZM_ERR_ARG;
   }
   const int H = hidden, F = head_hidden, V = support, A = h->A, S = num_simulations;
-  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || V > kMaxRounds * kThreads || A > H || H % kKC != 0 ||
+  if (H <= 0 || H > 1024 || F <= 0 || F > 1024 || V <= 0 || V + A > kMaxRounds * kThreads || A > H || H % kKC != 0 ||
       F % kKC != 0) {
     set_err("lzm_search_mlp: unsupported network shape (hidden and head widths must be multiples of 16)");
     return LZM_ERR_ARG;
@@ -1280,6 +1341,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   SearchArgs p;
   memset(&p, 0, sizeof(p));
   LayerShape shp[12];
+  KLayer kls[12];
+  int nkl = 0;
   size_t lay_w[12], lay_b[12];
   p.stat = h->stat; p.meta = h->meta; p.legal = h->legal; p.nlegal = h->nlegal;
   p.path = h->path; p.path_act = h->path_act; p.pathlen = h->pathlen; p.lut = h->lut;
@@ -1289,7 +1352,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   {
     LayerShape s[12];
     mlp_shapes(H, A, F, V, s);
-    kernel_layout(s, res_dynamics, lay_w, lay_b);
+    nkl = kernel_layers(s, res_dynamics, kls);
+    kernel_layout(kls, nkl, lay_w, lay_b);
     for (int l = 0; l < 12; ++l) shp[l] = s[l];
   }
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
@@ -1321,12 +1385,12 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.off_x1 = o; o += round4(tfl(H));          // also the policy logits [r][A]
   p.off_x2 = o; o += round4(tfl(H));
   p.off_n = o; o += round4(tfl(H));
-  p.off_h = o; o += round4(tfl(F));
+  p.off_h = o; o += round4(tfl(2 * F));        // [value hidden; policy hidden] (merged layer)
   p.off_logit = o; if (V < kThreads) o += round4((size_t)(V + 1) * R);  // wide supports decode from registers
   p.off_part = o;  // (unused: split-K partials meet through DPP)
   p.off_misc = o; o += round4((size_t)S + 32);  // staged seeds[S] + 16807^i table
   const size_t lds = o * sizeof(float);
-  build_schedule(p, shp, lay_w, lay_b, weights, res_dynamics, A, V);
+  build_schedule(p, kls, nkl, lay_w, lay_b, weights, res_dynamics, A, V, F, R);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_mlp: %zu B of LDS needed (network too wide)", lds);
     return LZM_ERR_ARG;

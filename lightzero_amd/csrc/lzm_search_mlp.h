@@ -46,6 +46,8 @@ struct StepRec {
   int K, N, wbytes;  // K: inputs rounded up to kKC (zero rows)
   int in, out, relu, resid, rowmajor, ldout, decode;  // resid < 0: none; decode 1 reward, 2 value
   int Np, splits, cpl, log2s;                        // layer_split(K, N)
+  // columns >= ncol1 (a second merged layer) read `in2` and store to `out2` (never decoded)
+  int ncol1, in2, out2, rowmajor2, ldout2;
 };
 
 struct SearchArgs {
@@ -80,7 +82,8 @@ struct SearchArgs {
   // network schedule (host-built)
   StepRec sched[12];
   int nsteps, stamp_at[4];
-  int diag_mode;  // timing experiments only (LZM_DIAG_MODE): 1 or 3 weight loads out of range, 2 no dense FMAs
+  int diag_mode;  // timing experiments only (LZM_DIAG_MODE; results invalid): 1/3 weight loads out of range,
+                  // 2 no dense FMAs, 4 no split-layer epilogue, 5 no step barrier, 6 no weight prefetch
   // dynamic LDS layout (float offsets)
   int tree_in_lds;
   size_t off_stat, off_meta, off_lut, off_legal, off_path, off_pact, off_x0, off_x1, off_x2, off_n, off_h, off_logit, off_part,
@@ -241,6 +244,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *p, int b
 }
 constexpr int kOOR = 0x7fffffff;  // out-of-range buffer offset: the load returns 0, no request
 
+#ifndef LZM_PREFETCH_AHEAD
+#define LZM_PREFETCH_AHEAD 2
+#endif
+// 1: each step prefetches the next step's weights, issuing exactly its chunk slots (uniform
+//    branches; the compiler's conservative vmcnt at the consumer costs nothing one step ahead).
+// 2: two register buffers, two steps ahead, branch-free fixed load counts (out-of-range slots).
+constexpr int kPrefetchAhead = LZM_PREFETCH_AHEAD;
+
 template <int kPreChunks>
 __device__ __forceinline__ void prefetch_step(const StepRec &s, float *w, float &bias, bool diag_no_loads = false,
                                               bool diag_skip = false) {
@@ -254,15 +265,28 @@ __device__ __forceinline__ void prefetch_step(const StepRec &s, float *w, float 
   const int nc = s.K / kKC;
   const int c0 = s.splits ? (tid & (s.splits - 1)) * s.cpl : 0;
   const int n = active ? min(s.cpl, nc - c0) : 0;
-  const __amdgpu_buffer_rsrc_t rw = wave_rsrc(s.w, diag_no_loads ? 0 : s.wbytes);
+  // the uniform part of each load's address lives in its descriptor (scalar ops); the lane part
+  // is tid * 16, or out of range for lanes / chunk slots without data (one select per chunk)
+  const char *wb = reinterpret_cast<const char *>(s.w);
+  const int wbytes = diag_no_loads ? 0 : s.wbytes;
+  // one-step-ahead: skip chunk slots no lane of the step has, and waves without any lane
+  const bool wave_on = kPrefetchAhead == 1 ? (__builtin_amdgcn_readfirstlane(tid & ~63) < nl) : true;
 #pragma unroll
   for (int c = 0; c < kPreChunks; ++c) {
-    // no branch around the loads, even for chunk slots no lane has: a branch makes the load count
-    // path-dependent and the compiler then drains vmcnt conservatively (measured slower)
+    if (kPrefetchAhead == 1 && !(c < s.cpl && wave_on)) {
+#pragma unroll
+      for (int j = 0; j < kKC; ++j) w[c * kKC + j] = 0.0f;
+      continue;
+    }
+    // (two-step-ahead) no branch around the loads, even for chunk slots no lane has: a branch makes
+    // the load count path-dependent and the compiler then drains vmcnt conservatively
+    const int vo = (c < n && !diag_skip) ? tid * 16 : kOOR;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int off = (c < n && !diag_skip) ? ((c * 4 + q) * nl + tid) * 16 : kOOR;
-      const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rw, off, 0, 0);
+      const int slot = (c * 4 + q) * nl * 16;  // byte offset of this (chunk, quarter) slot, uniform
+      const int left = wbytes - slot;
+      const __amdgpu_buffer_rsrc_t r = wave_rsrc(wb + slot, left > 0 ? left : 0);
+      const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, 0, 0);
       w[c * kKC + 4 * q] = v.x; w[c * kKC + 4 * q + 1] = v.y; w[c * kKC + 4 * q + 2] = v.z;
       w[c * kKC + 4 * q + 3] = v.w;
     }
@@ -338,15 +362,19 @@ constexpr int kWaves = kThreads / 64;
 // column rounds of a wide layer whose support is decoded in registers (supports up to 1024)
 constexpr int kMaxRounds = (1024 + kThreads - 1) / kThreads;
 
-// out column c of a step: activation, residual, layout
+// out column c of a step: activation, residual, layout (columns >= ncol1: the second merged layer)
 template <int R>
-__device__ __forceinline__ void store_col(const StepRec &s, float *out, const float *residT, int c, const float *v) {
+__device__ __forceinline__ void store_col(const StepRec &s, float *smem_f, const float *residT, int c, const float *v) {
+  const bool second = c >= s.ncol1;
+  float *out = smem_f + (second ? s.out2 : s.out);
+  const int cc = second ? c - s.ncol1 : c;
+  const int rowmajor = second ? s.rowmajor2 : s.rowmajor, ld = second ? s.ldout2 : s.ldout;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     float x = v[r];
     if (s.relu) x = fmaxf(x, 0.0f);
     if (residT) x += residT[tpos<R>(c, r)];
-    if (s.rowmajor) out[r * s.ldout + c] = x; else out[tpos<R>(c, r)] = x;
+    if (rowmajor) out[r * ld + cc] = x; else out[tpos<R>(cc, r)] = x;
   }
 }
 
@@ -361,8 +389,6 @@ __device__ __forceinline__ void dense_step(const StepRec &s, float *smem_f, floa
                                           float *dec_out, int nr, const StepRec &sn, int diag = 0) {
   const int tid = threadIdx.x;
   const int N = s.N;
-  const float *inT = smem_f + s.in;
-  float *out = smem_f + s.out;
   const float *residT = s.resid >= 0 ? smem_f + s.resid : nullptr;
   const bool wide = s.splits == 0;
   float acc[R];
@@ -372,10 +398,16 @@ __device__ __forceinline__ void dense_step(const StepRec &s, float *smem_f, floa
   const int nl = wide ? kThreads : (s.Np << s.log2s);
   const int part = wide ? 0 : tid & (s.splits - 1), col = wide ? tid : tid >> s.log2s;
   // ---- FMAs (the prefetched registers are only read here)
+  auto in_of = [&](int c) -> const float * { return smem_f + (c < s.ncol1 ? s.in : s.in2); };
   if (wide) {
-    if (diag != 2) dot_lane<R, P>((gfloat4_p)s.w, kThreads, tid, s.cpl, 0, inT, w, acc);
+    if (diag != 2) dot_lane<R, P>((gfloat4_p)s.w, kThreads, tid, s.cpl, 0, in_of(tid), w, acc);
 #pragma unroll
     for (int r = 0; r < R; ++r) lg[0][r] = acc[r];
+    if (s.decode && tid >= s.ncol1) {  // a second-layer column already in round 0
+      store_col<R>(s, smem_f, residT, tid, acc);
+#pragma unroll
+      for (int r = 0; r < R; ++r) lg[0][r] = -INFINITY;
+    }
 #pragma unroll
     for (int u = 1; u < kMaxRounds; ++u) {
 #pragma unroll
@@ -388,36 +420,36 @@ __device__ __forceinline__ void dense_step(const StepRec &s, float *smem_f, floa
           const float b = ((gfloat_p)s.b)[c];
 #pragma unroll
           for (int r = 0; r < R; ++r) a2[r] = b;
-          dot_stream<R>((gfloat4_p)(s.w + (size_t)u * kThreads * s.K), nu, tid, 0, s.cpl, 0, inT, a2);
-          if (s.decode) {
+          dot_stream<R>((gfloat4_p)(s.w + (size_t)u * kThreads * s.K), nu, tid, 0, s.cpl, 0, in_of(c), a2);
+          if (s.decode && c < s.ncol1) {
 #pragma unroll
             for (int r = 0; r < R; ++r) lg[u][r] = a2[r];
           } else {
-            store_col<R>(s, out, residT, c, a2);
+            store_col<R>(s, smem_f, residT, c, a2);
           }
         }
       }
     }
   } else {
     const int cnt = min(s.cpl, s.K / kKC - part * s.cpl);
-    if (tid < nl && diag != 2) dot_lane<R, P>((gfloat4_p)s.w, nl, tid, cnt, part * s.cpl * kKC, inT, w, acc);
+    if (tid < nl && diag != 2) dot_lane<R, P>((gfloat4_p)s.w, nl, tid, cnt, part * s.cpl * kKC, in_of(col), w, acc);
   }
   // ---- the next-but-one step's weights: ONE definition point of the register buffer per step, so
   // the loop-carried registers need no copies at control-flow joins
-  prefetch_step<P>(sn, w, bias, diag == 1, diag == 3);
+  if (diag != 6) prefetch_step<P>(sn, w, bias, diag == 1, diag == 3);
   // ---- epilogue
   if (!wide) {
-    if (tid < nl) {
+    if (tid < nl && diag != 4) {
       group_sum<R>(acc, s.log2s);
-      if (part == 0 && col < N) store_col<R>(s, out, residT, col, acc);
+      if (part == 0 && col < N) store_col<R>(s, smem_f, residT, col, acc);
     }
     return;
   }
   if (!s.decode) {
-    store_col<R>(s, out, residT, tid, acc);
+    store_col<R>(s, smem_f, residT, tid, acc);
     return;
   }
-  // fused support decode (N <= kMaxRounds * kThreads, checked on the host)
+  // fused support decode over the first ncol1 columns (<= kMaxRounds * kThreads, host-checked)
   const int wid = tid >> 6, lane = tid & 63;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -428,7 +460,8 @@ __device__ __forceinline__ void dense_step(const StepRec &s, float *smem_f, floa
     if (lane == 0) red[wid * R + r] = m;
   }
   __syncthreads();
-  const float half = (float)((N - 1) / 2);
+  const int V = s.ncol1;
+  const float half = (float)((V - 1) / 2);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     float M = red[r];
@@ -630,10 +663,11 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   float *X0 = smem + p.off_x0, *X1 = smem + p.off_x1, *NL = smem + p.off_n;
   float *LG = smem + p.off_logit;
   // this lane's weights for the next schedule step, loaded one step ahead (prefetch_step)
-  // weight prefetch buffers: A for even schedule steps, B for odd (schedules have an even length)
+  // weight prefetch buffers: two-step-ahead: A for even schedule steps, B for odd (schedules have an
+  // even length); one-step-ahead: A only
   float wA[pre_a<R>() * kKC], bA = 0.0f, wB[pre_b<R>() * kKC], bB = 0.0f;
   prefetch_step<pre_a<R>()>(p.sched[0], wA, bA);
-  prefetch_step<pre_b<R>()>(p.sched[1], wB, bB);
+  if (kPrefetchAhead == 2) prefetch_step<pre_b<R>()>(p.sched[1], wB, bB);
 
   for (int k = 0; k < p.S; ++k) {
     const uint32_t seed = s_seeds[k];
@@ -782,11 +816,11 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     const int st_ = (ST);                                                                            \
     const StepRec &q = p.sched[st_];                                                                 \
     unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;                         \
-    const int nx = st_ + 2 < p.nsteps ? st_ + 2 : st_ + 2 - p.nsteps;                               \
+    const int nx = st_ + kPrefetchAhead < p.nsteps ? st_ + kPrefetchAhead : st_ + kPrefetchAhead - p.nsteps; \
     float *dec = q.decode == 1 ? s_r : s_v;                                                          \
     dense_step<R, P>(q, smem, W, BIAS, s_red, dec, nr, p.sched[nx], p.diag_mode);                    \
     LZM_SUBSTAMP(16 + 4 * st_);                                                                      \
-    __syncthreads();                                                                                 \
+    if (p.diag_mode != 5) __syncthreads();                                                           \
     LZM_SUBSTAMP(17 + 4 * st_);                                                                      \
     if (q.decode && q.splits) { /* narrow support (< kThreads): logits in LG, one wave per row */    \
       for (int r = tid >> 6; r < nr; r += kWaves) {                                                  \
@@ -800,9 +834,13 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     if (st_ == p.stamp_at[2]) LZM_STAMP(5);                                                          \
     if (st_ == p.stamp_at[3]) LZM_STAMP(6);                                                          \
   } while (0)
-    for (int st = 0; st < p.nsteps; st += 2) {
-      LZM_NET_STEP(st, wA, bA, pre_a<R>());
-      LZM_NET_STEP(st + 1, wB, bB, pre_b<R>());
+    if (kPrefetchAhead == 2) {
+      for (int st = 0; st < p.nsteps; st += 2) {
+        LZM_NET_STEP(st, wA, bA, pre_a<R>());
+        LZM_NET_STEP(st + 1, wB, bB, pre_b<R>());
+      }
+    } else {
+      for (int st = 0; st < p.nsteps; ++st) LZM_NET_STEP(st, wA, bA, pre_a<R>());
     }
 #undef LZM_NET_STEP
     LZM_STAMP(7);
