@@ -49,9 +49,11 @@ def parse():
                    help="fused: one lzm_search_mlp launch per search; generic: HIP tree kernels around the "
                         "PyTorch network (any model)")
     p.add_argument("--graph", type=int, default=1, help="generic path: replay each search as one HIP graph")
-    p.add_argument("--step", choices=["graph", "python"], default="graph",
+    p.add_argument("--step", choices=["graph", "python", "collect"], default="graph",
                    help="graph: the collect-time search pass as one HIP graph (lightzero_amd.collect."
-                        "DeviceSearchStep); python: the same sequence driven call by call from Python")
+                        "DeviceSearchStep); python: the same sequence driven call by call from Python; "
+                        "collect: one full env step of the device collector (search + action selection + "
+                        "CartPole step + recording, lightzero_amd.collector.DeviceCollector)")
     p.add_argument("--cpu-baseline-secs", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--zero-heads", action="store_true", help="reference zero-init last layers (all-tie search)")
@@ -92,6 +94,25 @@ class GraphStep:
 
     def __call__(self):
         out = self.step.step()
+        self.last = (out["distributions"], out["values"], None)
+
+
+class CollectStep:
+    """One env step of the device collector for every env: search + select_action + CartPole step +
+    GameSegment recording, one HIP graph (muzero_collector.py:399-705 per step)."""
+
+    def __init__(self, B, S, model, device, rng_mode, seed):
+        from lightzero_amd.collector import DeviceCollector
+        self.B, self.S = B, S
+        self.col = DeviceCollector(model, B, S, device=device, seed=seed, rng_mode=rng_mode, graph=True,
+                                   episode_slots=64)
+        self.step = self.col.search
+        self.mcts = self.step.mcts
+        self.last = None
+
+    def __call__(self):
+        self.col.step()
+        out = self.col.search.out
         self.last = (out["distributions"], out["values"], None)
 
 
@@ -157,7 +178,7 @@ def kernel_timing(step, n_search=3):
         setattr(mc.DeviceTree, n, timed(n, orig[n]))
     mcts.record = True
     # a graph replay runs no Python: time the captured body eagerly (same kernels, same inputs)
-    run = step.step._body if isinstance(step, GraphStep) else step
+    run = step.step._body if isinstance(step, (GraphStep, CollectStep)) else step
     try:
         for _ in range(n_search):
             run()
@@ -298,6 +319,8 @@ def main():
     model = build_model(device, args.zero_heads, seed=0)
     if args.path == "fused" and args.step == "graph":
         step = GraphStep(B, S, model, device, args.rng, seed=shard_seed(rank))
+    elif args.path == "fused" and args.step == "collect":
+        step = CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank))
     else:
         step = GpuStep(B, S, model, device, args.rng, args.graph, seed=shard_seed(rank), fused=args.path == "fused")
 
@@ -367,8 +390,8 @@ def main():
                 "config": {"workload": "CartPole-v0 MuZero search, MuZeroModelMLP (latent 128, support 601), "
                                        f"{B} envs x {S} sims per GPU",
                            "global_batch": world * B, "num_simulations": S, "rng": args.rng,
-                           "path": args.path,
-                           "hip_graph": (args.step == "graph") if args.path == "fused" else bool(args.graph),
+                           "path": args.path, "step": args.step if args.path == "fused" else "python",
+                           "hip_graph": (args.step != "python") if args.path == "fused" else bool(args.graph),
                            "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
                 "roofline": roofline, "cpu_baseline": cpu}

@@ -173,6 +173,25 @@ int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream);
 int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset);
 int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*/, int n, void *stream);
 
+/* ---- Device collect loop, CartPole-v0 (lzero/worker/muzero_collector.py
+ * :399-705, zoo/classic_control/cartpole/envs/cartpole_lightzero_env.py) ----
+ * State: state double[n][4], steps int32[n], obs float[n][4] (the current root observation).
+ * lzm_cartpole_reset: every env to U(-0.05, 0.05)^4 (Philox stream `seed`).
+ * lzm_cartpole_collect_step, one thread per env, after a search over `obs`: select the action from
+ * `visits` int32[n][A] (select_action, lzero/policy/utils.py:515-539: visits^(1/temperature)
+ * sampling, or argmax when `deterministic`), record obs / action / reward / child visits / root
+ * value into episode slot ep_count[i] % E of rec_* ([n][E][T(+1)][...], GameSegment fields,
+ * game_segment.py:129-218), step the env (gymnasium CartPole equations in float64, truncation at
+ * max_steps), auto-reset finished episodes (ep_len[n][E], ep_count[n]) and write the next root's
+ * obs and Dirichlet(noise_alpha) noises float[n][A]. `counter` (int64, device) keys this step's
+ * Philox streams; the caller advances it. */
+int lzm_cartpole_reset(int n, double *state, int32_t *steps, float *obs, uint32_t seed, void *stream);
+int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
+                              double *state, int32_t *steps, float *obs, float *noises, float noise_alpha,
+                              float temperature, int deterministic, float *rec_obs, int32_t *rec_action,
+                              float *rec_reward, float *rec_child, float *rec_value, int32_t *ep_len,
+                              int32_t *ep_count, int max_steps, uint32_t seed, const int64_t *counter, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

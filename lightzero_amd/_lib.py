@@ -60,6 +60,9 @@ SIGNATURES = {
     "lzm_debug_glibc_rand": [_u32, _i, _vp, _vp],
     "lzm_debug_philox": [_vp, _vp, _i, _vp],
     "lzm_debug_phase_cycles": [_vp, _vp, _i],
+    "lzm_cartpole_reset": [_i, _vp, _vp, _vp, _u32, _vp],
+    "lzm_cartpole_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _i, _u32, _vp, _vp],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
             "lzm_mlp_kernel_floats": ctypes.c_int64}

@@ -10,8 +10,9 @@ usec_k = (1000003 * seed + n) mod 10^6 for the n-th traverse of the run (the Seq
 of tests and bench), so every replay is a fresh search.
 
 Inputs are static device buffers the caller refills before `step()` (obs, Dirichlet noises,
-to_play); outputs are static device tensors overwritten by each step (visit counts per legal
-action, root values, root latents and policy logits).
+to_play) — or that a captured `epilogue` rewrites on the device (the collector's env step);
+outputs are static device tensors overwritten by each step (visit counts per legal action, root
+values, root latents and policy logits). `step_counter` counts the steps (device int64).
 """
 import torch
 
@@ -21,7 +22,8 @@ from .utils import EasyDict
 
 class DeviceSearchStep:
     def __init__(self, model, num_envs, num_simulations, legal_actions, obs_shape, device, noise_weight=0.25,
-                 discount_factor=0.997, support_scale=300, seed=0, rng_mode="glibc", graph=True, cfg_extra=None):
+                 discount_factor=0.997, support_scale=300, seed=0, rng_mode="glibc", graph=True, cfg_extra=None,
+                 epilogue=None):
         self.model = model.eval()
         self.B, self.S = int(num_envs), int(num_simulations)
         self.device = torch.device(device)
@@ -44,6 +46,7 @@ class DeviceSearchStep:
         self._ar = torch.arange(self.S, dtype=torch.int64, device=dev)
         self.graph = None
         self.use_graph = bool(graph)
+        self.epilogue = epilogue  # fn(out dict), enqueued after the search inside the same graph
         self.roots = None
         self.out = None
 
@@ -69,32 +72,44 @@ class DeviceSearchStep:
                 self.mcts.search(self.roots, self.model, out.latent_state, self.to_play, seeds=seeds)
                 t = self.roots.tree
                 dist, values = t.distributions(), t.values()
+                res = dict(distributions=dist, values=values, latent_state=out.latent_state,
+                           policy_logits=out.policy_logits)
+                if self.epilogue is not None:
+                    self.epilogue(res)
                 self._count.add_(1)
-                return dict(distributions=dist, values=values, latent_state=out.latent_state,
-                            policy_logits=out.policy_logits)
+                return res
             finally:
                 self.mcts_cls.rng_mode = old
+
+    def build_graph(self):
+        """Warm up (allocations: tree handle, glibc tables, packed weights, torch workspaces) and
+        capture the body; runs the body twice eagerly, so callers with device state re-initialise it
+        afterwards. The step counter restarts at 0."""
+        if not self.use_graph or self.graph is not None:
+            return
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._body()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        self._count.zero_()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = self._body()
 
     def step(self):
         """One collect-time search pass over the current inputs; returns the static output dict."""
         if not self.use_graph:
             self.out = self._body()
             return self.out
-        if self.graph is None:
-            # warm-up outside capture: allocations (tree handle, glibc tables, packed weights,
-            # torch workspaces) happen here, so the captured body is launch-only
-            s = torch.cuda.Stream(device=self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):
-                for _ in range(2):
-                    self._body()
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            self._count.zero_()
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self.out = self._body()
+        self.build_graph()
         self.graph.replay()
         return self.out
 
     def reset_seed_counter(self):
         self._count.zero_()
+
+    @property
+    def step_counter(self):
+        return self._count

@@ -187,9 +187,15 @@ class TreePool:
 
     def acquire(self, B, A, max_sims, ez, fast_rng, device):
         key = (B, A, ez, fast_rng, str(device))
+        t = None
         with self._lock:
-            lst = self._free.get(key)
-            t = lst.pop() if lst else None
+            lst = self._free.get(key) or []
+            while lst and t is None:
+                c = lst.pop()
+                # a tree whose owner was reclaimed by the cyclic GC can be returned here by
+                # Roots.__del__ after its own finalizer closed the handle: skip it
+                if c.h is not None and c.h.value:
+                    t = c
         if t is None:
             t = DeviceTree(B, A, max_sims, ez=ez, fast_rng=fast_rng, device=device)
         else:
