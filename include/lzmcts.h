@@ -192,6 +192,34 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
                               float *rec_reward, float *rec_child, float *rec_value, int32_t *ep_len,
                               int32_t *ep_count, int max_steps, uint32_t seed, const int64_t *counter, void *stream);
 
+/* ---- batched AlphaZero for TicTacToe (replaces MCTS.get_next_action,
+ * lzero/mcts/ctree/ctree_alphazero/mcts_alphazero.cpp:131-207, called per env from
+ * lzero/policy/alphazero.py:266 and :327). B boards are searched together on the device; the caller
+ * evaluates the network between launches. Per search:
+ *   lzm_az_begin            boards int32[B][9] (0/1/2), start_player_index int32[B] -> state float[B][27]
+ *                           (current_state / 2 of every root, the network input)
+ *   network(state)          -> probs float[B][pstride >= 9] (softmax over the 9 actions), values float[B]
+ *   lzm_az_step(sim = -1)   expand the roots (+ default-seeded Dirichlet noise when with_noise), descend
+ *                           for simulation 0, write its leaf states
+ *   for sim in 0..S-1: network(state); lzm_az_step(sim)   finish simulation `sim`, descend for sim + 1
+ *   lzm_az_finish           visits int32[B][9], probs double[B][9] (visit_count_to_action_distribution),
+ *                           action int32[B] (first argmax, or a Philox draw keyed by seed, *counter, board)
+ * `ws` is a device buffer of lzm_az_workspace_bytes(B, S); lzm_az_set_constants fills its pUCT tables
+ * (glibc log / sqrt over the integer parent count) and noise table once (synchronous). The state
+ * buffer is overwritten by every begin / step. Everything but set_constants is graph-capturable. */
+int lzm_az_workspace_bytes(int B, int S, int64_t *out);
+int lzm_az_noise_table(double alpha, int max_n, double *out_host); /* host: row n-1 = vector for n children */
+int lzm_az_set_constants(int B, int S, void *ws, double pb_c_base, double pb_c_init, double alpha, void *stream);
+int lzm_az_begin(int B, int S, void *ws, const int32_t *boards, const int32_t *start_index, float *state,
+                 void *stream);
+int lzm_az_step(int B, int S, void *ws, int sim, const float *probs, int pstride, const float *values, int vstride,
+                int with_noise, double noise_weight, float *state, void *stream);
+int lzm_az_finish(int B, int S, void *ws, double temperature, int sample, uint32_t seed, const int64_t *counter,
+                  int32_t *visits, double *probs, int32_t *action, void *stream);
+/* test access: node visit / value_sum / first-child rows [B][1 + 9 (S + 1)] and node counts [B] (any may be NULL) */
+int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int32_t *first, int32_t *nnodes,
+                       void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,6 +27,7 @@ _i = ctypes.c_int
 _f = ctypes.c_float
 _i64 = ctypes.c_int64
 _u32 = ctypes.c_uint32
+_d = ctypes.c_double
 
 # name -> argtypes (all return int status unless listed in _RESTYPE)
 SIGNATURES = {
@@ -63,6 +64,13 @@ SIGNATURES = {
     "lzm_cartpole_reset": [_i, _vp, _vp, _vp, _u32, _vp],
     "lzm_cartpole_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _i, _u32, _vp, _vp],
+    "lzm_az_workspace_bytes": [_i, _i, ctypes.POINTER(_i64)],
+    "lzm_az_noise_table": [_d, _i, _vp],
+    "lzm_az_set_constants": [_i, _i, _vp, _d, _d, _d, _vp],
+    "lzm_az_begin": [_i, _i, _vp, _vp, _vp, _vp, _vp],
+    "lzm_az_step": [_i, _i, _vp, _i, _vp, _i, _vp, _i, _i, _d, _vp, _vp],
+    "lzm_az_finish": [_i, _i, _vp, _d, _i, _u32, _vp, _vp, _vp, _vp, _vp],
+    "lzm_az_export_tree": [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
             "lzm_mlp_kernel_floats": ctypes.c_int64}

@@ -25,11 +25,13 @@
 #include <string.h>
 
 #include <mutex>
+#include <random>
 #include <vector>
 
 #include "../../include/lzmcts.h"
 #include "lzm_numerics.h"
 #include "lzm_collect.h"
+#include "lzm_az.h"
 #include "lzm_tree.h"
 #include "lzm_search_mlp.h"
 
@@ -1460,6 +1462,166 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
   a.rec_value = rec_value; a.ep_len = ep_len; a.ep_count = ep_count;
   hipLaunchKernelGGL(cartpole_collect_kernel, dim3((n + 127) / 128), dim3(128), 0, (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+}  // extern "C"
+
+// ---- batched AlphaZero (lzm_az.h). One workspace buffer per (B, S), carved here.
+static int64_t az_carve(int B, int S, void *ws, AzTree *t) {
+  const int64_t cap = 1 + (int64_t)kAzCells * (S + 1);
+  char *p = (char *)ws;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) -> void * {
+    void *r = p ? (void *)(p + off) : nullptr;
+    off += (bytes + 255) & ~(int64_t)255;
+    return r;
+  };
+  AzTree x;
+  x.B = B; x.S = S; x.cap = (int)cap;
+  const int64_t nodes = (int64_t)B * cap;
+  x.visit = (int32_t *)take(nodes * 4);
+  x.vsum = (float *)take(nodes * 4);
+  x.prior = (float *)take(nodes * 4);
+  x.first = (int32_t *)take(nodes * 4);
+  x.nch = (int32_t *)take(nodes * 4);
+  x.act = (int32_t *)take(nodes * 4);
+  x.nnodes = (int32_t *)take((int64_t)B * 4);
+  x.root_board = (int32_t *)take((int64_t)B * kAzCells * 4);
+  x.root_player = (int32_t *)take((int64_t)B * 4);
+  x.path = (int32_t *)take((int64_t)B * kAzPath * 4);
+  x.leaf = (int32_t *)take((int64_t)B * 4 * 4);
+  x.leaf_board = (int32_t *)take((int64_t)B * kAzCells * 4);
+  x.lut_pb = (double *)take((int64_t)(S + 1) * 8);
+  x.lut_sqrt = (double *)take((int64_t)(S + 1) * 8);
+  x.noise = (double *)take((int64_t)kAzCells * kAzCells * 8);
+  if (t) *t = x;
+  return off;
+}
+
+static bool az_args_ok(int B, int S, const void *ws, const char *what) {
+  if (B <= 0 || S <= 0 || S > (1 << 20) || !ws) {
+    snprintf(g_err, sizeof(g_err), "%s: need B > 0, 0 < num_simulations <= 2^20 and a workspace", what);
+    return false;
+  }
+  return true;
+}
+
+extern "C" {
+
+int lzm_az_workspace_bytes(int B, int S, int64_t *out) {
+  if (B <= 0 || S <= 0 || S > (1 << 20) || !out) {
+    set_err("lzm_az_workspace_bytes: need B > 0, 0 < num_simulations <= 2^20");
+    return LZM_ERR_ARG;
+  }
+  *out = az_carve(B, S, nullptr, nullptr);
+  return LZM_OK;
+}
+
+int lzm_az_noise_table(double alpha, int max_n, double *out) {
+  if (!(alpha > 0.0) || max_n <= 0 || max_n > 4096 || !out) {
+    set_err("lzm_az_noise_table: need alpha > 0, 0 < max_n <= 4096");
+    return LZM_ERR_ARG;
+  }
+  // _add_exploration_noise (mcts_alphazero.cpp:57-83): a default-seeded engine per call, so the
+  // vector for n children is fixed: n gamma(alpha, 1) draws, each divided by their sum
+  for (int n = 1; n <= max_n; ++n) {
+    std::default_random_engine gen;
+    std::gamma_distribution<double> dist(alpha, 1.0);
+    std::vector<double> g((size_t)n);
+    double sum = 0;
+    for (int i = 0; i < n; ++i) {
+      g[(size_t)i] = dist(gen);
+      sum += g[(size_t)i];
+    }
+    for (int i = 0; i < max_n; ++i) out[(size_t)(n - 1) * max_n + i] = i < n ? g[(size_t)i] / sum : 0.0;
+  }
+  return LZM_OK;
+}
+
+int lzm_az_set_constants(int B, int S, void *ws, double pb_c_base, double pb_c_init, double alpha, void *stream) {
+  if (!az_args_ok(B, S, ws, "lzm_az_set_constants")) return LZM_ERR_ARG;
+  if (!(pb_c_base > 0.0) || !(alpha > 0.0)) {
+    set_err("lzm_az_set_constants: need pb_c_base > 0 and alpha > 0");
+    return LZM_ERR_ARG;
+  }
+  AzTree t;
+  az_carve(B, S, ws, &t);
+  // _ucb_score (mcts_alphazero.cpp:47-54) over the integer parent count: glibc log / sqrt on the host
+  std::vector<double> pb((size_t)S + 1), sq((size_t)S + 1), nz((size_t)kAzCells * kAzCells);
+  for (int n = 0; n <= S; ++n) {
+    pb[(size_t)n] = std::log((n + pb_c_base + 1) / pb_c_base) + pb_c_init;
+    sq[(size_t)n] = std::sqrt((double)n);
+  }
+  lzm_az_noise_table(alpha, kAzCells, nz.data());
+  hipStream_t s = (hipStream_t)stream;
+  LZM_HIP(hipMemcpyAsync(t.lut_pb, pb.data(), pb.size() * 8, hipMemcpyHostToDevice, s));
+  LZM_HIP(hipMemcpyAsync(t.lut_sqrt, sq.data(), sq.size() * 8, hipMemcpyHostToDevice, s));
+  LZM_HIP(hipMemcpyAsync(t.noise, nz.data(), nz.size() * 8, hipMemcpyHostToDevice, s));
+  LZM_HIP(hipStreamSynchronize(s));
+  return LZM_OK;
+}
+
+int lzm_az_begin(int B, int S, void *ws, const int32_t *boards, const int32_t *start_index, float *state,
+                 void *stream) {
+  if (!az_args_ok(B, S, ws, "lzm_az_begin")) return LZM_ERR_ARG;
+  if (!boards || !start_index || !state) {
+    set_err("lzm_az_begin: null buffer");
+    return LZM_ERR_ARG;
+  }
+  AzTree t;
+  az_carve(B, S, ws, &t);
+  const int per = kAzThreads / kAzGroup;
+  hipLaunchKernelGGL(az_begin_kernel, dim3((B + per - 1) / per), dim3(kAzThreads), 0, (hipStream_t)stream, t,
+                     boards, start_index, state);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_az_step(int B, int S, void *ws, int sim, const float *probs, int pstride, const float *values, int vstride,
+                int with_noise, double noise_weight, float *state, void *stream) {
+  if (!az_args_ok(B, S, ws, "lzm_az_step")) return LZM_ERR_ARG;
+  if (sim < -1 || sim >= S || !probs || pstride < kAzCells || (sim >= 0 && (!values || vstride < 1)) || !state) {
+    set_err("lzm_az_step: need -1 <= sim < num_simulations, probs [B][>=9], values [B] and a state buffer");
+    return LZM_ERR_ARG;
+  }
+  AzTree t;
+  az_carve(B, S, ws, &t);
+  AzStepArgs a;
+  a.sim = sim; a.with_noise = with_noise; a.noise_weight = noise_weight;
+  a.probs = probs; a.pstride = pstride; a.values = values ? values : probs; a.vstride = vstride; a.state = state;
+  const int per = kAzThreads / kAzGroup;
+  hipLaunchKernelGGL(az_step_kernel, dim3((B + per - 1) / per), dim3(kAzThreads), 0, (hipStream_t)stream, t, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_az_finish(int B, int S, void *ws, double temperature, int sample, uint32_t seed, const int64_t *counter,
+                  int32_t *visits, double *probs, int32_t *action, void *stream) {
+  if (!az_args_ok(B, S, ws, "lzm_az_finish")) return LZM_ERR_ARG;
+  if (temperature == 0.0 || !visits || !probs || !action) {
+    set_err("lzm_az_finish: temperature cannot be 0; visits / probs / action buffers required");
+    return LZM_ERR_ARG;
+  }
+  AzTree t;
+  az_carve(B, S, ws, &t);
+  hipLaunchKernelGGL(az_finish_kernel, dim3((B + 127) / 128), dim3(128), 0, (hipStream_t)stream, t, temperature,
+                     sample, seed, counter, visits, probs, action);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int32_t *first, int32_t *nnodes,
+                       void *stream) {
+  if (!az_args_ok(B, S, ws, "lzm_az_export_tree")) return LZM_ERR_ARG;
+  AzTree t;
+  az_carve(B, S, ws, &t);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t nodes = (size_t)B * t.cap;
+  if (visit) LZM_HIP(hipMemcpyAsync(visit, t.visit, nodes * 4, hipMemcpyDeviceToDevice, s));
+  if (vsum) LZM_HIP(hipMemcpyAsync(vsum, t.vsum, nodes * 4, hipMemcpyDeviceToDevice, s));
+  if (first) LZM_HIP(hipMemcpyAsync(first, t.first, nodes * 4, hipMemcpyDeviceToDevice, s));
+  if (nnodes) LZM_HIP(hipMemcpyAsync(nnodes, t.nnodes, (size_t)B * 4, hipMemcpyDeviceToDevice, s));
   return LZM_OK;
 }
 

@@ -37,11 +37,15 @@ def mlp(in_channels: int, hidden_channels: int, out_channels: int, layer_num: in
         layers.append(nn.Linear(channels[i], channels[i + 1]))
         if norm_type == 'BN':
             layers.append(nn.BatchNorm1d(channels[i + 1]))
+        elif norm_type == 'LN':
+            layers.append(nn.LayerNorm(channels[i + 1]))
         layers.append(activation)
     last = nn.Linear(channels[-2], channels[-1])
     layers.append(last)
     if output_norm and norm_type == 'BN':
         layers.append(nn.BatchNorm1d(channels[-1]))
+    elif output_norm and norm_type == 'LN':
+        layers.append(nn.LayerNorm(channels[-1]))
     if output_activation:
         layers.append(activation)
     if last_linear_layer_init_zero:

@@ -28,4 +28,10 @@ for pair in ctree_muzero:mz_tree ctree_efficientzero:ez_tree; do
   g++ $CXXFLAGS -I"$PYINC" -I"$CT/$d" "$OUT/build/$m.cpp" "$OUT/build/ref_time_hook.o" \
       -Wl,--wrap=gettimeofday -o "$OUT/$m$EXT"
 done
+# AlphaZero tree: pybind11 from pip; the reference's own sources, unchanged.
+AZ=$CT/ctree_alphazero
+if [ -f "$AZ/mcts_alphazero.cpp" ] && python3 -c "import pybind11" 2>/dev/null; then
+  g++ -O2 -shared -std=c++17 -fPIC -w $(python3 -m pybind11 --includes) -I"$AZ" "$AZ/mcts_alphazero.cpp" \
+      -o "$OUT/mcts_alphazero$EXT"
+fi
 echo "build_ref: built $(ls "$OUT"/*"$EXT" | xargs -n1 basename | tr '\n' ' ')"

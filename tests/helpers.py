@@ -249,3 +249,19 @@ def run_transcript(tr, factory, fast_rng=False):
         t.backprop(k + 1, DISC, tr["resp_reward"][k], tr["resp_value"][k], tr["resp_logits"][k], out[3], is_reset)
     rec.update(dist=t.distributions(), values=t.values(), traj=t.trajectories(S + 2))
     return rec
+
+
+def az_scripted_pv_torch(state):
+    """oracle.tictactoe.scripted_policy_value on the device, batched: the absolute board is rebuilt from
+    the network input (current_state / 2: own stones, opponent stones, player-to-move plane)."""
+    import torch
+    player = torch.round(state[:, 2, 0, 0] * 2).to(torch.int64)  # 1 / 2
+    cur = (state[:, 0] > 0).reshape(-1, 9).to(torch.int64)
+    opp = (state[:, 1] > 0).reshape(-1, 9).to(torch.int64)
+    board = cur * player[:, None] + opp * (3 - player)[:, None]
+    pw = torch.pow(3, torch.arange(9, dtype=torch.int64, device=state.device))  # no host copy: graph-capturable
+    h = (board * pw).sum(dim=1)
+    a = torch.arange(9, dtype=torch.int64, device=state.device)
+    priors = (1 + (7 * h[:, None] + 13 * a[None, :]) % 16).to(torch.float32) / 64.0
+    value = ((31 * h) % 129 - 64).to(torch.float32) / 64.0
+    return priors, value
