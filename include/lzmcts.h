@@ -220,6 +220,28 @@ int lzm_az_finish(int B, int S, void *ws, double temperature, int sample, uint32
 int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int32_t *first, int32_t *nnodes,
                        void *stream);
 
+/* ---- fused AlphaZero search: the TicTacToe config's AlphaZeroModel (alphazero_model.py:14-330; 16 channels,
+ * num_res_blocks 1 or 2, head width 8, 9 actions, scalar value) evaluated inside the search kernel; one
+ * launch per search of B boards (tree in LDS). Same inputs / outputs / ws / constants as lzm_az_begin ..
+ * lzm_az_finish; export_tree != 0 also writes the final trees into ws (lzm_az_export_tree).
+ * Weights: lzm_az_net_prepare(nres, raw, out) packs, on the host, `raw` =
+ *   conv0 W[16][27] (out, in*9 + tap), b[16];  4*nres x { conv W[16][144], b[16] } (representation
+ *   blocks' conv1, conv2, then the prediction's; BatchNorm folded in);  1x1 W[32][16] (value rows, then
+ *   policy rows), b[32];  head block [2448]: value FC1 [8][144] @0, b @1152, LN gamma @1160, beta @1168,
+ *   FC2 [8] @1176, b @1184; policy FC1 [8][144] @1188, b @2340, gamma @2348, beta @2356, FC2 [9][8]
+ *   @2364, b [9] @2436
+ * into lzm_az_net_floats(nres) floats, to be copied to the device.
+ * lzm_az_net_eval: the same network on state float[n][27] -> probs float[n][9], value float[n]
+ * (bit-identical to what the fused search computes for that input). */
+int64_t lzm_az_net_floats(int nres);
+int lzm_az_net_prepare(int nres, const float *raw, float *out_host);
+int lzm_az_net_eval(int nres, const float *weights, const float *state, int n, float *probs, float *value,
+                    void *stream);
+int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, const int32_t *boards,
+                        const int32_t *start_index, int with_noise, double noise_weight, double temperature,
+                        int sample, uint32_t seed, const int64_t *counter, int32_t *visits, double *probs,
+                        int32_t *action, int export_tree, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

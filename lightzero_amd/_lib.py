@@ -71,9 +71,13 @@ SIGNATURES = {
     "lzm_az_step": [_i, _i, _vp, _i, _vp, _i, _vp, _i, _i, _d, _vp, _vp],
     "lzm_az_finish": [_i, _i, _vp, _d, _i, _u32, _vp, _vp, _vp, _vp, _vp],
     "lzm_az_export_tree": [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_az_net_floats": [_i],
+    "lzm_az_net_prepare": [_i, _vp, _vp],
+    "lzm_az_net_eval": [_i, _vp, _vp, _i, _vp, _vp, _vp],
+    "lzm_az_search_fused": [_i, _i, _vp, _i, _vp, _vp, _vp, _i, _d, _d, _i, _u32, _vp, _vp, _vp, _vp, _i, _vp],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
-            "lzm_mlp_kernel_floats": ctypes.c_int64}
+            "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64}
 
 _lib = None
 

@@ -26,6 +26,68 @@ from ._lib import call, ptr, stream_ptr
 ACTIONS = 9
 
 
+def _fold_bn(conv, bn):
+    """eval-mode BatchNorm folded into the preceding convolution (float64, then float32)"""
+    scale = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    w = conv.weight.double() * scale.reshape(-1, *([1] * (conv.weight.dim() - 1)))
+    b = conv.bias.double() if conv.bias is not None else torch.zeros_like(scale)
+    b = (b - bn.running_mean.double()) * scale + bn.bias.double()
+    return w.float(), b.float()
+
+
+class FusedAZNet:
+    """The TicTacToe AlphaZeroModel (lightzero_amd.model_az, same module structure as
+    lzero/model/alphazero_model.py) packed for the fused kernels: BatchNorm folded, MFMA B-fragment
+    layout (lzm_az_net_prepare). Supported: 16 channels, 1 or 2 residual blocks per network, head
+    width 8, 9 actions, scalar value (the TicTacToe config); anything else raises ValueError."""
+
+    def __init__(self, model, device="cuda"):
+        m = model
+        nres = len(m.rep_blocks)
+        ok = (nres in (1, 2) and len(m.pred_blocks) == nres and m.conv.out_channels == 16 and m.conv.in_channels == 3
+              and m.flat_v == 144 and m.flat_p == 144 and m.fc_value_head[0].out_features == 8
+              and m.fc_policy_head[0].out_features == 8 and m.fc_policy_head[-1].out_features == ACTIONS
+              and m.fc_value_head[-1].out_features == 1 and isinstance(m.fc_value_head[1], torch.nn.LayerNorm))
+        if not ok:
+            raise ValueError("fused AlphaZero kernel supports the TicTacToe AlphaZeroModel config only")
+        if m.training:
+            raise ValueError("fused AlphaZero kernel evaluates the network in eval mode: call model.eval()")
+        self.nres = nres
+        with torch.no_grad():
+            parts = []
+            w, b = _fold_bn(m.conv, m.norm)
+            parts += [w.reshape(16, 27), b]
+            for blk in list(m.rep_blocks) + list(m.pred_blocks):
+                for conv, bn in ((blk.conv1, blk.bn1), (blk.conv2, blk.bn2)):
+                    w, b = _fold_bn(conv, bn)
+                    parts += [w.reshape(16, 144), b]
+            wv, bv = _fold_bn(m.conv1x1_value, m.norm_value)
+            wp, bp = _fold_bn(m.conv1x1_policy, m.norm_policy)
+            parts += [torch.cat([wv.reshape(16, 16), wp.reshape(16, 16)]), torch.cat([bv, bp])]
+            head = torch.zeros(2448, dtype=torch.float32)
+            fv, fp = m.fc_value_head, m.fc_policy_head
+            for off, t in ((0, fv[0].weight), (1152, fv[0].bias), (1160, fv[1].weight), (1168, fv[1].bias),
+                           (1176, fv[3].weight), (1184, fv[3].bias), (1188, fp[0].weight), (2340, fp[0].bias),
+                           (2348, fp[1].weight), (2356, fp[1].bias), (2364, fp[3].weight), (2436, fp[3].bias)):
+                t = t.detach().float().cpu().reshape(-1)
+                head[off:off + t.numel()] = t
+            parts.append(head)
+            raw = torch.cat([p.detach().float().cpu().reshape(-1) for p in parts]).contiguous()
+        n = int(_lib.load().lzm_az_net_floats(nres))
+        out = torch.zeros(n, dtype=torch.float32)
+        call("lzm_az_net_prepare", nres, ctypes.c_void_p(raw.data_ptr()), ctypes.c_void_p(out.data_ptr()))
+        self.weights = out.to(device)
+
+    def compute_policy_value(self, state):
+        """the fused network on its own: state [n, 3, 3, 3] -> (probs [n, 9], value [n, 1])"""
+        st = state.reshape(-1, 27).to(torch.float32).contiguous()
+        n = st.shape[0]
+        probs = torch.empty((n, ACTIONS), dtype=torch.float32, device=st.device)
+        value = torch.empty((n, 1), dtype=torch.float32, device=st.device)
+        call("lzm_az_net_eval", self.nres, ptr(self.weights), ptr(st), n, ptr(probs), ptr(value), stream_ptr())
+        return probs, value
+
+
 class AlphaZeroMCTS:
     def __init__(self, max_moves=9, num_simulations=50, pb_c_base=19652, pb_c_init=1.25, root_dirichlet_alpha=0.3,
                  root_noise_weight=0.25, simulate_env=None, device="cuda", graph=False, seed=0):
@@ -107,6 +169,23 @@ class AlphaZeroMCTS:
         else:
             g = g[0]
         g.replay()
+
+    def search_fused(self, boards, start_player_index, net, temperature=1.0, sample=True, export_tree=False):
+        """The whole search (root evaluation, S simulations with the network, finalisation) in one
+        launch; net: FusedAZNet. Same outputs as get_next_actions."""
+        if temperature == 0:
+            raise ValueError("Temperature cannot be 0")
+        b = torch.as_tensor(boards).reshape(-1, ACTIONS)
+        B = int(b.shape[0])
+        c = self._buffers(B)
+        c["boards"].copy_(b.to(device=self.device, dtype=torch.int32))
+        c["start"].copy_(torch.as_tensor(start_player_index).reshape(B).to(device=self.device, dtype=torch.int32))
+        call("lzm_az_search_fused", B, self.num_simulations, ptr(c["ws"]), net.nres, ptr(net.weights), ptr(c["boards"]),
+             ptr(c["start"]), int(bool(sample)), self.noise_weight, float(temperature), int(bool(sample)), self.seed,
+             ptr(self._count), ptr(c["visits"]), ptr(c["probs"]), ptr(c["action"]), int(bool(export_tree)),
+             stream_ptr())
+        self._count.add_(1)
+        return c["action"], c["probs"]
 
     # ------------------------------------------------------------------ public API
     def get_next_actions(self, boards, start_player_index, compute_policy_value, temperature=1.0, sample=True):

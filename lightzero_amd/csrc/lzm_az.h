@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(kAzThreads) az_step_kernel(AzTree t, AzStepArg
   int player = t.root_player[b];
   int node = 0, d = 0;
   if (l == 0) path[0] = 0;
-  for (;;) {
+  for (; d < kAzPath - 1;) {  // a board fills after 9 moves: bounded descent
     const int f = t.first[nb + node];
     if (f < 0) break;
     const int n = t.nch[nb + node];
@@ -231,18 +231,13 @@ __global__ void __launch_bounds__(kAzThreads) az_step_kernel(AzTree t, AzStepArg
   az_write_state(a.state + (size_t)b * 27, l, cell, player);
 }
 
-// get_next_action's tail: visit counts by action, visit_count_to_action_distribution (v / T, summed in
-// action order, divided), then argmax (first maximum) or a draw from the distribution (Philox; the
-// reference draws with std::random_device, so no stream is reproducible there)
-__global__ void az_finish_kernel(AzTree t, double temperature, int sample, uint32_t seed, const int64_t *counter,
-                                 int32_t *visits_out, double *probs_out, int32_t *action_out) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= t.B) return;
-  const size_t nb = (size_t)b * t.cap;
-  int v[kAzCells];
-  for (int k = 0; k < kAzCells; ++k) v[k] = 0;
-  const int f = t.first[nb], n = t.nch[nb];
-  for (int j = 0; f >= 0 && j < n; ++j) v[t.act[nb + f + j]] = t.visit[nb + f + j];
+// get_next_action's tail for one board: visit_count_to_action_distribution (v / T, summed in action
+// order, divided), then argmax (first maximum) or a draw from the distribution (Philox keyed by seed,
+// *counter and the board; the reference draws with std::random_device, so no stream is reproducible
+// there)
+__device__ inline void az_finalize(int b, const int *v, double temperature, int sample, uint32_t seed,
+                                   const int64_t *counter, int32_t *visits_out, double *probs_out,
+                                   int32_t *action_out) {
   double x[kAzCells], sum = 0.0;
   for (int k = 0; k < kAzCells; ++k) {
     x[k] = (double)v[k] / temperature;
@@ -271,6 +266,18 @@ __global__ void az_finish_kernel(AzTree t, double temperature, int sample, uint3
         if (x[k] > 0.0) best = k;
   }
   action_out[b] = best;
+}
+
+__global__ void az_finish_kernel(AzTree t, double temperature, int sample, uint32_t seed, const int64_t *counter,
+                                 int32_t *visits_out, double *probs_out, int32_t *action_out) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= t.B) return;
+  const size_t nb = (size_t)b * t.cap;
+  int v[kAzCells];
+  for (int k = 0; k < kAzCells; ++k) v[k] = 0;
+  const int f = t.first[nb], n = t.nch[nb];
+  for (int j = 0; f >= 0 && j < n; ++j) v[t.act[nb + f + j]] = t.visit[nb + f + j];
+  az_finalize(b, v, temperature, sample, seed, counter, visits_out, probs_out, action_out);
 }
 
 }  // namespace lzm

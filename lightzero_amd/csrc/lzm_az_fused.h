@@ -1,0 +1,539 @@
+// lzm_az_fused.h — the whole batched AlphaZero search in ONE launch (fused):
+// tree, TicTacToe simulation AND the policy-value network of the TicTacToe config
+// (AlphaZeroModel, lzero/model/alphazero_model.py:14-330 with RepresentationNetwork
+// common.py:370-460; 16 channels, 3x3 board, value / policy head width 8).
+//
+// A workgroup of 256 threads (4 waves) owns R boards: their trees live in LDS, the conv weights in
+// registers (MFMA B fragments), the head weights in LDS. Per simulation: 16-lane groups descend
+// (lzm_az.h's pUCT, tie rule and env replay, on LDS), write the leaf's network input, the 4 waves
+// evaluate the R leaves, the groups expand and back up. The roots are evaluated and expanded (with
+// the reference's noise) first; the root statistics are finalised (visit_count_to_action_distribution,
+// argmax / draw) at the end. One launch per search, no host round trip.
+//
+// Network (eval mode; BatchNorm folded into the preceding convolution on the host):
+//   conv3x3 3->16 +b, ReLU; per residual block: conv3x3 16->16 +b, ReLU, conv3x3 16->16 +b, + x, ReLU
+//   (the representation's blocks, then the prediction's); 1x1 conv 16->16 (value) | 16->16 (policy) +b,
+//   ReLU; per head: Linear 144->8, LayerNorm(8), ReLU, Linear 8->{1 | 9}; softmax over the 9 logits.
+// Convolutions are GEMMs with rows = (board, cell), K = in_channel x tap (im2col gathered from
+// zero-bordered 5x5 planes in LDS), N = out channels: v_mfma_f32_16x16x4_f32 (exact f32, a k-ordered
+// fmaf chain), K split over the 4 waves, partials summed in wave order. Every output element's
+// arithmetic is independent of which tile / workgroup its board lands in, so the standalone
+// evaluation kernel (az_net_eval_kernel) and the fused search produce identical bits.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lzm_az.h"
+
+namespace lzm {
+
+constexpr int kAzfThreads = 256;
+constexpr int kAzC = 16;      // channels
+constexpr int kAzFc = 8;      // head hidden width
+constexpr int kAzPlane = 25;  // 5x5 zero-bordered plane
+constexpr int kAzBoardX = kAzC * kAzPlane;
+
+typedef float azf4 __attribute__((ext_vector_type(4)));
+
+// head block: value FC1 [8][144], bias, LN gamma, beta, FC2 [8], bias; policy FC1 [8][144], bias, LN
+// gamma, beta, FC2 [9][8], bias [9]
+constexpr int kAzV1 = 0, kAzV1b = 1152, kAzVg = 1160, kAzVb = 1168, kAzV2 = 1176, kAzV2b = 1184;
+constexpr int kAzP1 = 1188, kAzP1b = 2340, kAzPg = 2348, kAzPb = 2356, kAzP2 = 2364, kAzP2b = 2436;
+constexpr int kAzHeadFloats = 2448;
+
+// prepared weight buffer (float offsets), see lzm_az_net_prepare
+struct AzNetLayout {
+  int conv0, conv0_b;      // frag [7][64], bias [16]
+  int res, res_b;          // frag [L][36][64], bias [L][16]   (L = 4 * nres conv layers)
+  int head, head_b;        // frag [4][2][64], bias [32]
+  int heads;               // kAzHeadFloats, inner offsets kAzH* below
+  int total;
+};
+
+__host__ __device__ inline AzNetLayout az_net_layout(int nres) {
+  AzNetLayout L;
+  int o = 0;
+  auto take = [&](int n) { int r = o; o += (n + 3) & ~3; return r; };
+  L.conv0 = take(7 * 64); L.conv0_b = take(16);
+  L.res = take(4 * nres * 36 * 64); L.res_b = take(4 * nres * 16);
+  L.head = take(4 * 2 * 64); L.head_b = take(32);
+  L.heads = take(kAzHeadFloats);
+  L.total = o;
+  return L;
+}
+
+// LDS plan of the network part (floats)
+template <int R>
+struct AzNetLds {
+  static constexpr int T = (9 * R + 15) / 16;            // row tiles
+  static constexpr int xin = (R + 1) * 3 * kAzPlane;     // network input planes (+ a zero board)
+  static constexpr int xbuf = (R + 1) * kAzBoardX;       // one activation buffer
+  static constexpr int hd = R * 32 * 9;                  // 1x1 head outputs [R][32][9]
+  static constexpr int red = 4 * T * 2 * 256;            // K-split partials
+  static constexpr int heads = kAzHeadFloats;
+  static constexpr int out = R * 10;                     // probs [R][9], value [R]
+  static constexpr int hid = R * 16;                     // FC1 outputs [R][2][8]
+  static constexpr int bias = 16 + 64 * 16 + 32;         // conv biases (<= 16 res layers) + head bias
+  static constexpr int total = xin + 3 * xbuf + hd + red + heads + out + hid + bias;
+};
+
+template <int R, int NRES>
+struct AzNetRegs {
+  static constexpr int T = AzNetLds<R>::T;
+  float b0[2];                  // conv0 fragments (steps w, w + 4)
+  float br[4 * NRES][9];        // 3x3 conv fragments (steps 9w .. 9w + 8)
+  float bh[2];                  // 1x1 head fragments (step w, two N tiles)
+  int koff[9];                  // im2col offsets of this lane's k for steps 9w + j
+  int koff0[2];
+  int rb[T], rb0[T];            // row base offsets per tile (activation / input planes)
+};
+
+struct AzNetSmem {
+  float *xin, *x[3], *hd, *red, *heads, *out, *hid, *bias;
+};
+
+template <int R>
+__device__ inline AzNetSmem az_net_carve(float *p) {
+  AzNetSmem s;
+  s.xin = p; p += AzNetLds<R>::xin;
+  for (int i = 0; i < 3; ++i) { s.x[i] = p; p += AzNetLds<R>::xbuf; }
+  s.hd = p; p += AzNetLds<R>::hd;
+  s.red = p; p += AzNetLds<R>::red;
+  s.heads = p; p += AzNetLds<R>::heads;
+  s.out = p; p += AzNetLds<R>::out;
+  s.hid = p; p += AzNetLds<R>::hid;
+  s.bias = p;
+  return s;
+}
+
+// zero every plane (borders stay zero forever), stage head weights / biases, load B fragments
+template <int R, int NRES>
+__device__ inline void az_net_init(const float *__restrict__ w, const AzNetSmem &s, AzNetRegs<R, NRES> &g) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const AzNetLayout L = az_net_layout(NRES);
+  const int nzero = AzNetLds<R>::xin + 3 * AzNetLds<R>::xbuf;
+  for (int i = tid; i < nzero; i += kAzfThreads) s.xin[i] = 0.0f;
+  for (int i = tid; i < kAzHeadFloats; i += kAzfThreads) s.heads[i] = w[L.heads + i];
+  for (int i = tid; i < 16; i += kAzfThreads) s.bias[i] = w[L.conv0_b + i];
+  for (int i = tid; i < 4 * NRES * 16; i += kAzfThreads) s.bias[16 + i] = w[L.res_b + i];
+  for (int i = tid; i < 32; i += kAzfThreads) s.bias[16 + 64 * 16 + i] = w[L.head_b + i];
+  const int q = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int st = wv + 4 * j;
+    g.b0[j] = st < 7 ? w[L.conv0 + st * 64 + lane] : 0.0f;
+    const int k = 4 * st + q;
+    g.koff0[j] = (st < 7 && k < 27) ? (k / 9) * kAzPlane + ((k % 9) / 3) * 5 + (k % 3) : 0;
+  }
+#pragma unroll
+  for (int l = 0; l < 4 * NRES; ++l)
+#pragma unroll
+    for (int j = 0; j < 9; ++j) g.br[l][j] = w[L.res + (l * 36 + 9 * wv + j) * 64 + lane];
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int k = 4 * (9 * wv + j) + q;
+    g.koff[j] = (k / 9) * kAzPlane + ((k % 9) / 3) * 5 + (k % 3);
+  }
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) g.bh[nt] = w[L.head + (wv * 2 + nt) * 64 + lane];
+#pragma unroll
+  for (int t = 0; t < AzNetLds<R>::T; ++t) {
+    const int m = 16 * t + (lane & 15);
+    const int r = m < 9 * R ? m / 9 : R, p = m < 9 * R ? m % 9 : 0;
+    g.rb[t] = r * kAzBoardX + (p / 3) * 5 + (p % 3);
+    g.rb0[t] = r * 3 * kAzPlane + (p / 3) * 5 + (p % 3);
+  }
+}
+
+__device__ inline int az_interior(int p) { return (p / 3 + 1) * 5 + (p % 3) + 1; }
+
+// sum the 4 waves' partials in wave order, + bias (+ residual), ReLU, into the interior of `dst`
+template <int R>
+__device__ inline void az_conv_epilogue(const AzNetSmem &s, const float *bias, const float *res, float *dst) {
+  constexpr int T = AzNetLds<R>::T;
+  for (int e = threadIdx.x; e < T * 256; e += kAzfThreads) {
+    const int t = e >> 8, lane = (e >> 2) & 63, v = e & 3;
+    const int m = 16 * t + 4 * (lane >> 4) + v, n = lane & 15;
+    if (m >= 9 * R) continue;
+    float acc = s.red[(0 * T + t) * 2 * 256 + (e & 255)];
+    acc += s.red[(1 * T + t) * 2 * 256 + (e & 255)];
+    acc += s.red[(2 * T + t) * 2 * 256 + (e & 255)];
+    acc += s.red[(3 * T + t) * 2 * 256 + (e & 255)];
+    acc += bias[n];
+    const int r = m / 9, p = m % 9;
+    const int o = r * kAzBoardX + n * kAzPlane + az_interior(p);
+    if (res) acc += res[o];
+    dst[o] = acc > 0.0f ? acc : 0.0f;
+  }
+}
+
+// evaluates the R boards whose input planes are in s.xin; leaves probs [R][9] / value [R] in s.out.
+// Starts and ends with a workgroup barrier.
+template <int R, int NRES>
+__device__ inline void az_net_forward(const AzNetSmem &s, const AzNetRegs<R, NRES> &g) {
+  constexpr int T = AzNetLds<R>::T;
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  __syncthreads();
+  // ---- conv0: 3 -> 16
+  {
+    azf4 acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      acc[t] = azf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (wv + 4 * j < 7) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(s.xin[g.rb0[t] + g.koff0[j]], g.b0[j], acc[t], 0, 0, 0);
+      *(azf4 *)&s.red[((wv * T + t) * 2) * 256 + lane * 4] = acc[t];
+    }
+  }
+  __syncthreads();
+  az_conv_epilogue<R>(s, s.bias, nullptr, s.x[0]);
+  int cur = 0;
+#pragma unroll
+  for (int l = 0; l < 4 * NRES; ++l) {
+    const int src = (l & 1) ? (cur + 1) % 3 : cur;          // second conv of a block reads the first's output
+    const int dst = (l & 1) ? (cur + 2) % 3 : (cur + 1) % 3;
+    __syncthreads();
+    azf4 acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = azf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(s.x[src][g.rb[t] + g.koff[j]], g.br[l][j], acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < T; ++t) *(azf4 *)&s.red[((wv * T + t) * 2) * 256 + lane * 4] = acc[t];
+    __syncthreads();
+    az_conv_epilogue<R>(s, s.bias + 16 + l * 16, (l & 1) ? s.x[cur] : nullptr, s.x[dst]);
+    if (l & 1) cur = dst;
+  }
+  __syncthreads();
+  // ---- 1x1 heads: 16 -> 32 (value 0..15 | policy 16..31), K step = this wave's 4 channels
+  {
+    const float *x = s.x[cur];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float a = x[g.rb[t] + (4 * wv + (lane >> 4)) * kAzPlane + 6];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        azf4 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g.bh[nt], azf4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        *(azf4 *)&s.red[((wv * T + t) * 2 + nt) * 256 + lane * 4] = acc;
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < T * 2 * 256; e += kAzfThreads) {
+    const int t = e >> 9, nt = (e >> 8) & 1, ln = (e >> 2) & 63, v = e & 3;
+    const int m = 16 * t + 4 * (ln >> 4) + v, n = 16 * nt + (ln & 15);
+    if (m >= 9 * R) continue;
+    const int i = e & 511;
+    float acc = s.red[(0 * T + t) * 512 + i];
+    acc += s.red[(1 * T + t) * 512 + i];
+    acc += s.red[(2 * T + t) * 512 + i];
+    acc += s.red[(3 * T + t) * 512 + i];
+    acc += s.bias[16 + 64 * 16 + n];
+    s.hd[(m / 9) * 288 + n * 9 + (m % 9)] = acc > 0.0f ? acc : 0.0f;
+  }
+  __syncthreads();
+  // ---- FC1 per head: (board, head, unit, quarter) -> 4 lanes per dot of 144
+  const float *hw = s.heads;
+  for (int e = tid; e < R * 64; e += kAzfThreads) {
+    const int r = e >> 6, head = (e >> 5) & 1, j = (e >> 2) & 7, qq = e & 3;
+    const float *wrow = hw + (head ? kAzP1 : kAzV1) + j * 144 + qq * 36;
+    const float *in = s.hd + r * 288 + head * 144 + qq * 36;
+    float acc = 0.0f;
+#pragma unroll 12
+    for (int i = 0; i < 36; ++i) acc = fmaf(wrow[i], in[i], acc);
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (qq == 0) s.hid[r * 16 + head * 8 + j] = acc + hw[(head ? kAzP1b : kAzV1b) + j];
+  }
+  __syncthreads();
+  // ---- LayerNorm(8), ReLU, FC2; softmax over the policy logits
+  if (tid < 2 * R) {
+    const int r = tid >> 1, head = tid & 1;
+    const float *h = s.hid + r * 16 + head * 8;
+    float mean = 0.0f;
+    for (int j = 0; j < 8; ++j) mean += h[j];
+    mean *= 0.125f;
+    float var = 0.0f;
+    for (int j = 0; j < 8; ++j) var = fmaf(h[j] - mean, h[j] - mean, var);
+    var *= 0.125f;
+    const float rs = 1.0f / sqrtf(var + 1e-5f);
+    float y[8];
+    const float *gg = hw + (head ? kAzPg : kAzVg), *bb = hw + (head ? kAzPb : kAzVb);
+    for (int j = 0; j < 8; ++j) {
+      const float z = (h[j] - mean) * rs * gg[j] + bb[j];
+      y[j] = z > 0.0f ? z : 0.0f;
+    }
+    if (head == 0) {
+      float v = hw[kAzV2b];
+      for (int j = 0; j < 8; ++j) v = fmaf(hw[kAzV2 + j], y[j], v);
+      s.out[R * 9 + r] = v;
+    } else {
+      float lg[9], mx = -3.4e38f;
+      for (int a = 0; a < 9; ++a) {
+        float z = hw[kAzP2b + a];
+        for (int j = 0; j < 8; ++j) z = fmaf(hw[kAzP2 + a * 8 + j], y[j], z);
+        lg[a] = z;
+        mx = fmaxf(mx, z);
+      }
+      float sum = 0.0f;
+      for (int a = 0; a < 9; ++a) {
+        lg[a] = expf(lg[a] - mx);
+        sum += lg[a];
+      }
+      for (int a = 0; a < 9; ++a) s.out[r * 9 + a] = lg[a] / sum;
+    }
+  }
+  __syncthreads();
+}
+
+// ---- standalone evaluation: state [n][3][3][3] -> probs [n][9], value [n]
+template <int R, int NRES>
+__global__ void __launch_bounds__(kAzfThreads) az_net_eval_kernel(const float *__restrict__ w,
+                                                                  const float *__restrict__ state, int n,
+                                                                  float *probs, float *value) {
+  extern __shared__ float az_smem[];
+  const AzNetSmem s = az_net_carve<R>(az_smem);
+  AzNetRegs<R, NRES> g;
+  az_net_init<R, NRES>(w, s, g);
+  const int b0 = blockIdx.x * R;
+  __syncthreads();
+  for (int e = threadIdx.x; e < R * 27; e += kAzfThreads) {
+    const int r = e / 27, ch = (e % 27) / 9, p = e % 9;
+    s.xin[r * 3 * kAzPlane + ch * kAzPlane + az_interior(p)] = b0 + r < n ? state[(size_t)(b0 + r) * 27 + e % 27] : 0.0f;
+  }
+  az_net_forward<R, NRES>(s, g);
+  for (int e = threadIdx.x; e < R * 10; e += kAzfThreads) {
+    const int r = e < R * 9 ? e / 9 : e - R * 9;
+    if (b0 + r >= n) continue;
+    if (e < R * 9) probs[(size_t)(b0 + r) * 9 + e % 9] = s.out[e];
+    else value[b0 + r] = s.out[e];
+  }
+}
+
+// ---- the fused search
+struct AzFusedArgs {
+  int B, S, cap, with_noise, sample, export_tree;
+  double noise_weight, temperature;
+  uint32_t seed;
+  const int64_t *counter;
+  const float *w;
+  const int32_t *boards, *start_index;
+  int32_t *visits_out;
+  double *probs_out;
+  int32_t *action_out;
+  AzTree t;  // constants (lut_pb, lut_sqrt, noise) and, when export_tree, the destination of the trees
+};
+
+template <int R>
+struct AzTreeLds {
+  static size_t bytes(int cap, int S) {
+    return (size_t)R * cap * 16 + (size_t)(S + 1) * 16 + 81 * 8 + (size_t)R * (9 + 1 + kAzPath + 4 + 1) * 4 + 64;
+  }
+};
+
+template <int R, int NRES>
+__global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArgs a) {
+  extern __shared__ float az_smem[];
+  const int tid = threadIdx.x;
+  const int cap = a.cap, S = a.S;
+  // ---- LDS: doubles first (alignment), then the tree, then the network
+  double *lut_pb = (double *)az_smem;
+  double *lut_sq = lut_pb + (S + 1);
+  double *noise = lut_sq + (S + 1);
+  int32_t *tvisit = (int32_t *)(noise + 81);
+  float *tvsum = (float *)(tvisit + R * cap);
+  float *tprior = tvsum + R * cap;
+  int32_t *tmeta = (int32_t *)(tprior + R * cap);  // first (16 bits, 0xffff: leaf) | nch << 16 | act << 20
+  int32_t *rboard = tmeta + R * cap;
+  int32_t *rplayer = rboard + R * 9;
+  int32_t *path = rplayer + R;
+  int32_t *leaf = path + R * kAzPath;  // depth, done, winner, player
+  int32_t *nnodes = leaf + R * 4;
+  float *netp = (float *)(((uintptr_t)(nnodes + R) + 15) & ~(uintptr_t)15);
+  const AzNetSmem s = az_net_carve<R>(netp);
+  AzNetRegs<R, NRES> g;
+  az_net_init<R, NRES>(a.w, s, g);
+  for (int i = tid; i <= S; i += kAzfThreads) {
+    lut_pb[i] = a.t.lut_pb[i];
+    lut_sq[i] = a.t.lut_sqrt[i];
+  }
+  for (int i = tid; i < 81; i += kAzfThreads) noise[i] = a.t.noise[i];
+  const int grp = tid >> 4, l = tid & 15, gbase = (tid & 63) & ~15;
+  const int b = blockIdx.x * R + grp;
+  const bool active = grp < R && b < a.B;  // group-uniform
+  __syncthreads();  // xin zeroed by az_net_init before the roots are written
+  if (active) {
+    const int player = a.start_index[b] == 0 ? 1 : 2;
+    const int cell = l < 9 ? a.boards[(size_t)b * 9 + l] : 0;
+    if (l < 9) rboard[grp * 9 + l] = cell;
+    if (l == 0) {
+      rplayer[grp] = player;
+      tvisit[grp * cap] = 0;
+      tvsum[grp * cap] = 0.0f;
+      tprior[grp * cap] = 1.0f;
+      tmeta[grp * cap] = 0xffff | (15 << 20);
+      nnodes[grp] = 1;
+    }
+    if (l < 9) {
+      float *st = s.xin + grp * 3 * kAzPlane;
+      const int p = az_interior(l);
+      st[p] = cell == player ? 0.5f : 0.0f;
+      st[kAzPlane + p] = cell == 3 - player ? 0.5f : 0.0f;
+      st[2 * kAzPlane + p] = 0.5f * (float)player;
+    }
+  }
+  const size_t tb = (size_t)grp * cap;
+  for (int sim = -1; sim < S; ++sim) {
+    // ---- descend (sim >= 0)
+    if (sim >= 0 && active) {
+      int cell = l < 9 ? rboard[grp * 9 + l] : 0;
+      int player = rplayer[grp];
+      int node = 0, d = 0;
+      if (l == 0) path[grp * kAzPath] = 0;
+      for (; d < kAzPath - 1;) {  // a board fills after 9 moves: bounded descent
+        const int meta = tmeta[tb + node];
+        const int f = meta & 0xffff;
+        if (f == 0xffff) break;
+        const int n = (meta >> 16) & 15;
+        const int pv = tvisit[tb + node];
+        double sc = -__builtin_inf();
+        if (l < n) {
+          const size_t c = tb + f + l;
+          const int cv = tvisit[c];
+          const float val = cv == 0 ? 0.0f : tvsum[c] / (float)cv;
+          double pb = lut_pb[pv];
+          pb *= lut_sq[pv] / (double)(cv + 1);
+          sc = pb * (double)tprior[c] + (double)val;
+        }
+        int bi = l;
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) {
+          const double os = __shfl_xor(sc, m, kAzGroup);
+          const int oi = __shfl_xor(bi, m, kAzGroup);
+          if (os > sc || (os == sc && oi < bi)) {
+            sc = os;
+            bi = oi;
+          }
+        }
+        node = f + bi;
+        const int mv = (tmeta[tb + node] >> 20) & 15;
+        if (l == mv) cell = player;
+        player = 3 - player;
+        ++d;
+        if (l == 0) path[grp * kAzPath + d] = node;
+      }
+      int bd[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) bd[k] = __shfl(cell, k, kAzGroup);
+      int done, winner;
+      az_done_winner(bd, done, winner);
+      if (l == 0) {
+        leaf[grp * 4 + 0] = d;
+        leaf[grp * 4 + 1] = done;
+        leaf[grp * 4 + 2] = winner;
+        leaf[grp * 4 + 3] = player;
+      }
+      if (l < 9) {
+        float *st = s.xin + grp * 3 * kAzPlane;
+        const int p = az_interior(l);
+        st[p] = cell == player ? 0.5f : 0.0f;
+        st[kAzPlane + p] = cell == 3 - player ? 0.5f : 0.0f;
+        st[2 * kAzPlane + p] = 0.5f * (float)player;
+      }
+      // the leaf board is re-derived from these planes after the network (xin is read-only there)
+    }
+    az_net_forward<R, NRES>(s, g);
+    // ---- expand / back up
+    if (active) {
+      const float pr = l < 9 ? s.out[grp * 9 + l] : 0.0f;
+      if (sim < 0) {
+        const int cell = l < 9 ? rboard[grp * 9 + l] : -1;
+        const bool legal = l < 9 && cell == 0;
+        const uint32_t gm = az_group_mask(legal, gbase);
+        const int n = __popc(gm), rank = __popc(gm & ((1u << l) - 1u));
+        if (legal) {
+          const size_t c = tb + 1 + rank;
+          float p = pr;
+          if (a.with_noise) p = (float)((double)pr * (1.0 - a.noise_weight) + noise[(n - 1) * 9 + rank] * a.noise_weight);
+          tvisit[c] = 0;
+          tvsum[c] = 0.0f;
+          tprior[c] = p;
+          tmeta[c] = 0xffff | (l << 20);
+        }
+        if (l == 0) {
+          tmeta[tb] = (n > 0 ? 1 : 0xffff) | (n << 16) | (15 << 20);
+          nnodes[grp] = 1 + n;
+        }
+      } else {
+        const int depth = leaf[grp * 4 + 0], done = leaf[grp * 4 + 1], winner = leaf[grp * 4 + 2],
+                  player = leaf[grp * 4 + 3];
+        const int node = path[grp * kAzPath + depth];
+        double lv;
+        if (!done) {
+          // leaf board from the network input planes (own stones -> player, opponent's -> 3 - player)
+          int cell = -1;
+          if (l < 9) {
+            const float *st = s.xin + grp * 3 * kAzPlane;
+            const int p = az_interior(l);
+            cell = st[p] > 0.0f ? player : (st[kAzPlane + p] > 0.0f ? 3 - player : 0);
+          }
+          const bool legal = l < 9 && cell == 0;
+          const uint32_t gm = az_group_mask(legal, gbase);
+          const int n = __popc(gm), rank = __popc(gm & ((1u << l) - 1u));
+          const int base = nnodes[grp];
+          if (legal) {
+            const size_t c = tb + base + rank;
+            tvisit[c] = 0;
+            tvsum[c] = 0.0f;
+            tprior[c] = pr;
+            tmeta[c] = 0xffff | (l << 20);
+          }
+          if (l == 0) {
+            tmeta[tb + node] = (tmeta[tb + node] & ~0xfffff) | (n > 0 ? base : 0xffff) | (n << 16);
+            nnodes[grp] = base + n;
+          }
+          lv = (double)s.out[R * 9 + grp];
+        } else {
+          lv = winner == -1 ? 0.0 : (player == winner ? 1.0 : -1.0);
+        }
+        const float v = (float)(-lv);
+        if (l <= depth) {
+          const size_t nd = tb + path[grp * kAzPath + depth - l];
+          tvisit[nd] += 1;
+          tvsum[nd] += (l & 1) ? -v : v;
+        }
+      }
+    }
+  }
+  // ---- finish: root statistics -> visits / probs / action; optional tree export
+  if (active && l == 0) {
+    int v[9];
+    for (int k = 0; k < 9; ++k) v[k] = 0;
+    const int meta = tmeta[tb];
+    const int f = meta & 0xffff, n = (meta >> 16) & 15;
+    for (int j = 0; f != 0xffff && j < n; ++j) v[(tmeta[tb + f + j] >> 20) & 15] = tvisit[tb + f + j];
+    az_finalize(b, v, a.temperature, a.sample, a.seed, a.counter, a.visits_out, a.probs_out, a.action_out);
+  }
+  if (a.export_tree && active) {
+    const size_t gb = (size_t)b * cap;
+    const int nn = nnodes[grp];
+    for (int i = l; i < cap; i += kAzGroup) {
+      const bool live = i < nn;
+      const int meta = tmeta[tb + i];
+      a.t.visit[gb + i] = live ? tvisit[tb + i] : 0;
+      a.t.vsum[gb + i] = live ? tvsum[tb + i] : 0.0f;
+      a.t.prior[gb + i] = live ? tprior[tb + i] : 0.0f;
+      a.t.first[gb + i] = live && (meta & 0xffff) != 0xffff ? (meta & 0xffff) : -1;
+      a.t.nch[gb + i] = live ? (meta >> 16) & 15 : 0;
+      const int act = (meta >> 20) & 15;
+      a.t.act[gb + i] = live && act != 15 ? act : -1;
+    }
+    if (l == 0) a.t.nnodes[b] = nn;
+  }
+}
+
+}  // namespace lzm

@@ -32,6 +32,7 @@
 #include "lzm_numerics.h"
 #include "lzm_collect.h"
 #include "lzm_az.h"
+#include "lzm_az_fused.h"
 #include "lzm_tree.h"
 #include "lzm_search_mlp.h"
 
@@ -1623,6 +1624,158 @@ int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int3
   if (first) LZM_HIP(hipMemcpyAsync(first, t.first, nodes * 4, hipMemcpyDeviceToDevice, s));
   if (nnodes) LZM_HIP(hipMemcpyAsync(nnodes, t.nnodes, (size_t)B * 4, hipMemcpyDeviceToDevice, s));
   return LZM_OK;
+}
+
+}  // extern "C"
+
+// ---- fused AlphaZero search (lzm_az_fused.h)
+static int az_fused_rows(int B) {
+  // boards per workgroup: the fewest that keep the grid within one wave of workgroups per CU
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount
+                                                                                                  : 256;
+  }
+  const char *e = getenv("LZM_AZ_BOARDS_PER_WG");
+  if (e && atoi(e) > 0) return atoi(e);
+  for (int r : {1, 2, 4}) if ((B + r - 1) / r <= cus) return r;
+  return 8;
+}
+
+template <int R>
+static size_t az_fused_lds(int cap, int S) {
+  size_t bytes = (size_t)(2 * (S + 1) + 81) * 8 + (size_t)R * cap * 16 + (size_t)R * (9 + 1 + kAzPath + 4 + 1) * 4;
+  bytes = (bytes + 15) & ~(size_t)15;
+  return bytes + (size_t)AzNetLds<R>::total * 4;
+}
+
+template <int R, int NRES>
+static int az_launch_fused(const AzFusedArgs &a, hipStream_t s) {
+  const size_t lds = az_fused_lds<R>(a.cap, a.S);
+  if (lds > 160 * 1024) {
+    snprintf(g_err, sizeof(g_err), "lzm_az_search_fused: %d boards x %d simulations need %zu B of LDS per workgroup (> 160 KiB)",
+             R, a.S, lds);
+    return LZM_ERR_CAPACITY;
+  }
+  static bool attr = false;
+  if (!attr) {
+    LZM_HIP(hipFuncSetAttribute((const void *)az_search_fused_kernel<R, NRES>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((az_search_fused_kernel<R, NRES>), dim3((a.B + R - 1) / R), dim3(kAzfThreads), lds, s, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+template <int NRES>
+static int az_launch_fused_r(int R, const AzFusedArgs &a, hipStream_t s) {
+  switch (R) {
+    case 1: return az_launch_fused<1, NRES>(a, s);
+    case 2: return az_launch_fused<2, NRES>(a, s);
+    case 4: return az_launch_fused<4, NRES>(a, s);
+    case 8: return az_launch_fused<8, NRES>(a, s);
+  }
+  set_err("lzm_az_search_fused: boards per workgroup must be 1, 2, 4 or 8");
+  return LZM_ERR_ARG;
+}
+
+template <int R, int NRES>
+static int az_launch_eval(const float *w, const float *state, int n, float *probs, float *value, hipStream_t s) {
+  const size_t lds = (size_t)AzNetLds<R>::total * 4;
+  static bool attr = false;
+  if (!attr) {
+    LZM_HIP(hipFuncSetAttribute((const void *)az_net_eval_kernel<R, NRES>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL((az_net_eval_kernel<R, NRES>), dim3((n + R - 1) / R), dim3(kAzfThreads), lds, s, w, state, n,
+                     probs, value);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" {
+
+int64_t lzm_az_net_floats(int nres) { return nres == 1 || nres == 2 ? az_net_layout(nres).total : -1; }
+
+int lzm_az_net_prepare(int nres, const float *raw, float *out) {
+  if ((nres != 1 && nres != 2) || !raw || !out) {
+    set_err("lzm_az_net_prepare: num_res_blocks must be 1 or 2");
+    return LZM_ERR_ARG;
+  }
+  const AzNetLayout L = az_net_layout(nres);
+  memset(out, 0, sizeof(float) * (size_t)L.total);
+  const float *p = raw;
+  const float *w0 = p; p += 16 * 27;
+  const float *b0 = p; p += 16;
+  for (int s = 0; s < 7; ++s)
+    for (int lane = 0; lane < 64; ++lane) {
+      const int k = 4 * s + (lane >> 4);
+      out[L.conv0 + s * 64 + lane] = k < 27 ? w0[(lane & 15) * 27 + k] : 0.0f;
+    }
+  memcpy(out + L.conv0_b, b0, 16 * sizeof(float));
+  for (int l = 0; l < 4 * nres; ++l) {
+    const float *wl = p; p += 16 * 144;
+    const float *bl = p; p += 16;
+    for (int s = 0; s < 36; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        out[L.res + (l * 36 + s) * 64 + lane] = wl[(lane & 15) * 144 + 4 * s + (lane >> 4)];
+    memcpy(out + L.res_b + l * 16, bl, 16 * sizeof(float));
+  }
+  const float *wh = p; p += 32 * 16;
+  const float *bh = p; p += 32;
+  for (int s = 0; s < 4; ++s)
+    for (int nt = 0; nt < 2; ++nt)
+      for (int lane = 0; lane < 64; ++lane)
+        out[L.head + (s * 2 + nt) * 64 + lane] = wh[(16 * nt + (lane & 15)) * 16 + 4 * s + (lane >> 4)];
+  memcpy(out + L.head_b, bh, 32 * sizeof(float));
+  memcpy(out + L.heads, p, kAzHeadFloats * sizeof(float));
+  return LZM_OK;
+}
+
+int lzm_az_net_eval(int nres, const float *weights, const float *state, int n, float *probs, float *value,
+                    void *stream) {
+  if ((nres != 1 && nres != 2) || !weights || !state || n <= 0 || !probs || !value) {
+    set_err("lzm_az_net_eval: need num_res_blocks 1 or 2, n > 0 and all buffers");
+    return LZM_ERR_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  return nres == 1 ? az_launch_eval<2, 1>(weights, state, n, probs, value, s)
+                   : az_launch_eval<2, 2>(weights, state, n, probs, value, s);
+}
+
+int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, const int32_t *boards,
+                        const int32_t *start_index, int with_noise, double noise_weight, double temperature,
+                        int sample, uint32_t seed, const int64_t *counter, int32_t *visits, double *probs,
+                        int32_t *action, int export_tree, void *stream) {
+  if (!az_args_ok(B, S, ws, "lzm_az_search_fused")) return LZM_ERR_ARG;
+  if ((nres != 1 && nres != 2) || !weights || !boards || !start_index || temperature == 0.0 || !visits || !probs ||
+      !action) {
+    set_err("lzm_az_search_fused: need num_res_blocks 1 or 2, temperature != 0 and all buffers");
+    return LZM_ERR_ARG;
+  }
+  if (1 + kAzCells * (S + 1) >= 0xffff) {
+    set_err("lzm_az_search_fused: num_simulations too large for the LDS tree (16-bit node index)");
+    return LZM_ERR_CAPACITY;
+  }
+  AzFusedArgs a;
+  az_carve(B, S, ws, &a.t);
+  a.B = B; a.S = S; a.cap = a.t.cap; a.with_noise = with_noise; a.sample = sample; a.export_tree = export_tree;
+  a.noise_weight = noise_weight; a.temperature = temperature; a.seed = seed; a.counter = counter; a.w = weights;
+  a.boards = boards; a.start_index = start_index; a.visits_out = visits; a.probs_out = probs; a.action_out = action;
+  int R = az_fused_rows(B);
+  if (!getenv("LZM_AZ_BOARDS_PER_WG")) {  // fewer boards per workgroup when the trees outgrow LDS
+    auto lds = [&](int r) {
+      return r == 8 ? az_fused_lds<8>(a.cap, S) : r == 4 ? az_fused_lds<4>(a.cap, S) : r == 2 ? az_fused_lds<2>(a.cap, S)
+                                                                                          : az_fused_lds<1>(a.cap, S);
+    };
+    while (R > 1 && lds(R) > 160 * 1024) R /= 2;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  return nres == 1 ? az_launch_fused_r<1>(R, a, s) : az_launch_fused_r<2>(R, a, s);
 }
 
 }  // extern "C"

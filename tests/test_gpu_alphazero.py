@@ -112,3 +112,88 @@ def test_az_single_board_signature():
     action, probs = m.get_next_action(cfg, az_scripted_pv_torch, 1.0, False)
     ref = az_oracle.search(b, 0, 25, scripted_policy_value, False)
     assert probs == list(ref / 25.0) and action == int(np.argmax(ref))
+
+
+# ---------------------------------------------------------------- fused search (network inside the kernel)
+def _net(seed=0, nres=1):
+    from lightzero_amd.model_az import AlphaZeroModel
+    torch.manual_seed(seed)
+    m = AlphaZeroModel(num_res_blocks=nres, last_linear_layer_init_zero=False)
+    with torch.no_grad():  # non-trivial BatchNorm statistics so the folding is exercised
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.uniform_(-0.2, 0.2)
+                mod.running_var.uniform_(0.5, 1.5)
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.uniform_(-0.1, 0.1)
+    return m.eval().cuda()
+
+
+@pytest.mark.parametrize("nres", [1, 2])
+def test_fused_net_matches_torch_fp32(nres):
+    """the fused network (BN folded, f32 MFMA convolutions) against the torch fp32 module; tolerance
+    |d| <= 2e-5 + 2e-4 |ref| (f32, different summation order and BN folding)"""
+    from lightzero_amd.alphazero import FusedAZNet
+    m = _net(1, nres)
+    net = FusedAZNet(m)
+    boards, starts = random_boards(300, 5, max_moves=8)
+    states = torch.stack([torch.from_numpy(_state(b, s)) for b, s in zip(boards, starts)]).cuda()
+    torch.backends.cudnn.allow_tf32 = False
+    with torch.no_grad():
+        rp, rv = m.compute_policy_value(states)
+        fp, fv = net.compute_policy_value(states)
+    torch.testing.assert_close(fp, rp, atol=2e-5, rtol=2e-4)
+    torch.testing.assert_close(fv, rv, atol=2e-5, rtol=2e-4)
+
+
+def _state(board, start):
+    from oracle.tictactoe import SimTicTacToe
+    e = SimTicTacToe(scale=True)
+    e.reset(int(start), board)
+    return e.current_state()[1].astype(np.float32)
+
+
+@pytest.mark.parametrize("rows", [0, 1, 2, 4, 8], ids=lambda r: f"R{r}")
+@pytest.mark.parametrize("sample", [False, True], ids=["nonoise", "noise"])
+def test_fused_search_equals_stepwise_search(rows, sample, monkeypatch):
+    """the one-launch search against the per-simulation path fed by the same network (lzm_az_net_eval):
+    identical trees (visit counts, value sums, children), action_probs and actions, bit for bit;
+    ragged B (not a multiple of the boards per workgroup)"""
+    from lightzero_amd.alphazero import FusedAZNet
+    if rows:
+        monkeypatch.setenv("LZM_AZ_BOARDS_PER_WG", str(rows))
+    net = FusedAZNet(_net(2))
+    boards, starts = random_boards(37, 9, max_moves=6)
+    S = 30 if rows == 8 else 60  # R = 8 trees of 60 simulations do not fit in LDS
+    a = _mcts(S)
+    with torch.no_grad():
+        act_f, pf = a.search_fused(boards, starts, net, 1.0, sample, export_tree=True)
+        tf = [t.clone() for t in a.export_tree(37)]
+        act_f, pf = act_f.clone(), pf.clone()
+    b = _mcts(S)
+    with torch.no_grad():
+        act_s, ps = b.get_next_actions(boards, starts, net.compute_policy_value, 1.0, sample)
+        ts = b.export_tree(37)
+    assert torch.equal(pf, ps)
+    assert torch.equal(act_f, act_s)
+    nn = ts[3]
+    assert torch.equal(tf[3], nn)
+    for i in range(37):
+        k = int(nn[i])
+        assert torch.equal(tf[0][i, :k], ts[0][i, :k])
+        assert torch.equal(tf[1][i, :k].view(torch.int32), ts[1][i, :k].view(torch.int32))
+        assert torch.equal(tf[2][i, :k], ts[2][i, :k])
+
+
+def test_fused_search_batch_512_properties():
+    from lightzero_amd.alphazero import FusedAZNet
+    net = FusedAZNet(_net(3))
+    boards, starts = random_boards(512, 13)
+    m = _mcts(100)
+    with torch.no_grad():
+        act, probs = m.search_fused(boards, starts, net, 1.0, True)
+    v = m.last_visits(512).cpu().numpy()
+    assert (v.sum(axis=1) == 100).all()
+    assert ((boards != 0) <= (v == 0)).all()
+    a = act.cpu().numpy()
+    assert all(v[i, a[i]] > 0 for i in range(512))
