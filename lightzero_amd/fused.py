@@ -81,8 +81,11 @@ def describe(model):
         raise NotPackable("state_norm")
     if getattr(model, "discrete_action_encoding_type", "one_hot") != "one_hot":
         raise NotPackable("non one-hot action encoding")
-    seqs = [dyn.fc_dynamics_1, dyn.fc_dynamics_2] if res else [dyn.fc_dynamics]
-    seqs += [dyn.fc_reward_head, pred.fc_prediction_common, pred.fc_value_head, pred.fc_policy_head]
+    try:
+        seqs = [dyn.fc_dynamics_1, dyn.fc_dynamics_2] if res else [dyn.fc_dynamics]
+        seqs += [dyn.fc_reward_head, pred.fc_prediction_common, pred.fc_value_head, pred.fc_policy_head]
+    except AttributeError as e:  # e.g. the convolutional MuZeroModel
+        raise NotPackable(f"not a MuZeroModelMLP: {e}") from None
     groups = [_linear_bn_pairs(s) for s in seqs]
     expect_relu = [[True, True]] * (2 if res else 1) + [[True, False], [True, True], [True, False], [True, False]]
     if [len(g) for g in groups] != [len(e) for e in expect_relu]:

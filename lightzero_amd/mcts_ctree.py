@@ -248,6 +248,7 @@ class EfficientZeroMCTSCtree(object):
             self._cfg.model.support_scale, self._cfg.device, self._cfg.model.categorical_distribution
         )
         self._buf = _SearchBuffers()
+        self._graphs = {}
 
     rng_mode = 'glibc'
 
@@ -255,8 +256,40 @@ class EfficientZeroMCTSCtree(object):
     def roots(cls: int, active_collect_env_num: int, legal_actions: List[Any]) -> "ez_tree.Roots":
         return ez_tree.Roots(active_collect_env_num, legal_actions, fast_rng=(cls.rng_mode == 'philox'))
 
+    def _loop(self, t, model, buf, S, row, Hl, rec=None):
+        """The S simulations (mcts_ctree.py:756-827), all enqueued on the current stream."""
+        cfg = self._cfg
+        disc = float(np.float32(cfg.discount_factor))
+        horizon = int(cfg.lstm_horizon_len)
+        cat = bool(cfg.model.get('categorical_distribution', True))
+        B = t.B
+        new_minmax(B, cfg.value_delta_max, t.device, out=buf.mm)
+        for k in range(S):
+            t.traverse(buf.mm, buf.seeds[k:k + 1], buf.vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+            t.gather(buf.pool, row, buf.net_in)
+            t.gather(buf.extra[0], Hl, buf.extra_in[0])
+            t.gather(buf.extra[1], Hl, buf.extra_in[1])
+            out = model.recurrent_inference(buf.net_in, (buf.extra_in[0].unsqueeze(0), buf.extra_in[1].unsqueeze(0)),
+                                            t.action64)
+            logits = out.policy_logits.float().contiguous()
+            if rec is not None:
+                rec.step(k, t, logits)
+            t.decode_backprop(k + 1, disc, buf.mm, out.value_prefix.float().contiguous(), out.value.float().contiguous(),
+                              cat, logits, t.vtp, lstm_horizon=horizon, out_is_reset=t.is_reset,
+                              next_latent=out.latent_state.float().contiguous(), pool_slot=buf.pool[k + 1],
+                              row_elems=row, out_decoded=None if rec is None else rec.decoded[k])
+            if rec is not None:
+                rec.is_reset[k].copy_(t.is_reset)
+            # reset the LSTM state of roots whose search_len % horizon == 0 (mcts_ctree.py:810-816)
+            keep = (1 - t.is_reset).to(torch.float32).unsqueeze(1)
+            hc, hh = out.reward_hidden_state
+            torch.mul(hc.reshape(B, Hl).float(), keep, out=buf.extra[0][k + 1])
+            torch.mul(hh.reshape(B, Hl).float(), keep, out=buf.extra[1][k + 1])
+
     def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
-               reward_hidden_state_roots: List[Any], to_play_batch: Union[int, List[Any]]) -> None:
+               reward_hidden_state_roots: List[Any], to_play_batch: Union[int, List[Any]],
+               seeds: torch.Tensor = None) -> None:
+        """seeds: optional device int32 [num_simulations] traverse seeds (see MuZeroMCTSCtree.search)."""
         with torch.no_grad():
             model.eval()
             t = roots.tree
@@ -264,7 +297,10 @@ class EfficientZeroMCTSCtree(object):
                 raise RuntimeError("search: roots must be prepared (Roots.prepare / prepare_no_noise) first")
             B, S = roots.num, int(self._cfg.num_simulations)
             t.reserve(S)
+            t.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
             dev = t.device
+            if int(self._cfg.lstm_horizon_len) <= 0:
+                raise ValueError("lstm_horizon_len must be > 0 (mcts_ctree.py:809)")
             lat0 = _latent_tensor(latent_state_roots, dev)
             shape = lat0.shape[1:]
             row = int(np.prod(shape)) if len(shape) else 1
@@ -275,29 +311,33 @@ class EfficientZeroMCTSCtree(object):
             buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             buf.extra[0][0].copy_(hc0)
             buf.extra[1][0].copy_(hh0)
-            cfg = self._cfg
-            disc = float(np.float32(cfg.discount_factor))
-            horizon = int(cfg.lstm_horizon_len)
-            if horizon <= 0:
-                raise ValueError("lstm_horizon_len must be > 0 (mcts_ctree.py:809)")
-            mm = new_minmax(B, cfg.value_delta_max, dev)
-            vtp_in = _to_play_tensor(to_play_batch, B, dev)
-            seeds = _seeds(S, dev)
-            cat = bool(cfg.model.get('categorical_distribution', True))
-            for k in range(S):
-                t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
-                t.gather(buf.pool, row, buf.net_in)
-                t.gather(buf.extra[0], Hl, buf.extra_in[0])
-                t.gather(buf.extra[1], Hl, buf.extra_in[1])
-                out = model.recurrent_inference(buf.net_in, (buf.extra_in[0].unsqueeze(0), buf.extra_in[1].unsqueeze(0)),
-                                                t.action64)
-                t.decode_backprop(k + 1, disc, mm, out.value_prefix.float().contiguous(), out.value.float().contiguous(),
-                                  cat, out.policy_logits.float().contiguous(), t.vtp, lstm_horizon=horizon,
-                                  out_is_reset=t.is_reset, next_latent=out.latent_state.float().contiguous(),
-                                  pool_slot=buf.pool[k + 1], row_elems=row)
-                # reset the LSTM state of roots whose search_len % horizon == 0 (mcts_ctree.py:810-816)
-                keep = (1 - t.is_reset).to(torch.float32).unsqueeze(1)
-                hc, hh = out.reward_hidden_state
-                torch.mul(hc.reshape(B, Hl).float(), keep, out=buf.extra[0][k + 1])
-                torch.mul(hh.reshape(B, Hl).float(), keep, out=buf.extra[1][k + 1])
-            roots._last_minmax = mm
+            buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
+            buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
+            rec = None
+            if getattr(self, "record", False):
+                rec = _Recorder(S, B, t.A, dev)
+                rec.is_reset = torch.zeros((S, B), dtype=torch.int32, device=dev)
+                rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
+            if rec is None and self._cfg.get('use_hip_graph', False):
+                self._graph_search(t, model, buf, S, row, Hl)
+            else:
+                self._loop(t, model, buf, S, row, Hl, rec)
+            roots._last_minmax = buf.mm
+            self.last_record = rec
+
+    def _graph_search(self, t, model, buf, S, row, Hl):
+        """The S-simulation loop replayed as one HIP graph (see MuZeroMCTSCtree._graph_search)."""
+        key = (t.h.value, t.generation, id(model), buf.key)
+        g = self._graphs.get(key)
+        if g is None:
+            scratch = DeviceTree(t.B, t.A, max(S, t.sims_capacity), ez=t.ez, fast_rng=t.fast_rng, device=t.device)
+            scratch.copy_roots_from(t)
+            scratch.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
+            self._loop(scratch, model, buf, S, row, Hl)
+            torch.cuda.synchronize(t.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._loop(t, model, buf, S, row, Hl)
+            self._graphs[key] = g
+            scratch.close()
+        g.replay()

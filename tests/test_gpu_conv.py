@@ -1,0 +1,163 @@
+"""GPU: the convolutional Atari configs through the drop-in search (BASELINE.json configs 3 and 5).
+
+Config 3 — Pong EfficientZero: EfficientZeroMCTSCtree.search with the restated EfficientZeroModel
+(latent 64x8x8, LSTM 512, support 101, 6 actions, lstm_horizon_len 5).
+Config 5 — Breakout MuZero: MuZeroMCTSCtree.search with the restated MuZeroModel (latent 64x8x8,
+support 601, 4 actions); the 8-GPU sharding itself is covered by tests/test_dist.py.
+
+Parity as for the other categorical searches (tests/test_gpu_search.py): the tree, fed the decoded
+values it consumed, equals the oracle bit for bit (requests at every simulation, visit counts,
+root values, trajectories; EZ also is_reset), and the decoded values equal a torch fp32
+InverseScalarTransform of the same network outputs within rtol 1e-4 / atol 1e-5 x support_scale.
+The network is the model's own PyTorch-ROCm forward (not pinned to the reference: DI-engine absent).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle.oracle import OracleTree  # noqa: E402
+from tests.helpers import DISC, NOISE_W, PB_C_BASE, PB_C_INIT, VDM  # noqa: E402
+from tests.test_gpu_numerics import torch_inverse_scalar_transform  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def conv_model(kind, seed=0, zero_heads=False):
+    from lightzero_amd.model_conv import atari_efficientzero_model, atari_muzero_model
+    torch.manual_seed(seed)
+    m = (atari_efficientzero_model if kind == "ez" else atari_muzero_model)(last_linear_layer_init_zero=zero_heads)
+    g = torch.Generator().manual_seed(seed + 1)
+    for mod in m.modules():  # non-trivial eval-mode BatchNorm statistics
+        if isinstance(mod, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+            n = mod.num_features
+            mod.running_mean.copy_(torch.randn(n, generator=g) * 0.1)
+            mod.running_var.copy_(torch.rand(n, generator=g) + 0.5)
+            mod.weight.data.copy_(torch.rand(n, generator=g) + 0.5)
+            mod.bias.data.copy_(torch.randn(n, generator=g) * 0.1)
+    return m.to(DEV).eval()
+
+
+def run_search(kind, B, S, seed, graph=False, record=True, model=None, mcts=None):
+    from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree, MuZeroMCTSCtree
+    from lightzero_amd.tree import SequentialSeeds, set_seed_source
+    from lightzero_amd.utils import EasyDict
+    model = conv_model(kind, seed) if model is None else model
+    A = model.action_space_size
+    scale = 50 if kind == "ez" else 300
+    rng = np.random.default_rng(seed)
+    obs = torch.from_numpy(rng.integers(0, 256, size=(B, 4, 64, 64)).astype(np.float32) / 255.0).to(DEV)
+    with torch.no_grad():
+        out = model.initial_inference(obs)
+    noises = rng.dirichlet([0.3] * A, size=B).astype(np.float32)
+    logits0 = out.policy_logits.float().cpu().numpy()
+    cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5,
+                        use_hip_graph=graph, model=dict(support_scale=scale, categorical_distribution=True)))
+    cls = EfficientZeroMCTSCtree if kind == "ez" else MuZeroMCTSCtree
+    mcts = cls(cfg) if mcts is None else mcts
+    mcts.record = record
+    roots = cls.roots(B, [list(range(A))] * B)
+    roots.prepare(0.25, [n.tolist() for n in noises], [0.0] * B, logits0.tolist(), [-1] * B)
+    set_seed_source(SequentialSeeds(seed))
+    try:
+        if kind == "ez":
+            mcts.search(roots, model, out.latent_state, out.reward_hidden_state, [-1] * B)
+        else:
+            mcts.search(roots, model, out.latent_state, [-1] * B)
+    finally:
+        set_seed_source(None)
+    t = roots.tree
+    res = dict(dist=t.distributions().cpu().numpy(), values=t.values().cpu().numpy(),
+               traj=t.trajectories(S + 2).cpu().numpy(), noises=noises, logits0=logits0, model=model,
+               lat0=out.latent_state, hidden0=getattr(out, "reward_hidden_state", None), A=A, scale=scale)
+    res["rec"] = None if mcts.last_record is None else mcts.last_record.numpy() | (
+        {"is_reset": mcts.last_record.is_reset.cpu().numpy()} if kind == "ez" else {})
+    roots.clear()
+    return res
+
+
+def oracle_replay(kind, res, B, S):
+    rec, A = res["rec"], res["A"]
+    ot = OracleTree(B, A, S, ez=(kind == "ez"))
+    ot.set_delta(VDM)
+    ot.prepare(NOISE_W, res["noises"], np.zeros(B, np.float32), res["logits0"], np.full(B, -1, np.int32))
+    for k in range(S):
+        x, y, a, vtp, slen = ot.traverse(PB_C_BASE, PB_C_INIT, DISC, int(rec["seeds"][k]), np.full(B, -1, np.int32))
+        assert np.array_equal(x, rec["x"][k]), f"sim {k}: latent index differs"
+        assert np.array_equal(a, rec["action"][k]), f"sim {k}: action differs"
+        assert np.array_equal(slen, rec["search_len"][k]), f"sim {k}: search_len differs"
+        is_reset = None
+        if kind == "ez":
+            is_reset = (slen % 5 == 0).astype(np.int32)
+            assert np.array_equal(is_reset, rec["is_reset"][k]), f"sim {k}: is_reset differs"
+        ot.backprop(k + 1, DISC, rec["decoded"][k][:, 0], rec["decoded"][k][:, 1], rec["policy_logits"][k], vtp,
+                    is_reset)
+    assert np.array_equal(res["dist"], ot.distributions())
+    assert np.array_equal(res["values"], ot.values())
+    assert np.array_equal(res["traj"], ot.trajectories(S + 2))
+
+
+def torch_replay(kind, res, B, S):
+    """the decoded values the kernel consumed == torch InverseScalarTransform of the same net outputs"""
+    rec, model, scale = res["rec"], res["model"], res["scale"]
+    pool = [res["lat0"].float()]
+    if kind == "ez":
+        hpool = [(res["hidden0"][0].reshape(B, -1).float(), res["hidden0"][1].reshape(B, -1).float())]
+    rows = torch.arange(B, device=DEV)
+    with torch.no_grad():
+        for k in range(S):
+            xs = torch.from_numpy(rec["x"][k]).long().to(DEV)
+            lat = torch.stack(pool)[xs, rows]
+            act = torch.from_numpy(rec["action"][k]).long().to(DEV)
+            if kind == "ez":
+                hs = torch.stack([h[0] for h in hpool])[xs, rows], torch.stack([h[1] for h in hpool])[xs, rows]
+                out = model.recurrent_inference(lat, (hs[0].unsqueeze(0), hs[1].unsqueeze(0)), act)
+                r_logits = out.value_prefix
+                keep = torch.from_numpy(1 - rec["is_reset"][k]).float().to(DEV).unsqueeze(1)
+                hc, hh = out.reward_hidden_state
+                hpool.append((hc.reshape(B, -1) * keep, hh.reshape(B, -1) * keep))
+            else:
+                out = model.recurrent_inference(lat, act)
+                r_logits = out.reward
+            dec = torch.from_numpy(rec["decoded"][k]).to(DEV)
+            torch.testing.assert_close(dec[:, 0], torch_inverse_scalar_transform(r_logits, scale).squeeze(1),
+                                       rtol=1e-4, atol=1e-5 * scale)
+            torch.testing.assert_close(dec[:, 1], torch_inverse_scalar_transform(out.value, scale).squeeze(1),
+                                       rtol=1e-4, atol=1e-5 * scale)
+            torch.testing.assert_close(torch.from_numpy(rec["policy_logits"][k]).to(DEV), out.policy_logits.float(),
+                                       rtol=1e-4, atol=1e-5)
+            pool.append(out.latent_state.float())
+
+
+@pytest.mark.parametrize("kind,B,S", [("ez", 16, 12), ("mz", 16, 12)])
+def test_conv_search_tree_and_decode_parity(kind, B, S):
+    res = run_search(kind, B, S, seed=1)
+    oracle_replay(kind, res, B, S)
+    torch_replay(kind, res, B, S)
+
+
+@pytest.mark.parametrize("kind", ["ez", "mz"])
+def test_conv_search_full_config_tree_parity(kind):
+    """configs 3 / 5 at their per-GPU size: 256 envs x 50 simulations"""
+    B, S = 256, 50
+    res = run_search(kind, B, S, seed=2)
+    oracle_replay(kind, res, B, S)
+    assert (res["dist"].sum(axis=1) == S).all()
+
+
+@pytest.mark.parametrize("kind", ["ez", "mz"])
+def test_conv_search_graph_replay_equals_eager(kind):
+    B, S = 64, 20
+    model = conv_model(kind, 3)
+    from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree, MuZeroMCTSCtree
+    from lightzero_amd.utils import EasyDict
+    eager = run_search(kind, B, S, seed=3, model=model, record=False)
+    cls = EfficientZeroMCTSCtree if kind == "ez" else MuZeroMCTSCtree
+    cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5, use_hip_graph=True,
+                        model=dict(support_scale=50 if kind == "ez" else 300, categorical_distribution=True)))
+    mcts = cls(cfg)
+    for _ in range(2):  # capture, then a plain replay of the cached graph
+        graph = run_search(kind, B, S, seed=3, model=model, record=False, mcts=mcts)
+        assert np.array_equal(graph["dist"], eager["dist"])
+        np.testing.assert_allclose(graph["values"], eager["values"], rtol=0, atol=1e-6)

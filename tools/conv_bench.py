@@ -1,0 +1,104 @@
+"""Search throughput at the convolutional Atari configs (BASELINE.json configs 3 and 5, per GPU):
+256 envs x 50 simulations through the drop-in EfficientZeroMCTSCtree (Pong: restated
+EfficientZeroModel, 6 actions, LSTM 512, support 101) or MuZeroMCTSCtree (Breakout: restated
+MuZeroModel, 4 actions, support 601), random-init weights with non-zero heads, synthetic frames.
+
+Times `searches` full searches (root preparation + search + visit counts, inputs resident in HBM)
+and prints one JSON line with sims/s, the network FLOPs per simulation (torch FlopCounterMode over
+one recurrent_inference at batch B) and the achieved network TFLOP/s against the fp32 MFMA peak.
+
+    python tools/conv_bench.py --kind ez|mz [--envs 256] [--sims 50] [--searches 5] [--graph 1]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree, MuZeroMCTSCtree  # noqa: E402
+from lightzero_amd.model_conv import atari_efficientzero_model, atari_muzero_model  # noqa: E402
+from lightzero_amd.utils import EasyDict  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3
+
+
+def recurrent_flops(model, kind, B, dev):
+    from torch.utils.flop_counter import FlopCounterMode
+    lat = torch.zeros(B, 64, 8, 8, device=dev)
+    act = torch.zeros(B, dtype=torch.int64, device=dev)
+    with torch.no_grad(), FlopCounterMode(display=False) as fc:
+        if kind == "ez":
+            z = torch.zeros(1, B, model.lstm_hidden_size, device=dev)
+            model.recurrent_inference(lat, (z, z), act)
+        else:
+            model.recurrent_inference(lat, act)
+    return fc.get_total_flops() / B
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kind", choices=["ez", "mz"], default="ez")
+    ap.add_argument("--envs", type=int, default=256)
+    ap.add_argument("--sims", type=int, default=50)
+    ap.add_argument("--searches", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--graph", type=int, default=1)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, S = a.envs, a.sims
+    torch.manual_seed(0)
+    model = (atari_efficientzero_model if a.kind == "ez" else atari_muzero_model)(last_linear_layer_init_zero=False)
+    model = model.to(dev).eval()
+    A = model.action_space_size
+    scale = 50 if a.kind == "ez" else 300
+    cls = EfficientZeroMCTSCtree if a.kind == "ez" else MuZeroMCTSCtree
+    cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=dev, lstm_horizon_len=5,
+                        use_hip_graph=bool(a.graph), model=dict(support_scale=scale, categorical_distribution=True)))
+    mcts = cls(cfg)
+    rng = np.random.default_rng(0)
+    obs = torch.from_numpy(rng.integers(0, 256, size=(B, 4, 64, 64)).astype(np.float32) / 255.0).to(dev)
+    noises = torch.from_numpy(rng.dirichlet([0.3] * A, size=B).astype(np.float32)).to(dev)
+    legal = [list(range(A))] * B
+    to_play = torch.full((B,), -1, dtype=torch.int32, device=dev)
+    rewards = torch.zeros(B, dtype=torch.float32, device=dev)
+    seeds = torch.arange(S, dtype=torch.int32, device=dev)
+    with torch.no_grad():
+        out = model.initial_inference(obs)
+    roots = cls.roots(B, legal)
+
+    def one():
+        roots.prepare_device(0.25, noises, rewards, out.policy_logits.float(), to_play)
+        if a.kind == "ez":
+            mcts.search(roots, model, out.latent_state, out.reward_hidden_state, to_play, seeds=seeds)
+        else:
+            mcts.search(roots, model, out.latent_state, to_play, seeds=seeds)
+        return roots.tree.distributions()
+
+    for _ in range(a.warmup):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.searches):
+        d = one()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.searches
+    assert int(d.sum()) == B * S
+    flops = recurrent_flops(model, a.kind, B, dev)
+    net_tflops = flops * B * S / dt / 1e12
+    print(json.dumps({
+        "metric": "MCTS simulations/sec", "value": B * S / dt, "unit": "sims/s", "ms_per_search": dt * 1e3,
+        "config": {"workload": "C3 Pong EfficientZero" if a.kind == "ez" else "C5 Breakout MuZero (per GPU)",
+                   "envs": B, "num_simulations": S, "actions": A, "support": 2 * scale + 1, "latent": [64, 8, 8],
+                   "path": "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph)},
+        "net_flops_per_sim": flops, "net_tflops_whole_search": net_tflops,
+        "fp32_mfma_peak_tflops": FP32_MFMA_PEAK_TFLOPS, "net_frac_of_peak": net_tflops / FP32_MFMA_PEAK_TFLOPS}))
+
+
+if __name__ == "__main__":
+    main()
