@@ -20,10 +20,12 @@ import weakref
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 from . import _lib
 from ._lib import call, ptr, stream_ptr
 from .collect import DeviceSearchStep
+from .trajectory import all_gather_packed, allreduce_stats, pack_episodes, unpack_episodes
 
 
 class DeviceCollector:
@@ -89,8 +91,14 @@ class DeviceCollector:
         self.search.step()
         self.envstep += self.n
 
-    def collect(self, n_episode):
-        """Step until `n_episode` new episodes have finished; returns (episodes, stats)."""
+    def collect(self, n_episode, group=None):
+        """Step until `n_episode` new episodes have finished on this rank; returns (episodes, stats).
+
+        With an initialised torch.distributed process group of more than one rank (one collector
+        per GPU, env-sharded), every rank's finished episodes are packed on its device and
+        all-gathered (lightzero_amd.trajectory, RCCL over xGMI), and the step / episode / duration
+        statistics are sum-reduced (muzero_collector.py:709-712): every rank returns the episodes
+        of all ranks, each tagged with its `rank`."""
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
         steps0 = self.envstep
@@ -105,24 +113,30 @@ class DeviceCollector:
             if new.sum() >= n_episode:
                 break
         el = time.perf_counter() - t0
-        episodes = self._gather(counts)
+        packed, index = self._pack(counts)
         steps = self.envstep - steps0
+        world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        if world > 1:
+            rank = dist.get_rank(group)
+            blocks = all_gather_packed(packed, index, group)
+            episodes = [e for r, (p, i) in enumerate(blocks) for e in unpack_episodes(p, i, self.OBS_DIM, self.A, r)]
+            tot_steps, tot_eps, tot_secs = allreduce_stats(steps, len(index), el, self.dev, group)
+        else:
+            rank = 0
+            episodes = unpack_episodes(packed.cpu().numpy(), index.numpy(), self.OBS_DIM, self.A)
+            tot_steps, tot_eps, tot_secs = steps, len(episodes), el
         stats = dict(envstep=steps, seconds=el, env_steps_per_s=steps / el, sims_per_s=steps * self.S / el,
-                     episode_returns=[float(e["reward_segment"].sum()) for e in episodes])
+                     episode_returns=[float(e["reward_segment"].sum()) for e in episodes], rank=rank, world=world,
+                     total_envstep=tot_steps, total_episodes=tot_eps, total_duration=tot_secs)
         return episodes, stats
 
-    def _gather(self, counts):
+    def _pack(self, counts):
+        """the episodes finished since the last collect, packed on the device (trajectory.pack_episodes)"""
         ln = self.ep_len.cpu().numpy()
-        obs, act = self.rec_obs.cpu().numpy(), self.rec_action.cpu().numpy()
-        rew, child, val = self.rec_reward.cpu().numpy(), self.rec_child.cpu().numpy(), self.rec_value.cpu().numpy()
-        eps = []
+        todo = []
         for i in range(self.n):
             for k in range(int(self._consumed[i]), int(counts[i])):
                 e = k % self.E
-                L = int(ln[i, e])
-                eps.append(dict(env_id=i, obs_segment=obs[i, e, :L + 1].copy(), action_segment=act[i, e, :L].copy(),
-                                reward_segment=rew[i, e, :L].copy(), child_visit_segment=child[i, e, :L].copy(),
-                                root_value_segment=val[i, e, :L].copy(), to_play_segment=np.full(L, -1, np.int32),
-                                action_mask_segment=np.ones((L, self.A), np.int8)))
+                todo.append((i, e, int(ln[i, e])))
             self._consumed[i] = counts[i]
-        return eps
+        return pack_episodes(self.rec_obs, self.rec_action, self.rec_reward, self.rec_child, self.rec_value, todo)

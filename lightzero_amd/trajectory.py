@@ -1,0 +1,101 @@
+"""Trajectory return across ranks: the only data-path collective of the sharded
+collector.
+
+Each rank's DeviceCollector records its envs' episodes in device-resident slots (rec_obs
+[n, E, T+1, obs], rec_action / rec_reward / rec_value [n, E, T], rec_child [n, E, T, A]). After
+`collect()`, the finished episodes are packed on the device into one float32 block (no host copy
+of the payload), the blocks of all ranks are exchanged with one all-gather over the process group
+(RCCL over xGMI on the GPU node, gloo in the CPU tests), and unpacked into GameSegment-shaped
+dicts (the fields of lzero/mcts/buffer/game_segment.py:229-294). The collector statistics are
+sum-reduced as MuZeroCollector does under DDP (lzero/worker/muzero_collector.py:709-712).
+
+Packed layout: episode j of length L occupies L + 1 consecutive rows of width
+W = obs_dim + 1 + 1 + A + 1: [obs_t | action_t | reward_t | child_visits_t (A) | root_value_t];
+row L carries the final observation (the obs segment has L + 1 entries) and zeros elsewhere.
+Actions are small integers, exact in float32. The index is int64 [n_ep, 3] = (env_id, L, first row).
+"""
+from typing import List, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def row_width(obs_dim: int, A: int) -> int:
+    return obs_dim + 3 + A
+
+
+def pack_episodes(rec_obs, rec_action, rec_reward, rec_child, rec_value, episodes: List[Tuple[int, int, int]]):
+    """episodes: [(env_id, slot, L)] -> (packed f32 [rows, W] on the buffers' device, index i64 [n_ep, 3])."""
+    dev = rec_obs.device
+    obs_dim, A = rec_obs.shape[-1], rec_child.shape[-1]
+    W = row_width(obs_dim, A)
+    lens = np.array([L for _, _, L in episodes], np.int64)
+    rows = int((lens + 1).sum())
+    index = np.zeros((len(episodes), 3), np.int64)
+    if not episodes:
+        return torch.zeros((0, W), dtype=torch.float32, device=dev), torch.from_numpy(index)
+    ii = np.repeat([i for i, _, _ in episodes], lens + 1)
+    ee = np.repeat([e for _, e, _ in episodes], lens + 1)
+    starts = np.concatenate([[0], np.cumsum(lens + 1)[:-1]])
+    tt = np.arange(rows) - np.repeat(starts, lens + 1)
+    last = tt == np.repeat(lens, lens + 1)  # the final-observation row of each episode
+    index[:, 0] = [i for i, _, _ in episodes]
+    index[:, 1] = lens
+    index[:, 2] = starts
+    i_t, e_t, t_t = (torch.from_numpy(a).to(dev) for a in (ii, ee, tt))
+    tc = torch.from_numpy(np.where(last, 0, tt)).to(dev)  # clamp to a valid step for the other fields
+    keep = torch.from_numpy(~last).to(dev).to(torch.float32).unsqueeze(1)
+    out = torch.empty((rows, W), dtype=torch.float32, device=dev)
+    out[:, :obs_dim] = rec_obs[i_t, e_t, t_t]
+    out[:, obs_dim:obs_dim + 1] = rec_action[i_t, e_t, tc].to(torch.float32).unsqueeze(1) * keep
+    out[:, obs_dim + 1:obs_dim + 2] = rec_reward[i_t, e_t, tc].unsqueeze(1) * keep
+    out[:, obs_dim + 2:obs_dim + 2 + A] = rec_child[i_t, e_t, tc] * keep
+    out[:, obs_dim + 2 + A:] = rec_value[i_t, e_t, tc].unsqueeze(1) * keep
+    return out, torch.from_numpy(index)
+
+
+def unpack_episodes(packed: np.ndarray, index: np.ndarray, obs_dim: int, A: int, rank: int = 0) -> List[dict]:
+    """GameSegment-shaped dicts from one rank's block (host arrays)."""
+    eps = []
+    for env_id, L, r0 in np.asarray(index, np.int64):
+        blk = packed[r0:r0 + L + 1]
+        eps.append(dict(rank=rank, env_id=int(env_id), obs_segment=blk[:, :obs_dim].copy(),
+                        action_segment=blk[:L, obs_dim].astype(np.int64),
+                        reward_segment=blk[:L, obs_dim + 1].copy(),
+                        child_visit_segment=blk[:L, obs_dim + 2:obs_dim + 2 + A].copy(),
+                        root_value_segment=blk[:L, obs_dim + 2 + A].copy(),
+                        to_play_segment=np.full(L, -1, np.int32), action_mask_segment=np.ones((L, A), np.int8)))
+    return eps
+
+
+def all_gather_packed(packed: torch.Tensor, index: torch.Tensor, group=None):
+    """All-gather variable-size (packed, index) blocks: one size exchange, then one padded
+    all-gather of the payload and one of the index (on the payload's device: RCCL for GPU tensors).
+    Returns host numpy [(packed_r, index_r)] for every rank r."""
+    world = dist.get_world_size(group)
+    dev = packed.device
+    W = packed.shape[1]
+    sizes = torch.tensor([packed.shape[0], index.shape[0]], dtype=torch.int64, device=dev)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    all_sizes = [s.cpu().tolist() for s in all_sizes]
+    max_rows = max(1, max(s[0] for s in all_sizes))
+    max_eps = max(1, max(s[1] for s in all_sizes))
+    pay = torch.zeros((max_rows, W), dtype=torch.float32, device=dev)
+    pay[:packed.shape[0]] = packed
+    idx = torch.zeros((max_eps, 3), dtype=torch.int64, device=dev)
+    idx[:index.shape[0]] = index.to(dev)
+    pays = [torch.empty_like(pay) for _ in range(world)]
+    idxs = [torch.empty_like(idx) for _ in range(world)]
+    dist.all_gather(pays, pay, group=group)
+    dist.all_gather(idxs, idx, group=group)
+    return [(p[:s[0]].cpu().numpy(), i[:s[1]].cpu().numpy()) for p, i, s in zip(pays, idxs, all_sizes)]
+
+
+def allreduce_stats(collected_step: float, collected_episode: float, collected_duration: float, device,
+                    group=None):
+    """muzero_collector.py:709-712: sum the three collector statistics over ranks."""
+    t = torch.tensor([collected_step, collected_episode, collected_duration], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return tuple(float(v) for v in t.cpu().tolist())
