@@ -242,6 +242,24 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
                         int sample, uint32_t seed, const int64_t *counter, int32_t *visits, double *probs,
                         int32_t *action, int export_tree, void *stream);
 
+/* ---- convolutional recurrent trunk (configs 3 / 5: conv MuZeroModel / EfficientZeroModel) --------
+ * The conv part of recurrent_inference (muzero_model.py:505-530, efficientzero_model.py:526-574,
+ * common.py:854-881) with eval BatchNorm folded, one workgroup per env (lzm_conv.h): dynamics conv over
+ * the gathered latent + action map + residual, n_dres basic blocks -> next latent; 1x1 reward conv;
+ * n_pres basic blocks; stacked 1x1 value/policy head conv. Latent 64 x 8 x 8 only.
+ * lzm_conv_trunk_prepare packs, on the host, raw = dyn W[64][64][9] (latent input channels);
+ *   n_dres x { W1[64][64][9], b1[64], W2[64][64][9], b2[64] };  reward W[r_ch][64], b[r_ch];
+ *   n_pres x { same };  head W[h_ch][64], b[h_ch]
+ * into lzm_conv_trunk_floats() floats (copy to the device, 16-byte aligned).
+ * lzm_conv_trunk: input latent of env b = pool[(x[b] * B + b) * 4096 ..] (x nullable: pool[b * 4096]);
+ * actmap float[A][64][64] (action planes' conv + dynamics bias), action int32[B];
+ * outputs out_latent float[B][4096], out_r float[B][r_ch*64], out_h float[B][h_ch*64]. */
+int64_t lzm_conv_trunk_floats(int n_dres, int n_pres);
+int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const float *raw, float *out_host);
+int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,
+                   const float *pool, const int32_t *x, const int32_t *action, float *out_latent, float *out_r,
+                   float *out_h, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -75,9 +75,13 @@ SIGNATURES = {
     "lzm_az_net_prepare": [_i, _vp, _vp],
     "lzm_az_net_eval": [_i, _vp, _vp, _i, _vp, _vp, _vp],
     "lzm_az_search_fused": [_i, _i, _vp, _i, _vp, _vp, _vp, _i, _d, _d, _i, _u32, _vp, _vp, _vp, _vp, _i, _vp],
+    "lzm_conv_trunk_floats": [_i, _i],
+    "lzm_conv_trunk_prepare": [_i, _i, _i, _i, _vp, _vp],
+    "lzm_conv_trunk": [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
-            "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64}
+            "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64,
+            "lzm_conv_trunk_floats": ctypes.c_int64}
 
 _lib = None
 

@@ -1,0 +1,270 @@
+"""Inference-packed recurrent step of the convolutional MuZeroModel / EfficientZeroModel (configs 3, 5).
+
+`recurrent_inference` is what the search calls every simulation (mcts_ctree.py:291-298 /
+:776-790); in eval mode every BatchNorm there is an affine map, so the packed form folds each one
+into the convolution or Linear in front of it (in float64, rounded once to float32):
+
+  dynamics (muzero_model.py:505-530 / efficientzero_model.py:526-574)
+    conv3x3([latent | one-hot action planes]) + BN      -> conv3x3(latent, W_lat) + actmap[a] + b
+        the action planes are constant over the 8x8 plane, so their contribution is a per-action
+        [C, 8, 8] map (border cells see fewer taps), computed once per parameter version;
+    + latent, ReLU; residual blocks (conv+BN folded); 1x1 reward conv + BN folded, ReLU;
+    MuZero: Linear+BN folded, ReLU, Linear -> reward logits;
+    EfficientZero: LSTM cell (one GEMM over [x | h] with both biases), BN1d affine, ReLU,
+    Linear+BN folded, ReLU, Linear -> value-prefix logits;
+  prediction (common.py:854-881)
+    residual blocks; the value and policy 1x1 convs (+BN) as ONE 1x1 conv with 2x16 outputs, ReLU;
+    the two 1024->32 hidden Linears (+BN) as one block-diagonal 2048->64 Linear, ReLU; the two
+    output Linears.
+
+Same outputs as the module within float32 rounding (tests/test_gpu_conv.py); `initial_inference`
+(once per search) is the module's own. Parameters are re-folded in place when the module's
+tensors change (version counters), so captured HIP graphs keep valid pointers.
+
+On the GPU the convolutional trunk (dynamics conv, residual blocks, reward 1x1, prediction blocks,
+head 1x1) is ONE hand-written HIP launch per simulation, one workgroup per env with the
+activations in LDS and f32 MFMA convolutions (csrc/lzm_conv.h, lzm_conv_trunk): it reads the leaf
+latent straight from the search's latent pool and writes the next latent straight into the next
+pool slot (`step_from_pool`), so the gather and the pool filing kernels disappear too. The head
+MLPs and the EfficientZero LSTM cell stay batched GEMMs over the envs.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+class NotFoldable(Exception):
+    pass
+
+
+def _bn_affine(bn):
+    s = bn.weight.double() / torch.sqrt(bn.running_var.double() + bn.eps)
+    return s, bn.bias.double() - bn.running_mean.double() * s
+
+
+def _fold(w, b, bn):
+    """(weight, bias) of a conv / Linear followed by eval BatchNorm -> folded float64 pair"""
+    s, t = _bn_affine(bn)
+    w = w.double() * s.reshape(-1, *([1] * (w.dim() - 1)))
+    b = (b.double() if b is not None else torch.zeros_like(s)) * s + t
+    return w, b
+
+
+def _mlp_linears(seq):
+    """DI-engine MLP (model_mlp.mlp) with one hidden layer: [Linear, BN, act, Linear] -> pairs"""
+    mods = list(seq)
+    if len(mods) != 4 or not isinstance(mods[0], torch.nn.Linear) or not isinstance(mods[1], torch.nn.BatchNorm1d) \
+            or not isinstance(mods[2], torch.nn.ReLU) or not isinstance(mods[3], torch.nn.Linear):
+        raise NotFoldable("head MLP is not [Linear, BatchNorm1d, ReLU, Linear]")
+    return _fold(mods[0].weight, mods[0].bias, mods[1]), (mods[3].weight.double(), mods[3].bias.double())
+
+
+def _resblocks(blocks):
+    out = []
+    for blk in blocks:
+        if getattr(blk, "res_type", "basic") != "basic" or not isinstance(blk.act, torch.nn.ReLU):
+            raise NotFoldable("only basic ReLU residual blocks")
+        out.append((_fold(blk.conv1.weight, None, blk.bn1), _fold(blk.conv2.weight, None, blk.bn2)))
+    return out
+
+
+def fold_tensors(model):
+    """dict name -> float32 tensor of the packed recurrent step"""
+    dyn, pred = model.dynamics_network, model.prediction_network
+    if getattr(model, "state_norm", False):
+        raise NotFoldable("state_norm")
+    if not isinstance(dyn.norm_common, torch.nn.BatchNorm2d) or not isinstance(dyn.activation, torch.nn.ReLU):
+        raise NotFoldable("BN / ReLU variant only")
+    A = dyn.action_encoding_dim
+    C = dyn.num_channels - A
+    hw = tuple(model.latent_hw)
+    t = {}
+    w, b = _fold(dyn.conv.weight, None, dyn.norm_common)
+    t["dyn_w"], t["dyn_b"] = w[:, :C], b
+    planes = torch.zeros(A, A, *hw, dtype=torch.float64, device=w.device)
+    for a in range(A):
+        planes[a, a] = 1.0
+    t["dyn_actmap"] = F.conv2d(planes, w[:, C:], None, padding=1) + b.reshape(1, -1, 1, 1)  # [A, C, h, w]
+    for name, blocks in (("dres", dyn.resblocks), ("pres", pred.resblocks)):
+        for i, ((w1, b1), (w2, b2)) in enumerate(_resblocks(blocks)):
+            t[f"{name}{i}_w1"], t[f"{name}{i}_b1"], t[f"{name}{i}_w2"], t[f"{name}{i}_b2"] = w1, b1, w2, b2
+    t["rw_w"], t["rw_b"] = _fold(dyn.conv1x1_reward.weight, dyn.conv1x1_reward.bias, dyn.norm_reward)
+    (w1, b1), (w2, b2) = _mlp_linears(dyn.fc_reward_head)
+    t["rh_w1"], t["rh_b1"], t["rh_w2"], t["rh_b2"] = w1, b1, w2, b2
+    if hasattr(dyn, "lstm"):
+        l = dyn.lstm
+        if l.num_layers != 1 or l.bidirectional or not l.bias:
+            raise NotFoldable("single-layer LSTM with biases only")
+        t["lstm_w"] = torch.cat([l.weight_ih_l0.double(), l.weight_hh_l0.double()], dim=1)  # [4L, in + L]
+        t["lstm_b"] = l.bias_ih_l0.double() + l.bias_hh_l0.double()
+        t["vp_s"], t["vp_t"] = _bn_affine(dyn.norm_value_prefix)
+    wv, bv = _fold(pred.conv1x1_value.weight, pred.conv1x1_value.bias, pred.norm_value)
+    wp, bp = _fold(pred.conv1x1_policy.weight, pred.conv1x1_policy.bias, pred.norm_policy)
+    t["head_w"], t["head_b"] = torch.cat([wv, wp]), torch.cat([bv, bp])
+    (v1, vb1), (v2, vb2) = _mlp_linears(pred.fc_value)
+    (p1, pb1), (p2, pb2) = _mlp_linears(pred.fc_policy)
+    fv, fp = v1.shape[1], p1.shape[1]
+    hid = torch.zeros(v1.shape[0] + p1.shape[0], fv + fp, dtype=torch.float64, device=v1.device)
+    hid[:v1.shape[0], :fv] = v1
+    hid[v1.shape[0]:, fv:] = p1
+    t["ph_w1"], t["ph_b1"] = hid, torch.cat([vb1, pb1])
+    t["v_w2"], t["v_b2"], t["p_w2"], t["p_b2"] = v2, vb2, p2, pb2
+    return {k: v.float().contiguous() for k, v in t.items()}
+
+
+class FoldedConvNet:
+    """recurrent_inference of a conv MuZeroModel / EfficientZeroModel with every BN folded."""
+
+    def __init__(self, model):
+        self.model = model
+        self.ez = hasattr(model.dynamics_network, "lstm")
+        self.A = model.dynamics_network.action_encoding_dim
+        self.n_dres = len(model.dynamics_network.resblocks)
+        self.n_pres = len(model.prediction_network.resblocks)
+        self.hv = model.prediction_network.conv1x1_value.out_channels
+        self.t = None
+        self._ver = None
+        self.native = None  # device weight blob of lzm_conv_trunk (GPU models with a 64x8x8 latent)
+        self.refresh()
+
+    def _version(self):
+        m = self.model
+        return tuple(x._version for x in list(m.parameters()) + list(m.buffers()))
+
+    def refresh(self):
+        ver = self._version()
+        if ver == self._ver:
+            return
+        with torch.no_grad():
+            new = fold_tensors(self.model)
+            if self.t is None:
+                self.t = new
+            else:  # in place: graphs captured over these tensors stay valid
+                for k, v in new.items():
+                    self.t[k].copy_(v)
+            self._pack_native()
+        self._ver = ver
+
+    def _pack_native(self):
+        t = self.t
+        dev = t["dyn_w"].device
+        if dev.type != "cuda" or tuple(t["dyn_w"].shape) != (64, 64, 3, 3) or t["rw_w"].shape[0] > 32 \
+                or t["head_w"].shape[0] > 32 or tuple(self.model.latent_hw) != (8, 8):
+            return
+        parts = [t["dyn_w"]]
+        for name, n in (("dres", self.n_dres), ("pres", self.n_pres)):
+            if name == "pres":
+                parts += [t["rw_w"], t["rw_b"]]
+            for i in range(n):
+                parts += [t[f"{name}{i}_w1"], t[f"{name}{i}_b1"], t[f"{name}{i}_w2"], t[f"{name}{i}_b2"]]
+        parts += [t["head_w"], t["head_b"]]
+        raw = np.ascontiguousarray(torch.cat([p.reshape(-1) for p in parts]).cpu().numpy(), dtype=np.float32)
+        L = _lib.load()
+        n = L.lzm_conv_trunk_floats(self.n_dres, self.n_pres)
+        host = np.zeros(n, np.float32)
+        self.r_ch, self.h_ch = int(t["rw_w"].shape[0]), int(t["head_w"].shape[0])
+        _lib.check(L.lzm_conv_trunk_prepare(self.n_dres, self.n_pres, self.r_ch, self.h_ch,
+                                            raw.ctypes.data, host.ctypes.data), "lzm_conv_trunk_prepare")
+        blob = torch.from_numpy(host).to(dev)
+        if self.native is None:
+            self.native = blob
+            self.actmap = t["dyn_actmap"]  # [A, 64, 8, 8], re-folded in place
+        else:
+            self.native.copy_(blob)
+
+    def _trunk(self, pool, x, action, out_latent):
+        """lzm_conv_trunk: (reward planes [B, r_ch*64], head planes [B, h_ch*64]); next latent -> out_latent"""
+        B = out_latent.shape[0]
+        act = action if action.dtype == torch.int32 else action.to(torch.int32)
+        r = torch.empty((B, self.r_ch * 64), dtype=torch.float32, device=out_latent.device)
+        h = torch.empty((B, self.h_ch * 64), dtype=torch.float32, device=out_latent.device)
+        _lib.call("lzm_conv_trunk", B, self.n_dres, self.n_pres, self.r_ch, self.h_ch, _lib.ptr(self.native),
+                  _lib.ptr(self.actmap), _lib.ptr(pool), _lib.ptr(x), _lib.ptr(act.contiguous()), _lib.ptr(out_latent),
+                  _lib.ptr(r), _lib.ptr(h), _lib.stream_ptr())
+        return r, h
+
+    def step_from_pool(self, pool, x, action, out_latent, hidden=None):
+        """The recurrent step for leaf latents pool[x[b]][b] (pool [S+1, B, 64, 8, 8]); the next latent
+        is written to out_latent ([B, 64, 8, 8], e.g. the next pool slot). Native trunk only."""
+        r, h = self._trunk(pool, x, action, out_latent)
+        return self._heads(r, h, out_latent, hidden)
+
+    def initial_inference(self, obs):
+        return self.model.initial_inference(obs)
+
+    def _res(self, x, name, n):
+        t = self.t
+        for i in range(n):
+            y = F.conv2d(x, t[f"{name}{i}_w1"], t[f"{name}{i}_b1"], padding=1).relu_()
+            x = F.conv2d(y, t[f"{name}{i}_w2"], t[f"{name}{i}_b2"], padding=1).add_(x).relu_()
+        return x
+
+    def recurrent_inference(self, latent_state, *args):
+        t = self.t
+        if self.ez:
+            hidden, action = args
+        else:
+            (action,), hidden = args, None
+        B = latent_state.shape[0]
+        if self.native is not None and latent_state.is_cuda:
+            nxt = torch.empty((B, 64, 8, 8), dtype=torch.float32, device=latent_state.device)
+            r, h = self._trunk(latent_state.float().contiguous(), None, action, nxt)
+            return self._heads(r, h, nxt, hidden)
+        x = F.conv2d(latent_state, t["dyn_w"], None, padding=1)
+        x.add_(t["dyn_actmap"].index_select(0, action.reshape(-1).long())).add_(latent_state).relu_()
+        nxt = self._res(x, "dres", self.n_dres)
+        r = F.conv2d(nxt, t["rw_w"], t["rw_b"]).relu_().reshape(B, -1)
+        p = self._res(nxt, "pres", self.n_pres)
+        h = F.conv2d(p, t["head_w"], t["head_b"]).relu_().reshape(B, -1)
+        return self._heads(r, h, nxt, hidden)
+
+    def _heads(self, r, hd, nxt, hidden):
+        t = self.t
+        B = r.shape[0]
+        if self.ez:
+            h0, c0 = hidden
+            h0, c0 = h0.reshape(B, -1), c0.reshape(B, -1)
+            gates = torch.addmm(t["lstm_b"], torch.cat([r, h0], dim=1), t["lstm_w"].t())
+            i, f, g, o = gates.chunk(4, dim=1)
+            c1 = torch.sigmoid(f) * c0 + torch.sigmoid(i) * torch.tanh(g)
+            h1 = torch.sigmoid(o) * torch.tanh(c1)
+            r = torch.addcmul(t["vp_t"], h1, t["vp_s"]).relu_()
+        r = F.linear(r, t["rh_w1"], t["rh_b1"]).relu_()
+        reward = F.linear(r, t["rh_w2"], t["rh_b2"])
+        hid = F.linear(hd, t["ph_w1"], t["ph_b1"]).relu_()
+        nv = t["v_w2"].shape[1]
+        value = F.linear(hid[:, :nv], t["v_w2"], t["v_b2"])
+        policy = F.linear(hid[:, nv:], t["p_w2"], t["p_b2"])
+        out = _Out()
+        out.latent_state, out.value, out.policy_logits = nxt, value, policy
+        if self.ez:
+            out.value_prefix = reward
+            out.reward_hidden_state = (h1.unsqueeze(0), c1.unsqueeze(0))
+        else:
+            out.reward = reward
+        return out
+
+
+class _Out:
+    pass
+
+
+class FoldedCache:
+    """FoldedConvNet per model (None for models it does not recognise)."""
+
+    def __init__(self):
+        self._id = None
+        self._net = None
+
+    def get(self, model):
+        if id(model) != self._id:
+            self._id = id(model)
+            try:
+                self._net = FoldedConvNet(model) if hasattr(model, "latent_hw") else None
+            except (NotFoldable, AttributeError):
+                self._net = None
+        elif self._net is not None:
+            self._net.refresh()
+        return self._net

@@ -35,6 +35,7 @@
 #include "lzm_az_fused.h"
 #include "lzm_tree.h"
 #include "lzm_search_mlp.h"
+#include "lzm_conv.h"
 
 namespace lzm {
 
@@ -1776,6 +1777,67 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
   }
   hipStream_t s = (hipStream_t)stream;
   return nres == 1 ? az_launch_fused_r<1>(R, a, s) : az_launch_fused_r<2>(R, a, s);
+}
+
+
+int64_t lzm_conv_trunk_floats(int n_dres, int n_pres) {
+  if (n_dres < 0 || n_pres < 0 || n_dres > 8 || n_pres > 8) return -1;
+  return conv_trunk_layout(n_dres, n_pres).total;
+}
+
+int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const float *raw, float *out) {
+  if (lzm_conv_trunk_floats(n_dres, n_pres) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 || h_ch > 32 || !raw || !out) {
+    set_err("lzm_conv_trunk_prepare: need 0..8 residual blocks, 1..32 reward / head channels and buffers");
+    return LZM_ERR_ARG;
+  }
+  const ConvTrunkLayout L = conv_trunk_layout(n_dres, n_pres);
+  memset(out, 0, sizeof(float) * (size_t)L.total);
+  const float *r = raw;
+  const int W3 = 64 * 64 * 9;
+  conv_pack3(r, out + L.dyn); r += W3;
+  auto blocks = [&](int n, int base) {
+    for (int k = 0; k < n; ++k) {
+      float *o = out + base + k * kCvBlock;
+      conv_pack3(r, o); r += W3;
+      memcpy(o + kCv3Frag, r, 64 * sizeof(float)); r += 64;
+      conv_pack3(r, o + kCv3Frag + 64); r += W3;
+      memcpy(o + 2 * kCv3Frag + 64, r, 64 * sizeof(float)); r += 64;
+    }
+  };
+  blocks(n_dres, L.dres);
+  conv_pack1(r, r_ch, out + L.rw); r += r_ch * 64;
+  memcpy(out + L.rb, r, r_ch * sizeof(float)); r += r_ch;
+  blocks(n_pres, L.pres);
+  conv_pack1(r, h_ch, out + L.hw); r += h_ch * 64;
+  memcpy(out + L.hb, r, h_ch * sizeof(float));
+  return LZM_OK;
+}
+
+int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,
+                   const float *pool, const int32_t *x, const int32_t *action, float *out_latent, float *out_r,
+                   float *out_h, void *stream) {
+  if (B <= 0 || lzm_conv_trunk_floats(n_dres, n_pres) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 || h_ch > 32 ||
+      !weights || !actmap || !pool || !action || !out_latent || !out_r || !out_h) {
+    set_err("lzm_conv_trunk: bad arguments");
+    return LZM_ERR_ARG;
+  }
+  if (((uintptr_t)weights | (uintptr_t)pool) & 15) {
+    set_err("lzm_conv_trunk: weights and pool must be 16-byte aligned");
+    return LZM_ERR_ARG;
+  }
+  static std::once_flag once;
+  static hipError_t attr_err = hipSuccess;
+  const size_t lds = 3 * kCvBuf * sizeof(float);
+  std::call_once(once, [&] {
+    attr_err = hipFuncSetAttribute((const void *)conv_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  });
+  LZM_HIP(attr_err);
+  ConvTrunkArgs a;
+  a.B = B; a.n_dres = n_dres; a.n_pres = n_pres; a.r_ch = r_ch; a.h_ch = h_ch; a.w = weights; a.actmap = actmap;
+  a.pool = pool; a.x = x; a.action = action; a.out_latent = out_latent; a.out_r = out_r; a.out_h = out_h;
+  hipLaunchKernelGGL(conv_trunk_kernel, dim3(B), dim3(kCvThreads), lds, (hipStream_t)stream, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
 }
 
 }  // extern "C"

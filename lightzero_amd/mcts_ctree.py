@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from .ctree import ez_tree, mz_tree
+from .conv_infer import FoldedCache
 from .fused import NotPackable, PackedCache
 from .scaling_transform import InverseScalarTransform
 from .tree import DeviceTree, new_minmax, next_seed
@@ -93,6 +94,21 @@ class _SearchBuffers:
         return self
 
 
+def _step_net(mcts, model):
+    """the BN-folded recurrent step for the conv MuZeroModel / EfficientZeroModel family
+    (conv_infer.FoldedConvNet, cfg.fold_network, default on), else the model itself"""
+    if mcts._cfg.get('fold_network', True):
+        net = mcts._folded.get(model)
+        if net is not None:
+            return net
+    return model
+
+
+def _native_trunk(net, buf):
+    """the step net runs the lzm_conv_trunk kernel straight on the latent pool"""
+    return getattr(net, "native", None) is not None and tuple(buf.pool.shape[2:]) == (64, 8, 8)
+
+
 class MuZeroMCTSCtree(object):
     """MCTS for MuZero on the GPU (reference: mcts_ctree.py:172-321)."""
 
@@ -121,6 +137,7 @@ class MuZeroMCTSCtree(object):
         self._buf = _SearchBuffers()
         self._graphs = {}
         self._packed = PackedCache()
+        self._folded = FoldedCache()
 
     # 'glibc': the reference's tie-break stream, bit-exact (default); 'philox': independent
     # counter-based stream per root (LZM_RNG_FAST), no batch-serial dependency.
@@ -152,16 +169,21 @@ class MuZeroMCTSCtree(object):
         disc = float(np.float32(cfg.discount_factor))
         cat = self._categorical()
         new_minmax(t.B, cfg.value_delta_max, t.device, out=mm)
+        model = _step_net(self, model)
+        native = _native_trunk(model, buf)
         for k in range(S):
             t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
-            t.gather(buf.pool, row, buf.net_in)
-            out = model.recurrent_inference(buf.net_in, t.action64)
+            if native:  # leaf latents read from the pool and the next latents filed by the trunk kernel
+                out = model.step_from_pool(buf.pool, t.x, t.action, buf.pool[k + 1])
+            else:
+                t.gather(buf.pool, row, buf.net_in)
+                out = model.recurrent_inference(buf.net_in, t.action64)
             logits = out.policy_logits.float().contiguous()
             if rec is not None:
                 rec.step(k, t, logits)
             t.decode_backprop(k + 1, disc, mm, out.reward.float().contiguous(), out.value.float().contiguous(), cat,
-                              logits, t.vtp, next_latent=out.latent_state.float().contiguous(),
-                              pool_slot=buf.pool[k + 1], row_elems=row,
+                              logits, t.vtp, next_latent=None if native else out.latent_state.float().contiguous(),
+                              pool_slot=None if native else buf.pool[k + 1], row_elems=0 if native else row,
                               out_decoded=None if rec is None else rec.decoded[k])
 
     def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
@@ -219,6 +241,7 @@ class MuZeroMCTSCtree(object):
                 self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row)
             self._graphs[key] = g
             scratch.close()
+        _step_net(self, model)  # re-fold in place if the parameters changed since capture
         g.replay()
 
 
@@ -249,6 +272,7 @@ class EfficientZeroMCTSCtree(object):
         )
         self._buf = _SearchBuffers()
         self._graphs = {}
+        self._folded = FoldedCache()
 
     rng_mode = 'glibc'
 
@@ -264,20 +288,26 @@ class EfficientZeroMCTSCtree(object):
         cat = bool(cfg.model.get('categorical_distribution', True))
         B = t.B
         new_minmax(B, cfg.value_delta_max, t.device, out=buf.mm)
+        model = _step_net(self, model)
+        native = _native_trunk(model, buf)
         for k in range(S):
             t.traverse(buf.mm, buf.seeds[k:k + 1], buf.vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
-            t.gather(buf.pool, row, buf.net_in)
             t.gather(buf.extra[0], Hl, buf.extra_in[0])
             t.gather(buf.extra[1], Hl, buf.extra_in[1])
-            out = model.recurrent_inference(buf.net_in, (buf.extra_in[0].unsqueeze(0), buf.extra_in[1].unsqueeze(0)),
-                                            t.action64)
+            hidden = (buf.extra_in[0].unsqueeze(0), buf.extra_in[1].unsqueeze(0))
+            if native:
+                out = model.step_from_pool(buf.pool, t.x, t.action, buf.pool[k + 1], hidden)
+            else:
+                t.gather(buf.pool, row, buf.net_in)
+                out = model.recurrent_inference(buf.net_in, hidden, t.action64)
             logits = out.policy_logits.float().contiguous()
             if rec is not None:
                 rec.step(k, t, logits)
             t.decode_backprop(k + 1, disc, buf.mm, out.value_prefix.float().contiguous(), out.value.float().contiguous(),
                               cat, logits, t.vtp, lstm_horizon=horizon, out_is_reset=t.is_reset,
-                              next_latent=out.latent_state.float().contiguous(), pool_slot=buf.pool[k + 1],
-                              row_elems=row, out_decoded=None if rec is None else rec.decoded[k])
+                              next_latent=None if native else out.latent_state.float().contiguous(),
+                              pool_slot=None if native else buf.pool[k + 1], row_elems=0 if native else row,
+                              out_decoded=None if rec is None else rec.decoded[k])
             if rec is not None:
                 rec.is_reset[k].copy_(t.is_reset)
             # reset the LSTM state of roots whose search_len % horizon == 0 (mcts_ctree.py:810-816)
@@ -340,4 +370,5 @@ class EfficientZeroMCTSCtree(object):
                 self._loop(t, model, buf, S, row, Hl)
             self._graphs[key] = g
             scratch.close()
+        _step_net(self, model)  # re-fold in place if the parameters changed since capture
         g.replay()

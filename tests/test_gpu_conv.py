@@ -161,3 +161,39 @@ def test_conv_search_graph_replay_equals_eager(kind):
         graph = run_search(kind, B, S, seed=3, model=model, record=False, mcts=mcts)
         assert np.array_equal(graph["dist"], eager["dist"])
         np.testing.assert_allclose(graph["values"], eager["values"], rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["ez", "mz"])
+def test_native_trunk_matches_module(kind):
+    """lzm_conv_trunk (+ batched heads) == the module's recurrent_inference (fp32, rtol 1e-4 / atol 1e-5)"""
+    from lightzero_amd.conv_infer import FoldedConvNet
+    model = conv_model(kind, 5)
+    net = FoldedConvNet(model)
+    assert net.native is not None, "native trunk not packed on the GPU"
+    B = 37
+    g = torch.Generator(device=DEV).manual_seed(0)
+    lat = torch.relu(torch.randn(B, 64, 8, 8, generator=g, device=DEV))
+    act = torch.randint(0, model.action_space_size, (B,), generator=g, device=DEV)
+    with torch.no_grad():
+        if kind == "ez":
+            hc = (torch.randn(1, B, 512, generator=g, device=DEV) * 0.5, torch.randn(1, B, 512, generator=g, device=DEV) * 0.5)
+            ref, got = model.recurrent_inference(lat, hc, act), net.recurrent_inference(lat, hc, act)
+            torch.testing.assert_close(got.value_prefix, ref.value_prefix, rtol=1e-4, atol=1e-5)
+            for a, b in zip(got.reward_hidden_state, ref.reward_hidden_state):
+                torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
+        else:
+            ref, got = model.recurrent_inference(lat, act), net.recurrent_inference(lat, act)
+            torch.testing.assert_close(got.reward, ref.reward, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(got.latent_state, ref.latent_state, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(got.value, ref.value, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(got.policy_logits, ref.policy_logits, rtol=1e-4, atol=1e-5)
+        # pool-indexed form: leaf latents pool[x[b]][b], next latent into a pool slot
+        pool = torch.relu(torch.randn(4, B, 64, 8, 8, generator=g, device=DEV))
+        x = torch.randint(0, 4, (B,), generator=g, device=DEV).to(torch.int32)
+        slot = torch.empty(B, 64, 8, 8, device=DEV)
+        hid = hc if kind == "ez" else None
+        o1 = net.step_from_pool(pool, x, act.to(torch.int32), slot, hid)
+        leaf = pool[x.long(), torch.arange(B, device=DEV)]
+        o2 = net.recurrent_inference(leaf, hc, act) if kind == "ez" else net.recurrent_inference(leaf, act)
+        assert torch.equal(slot, o2.latent_state) and torch.equal(o1.value, o2.value)
+        assert torch.equal(o1.policy_logits, o2.policy_logits)
