@@ -1,4 +1,5 @@
 """Builds liblzmcts.so in-tree for gfx950 (hipcc). Invoked by __graft_entry__.build()."""
+import glob
 import os
 import subprocess
 import sys
@@ -14,7 +15,7 @@ ARCH = os.environ.get("LZM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-fPIC", "-shared", "-Wall",
          f"--offload-arch={ARCH}"]
 SOURCES = [os.path.join(HERE, "csrc", "lzm_kernels.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", h) for h in ("lzm_numerics.h", "lzm_tree.h", "lzm_search_mlp.h", "lzm_collect.h", "lzm_az.h", "lzm_az_fused.h")] + [
+DEPS = SOURCES + sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))) + [
     os.path.join(REPO, "include", "lzmcts.h")]
 OUT = os.path.join(HERE, "liblzmcts.so")
 
