@@ -35,6 +35,7 @@
 #include "lzm_az_fused.h"
 #include "lzm_tree.h"
 #include "lzm_search_mlp.h"
+#include "lzm_search_res.h"
 #include "lzm_conv.h"
 
 namespace lzm {
@@ -1247,6 +1248,73 @@ void build_schedule(SearchArgs &p, const KLayer *kl, int nk, const size_t *w_off
   p.nsteps = n;
   (void)nk;
 }
+// ---- network-resident search (lzm_search_res.h): the config-2 shape, one root per workgroup
+bool res_shape_ok(int H, int A, int F, int V, int res) {
+  return H == kRHid && F == kRF && V == kRV && res && A >= 1 && A <= kRMaxA;
+}
+bool res_enabled() {
+  const char *e = getenv("LZM_FUSED_RES");  // "0": always the streaming kernel (experiments)
+  return !(e && atoi(e) == 0);
+}
+struct ResSrc {
+  size_t pw[12], pb[12];
+  int N[12];
+};
+// resident float d <- packed network (res_source defines the layout)
+__global__ void mlp_res_swizzle_kernel(const float *packed, ResSrc src, int A, float *dst, size_t n) {
+  const size_t d = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  int b = 0;
+  size_t o = 0;
+  while (b + 1 < kRbN && d >= o + res_block_floats(b, A)) o += res_block_floats(b++, A);
+  int layer, k, col;
+  res_source(b, d - o, A, &layer, &k, &col);
+  float v = 0.0f;
+  if (layer >= 0) v = k < 0 ? packed[src.pb[layer] + col] : packed[src.pw[layer] + (size_t)k * src.N[layer] + col];
+  dst[d] = v;
+}
+// LDS plan of search_res_kernel (float offsets, 16-B aligned); returns bytes, or 0 if it does not fit
+size_t plan_res(SearchArgs &p, ResNet &n, const lzm_handle *h, int S, int A) {
+  size_t o = 0;
+  p.tree_in_lds = 1;
+  p.off_stat = o; o += (size_t)h->cap * 4;
+  p.off_meta = o; o += (size_t)h->cap * 4;
+  p.off_lut = o; o += round4((size_t)2 * h->lut_n);
+  p.off_legal = o; o += round4((size_t)A + 1);
+  p.off_val = o; o += round4((size_t)h->cap);
+  p.off_path = o; o += round4((size_t)h->depth_cap);
+  p.off_pact = o; o += round4((size_t)h->depth_cap);
+  n.off_x0 = (int)o; o += kRHid;
+  n.off_t1 = (int)o; o += kRHid;
+  n.off_nl = (int)o; o += kRHid;
+  n.off_t2 = (int)o; o += kRHid;
+  n.off_t3 = (int)o; o += kRHid;
+  n.off_rh = (int)o; o += kRF;
+  n.off_hv = (int)o; o += 2 * kRF;
+  n.off_lg = (int)o; o += kRMaxA;
+  n.off_act = (int)o; o += (size_t)A * kRHid;
+  p.off_misc = o; o += round4((size_t)S + 32);
+  n.off_wd1 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
+  n.off_wd2 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
+  constexpr size_t kResMax = 160 * 1024 - 2048;  // static LDS of the kernel below 2 KiB
+  // pUCT visit table (optional: the descent divides without it)
+  const size_t tri = round4((size_t)h->lut_n * (h->lut_n + 1) / 2);
+  p.pbt_rows = ((o + tri) * sizeof(float) <= kResMax && tri <= 8192) ? h->lut_n : 0;
+  p.off_pbt = o;
+  if (p.pbt_rows) o += tri;
+  return o * sizeof(float) <= kResMax ? o * sizeof(float) : 0;
+}
+void res_net(ResNet &n, const float *wres, int A) {
+  auto blk = [&](int b) { return wres + res_block_offset(b, A); };
+  for (int q = 0; q < 6; ++q) n.d[q] = reinterpret_cast<const float4 *>(blk(kRbD + q));
+  n.rh = reinterpret_cast<const float4 *>(blk(kRbRH));
+  n.vph = reinterpret_cast<const float4 *>(blk(kRbVPH));
+  n.rs = reinterpret_cast<const float4 *>(blk(kRbRS));
+  n.vs = reinterpret_cast<const float4 *>(blk(kRbVS));
+  n.po = reinterpret_cast<const float4 *>(blk(kRbPO));
+  n.bd = blk(kRbBD); n.brh = blk(kRbBRH); n.bvph = blk(kRbBVPH); n.brs = blk(kRbBRS); n.bvs = blk(kRbBVS);
+  n.bpo = blk(kRbBPO); n.act = blk(kRbAct);
+}
 }  // namespace
 
 extern "C" {
@@ -1270,7 +1338,10 @@ int64_t lzm_mlp_kernel_floats(int hidden, int actions, int head_hidden, int supp
   KLayer kl[12];
   const int nk = kernel_layers(s, res_dynamics, kl);
   size_t w_off[12], b_off[12];
-  return (int64_t)kernel_layout(kl, nk, w_off, b_off);
+  size_t total = kernel_layout(kl, nk, w_off, b_off);
+  // the network-resident kernel's layout follows (lzm_search_res.h), for the shape it serves
+  if (res_shape_ok(hidden, actions, head_hidden, support, res_dynamics)) total = round4(total) + res_block_offset(kRbN, actions);
+  return (int64_t)total;
 }
 
 int lzm_mlp_prepare(int hidden, int actions, int head_hidden, int support, int res_dynamics, const float *packed,
@@ -1301,6 +1372,19 @@ int lzm_mlp_prepare(int hidden, int actions, int head_hidden, int support, int r
     if (q.src1 >= 0)
       LZM_HIP(hipMemcpyAsync(out + b_off[l] + q.N0, packed + pb[q.src1], (size_t)(q.N - q.N0) * sizeof(float),
                              hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  }
+  if (res_shape_ok(hidden, actions, head_hidden, support, res_dynamics)) {
+    ResSrc src;
+    for (int l = 0; l < 12; ++l) {
+      src.pw[l] = pw[l];
+      src.pb[l] = pb[l];
+      src.N[l] = s[l].N;
+    }
+    const size_t base = round4(kernel_layout(kl, nk, w_off, b_off));
+    const size_t n = res_block_offset(kRbN, actions);
+    hipLaunchKernelGGL(mlp_res_swizzle_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       packed, src, actions, out + base, n);
+    LZM_CHECK_LAUNCH();
   }
   return LZM_OK;
 }
@@ -1370,6 +1454,25 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.phase = h->phase;
   p.diag_mode = getenv("LZM_DIAG_MODE") ? atoi(getenv("LZM_DIAG_MODE")) : 0;  // timing experiments only
   p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
+  if (R == 1 && res_enabled() && res_shape_ok(H, A, F, V, res_dynamics)) {
+    // the network-resident kernel (lzm_search_res.h); its weights follow the generic layout
+    SearchArgs q = p;
+    ResNet n;
+    memset(&n, 0, sizeof(n));
+    const size_t lds = plan_res(q, n, h, S, A);
+    if (lds) {
+      res_net(n, weights + round4(kernel_layout(kls, nkl, lay_w, lay_b)), A);
+      hipError_t e = hipFuncSetAttribute((const void *)search_res_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds);
+      if (e == hipSuccess) {
+        hipLaunchKernelGGL(search_res_kernel, dim3(G), dim3(kRT), lds, (hipStream_t)stream, q, n);
+        e = hipGetLastError();
+      }
+      LZM_HIP(e);
+      LZM_CHECK_LAUNCH();
+      return LZM_OK;
+    }
+  }
   // dynamic LDS plan (float offsets, 16-B aligned)
   size_t o = 0;
   const size_t tree_floats = (size_t)h->cap * R * 4;
