@@ -238,8 +238,13 @@ def roots_per_workgroup(B, device):
 
 
 def _lib_kernel_floats(H=128, A=2, F=32, V=601, res=1):
+    """floats of the weight-streaming kernel's layout (lzm_mlp_kernel_floats, minus the resident
+    kernel's blocks that follow it for the config-2 shape: lzm_search_res.h res_block_floats)"""
     from lightzero_amd import _lib
-    return int(_lib.load().lzm_mlp_kernel_floats(H, A, F, V, res))
+    n = int(_lib.load().lzm_mlp_kernel_floats(H, A, F, V, res))
+    if (H, F, V, res) == (128, 32, 601, 1) and A <= 32:
+        n -= 6 * 16384 + 4096 + 8192 + 2 * 20480 + 1024 + 6 * 128 + 32 + 64 + 2 * 604 + 32 + A * 128
+    return n
 
 
 def pmc_traffic(kernel):
@@ -356,11 +361,20 @@ def main():
             sec = ms["search_mlp"] * 1e-3
             achieved = flops / sec / 1e12
             R = roots_per_workgroup(B, device)
-            wbytes = 4 * _lib_kernel_floats()
-            l2 = -(-B // R) * S * wbytes  # every workgroup streams the kernel-layout weights once per simulation
-            roofline = {"bound": "mfma", "kernel": "search_mlp_kernel", "achieved": round(achieved, 3),
+            from lightzero_amd import _lib
+            resident = int(_lib.load().lzm_search_mlp_kind(B, 2, 128, 32, 601, 1)) == 1
+            if resident:
+                # search_res_kernel streams fc_dynamics[0] (16 slots) and the two support heads
+                # (20 slots each) per simulation, slots of 256 lanes x 16 B (lzm_search_res.h)
+                kname = "search_res_kernel"
+                l2 = B * S * (16 + 20 + 20) * 256 * 16
+            else:
+                kname = "search_mlp_kernel"
+                wbytes = 4 * _lib_kernel_floats()
+                l2 = -(-B // R) * S * wbytes  # every workgroup streams the kernel-layout weights once per simulation
+            roofline = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-                        "traffic": pmc_traffic("search_mlp_kernel"), "alg_flops_per_launch": int(flops),
+                        "traffic": pmc_traffic(kname), "alg_flops_per_launch": int(flops),
                         "alg_hbm_bytes_per_launch": int(hbm), "hbm_achieved_GBs": round(hbm / sec / 1e9, 2),
                         "l2_weight_bytes_per_launch": int(l2), "l2_achieved_TBs": round(l2 / sec / 1e12, 3),
                         "l2_peak_TBs": L2_PEAK_TBS, "roots_per_workgroup": R,

@@ -154,6 +154,10 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
                    int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
                    const uint32_t *seeds, const int32_t *virtual_to_play, float *latent_pool, int32_t *rec_x,
                    int32_t *rec_a, int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream);
+/* Which kernel lzm_search_mlp launches for a batch of B roots with `actions` actions and this
+ * network: 1 = network-resident (search_res_kernel, lzm_search_res.h: the config-2 shape with one
+ * root per workgroup), 0 = weight-streaming (search_mlp_kernel). Host-only, no GPU work. */
+int lzm_search_mlp_kind(int B, int actions, int hidden, int head_hidden, int support, int res_dynamics);
 /* int32[2]: {look-back spin timeouts (must stay 0), slices resolved serially (ties that reached
  * an expanded child)} accumulated over the handle's fused searches. */
 int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream);

@@ -54,6 +54,7 @@ SIGNATURES = {
     "lzm_last_traverse_passes": [_vp, _vp, _vp],
     "lzm_mlp_packed_floats": [_i, _i, _i, _i, _i],
     "lzm_mlp_kernel_floats": [_i, _i, _i, _i, _i],
+    "lzm_search_mlp_kind": [_i, _i, _i, _i, _i, _i],
     "lzm_mlp_prepare": [_i, _i, _i, _i, _i, _vp, _vp, _vp],
     "lzm_search_mlp": [_vp, _i, _i, _i, _i, _vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_diagnostics": [_vp, _vp, _vp],

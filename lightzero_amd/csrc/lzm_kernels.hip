@@ -1284,19 +1284,13 @@ size_t plan_res(SearchArgs &p, ResNet &n, const lzm_handle *h, int S, int A) {
   p.off_val = o; o += round4((size_t)h->cap);
   p.off_path = o; o += round4((size_t)h->depth_cap);
   p.off_pact = o; o += round4((size_t)h->depth_cap);
-  n.off_x0 = (int)o; o += kRHid;
-  n.off_t1 = (int)o; o += kRHid;
-  n.off_nl = (int)o; o += kRHid;
-  n.off_t2 = (int)o; o += kRHid;
-  n.off_t3 = (int)o; o += kRHid;
-  n.off_rh = (int)o; o += kRF;
-  n.off_hv = (int)o; o += 2 * kRF;
-  n.off_lg = (int)o; o += kRMaxA;
   n.off_act = (int)o; o += (size_t)A * kRHid;
   p.off_misc = o; o += round4((size_t)S + 32);
   n.off_wd1 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
   n.off_wd2 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
-  constexpr size_t kResMax = 160 * 1024 - 2048;  // static LDS of the kernel below 2 KiB
+  // static LDS of the kernel: activations (two rows), biases, scalars (below 2 KiB)
+  constexpr size_t kResStatic = (kRHid + 2 * (6 * kRHid + kRF + 2 * kRF + kRMaxA) + kResBiasFloats) * 4 + 2048;
+  constexpr size_t kResMax = 160 * 1024 - kResStatic;
   // pUCT visit table (optional: the descent divides without it)
   const size_t tri = round4((size_t)h->lut_n * (h->lut_n + 1) / 2);
   p.pbt_rows = ((o + tri) * sizeof(float) <= kResMax && tri <= 8192) ? h->lut_n : 0;
@@ -1389,6 +1383,13 @@ int lzm_mlp_prepare(int hidden, int actions, int head_hidden, int support, int r
   return LZM_OK;
 }
 
+int lzm_search_mlp_kind(int B, int actions, int hidden, int head_hidden, int support, int res_dynamics) {
+  if (B <= 0) return 0;
+  return (roots_per_wg(B) == 1 && res_enabled() && res_shape_ok(hidden, actions, head_hidden, support, res_dynamics))
+             ? 1
+             : 0;
+}
+
 int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int res_dynamics, const float *weights,
                    int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
                    const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, int32_t *rec_x, int32_t *rec_a,
@@ -1462,10 +1463,17 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     const size_t lds = plan_res(q, n, h, S, A);
     if (lds) {
       res_net(n, weights + round4(kernel_layout(kls, nkl, lay_w, lay_b)), A);
-      hipError_t e = hipFuncSetAttribute((const void *)search_res_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds);
+      // LZM_RES_SPEC=1 (parity mode): evaluate two-way leaf ties speculatively as a second network
+      // row instead of waiting for the look-back (measured slower: every simulation pays the row)
+      const char *se = getenv("LZM_RES_SPEC");
+      const bool spec = !fast && se && atoi(se) == 1;
+      const void *fn = spec ? (const void *)search_res_kernel<2> : (const void *)search_res_kernel<1>;
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e == hipSuccess) {
-        hipLaunchKernelGGL(search_res_kernel, dim3(G), dim3(kRT), lds, (hipStream_t)stream, q, n);
+        if (!spec)
+          hipLaunchKernelGGL(search_res_kernel<1>, dim3(G), dim3(kRT), lds, (hipStream_t)stream, q, n);
+        else
+          hipLaunchKernelGGL(search_res_kernel<2>, dim3(G), dim3(kRT), lds, (hipStream_t)stream, q, n);
         e = hipGetLastError();
       }
       LZM_HIP(e);

@@ -61,9 +61,11 @@ struct ResNet {
   const float4 *rh, *vph, *rs, *vs, *po;
   const float *bd, *brh, *bvph, *brs, *bvs, *bpo, *act;
   // LDS float offsets beyond SearchArgs' tree plan
-  int off_x0, off_t1, off_nl, off_t2, off_t3, off_rh, off_hv, off_lg, off_act, off_wd1, off_wd2;
+  int off_act, off_wd1, off_wd2;
 };
 
+// floats of the bias blocks ([6][128] D, [32] RH, [64] VPH, [604] RS, [604] VS, [32] PO)
+constexpr int kResBiasFloats = 6 * 128 + 32 + 64 + 2 * 604 + 32;
 enum ResBlock { kRbD = 0, kRbRH = 6, kRbVPH, kRbRS, kRbVS, kRbPO, kRbBD, kRbBRH, kRbBVPH, kRbBRS, kRbBVS, kRbBPO, kRbAct, kRbN };
 
 // float count of each block (A actions)
@@ -167,47 +169,98 @@ __device__ __forceinline__ float dense128(const float *x, WF w) {
 
 // Logits of one support head (input: 32 floats in LDS; weights: the 20-slot buffer P): lane l
 // gets columns l, 256 + l and (l < 2 * kRTail, l even) 512 + (l >> 1).
-__device__ __forceinline__ void support_logits(const float *h, const float4 *P, float b0, float b1, float b2,
-                                               float &z0, float &z1, float &z2) {
+__device__ __forceinline__ void support_logits(const float *h, const float4 *P, const float *bias, float &z0, float &z1,
+                                               float &z2) {
+  const int tid = threadIdx.x;
   const float4 *h4 = reinterpret_cast<const float4 *>(h);
-  z0 = dot4<8>(h4, [&](int j) { return P[j]; }) + b0;
-  z1 = dot4<8>(h4, [&](int j) { return P[8 + j]; }) + b1;
-  const float t = dot4<4>(h4 + 4 * (threadIdx.x & 1), [&](int j) { return P[16 + j]; });
-  z2 = (t + dpp_f<0xB1>(t)) + b2;
+  z0 = dot4<8>(h4, [&](int j) { return P[j]; }) + bias[tid];
+  z1 = dot4<8>(h4, [&](int j) { return P[8 + j]; }) + bias[kRT + tid];
+  const float t = dot4<4>(h4 + 4 * (tid & 1), [&](int j) { return P[16 + j]; });
+  z2 = (t + dpp_f<0xB1>(t)) + (tid < 2 * kRTail ? bias[2 * kRT + (tid >> 1)] : 0.0f);
 }
 
-// Support expectation + h^-1 (scaling_transform.py:118-128) over the workgroup; every wave returns
-// the same value. red: 12 floats of LDS owned by this call site. Two barriers.
-__device__ __forceinline__ float support_decode(float z0, float z1, float z2, float *red) {
+// NR rows of a 128 x 128 layer (inputs x + r * 128): each weight read once for all rows.
+template <int NR, typename WF>
+__device__ __forceinline__ void dense128n(const float *x, WF w, float *z) {
+  const int p = threadIdx.x & 1;
+  float a[NR][4];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float4 q = w(j);
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const float4 v = reinterpret_cast<const float4 *>(x + r * kRHid)[16 * p + j];
+      a[r][0] = __fmaf_rn(v.x, q.x, a[r][0]);
+      a[r][1] = __fmaf_rn(v.y, q.y, a[r][1]);
+      a[r][2] = __fmaf_rn(v.z, q.z, a[r][2]);
+      a[r][3] = __fmaf_rn(v.w, q.w, a[r][3]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const float h = (a[r][0] + a[r][1]) + (a[r][2] + a[r][3]);
+    z[r] = h + dpp_f<0xB1>(h);
+  }
+}
+
+// NH supports decoded together (z[h] = this lane's logits of support h, see support_logits):
+// the reductions of support_decode sharing its two barriers. red: 12 * NH floats of LDS.
+template <int NH>
+__device__ __forceinline__ void support_decode_n(const float (*z)[3], float *red, float *out) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const bool v2 = tid < 2 * kRTail && !(tid & 1);
-  float m = fmaxf(z0, z1);
-  if (v2) m = fmaxf(m, z2);
-  m = wave_max_dpp(m);
-  if (lane == 0) red[wid] = m;
-  __syncthreads();
-  const float M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  const float half = (float)((kRV - 1) / 2);
-  const float e0 = expf(z0 - M), e1 = expf(z1 - M), e2 = v2 ? expf(z2 - M) : 0.0f;
-  float se = (e0 + e1) + e2;
-  float sj = (e0 * ((float)tid - half) + e1 * ((float)(kRT + tid) - half)) + e2 * ((float)(2 * kRT + (tid >> 1)) - half);
-  se = wave_sum(se);
-  sj = wave_sum(sj);
-  if (lane == 0) {
-    red[4 + wid] = se;
-    red[8 + wid] = sj;
+  const bool ok2 = tid < 2 * kRTail && !(tid & 1);
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    float m = fmaxf(z[h][0], z[h][1]);
+    if (ok2) m = fmaxf(m, z[h][2]);
+    m = wave_max_dpp(m);
+    if (lane == 0) red[4 * h + wid] = m;
   }
   __syncthreads();
-  const float SE = (red[4] + red[5]) + (red[6] + red[7]);
-  const float SJ = (red[8] + red[9]) + (red[10] + red[11]);
-  return h_inverse(SJ / SE);
+  const float half = (float)((kRV - 1) / 2);
+  const float j0 = (float)tid - half, j1 = (float)(kRT + tid) - half, j2 = (float)(2 * kRT + (tid >> 1)) - half;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const float M = fmaxf(fmaxf(red[4 * h], red[4 * h + 1]), fmaxf(red[4 * h + 2], red[4 * h + 3]));
+    const float e0 = expf(z[h][0] - M), e1 = expf(z[h][1] - M), e2 = ok2 ? expf(z[h][2] - M) : 0.0f;
+    float se = (e0 + e1) + e2, sj = (e0 * j0 + e1 * j1) + e2 * j2;
+    se = wave_sum(se);
+    sj = wave_sum(sj);
+    if (lane == 0) {
+      red[4 * NH + 8 * h + wid] = se;
+      red[4 * NH + 8 * h + 4 + wid] = sj;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const float *q = red + 4 * NH + 8 * h;
+    out[h] = h_inverse(((q[4] + q[5]) + (q[6] + q[7])) / ((q[0] + q[1]) + (q[2] + q[3])));
+  }
 }
 
-// Sum of the draw counts published by workgroups < g for simulation k (wave-wide; bounded spin).
-__device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, unsigned long long epoch) {
+// A parity-mode tie among unexpanded children resolved with its draw rr: the chosen child ends
+// the path (cselect_child's list[rand() % len], cnode.cpp:592); one thread.
+__device__ inline void resolve_tie(const TreeView &t, int A, int lvl, unsigned long long m, uint32_t rr, int *act) {
+  int kk = (int)(rr % (uint32_t)__popcll(m));
+  for (; kk > 0; --kk) m &= m - 1;
+  const int jsel = __ffsll((long long)m) - 1;
+  const int parent = t.path[lvl];
+  const int action = legal_at(t, 0, parent, jsel);
+  t.path_act[lvl] = action;
+  t.path[lvl + 1] = 1 + A * t.meta[parent].latent + action;
+  *act = action;
+}
+
+// Sum of the draw counts published by workgroups < g for simulation k, by the whole workgroup: one
+// flag per thread (every poll in flight at once, not one round per 64 predecessors), reduced
+// through LDS (part: kRWaves ints). Bounded spin; ends with a barrier.
+__device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, unsigned long long epoch, int *part) {
   const int lane = threadIdx.x & 63;
   int sum = 0;
-  for (int q = lane; q < g; q += 64) {
+  for (int q = threadIdx.x; q < g; q += kRT) {
     unsigned long long v;
     long long spins = 0;
     while (true) {
@@ -224,9 +277,13 @@ __device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, uns
   }
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
-  return sum;
+  if (lane == 0) part[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  return (part[0] + part[1]) + (part[2] + part[3]);
 }
 
+// NR = 2 (parity mode): the network carries a second, speculative row for two-way leaf ties.
+template <int NR>
 __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) void search_res_kernel(SearchArgs p, ResNet n) {
   extern __shared__ float4 smem4[];
   float *smem = reinterpret_cast<float *>(smem4);
@@ -237,10 +294,10 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   __shared__ uint32_t s_z0[31];
   __shared__ int s_players, s_epoch, s_x, s_act, s_status, s_tlevel, s_vtp;
-  __shared__ int s_len[1];
+  __shared__ int s_len[1], s_part[kRWaves];
   __shared__ unsigned long long s_tmask;
   __shared__ float4 s_mm;
-  __shared__ float s_red[24];
+  __shared__ float s_red[12 * 2 * NR];
   __shared__ unsigned long long s_phase[64];
   if (p.phase && tid < 64) s_phase[tid] = 0ull;
 
@@ -288,9 +345,14 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int e = tid; e < 31; e += kRT) s_pow[e] = p.pow16807[e];
 
   // ---- network residency: LDS layers, action rows, register layers and biases
-  float *X0 = smem + n.off_x0, *T1 = smem + n.off_t1, *NL = smem + n.off_nl, *T2 = smem + n.off_t2,
-        *T3 = smem + n.off_t3, *RHo = smem + n.off_rh, *HV = smem + n.off_hv, *LG = smem + n.off_lg,
-        *ACT = smem + n.off_act;
+  // activations and biases at static LDS addresses: lane-dependent addresses then share a few base
+  // registers and fold the arrays' offsets into the instructions' immediates
+  __shared__ float4 s_acts[(kRHid + NR * (6 * kRHid + kRF + 2 * kRF + kRMaxA)) / 4];
+  __shared__ float4 s_bias[kResBiasFloats / 4];
+  float *X0 = reinterpret_cast<float *>(s_acts), *T1 = X0 + kRHid, *NL = T1 + NR * kRHid, *T2 = NL + NR * kRHid,
+        *T3 = T2 + NR * kRHid, *U2 = T3 + NR * kRHid, *U3 = U2 + NR * kRHid, *RHo = U3 + NR * kRHid,
+        *HV = RHo + NR * kRF, *LG = HV + NR * 2 * kRF;
+  float *ACT = smem + n.off_act;
   const float4 *WD1 = reinterpret_cast<const float4 *>(smem + n.off_wd1);
   const float4 *WD2 = reinterpret_cast<const float4 *>(smem + n.off_wd2);
   for (int e = tid; e < kRSlotsD * kRT; e += kRT) {
@@ -298,21 +360,19 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     reinterpret_cast<float4 *>(smem + n.off_wd2)[e] = n.d[2][e];
   }
   for (int e = tid; e < A * kRHid; e += kRT) ACT[e] = n.act[e];
-  float4 wD3[kRSlotsD], wD4[kRSlotsD], wD5[kRSlotsD], wRH[kRSlotsRH], wVPH[kRSlotsVPH], wPO[1];
+  float4 wD3[kRSlotsD], wD4[kRSlotsD], wRS[kRSlotsS], wRH[kRSlotsRH], wVPH[kRSlotsVPH], wPO[1];
   res_fetch<kRSlotsD>(n.d[3], wD3);
   res_fetch<kRSlotsD>(n.d[4], wD4);
-  res_fetch<kRSlotsD>(n.d[5], wD5);
+  res_fetch<kRSlotsS>(n.rs, wRS);
   res_fetch<kRSlotsRH>(n.rh, wRH);
   res_fetch<kRSlotsVPH>(n.vph, wVPH);
   res_fetch<kRSlotsPO>(n.po, wPO);
   const int cD = tid >> 1, pD = tid & 1, cRH = tid >> 3, pRH = tid & 7, cVP = tid >> 2, pVP = tid & 3, cPO = tid >> 3;
-  float bD[6];
-#pragma unroll
-  for (int q = 0; q < 6; ++q) bD[q] = n.bd[q * kRHid + cD];
-  const float bRH = n.brh[cRH], bVP = n.bvph[cVP], bPO = cPO < A ? n.bpo[cPO] : 0.0f;
-  const int ct = 2 * kRT + (tid >> 1);
-  const float bRS0 = n.brs[tid], bRS1 = n.brs[kRT + tid], bRS2 = tid < 2 * kRTail ? n.brs[ct] : 0.0f;
-  const float bVS0 = n.bvs[tid], bVS1 = n.bvs[kRT + tid], bVS2 = tid < 2 * kRTail ? n.bvs[ct] : 0.0f;
+  // biases live in LDS (registers are the scarce resource): the bias blocks are contiguous
+  float *BB = reinterpret_cast<float *>(s_bias);
+  for (int e = tid; e < kResBiasFloats; e += kRT) BB[e] = n.bd[e];
+  const float *BD = BB, *BRH = BD + 6 * kRHid, *BVP = BRH + kRF, *BRS = BVP + 2 * kRF,
+              *BVS = BRS + ((kRV + 3) & ~3), *BPO = BVS + ((kRV + 3) & ~3);
   // the streamed buffer: fc_dynamics[0] for the first simulation
   float4 P[kRSlotsS];
   res_fetch<kRSlotsD>(n.d[0], P);
@@ -355,9 +415,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int status = s_status;
     if (status == 2) {
       // the depth depends on a draw: look back now, then walk with the draws (exact semantics)
-      if (wid == 0) {
-        const int base = lookback_sum(p, k, g, G, epoch);
-        if (lane == 0) {
+      const int base = lookback_sum(p, k, g, G, epoch, s_part);
+      if (tid == 0) {
+        {
           atomicAdd(p.diag + 1, 1);
           const uint32_t *coef = p.coef;
           const int npos = p.coef_positions;
@@ -380,116 +440,151 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           reinterpret_cast<const float4 *>(p.pool + ((size_t)max(s_x, 0) * B + i) * kRHid)[tid];
     __syncthreads();
     LZM_STAMP(2);
-    // ---- fc_dynamics[0], latent rows (streamed weights in P)
+    unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
+    // ---- fc_dynamics[0], latent rows (streamed weights in P): shared by the speculative rows
     const float z0 = dense128(X0, [&](int j) { return P[j]; });
+    LZM_SUBSTAMP(16);
+    // Rows: row r carries the network for action act_r. A tie between exactly two unexpanded
+    // children (status 1) is evaluated speculatively for both (NR = 2) and resolved after the
+    // network, when the predecessors' draw counts have long been published; other ties wait here.
+    bool spec = false;
+    int act_r[2];
     if (status == 1) {
-      // a tie among unexpanded children: the draw picks the action (the latent is known)
-      if (wid == 0) {
-        const int base = lookback_sum(p, k, g, G, epoch);
-        if (lane == 0) {
-          const int lvl = s_tlevel;
-          const uint32_t rr = glibc_draw(p.coef, p.coef_positions, s_z0, base + lvl, p.diag);
-          unsigned long long m = s_tmask;
-          int kk = (int)(rr % (uint32_t)__popcll(m));
-          for (; kk > 0; --kk) m &= m - 1;
-          const int jsel = __ffsll((long long)m) - 1;
-          const int parent = t.path[lvl];
-          const int action = legal_at(t, 0, parent, jsel);
-          t.path_act[lvl] = action;
-          t.path[lvl + 1] = 1 + A * t.meta[parent].latent + action;
-          s_act = action;
-        }
+      const unsigned long long m = s_tmask;
+      const int parent = t.path[s_tlevel];
+      if (NR == 2 && __popcll(m) == 2) {
+        spec = true;
+        act_r[0] = legal_at(t, 0, parent, __ffsll((long long)m) - 1);
+        act_r[1] = legal_at(t, 0, parent, __ffsll((long long)(m & (m - 1))) - 1);
+      } else {
+        const int base = lookback_sum(p, k, g, G, epoch, s_part);
+        if (tid == 0) resolve_tie(t, A, s_tlevel, m, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+        __syncthreads();
       }
-      __syncthreads();
     }
-    res_fetch<kRSlotsS>(n.rs, P);  // the reward support head, five steps on
-    const int act = s_act;
-    if (p.rec_x && tid == 0) {
-      p.rec_x[(size_t)k * B + i] = s_x;
-      p.rec_a[(size_t)k * B + i] = act;
-      p.rec_len[(size_t)k * B + i] = s_len[0];
-    }
+    if (!spec) act_r[0] = act_r[1] = s_act;
+    LZM_SUBSTAMP(17);
+    __builtin_amdgcn_sched_barrier(0);
+    res_fetch<kRSlotsD>(n.d[5], P);  // fc_prediction_common[1], three steps on
     // + the action's one-hot row, bias, ReLU (muzero_model_mlp.py:188-190)
-    if (pD == 0) T1[cD] = fmaxf((z0 + ACT[act * kRHid + cD]) + bD[0], 0.0f);
+    if (pD == 0) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) T1[r * kRHid + cD] = fmaxf((z0 + ACT[act_r[r] * kRHid + cD]) + BD[cD], 0.0f);
+    }
     __syncthreads();
+    LZM_SUBSTAMP(18);
     // ---- fc_dynamics[1] (LDS weights) + latent residual -> next latent
     {
-      const float z = dense128(T1, [&](int j) { return WD1[j * kRT + tid]; });
-      if (pD == 0) NL[cD] = fmaxf(z + bD[1], 0.0f) + X0[cD];
+      float z[NR];
+      dense128n<NR>(T1, [&](int j) { return WD1[j * kRT + tid]; }, z);
+      if (pD == 0) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) NL[r * kRHid + cD] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[cD];
+      }
     }
     __syncthreads();
     LZM_STAMP(3);
-    // file the next latent (mcts_ctree.py:305): pool[k + 1][i]
-    if (tid < kRHid / 4)
-      reinterpret_cast<float4 *>(p.pool + ((size_t)(k + 1) * B + i) * kRHid)[tid] = reinterpret_cast<const float4 *>(NL)[tid];
-    // ---- fc_dynamics_2 (LDS, registers) -> reward head hidden -> reward support, decoded
+    // The reward chain (fc_dynamics_2 -> reward head) and the prediction chain (prediction
+    // common -> value / policy heads) both start from the next latent: one step per layer pair.
+    // ---- [fc_dynamics_2[0] (LDS) | fc_prediction_common[0] (registers)]
     {
-      const float z = dense128(NL, [&](int j) { return WD2[j * kRT + tid]; });
-      if (pD == 0) T2[cD] = fmaxf(z + bD[2], 0.0f);
+      float z2[NR], z6[NR];
+      dense128n<NR>(NL, [&](int j) { return WD2[j * kRT + tid]; }, z2);
+      dense128n<NR>(NL, [&](int j) { return wD4[j]; }, z6);
+      if (pD == 0) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          T2[r * kRHid + cD] = fmaxf(z2[r] + BD[2 * kRHid + cD], 0.0f);
+          U2[r * kRHid + cD] = fmaxf(z6[r] + BD[4 * kRHid + cD], 0.0f);
+        }
+      }
     }
     __syncthreads();
+    LZM_SUBSTAMP(19);
+    // ---- [fc_prediction_common[1] (streamed) | fc_dynamics_2[1] (registers)]
     {
-      const float z = dense128(T2, [&](int j) { return wD3[j]; });
-      if (pD == 0) T3[cD] = fmaxf(z + bD[3], 0.0f);
+      float z7[NR], z3[NR];
+      dense128n<NR>(U2, [&](int j) { return P[j]; }, z7);
+      __builtin_amdgcn_sched_barrier(0);
+      res_fetch<kRSlotsS>(n.vs, P);  // the value support head, two steps on
+      dense128n<NR>(T2, [&](int j) { return wD3[j]; }, z3);
+      if (pD == 0) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          T3[r * kRHid + cD] = fmaxf(z3[r] + BD[3 * kRHid + cD], 0.0f);
+          U3[r * kRHid + cD] = fmaxf(z7[r] + BD[5 * kRHid + cD], 0.0f);
+        }
+      }
     }
     __syncthreads();
-    {
-      float h = dot4<kRSlotsRH>(reinterpret_cast<const float4 *>(T3) + 4 * pRH, [&](int j) { return wRH[j]; });
-      h += dpp_f<0xB1>(h);
-      h += dpp_f<0x4E>(h);
-      h += dpp_f<0x141>(h);
-      if (pRH == 0) RHo[cRH] = fmaxf(h + bRH, 0.0f);
-    }
-    __syncthreads();
-    float rdec;
-    {
-      float a0, a1, a2;
-      support_logits(RHo, P, bRS0, bRS1, bRS2, a0, a1, a2);
-      res_fetch<kRSlotsS>(n.vs, P);  // the value support head, four steps on
-      rdec = support_decode(a0, a1, a2, s_red);
-    }
     LZM_STAMP(4);
-    // ---- prediction trunk (registers) on the next latent
-    {
-      const float z = dense128(NL, [&](int j) { return wD4[j]; });
-      if (pD == 0) T2[cD] = fmaxf(z + bD[4], 0.0f);
-    }
-    __syncthreads();
-    {
-      const float z = dense128(T2, [&](int j) { return wD5[j]; });
-      if (pD == 0) T3[cD] = fmaxf(z + bD[5], 0.0f);
+    // ---- [reward head hidden | (value | policy) head hidden]
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      float h = dot4<kRSlotsRH>(reinterpret_cast<const float4 *>(T3 + r * kRHid) + 4 * pRH, [&](int j) { return wRH[j]; });
+      float u = dot4<kRSlotsVPH>(reinterpret_cast<const float4 *>(U3 + r * kRHid) + 8 * pVP, [&](int j) { return wVPH[j]; });
+      h += dpp_f<0xB1>(h);
+      u += dpp_f<0xB1>(u);
+      h += dpp_f<0x4E>(h);
+      u += dpp_f<0x4E>(u);
+      h += dpp_f<0x141>(h);
+      if (pRH == 0) RHo[r * kRF + cRH] = fmaxf(h + BRH[cRH], 0.0f);
+      if (pVP == 0) HV[r * 2 * kRF + cVP] = fmaxf(u + BVP[cVP], 0.0f);
     }
     __syncthreads();
     LZM_STAMP(5);
-    // ---- [value | policy] head hidden, then value support (decoded) and policy logits
+    // ---- reward support (registers), value support (streamed), policy logits; every support
+    // decoded together
+    float dec[2 * NR];  // [row][reward, value]
     {
-      float h = dot4<kRSlotsVPH>(reinterpret_cast<const float4 *>(T3) + 8 * pVP, [&](int j) { return wVPH[j]; });
-      h += dpp_f<0xB1>(h);
-      h += dpp_f<0x4E>(h);
-      if (pVP == 0) HV[cVP] = fmaxf(h + bVP, 0.0f);
-    }
-    __syncthreads();
-    float vdec;
-    {
-      const float4 hp = reinterpret_cast<const float4 *>(HV + kRF)[tid & 7];
-      float q = __fmaf_rn(hp.x, wPO[0].x, 0.0f);
-      q = __fmaf_rn(hp.y, wPO[0].y, q);
-      q = __fmaf_rn(hp.z, wPO[0].z, q);
-      q = __fmaf_rn(hp.w, wPO[0].w, q);
-      q += dpp_f<0xB1>(q);
-      q += dpp_f<0x4E>(q);
-      q += dpp_f<0x141>(q);
-      if ((tid & 7) == 0 && cPO < A) LG[cPO] = q + bPO;
-      float a0, a1, a2;
-      support_logits(HV, P, bVS0, bVS1, bVS2, a0, a1, a2);
+      float zz[2 * NR][3];
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        const float4 hp = reinterpret_cast<const float4 *>(HV + r * 2 * kRF + kRF)[tid & 7];
+        float q = __fmaf_rn(hp.x, wPO[0].x, 0.0f);
+        q = __fmaf_rn(hp.y, wPO[0].y, q);
+        q = __fmaf_rn(hp.z, wPO[0].z, q);
+        q = __fmaf_rn(hp.w, wPO[0].w, q);
+        q += dpp_f<0xB1>(q);
+        q += dpp_f<0x4E>(q);
+        q += dpp_f<0x141>(q);
+        if ((tid & 7) == 0 && cPO < A) LG[r * kRMaxA + cPO] = q + BPO[cPO];
+        support_logits(HV + r * 2 * kRF, P, BVS, zz[2 * r + 1][0], zz[2 * r + 1][1], zz[2 * r + 1][2]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        support_logits(RHo + r * kRF, wRS, BRS, zz[2 * r][0], zz[2 * r][1], zz[2 * r][2]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
       res_fetch<kRSlotsD>(n.d[0], P);  // fc_dynamics[0] for the next simulation
-      vdec = support_decode(a0, a1, a2, s_red + 12);
+      support_decode_n<2 * NR>(zz, s_red, dec);
     }
     LZM_STAMP(6);
+    // ---- resolve a speculative tie: the draw picks the row (predecessors published long ago)
+    if (spec) {
+      const int base = lookback_sum(p, k, g, G, epoch, s_part);
+      if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+      __syncthreads();
+    }
+    const int row = (spec && s_act == act_r[1]) ? 1 : 0;
+    const float rdec = (NR == 2 && row) ? dec[2 * NR - 2] : dec[0];  // static indices: no scratch
+    const float vdec = (NR == 2 && row) ? dec[2 * NR - 1] : dec[1];
+    LZM_STAMP(7);
+    // file the next latent (mcts_ctree.py:305): pool[k + 1][i]
+    if (tid < kRHid / 4)
+      reinterpret_cast<float4 *>(p.pool + ((size_t)(k + 1) * B + i) * kRHid)[tid] =
+          reinterpret_cast<const float4 *>(NL + row * kRHid)[tid];
+    if (p.rec_x && tid == 0) {
+      p.rec_x[(size_t)k * B + i] = s_x;
+      p.rec_a[(size_t)k * B + i] = s_act;
+      p.rec_len[(size_t)k * B + i] = s_len[0];
+    }
     if (p.rec_dec && tid == 0) {
       p.rec_dec[((size_t)k * B + i) * 2] = rdec;
       p.rec_dec[((size_t)k * B + i) * 2 + 1] = vdec;
-      for (int a = 0; a < A; ++a) p.rec_logits[((size_t)k * B + i) * A + a] = LG[a];
+      for (int a = 0; a < A; ++a) p.rec_logits[((size_t)k * B + i) * A + a] = LG[row * kRMaxA + a];
     }
     // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500), wave 0
     if (wid == 0) {
@@ -498,7 +593,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       int vtp = s_vtp;
       if (players > 1)
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
-      expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG);
+      expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA);
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
     }
     LZM_STAMP(9);

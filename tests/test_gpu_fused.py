@@ -106,6 +106,24 @@ def test_fused_roots_per_workgroup(case, roots, monkeypatch):
     check_tree_exact(case)
 
 
+# the config-2 shape takes the network-resident kernel (lzm_search_res.h); the same cases through
+# the weight-streaming kernel (LZM_FUSED_RES=0) and the speculative two-row variant (LZM_RES_SPEC=1)
+@pytest.mark.parametrize("env", ["LZM_FUSED_RES=0", "LZM_RES_SPEC=1"])
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[4]], ids=_case_id)
+def test_fused_kernel_variants(case, env, monkeypatch):
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
+    check_tree_exact(case)
+
+
+def test_resident_kernel_serves_config2():
+    from lightzero_amd import _lib
+    L = _lib.load()
+    assert L.lzm_search_mlp_kind(256, 2, 128, 32, 601, 1) == 1
+    assert L.lzm_search_mlp_kind(256, 2, 64, 32, 601, 1) == 0   # other shapes: weight-streaming kernel
+    assert L.lzm_search_mlp_kind(4096, 2, 128, 32, 601, 1) == 0  # several roots per workgroup
+
+
 def check_tree_exact(case):
     B, S, A, H, zero, players, fast = case
     r = fused_search(B, S, A, H, zero, players, fast, seed=B + S + A)

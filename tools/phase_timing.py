@@ -52,11 +52,9 @@ def main():
     for name, c in zip(NAMES, per):
         print(f"  {name:20s} {c:12.0f}  per-sim {c / a.sims:9.0f}  {100 * c / tot:5.1f}%")
     print(f"  total {tot:.0f} cycles = {tot / 2.1e3:.0f} us at 2.1 GHz")
-    sub = np.array(buf[16:64], dtype=np.float64).reshape(12, 4) / (n * G * a.sims)
-    print("per schedule step, per simulation (cycles): step body, barrier (+ narrow decode)")
-    for st in range(12):
-        if sub[st].sum() > 0:
-            print(f"  step {st:2d}  " + "  ".join(f"{c:8.0f}" for c in sub[st][:2]))
+    sub = np.array(buf[16:64], dtype=np.float64) / (n * G * a.sims)
+    print("sub-stamps per simulation (cycles; index = stamp id - 16, meaning per kernel):")
+    print("  " + "  ".join(f"{q}:{c:.0f}" for q, c in enumerate(sub) if c > 0))
 
 
 if __name__ == "__main__":
