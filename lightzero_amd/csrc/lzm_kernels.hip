@@ -1285,6 +1285,9 @@ size_t plan_res(SearchArgs &p, ResNet &n, const lzm_handle *h, int S, int A) {
   p.off_path = o; o += round4((size_t)h->depth_cap);
   p.off_pact = o; o += round4((size_t)h->depth_cap);
   n.off_act = (int)o; o += (size_t)A * kRHid;
+  n.off_l2n = (int)o; o += round4((size_t)S + 2);
+  n.off_nq = (int)o; o += round4((size_t)2 * (S + 2));
+  n.off_cs = (int)o; o += (size_t)4 * h->cap;
   p.off_misc = o; o += round4((size_t)S + 32);
   n.off_wd1 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
   n.off_wd2 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
@@ -1463,6 +1466,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     const size_t lds = plan_res(q, n, h, S, A);
     if (lds) {
       res_net(n, weights + round4(kernel_layout(kls, nkl, lay_w, lay_b)), A);
+      const char *sm = getenv("LZM_RES_SELECT");
+      n.select_mode = sm ? atoi(sm) : 1;  // measured: 1 < 0 < 2 < 3
       // LZM_RES_SPEC=1 (parity mode): evaluate two-way leaf ties speculatively as a second network
       // row instead of waiting for the look-back (measured slower: every simulation pays the row)
       const char *se = getenv("LZM_RES_SPEC");

@@ -61,7 +61,8 @@ struct ResNet {
   const float4 *rh, *vph, *rs, *vs, *po;
   const float *bd, *brh, *bvph, *brs, *bvs, *bpo, *act;
   // LDS float offsets beyond SearchArgs' tree plan
-  int off_act, off_wd1, off_wd2;
+  int off_act, off_wd1, off_wd2, off_l2n, off_nq, off_cs;
+  int select_mode;  // LZM_RES_SELECT (experiments): how the walk runs, see the simulation loop
 };
 
 // floats of the bias blocks ([6][128] D, [32] RH, [64] VPH, [604] RS, [604] VS, [32] PO)
@@ -179,6 +180,202 @@ __device__ __forceinline__ void support_logits(const float *h, const float4 *P, 
   z2 = (t + dpp_f<0xB1>(t)) + (tid < 2 * kRTail ? bias[2 * kRT + (tid >> 1)] : 0.0f);
 }
 
+// ---- selection split in two (MuZero, tree slice in LDS, one root):
+// (1) every expanded node's pUCT terms that do not depend on the walk, one thread per node
+//     (cucb_score, cnode.cpp:655-699: prior_score, and for visited children the normalised,
+//     clamped value term; compute_mean_q's sums over visited children, cnode.cpp:169-203);
+// (2) the walk itself (wave 0), left with the mean-q chain (the only walk-dependent term: it is
+//     what unvisited children score) and the argmax / tie list per level.
+// Same float operations in the same order as descend_wave, so the same bits.
+// nq[latent] = {total_q, total_v}; cs[child node] = {prior_score, value term, child latent, visited}
+__device__ inline void precompute_terms(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
+                                        float4 mm, int players, float disc) {
+  for (int L = threadIdx.x; L < nlat; L += kRT) {
+    const int n = lat2node[L];
+    if (n < 0) continue;
+    const NodeStat s = t.stat[n];
+    const int nleg = legal_n(t, 0, n);
+    const int base = 1 + t.A * L;
+    int N = s.visit - 1;
+    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
+    const float2 Lx = t.lut[N];
+    float total_q = 0.0f;
+    int total_v = 0;
+    for (int j = 0; j < nleg; ++j) {
+      const int c = base + legal_at(t, 0, n, j);
+      const NodeStat cst = t.stat[c];
+      const float cv = t.val[c];
+      const float tr = cst.reward;
+      float vv = 0.0f;
+      if (cst.visit > 0) {
+        total_q += tr + disc * cv;
+        ++total_v;
+        float v = (players == 1) ? tr + disc * cv : tr + disc * (-cv);
+        v = mm_normalize(mm, v);
+        if (v < 0) v = 0;
+        if (v > 1) v = 1;
+        vv = v;
+      }
+      float pb_c = Lx.x;
+      pb_c *= (t.pbt && cst.visit <= N) ? t.pbt[N * (N + 1) / 2 + cst.visit] : (Lx.y / (float)(cst.visit + 1));
+      cs[c] = make_float4(pb_c * cst.prior, vv, __int_as_float(t.meta[c].latent), __int_as_float(cst.visit > 0 ? 1 : 0));
+    }
+    nq[L] = make_float2(total_q, __int_as_float(total_v));
+  }
+}
+
+// The walk over the precomputed terms (descend_wave's contract and outputs; wave 0).
+template <bool CLASSIFY, typename Draw>
+__device__ inline Descent descend_terms(const TreeView &t, const float2 *nq, const float4 *cs, float4 mm, int vtp,
+                                        int players, Draw draw, TieInfo *tie) {
+  const int lane = threadIdx.x & 63;
+  int node = 0, is_root = 1, len = 0, last_action = -1, plat = -1;
+  float parent_q = 0.0f;
+  int lat = t.meta[0].latent;
+  if (lane == 0) t.path[0] = 0;
+  if (CLASSIFY) tie->status = 0;
+  while (lat >= 0 && len < t.depth_cap - 1) {
+    const int n = legal_n(t, 0, node);
+    const int base = 1 + t.A * lat;
+    const bool valid = lane < n;
+    const int a = valid ? legal_at(t, 0, node, lane) : 0;
+    const float4 c = valid ? cs[base + a] : make_float4(0.0f, 0.0f, __int_as_float(-1), __int_as_float(0));
+    const float2 q = nq[lat];
+    const int total_v = __float_as_int(q.y);
+    float mean_q;
+    if (is_root && total_v > 0)
+      mean_q = q.x / (float)total_v;
+    else
+      mean_q = (parent_q + q.x) / (float)(total_v + 1);
+    is_root = 0;
+    parent_q = mean_q;
+    float vu = mm_normalize(mm, mean_q);
+    if (vu < 0) vu = 0;
+    if (vu > 1) vu = 1;
+    const float score = c.x + (__float_as_int(c.w) ? c.y : vu);
+    const float M = wave_max_dpp(valid ? score : -INFINITY);
+    const int r = __ffsll((long long)__ballot(valid && score == M)) - 1;
+    const uint64_t mask = __ballot(valid && lane > r && score >= M - 0.000001f) | (1ull << r);
+    const int nl = __popcll(mask);
+    if (CLASSIFY && nl > 1) {
+      const bool leaf_child = !((mask >> lane) & 1ull) || __float_as_int(c.z) < 0;
+      const bool all_leaves = __ballot(!leaf_child) == 0ull;
+      if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+      tie->status = all_leaves ? 1 : 2;
+      tie->level = len;
+      tie->mask = mask;
+      Descent d;
+      d.len = len + 1;
+      d.x = lat;
+      d.action = -1;
+      d.vtp = vtp;
+      d.leaf = -1;
+      return d;
+    }
+    const uint32_t rr = CLASSIFY ? 0u : draw(len);
+    int kk = (int)(rr % (uint32_t)nl);
+    uint64_t mm_ = mask;
+    for (; kk > 0; --kk) mm_ &= mm_ - 1;
+    const int jsel = __ffsll((long long)mm_) - 1;
+    const int action = __builtin_amdgcn_readlane(a, jsel);
+    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+    node = base + action;
+    last_action = action;
+    if (lane == 0) {
+      t.path_act[len] = action;
+      t.path[len + 1] = node;
+    }
+    ++len;
+    plat = lat;
+    lat = __builtin_amdgcn_readlane(__float_as_int(c.z), jsel);
+  }
+  Descent d;
+  d.len = len;
+  d.x = plat;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
+// descend_terms by one lane: the reference's sequential tie-list scan (cselect_child,
+// cnode.cpp:551-596) over the precomputed terms, no cross-lane operations.
+template <bool CLASSIFY, typename Draw>
+__device__ inline Descent descend_terms_lane(const TreeView &t, const float2 *nq, const float4 *cs, float4 mm, int vtp,
+                                             int players, Draw draw, TieInfo *tie) {
+  int node = 0, is_root = 1, len = 0, last_action = -1, plat = -1;
+  float parent_q = 0.0f;
+  int lat = t.meta[0].latent;
+  t.path[0] = 0;
+  if (CLASSIFY) tie->status = 0;
+  while (lat >= 0 && len < t.depth_cap - 1) {
+    const int n = legal_n(t, 0, node);
+    const int base = 1 + t.A * lat;
+    const float2 q = nq[lat];
+    const int total_v = __float_as_int(q.y);
+    float mean_q;
+    if (is_root && total_v > 0)
+      mean_q = q.x / (float)total_v;
+    else
+      mean_q = (parent_q + q.x) / (float)(total_v + 1);
+    is_root = 0;
+    parent_q = mean_q;
+    float vu = mm_normalize(mm, mean_q);
+    if (vu < 0) vu = 0;
+    if (vu > 1) vu = 1;
+    float max_score = kFloatMin;
+    uint64_t mask = 0;
+    bool all_leaves = true;
+    for (int j = 0; j < n; ++j) {
+      const float4 c = cs[base + legal_at(t, 0, node, j)];
+      const float score = c.x + (__float_as_int(c.w) ? c.y : vu);
+      if (max_score < score) {
+        max_score = score;
+        mask = 1ull << j;
+        all_leaves = __float_as_int(c.z) < 0;
+      } else if (score >= max_score - 0.000001f) {
+        mask |= 1ull << j;
+        all_leaves = all_leaves && __float_as_int(c.z) < 0;
+      }
+    }
+    const int nl = __popcll(mask);
+    if (CLASSIFY && nl > 1) {
+      if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+      tie->status = all_leaves ? 1 : 2;
+      tie->level = len;
+      tie->mask = mask;
+      Descent d;
+      d.len = len + 1;
+      d.x = lat;
+      d.action = -1;
+      d.vtp = vtp;
+      d.leaf = -1;
+      return d;
+    }
+    const uint32_t rr = CLASSIFY ? 0u : draw(len);
+    int kk = (int)(rr % (uint32_t)nl);
+    uint64_t mm_ = mask;
+    for (; kk > 0; --kk) mm_ &= mm_ - 1;
+    const int jsel = __ffsll((long long)mm_) - 1;
+    const int action = legal_at(t, 0, node, jsel);
+    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+    node = base + action;
+    last_action = action;
+    t.path_act[len] = action;
+    t.path[len + 1] = node;
+    ++len;
+    plat = lat;
+    lat = __float_as_int(cs[node].z);
+  }
+  Descent d;
+  d.len = len;
+  d.x = plat;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
 // NR rows of a 128 x 128 layer (inputs x + r * 128): each weight read once for all rows.
 template <int NR, typename WF>
 __device__ __forceinline__ void dense128n(const float *x, WF w, float *z) {
@@ -294,7 +491,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   __shared__ uint32_t s_z0[31];
   __shared__ int s_players, s_epoch, s_x, s_act, s_status, s_tlevel, s_vtp;
-  __shared__ int s_len[1], s_part[kRWaves];
+  __shared__ int s_len[1], s_part[kRWaves], s_nlat;
   __shared__ unsigned long long s_tmask;
   __shared__ float4 s_mm;
   __shared__ float s_red[12 * 2 * NR];
@@ -330,6 +527,15 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     t.stat = ls; t.meta = lm; t.lut = llut; t.legal = llegal; t.nlegal = llegal + A; t.val = lval;
     t.pbt = p.pbt_rows ? lpbt : nullptr;
   }
+  // latent -> node map of the expanded nodes (children of latent L sit at 1 + A L)
+  int *L2N = reinterpret_cast<int *>(smem + n.off_l2n);
+  float2 *NQ = reinterpret_cast<float2 *>(smem + n.off_nq);
+  float4 *CS = reinterpret_cast<float4 *>(smem + n.off_cs);
+  // A search starts from prepared roots: only the root is expanded, with latent 0 (cnode.cpp:
+  // 301-358); simulation k gives its leaf latent k + 1. (Nodes past the root's children may hold a
+  // previous search's records: never scan them.)
+  for (int e = tid; e < p.S + 2; e += kRT) L2N[e] = e == 0 ? 0 : -1;
+  if (tid == 0) s_nlat = 1;
   if (tid == 0) {
     s_mm = p.minmax[i];
     s_vtp = p.vtp_in[i];
@@ -386,7 +592,16 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int k = 0; k < p.S; ++k) {
     const uint32_t seed = s_seeds[k];
     if (!p.fast) seed_state_parallel(seed, s_pow, s_z0);
-    // ---- selection (wave 0, one lane per child): descend_wave, lzm_tree.h
+    // ---- selection, part 1: every expanded node's walk-independent pUCT terms (all threads)
+    // 0: descend_wave; 1 (default): terms + wave walk; 2: terms + lane walk; 3: descend_slice
+    const int smode = n.select_mode;
+    if (smode == 1 || smode == 2) {
+      __syncthreads();  // the previous simulation's backup (wave 0) is complete
+      precompute_terms(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc);
+      __syncthreads();
+    }
+    LZM_STAMP(12);
+    // ---- selection, part 2: the walk (wave 0, one lane per child)
     if (wid == 0) {
       const float4 mm = s_mm;
       if (p.fast) {
@@ -394,12 +609,28 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)i, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
           return o.x >> 1;
         };
-        Descent d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp, p.disc, draw, nullptr);
+        Descent d;
+        if (smode == 1) {
+          d = descend_terms<false>(t, NQ, CS, mm, s_vtp, players, draw, nullptr);
+        } else if (smode == 0) {
+          d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp, p.disc, draw, nullptr);
+        } else if (lane == 0) {
+          d = smode == 2 ? descend_terms_lane<false>(t, NQ, CS, mm, s_vtp, players, draw, nullptr)
+                         : descend_slice<false, false>(t, 0, 0, 1, mm, players, s_vtp, p.disc, draw, nullptr);
+        }
         if (lane == 0) { s_len[0] = d.len; s_x = d.x; s_act = d.action; s_status = 0; }
       } else {
         TieInfo ti;
         auto nodraw = [](int) -> uint32_t { return 0u; };
-        Descent d = descend_wave<false, true>(t, 0, 0, 1, mm, players, s_vtp, p.disc, nodraw, &ti);
+        Descent d;
+        if (smode == 1) {
+          d = descend_terms<true>(t, NQ, CS, mm, s_vtp, players, nodraw, &ti);
+        } else if (smode == 0) {
+          d = descend_wave<false, true>(t, 0, 0, 1, mm, players, s_vtp, p.disc, nodraw, &ti);
+        } else if (lane == 0) {
+          d = smode == 2 ? descend_terms_lane<true>(t, NQ, CS, mm, s_vtp, players, nodraw, &ti)
+                         : descend_slice<false, true>(t, 0, 0, 1, mm, players, s_vtp, p.disc, nodraw, &ti);
+        }
         if (lane == 0) {
           s_len[0] = d.len; s_x = d.x; s_act = d.action;
           s_status = ti.status; s_tlevel = ti.level; s_tmask = ti.mask;
@@ -594,6 +825,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (players > 1)
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
       expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA);
+      if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
     }
     LZM_STAMP(9);

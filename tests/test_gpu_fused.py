@@ -108,7 +108,8 @@ def test_fused_roots_per_workgroup(case, roots, monkeypatch):
 
 # the config-2 shape takes the network-resident kernel (lzm_search_res.h); the same cases through
 # the weight-streaming kernel (LZM_FUSED_RES=0) and the speculative two-row variant (LZM_RES_SPEC=1)
-@pytest.mark.parametrize("env", ["LZM_FUSED_RES=0", "LZM_RES_SPEC=1"])
+@pytest.mark.parametrize("env", ["LZM_FUSED_RES=0", "LZM_RES_SPEC=1", "LZM_RES_SELECT=0", "LZM_RES_SELECT=2",
+                                 "LZM_RES_SELECT=3"])
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[4]], ids=_case_id)
 def test_fused_kernel_variants(case, env, monkeypatch):
     k, v = env.split("=")

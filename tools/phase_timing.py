@@ -17,7 +17,8 @@ import bench  # noqa: E402
 from lightzero_amd import _lib  # noqa: E402
 
 NAMES = ["select", "offsets+lookback", "gather", "dynamics", "reward head+decode", "pred trunk",
-         "value head+decode", "policy head", "file latents", "expand+backup", "stage-in", "write-back"]
+         "value head+decode", "policy head", "file latents", "expand+backup", "stage-in", "write-back",
+         "select terms (res)"]
 
 
 def main():
@@ -46,7 +47,7 @@ def main():
     torch.cuda.synchronize()
     _lib.load().lzm_debug_phase_cycles(t.h, buf, 0)
     G = -(-a.envs // R)
-    per = np.array(buf[:12], dtype=np.float64) / (n * G)
+    per = np.array(buf[:13], dtype=np.float64) / (n * G)
     tot = per.sum()
     print(f"per workgroup per search (cycles), R={R}, G={G}, sims={a.sims}:")
     for name, c in zip(NAMES, per):
