@@ -225,16 +225,36 @@ __device__ inline void precompute_terms(const TreeView &t, int nlat, const int *
 }
 
 // The walk over the precomputed terms (descend_wave's contract and outputs; wave 0).
+// Where a walk stands at the top of a level (a classification walk stops at a tie with the
+// state of that level, so the resolution resumes there instead of walking from the root).
+struct WalkState {
+  int node, lat, len, plat, last_action, is_root, vtp;
+  float parent_q;
+};
+__device__ inline WalkState walk_start(const TreeView &t, int vtp) {
+  WalkState w;
+  w.node = 0; w.lat = t.meta[0].latent; w.len = 0; w.plat = -1; w.last_action = -1; w.is_root = 1; w.vtp = vtp;
+  w.parent_q = 0.0f;
+  return w;
+}
+
 template <bool CLASSIFY, typename Draw>
 __device__ inline Descent descend_terms(const TreeView &t, const float2 *nq, const float4 *cs, float4 mm, int vtp,
-                                        int players, Draw draw, TieInfo *tie) {
+                                        int players, Draw draw, TieInfo *tie, WalkState *resume = nullptr,
+                                        WalkState *at_tie = nullptr) {
   const int lane = threadIdx.x & 63;
-  int node = 0, is_root = 1, len = 0, last_action = -1, plat = -1;
-  float parent_q = 0.0f;
-  int lat = t.meta[0].latent;
-  if (lane == 0) t.path[0] = 0;
+  WalkState w0 = resume ? *resume : walk_start(t, vtp);
+  int node = w0.node, is_root = w0.is_root, len = w0.len, last_action = w0.last_action, plat = w0.plat;
+  float parent_q = w0.parent_q;
+  int lat = w0.lat;
+  vtp = w0.vtp;
+  if (lane == 0 && !resume) t.path[0] = 0;
   if (CLASSIFY) tie->status = 0;
   while (lat >= 0 && len < t.depth_cap - 1) {
+    if (CLASSIFY && at_tie) {
+      at_tie->node = node; at_tie->lat = lat; at_tie->len = len; at_tie->plat = plat;
+      at_tie->last_action = last_action; at_tie->is_root = is_root; at_tie->vtp = vtp; at_tie->parent_q = parent_q;
+    }
     const int n = legal_n(t, 0, node);
     const int base = 1 + t.A * lat;
     const bool valid = lane < n;
@@ -493,6 +513,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ int s_players, s_epoch, s_x, s_act, s_status, s_tlevel, s_vtp;
   __shared__ int s_len[1], s_part[kRWaves], s_nlat;
   __shared__ unsigned long long s_tmask;
+  __shared__ WalkState s_walk;
   __shared__ float4 s_mm;
   __shared__ float s_red[12 * 2 * NR];
   __shared__ unsigned long long s_phase[64];
@@ -624,7 +645,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         auto nodraw = [](int) -> uint32_t { return 0u; };
         Descent d;
         if (smode == 1) {
-          d = descend_terms<true>(t, NQ, CS, mm, s_vtp, players, nodraw, &ti);
+          WalkState ws;
+          d = descend_terms<true>(t, NQ, CS, mm, s_vtp, players, nodraw, &ti, nullptr, &ws);
+          if (lane == 0 && ti.status == 2) s_walk = ws;
         } else if (smode == 0) {
           d = descend_wave<false, true>(t, 0, 0, 1, mm, players, s_vtp, p.disc, nodraw, &ti);
         } else if (lane == 0) {
@@ -644,7 +667,28 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
     LZM_STAMP(0);
     const int status = s_status;
-    if (status == 2) {
+    if (status == 2 && smode == 1) {
+      // the depth depends on a draw: look back now, then resume the walk at the tie with the draws
+      // (exact semantics; the draws of the forced levels above the tie are never read)
+      const int base = lookback_sum(p, k, g, G, epoch, s_part);
+      if (wid == 0) {
+        if (lane == 0) atomicAdd(p.diag + 1, 1);
+        const uint32_t *coef = p.coef;
+        const int npos = p.coef_positions;
+        int32_t *diag = p.diag;
+        auto draw = [coef, npos, diag, base](int level) -> uint32_t {
+          return glibc_draw(coef, npos, s_z0, base + level, diag);
+        };
+        WalkState ws = s_walk;
+        Descent d = descend_terms<false>(t, NQ, CS, s_mm, s_vtp, players, draw, nullptr, &ws);
+        if (lane == 0) {
+          s_len[0] = d.len; s_x = d.x; s_act = d.action;
+          __hip_atomic_store(&p.flags[(size_t)k * G + g], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      __syncthreads();
+    } else if (status == 2) {
       // the depth depends on a draw: look back now, then walk with the draws (exact semantics)
       const int base = lookback_sum(p, k, g, G, epoch, s_part);
       if (tid == 0) {
