@@ -245,6 +245,7 @@ __global__ __launch_bounds__(256) void traverse_fast_kernel(TraverseArgs p) {
 }
 
 
+
 struct BackpropArgs {
   TreeView t;
   float4 *minmax;
@@ -538,6 +539,8 @@ __global__ void debug_glibc_kernel(uint32_t seed, int n, int32_t *out, const uin
 
 }  // namespace lzm
 
+#include "lzm_traverse_lb.h"  // uses block_players above
+
 // ============================================================================ host side
 using namespace lzm;
 
@@ -653,6 +656,11 @@ static int fill_lut(lzm_handle *h, int base, float init) {
   return LZM_OK;
 }
 
+namespace {
+int ensure_coef(lzm_handle *h, int positions);
+int ensure_flags(lzm_handle *h, int sims, int G);
+}  // namespace
+
 static int alloc_tree(lzm_handle *h, int sims) {
   h->sims_cap = sims;
   h->cap = 1 + h->A * (sims + 1);
@@ -669,6 +677,14 @@ static int alloc_tree(lzm_handle *h, int sims) {
   h->lut_n = sims + 8;
   LZM_HIP(hipMalloc(&h->lut, sizeof(float2) * h->lut_n));
   h->lut_base = -1;
+  if (!(h->flags & LZM_RNG_FAST)) {
+    // parity-mode draw tables and look-back words, allocated here rather than at first use so
+    // that a search captured into a HIP graph never allocates
+    int rc = ensure_coef(h, h->B * h->depth_cap + 64);
+    if (rc != LZM_OK) return rc;
+    rc = ensure_flags(h, sims, h->B);
+    if (rc != LZM_OK) return rc;
+  }
   return fill_lut(h, 19652, 1.25f);
 }
 
@@ -824,7 +840,24 @@ int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, 
     dim3 g((h->B + 255) / 256), b(256);
     if (ez) hipLaunchKernelGGL(traverse_fast_kernel<true>, g, b, 0, s, p);
     else hipLaunchKernelGGL(traverse_fast_kernel<false>, g, b, 0, s, p);
+  } else if (!(getenv("LZM_TRAVERSE") && strcmp(getenv("LZM_TRAVERSE"), "serial") == 0)) {
+    // one wave per root, decoupled look-back of the draw offsets (lzm_traverse_lb.h)
+    rc = ensure_coef(h, h->B * h->depth_cap + 64);
+    if (rc != LZM_OK) return rc;
+    rc = ensure_flags(h, 1, 1);
+    if (rc != LZM_OK) return rc;
+    TraverseLbArgs q;
+    q.t = p.t; q.minmax = p.minmax; q.seed = seed; q.vtp_in = vtp_in;
+    q.out_x = out_x; q.out_y = out_y; q.out_a = out_a; q.out_vtp = out_vtp; q.out_len = out_len;
+    q.out_a64 = p.out_a64; q.disc = discount;
+    q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
+    q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag;
+    const int per = kTlbThreads / 64;
+    dim3 g((h->B + per - 1) / per), b(kTlbThreads);
+    if (ez) hipLaunchKernelGGL(traverse_lookback_kernel<true>, g, b, 0, s, q);
+    else hipLaunchKernelGGL(traverse_lookback_kernel<false>, g, b, 0, s, q);
   } else {
+    // LZM_TRAVERSE=serial: one workgroup, speculative fixed-point passes over the stream
     int W = ((h->B + 63) / 64) * 64;
     if (W > kMaxWG) W = kMaxWG;
     if (W < 64) W = 64;

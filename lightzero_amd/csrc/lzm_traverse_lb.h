@@ -1,0 +1,141 @@
+// lzm_traverse_lb.h — parity-mode batch_traverse over many workgroups (generic search path).
+//
+// cbatch_traverse (lzero/mcts/ctree/ctree_muzero/lib/cnode.cpp:755-824; EfficientZero
+// ctree_efficientzero/lib/cnode.cpp:756-814) walks the roots in order while drawing one rand()
+// per tree level from ONE process-wide glibc stream, so root i's draws start at the sum of the
+// depths of roots < i. traverse_glibc_kernel honours that in one workgroup by iterating the
+// offsets to their fixed point. Here every root gets its own wave, as in the fused search
+// (lzm_search_mlp.h): the walk first runs draw-free (descend_wave CLASSIFY: a tie among
+// unexpanded children ends the walk at the same depth whichever child wins), the root publishes
+// its depth in a 64-bit {epoch, count} word at once, and only a root that needs a draw VALUE
+// sums its predecessors' words (decoupled look-back) and evaluates its draws straight from the
+// seeded state through the coefficient table (random_r is linear over Z/2^32). A root whose depth
+// depends on a draw (a tie reaching an expanded child) publishes after walking with its draws.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lzm_search_mlp.h"
+#include "lzm_tree.h"
+
+namespace lzm {
+
+constexpr int kTlbThreads = 256;  // four roots per workgroup, one wave each
+
+struct TraverseLbArgs {
+  TreeView t;
+  const float4 *minmax;
+  const uint32_t *seed;
+  const int32_t *vtp_in;
+  int32_t *out_x, *out_y, *out_a, *out_vtp, *out_len;
+  long long *out_a64;
+  float disc;
+  const uint32_t *coef;  // [coef_positions][31]
+  int coef_positions;
+  const uint32_t *pow16807;   // [31]
+  unsigned long long *flags;  // [B] {epoch, depth}
+  uint32_t *epoch;            // [2] epoch, done counter
+  int32_t *diag;              // [0] passes (1), [1] spin timeouts (must stay 0)
+};
+
+template <bool EZ>
+__global__ __launch_bounds__(kTlbThreads) void traverse_lookback_kernel(TraverseLbArgs p) {
+  const TreeView &t = p.t;
+  const int tid = threadIdx.x, lane = tid & 63, B = t.B;
+  const int i = blockIdx.x * (kTlbThreads / 64) + (tid >> 6);
+  __shared__ uint32_t s_z0[31], s_pow[31];
+  __shared__ int s_epoch;
+  const int players = block_players(p.vtp_in, B);
+  const uint32_t seed = *p.seed;
+  if (tid < 31) s_pow[tid] = p.pow16807[tid];
+  if (tid == 0) s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  seed_state_parallel(seed, s_pow, s_z0);
+  __syncthreads();
+  const unsigned long long epoch = (unsigned long long)(uint32_t)s_epoch;
+  if (i < B) {
+    const float4 mm = p.minmax[i];
+    const int vtp0 = p.vtp_in[i];
+    TieInfo ti;
+    auto nodraw = [](int) -> uint32_t { return 0u; };
+    Descent d = descend_wave<EZ, true>(t, i, i, B, mm, players, vtp0, p.disc, nodraw, &ti);
+    if (lane == 0 && ti.status != 2)
+      __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ti.status != 0) {
+      // draw offset: the depths of every earlier root (wave-wide look-back, bounded spin)
+      int base = 0;
+      for (int q = lane; q < i; q += 64) {
+        unsigned long long v;
+        long long spins = 0;
+        while (true) {
+          v = __hip_atomic_load(&p.flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((v >> 32) == epoch) break;
+          if (++spins > (1ll << 22)) {
+            atomicAdd(p.diag + 1, 1);
+            v = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        base += (int)(v & 0xffffffffu);
+      }
+#pragma unroll
+      for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
+      const uint32_t *coef = p.coef;
+      const int npos = p.coef_positions;
+      int32_t *diag = p.diag;
+      if (ti.status == 1) {
+        // a tie among unexpanded children: the draw picks the leaf, the depth stays
+        const uint32_t rr = glibc_draw(coef, npos, s_z0, base + ti.level, diag);
+        unsigned long long m = ti.mask;
+        int kk = (int)(rr % (uint32_t)__popcll(m));
+        for (; kk > 0; --kk) m &= m - 1;
+        const int jsel = __ffsll((long long)m) - 1;
+        const int parent = t.path[(size_t)ti.level * B + i];
+        const int action = legal_at(t, i, parent, jsel);
+        if (lane == 0) {
+          t.path_act[(size_t)ti.level * B + i] = action;
+          t.path[(size_t)(ti.level + 1) * B + i] = 1 + t.A * t.meta[nidx(t, parent, i)].latent + action;
+        }
+        d.action = action;
+        d.leaf = 1 + t.A * t.meta[nidx(t, parent, i)].latent + action;
+      } else {
+        // the depth depends on the draws: walk with them, then publish
+        auto draw = [coef, npos, diag, base](int level) -> uint32_t {
+          return glibc_draw(coef, npos, s_z0, base + level, diag);
+        };
+        d = descend_wave<EZ, false>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr);
+        if (lane == 0)
+          __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (lane == 0) {
+      p.out_x[i] = d.x;
+      p.out_y[i] = i;
+      p.out_a[i] = d.action;
+      if (p.out_a64) p.out_a64[i] = d.action;
+      p.out_vtp[i] = d.vtp;
+      p.out_len[i] = d.len;
+      t.pathlen[i] = d.len;
+    }
+    // best_action along the final path (cnode.cpp:806)
+    for (int l = lane; l < d.len; l += 64) {
+      const int node = t.path[(size_t)l * B + i];
+      t.meta[nidx(t, node, i)].best = t.path_act[(size_t)l * B + i];
+    }
+  }
+  // the last workgroup to finish advances the epoch for the next launch
+  __syncthreads();
+  if (tid == 0) {
+    if (blockIdx.x == 0) p.diag[0] = 1;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const uint32_t done = atomicAdd(p.epoch + 1, 1u);
+    if (done == gridDim.x - 1) {
+      p.epoch[1] = 0;
+      __hip_atomic_store(p.epoch, (uint32_t)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace lzm

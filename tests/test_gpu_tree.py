@@ -55,6 +55,14 @@ def test_gpu_matches_oracle_parity_mode(case):
     assert_same(run_transcript(tr, GpuTree), run_transcript(tr, OracleTree))
 
 
+# parity mode runs one wave per root with a decoupled look-back of the draw offsets
+# (lzm_traverse_lb.h); LZM_TRAVERSE=serial keeps the one-workgroup fixed-point kernel
+@pytest.mark.parametrize("case", [CASES[1], CASES[3], CASES[5], CASES[9]], ids=lambda c: f"b{c[0]}_a{c[2]}_{c[5]}")
+def test_serial_traverse_kernel_matches_oracle(case, monkeypatch):
+    monkeypatch.setenv("LZM_TRAVERSE", "serial")
+    test_gpu_matches_oracle_parity_mode(case)
+
+
 @pytest.mark.parametrize("case", [(256, 50, 2, 1, False), (512, 30, 9, 2, False), (128, 40, 6, 1, True)])
 def test_gpu_matches_oracle_fast_mode(case):
     B, S, A, players, ez = case
