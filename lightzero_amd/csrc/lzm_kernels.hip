@@ -318,20 +318,34 @@ struct DecodeArgs {
 };
 
 // ensure_softmax (scaling_transform.py:36-62): softmax is skipped only when EVERY row of the
-// batch already sums to 1 within allclose(atol=1e-5, rtol=1e-5). Pass 1 clears a word per
-// call and tensor (flag[0]: reward rows, flag[1]: value rows — the reference calls the
-// transform once per head); this kernel ANDs each row's verdict into its word.
+// batch already sums to 1 within allclose(atol=1e-5, rtol=1e-5) — judged per tensor (the
+// reference calls the transform once per head: a = reward rows, b = value rows). Each workgroup
+// (4 rows) overwrites its own verdict words part[2 * block + head] (1: no row of that head in the
+// block fails), so nothing has to be cleared between calls; consumers AND the words (norm_ok).
 __global__ __launch_bounds__(256) void normalized_check_kernel(const float *a, const float *b, int rows, int V,
-                                                               int32_t *flag) {
+                                                               int32_t *part) {
+  __shared__ int s_ok[2];
+  if (threadIdx.x == 0) s_ok[0] = s_ok[1] = 1;
+  __syncthreads();
   const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (w >= 2 * rows) return;
-  const float *row = (w < rows) ? a + (size_t)w * V : b + (size_t)(w - rows) * V;
-  const float s = wave_row_sum(row, V);
-  if ((threadIdx.x & 63) == 0 && !(fabsf(s - 1.0f) <= 1e-5f + 1e-5f)) atomicAnd(flag + (w < rows ? 0 : 1), 0);
+  if (w < 2 * rows) {
+    const float *row = (w < rows) ? a + (size_t)w * V : b + (size_t)(w - rows) * V;
+    const float s = wave_row_sum(row, V);
+    if ((threadIdx.x & 63) == 0 && !(fabsf(s - 1.0f) <= 1e-5f + 1e-5f)) atomicAnd(&s_ok[w < rows ? 0 : 1], 0);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) part[2 * blockIdx.x + threadIdx.x] = s_ok[threadIdx.x];
+}
+__host__ __device__ inline int norm_parts(int rows) { return (2 * rows * 64 + 255) / 256; }
+// head's verdict over every block's word (wave-uniform result)
+__device__ inline bool norm_ok(const int32_t *part, int nparts, int head) {
+  int bad = 0;
+  for (int q = (threadIdx.x & 63); q < nparts; q += 64) bad |= part[2 * q + head] == 0;
+  return __ballot(bad) == 0ull;
 }
 
 template <bool EZ>
-__global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, const int32_t *norm_flag) {
+__global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, const int32_t *norm_part) {
   const TreeView &t = p.t;
   const int lane = threadIdx.x & 63;
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per root
@@ -344,8 +358,9 @@ __global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, cons
   }
   float r, v;
   if (p.categorical) {
-    r = wave_support_expectation(p.reward_logits + (size_t)i * p.V, p.V, norm_flag[0] == 0);
-    v = wave_support_expectation(p.value_logits + (size_t)i * p.V, p.V, norm_flag[1] == 0);
+    const int np = norm_parts(t.B);
+    r = wave_support_expectation(p.reward_logits + (size_t)i * p.V, p.V, !norm_ok(norm_part, np, 0));
+    v = wave_support_expectation(p.value_logits + (size_t)i * p.V, p.V, !norm_ok(norm_part, np, 1));
   } else {
     r = p.reward_logits[(size_t)i * p.V];
     v = p.value_logits[(size_t)i * p.V];
@@ -368,19 +383,18 @@ __global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, cons
 }
 
 __global__ __launch_bounds__(256) void inverse_transform_kernel(const float *logits, int rows, int V, int categorical,
-                                                                const int32_t *norm_flag, float *out) {
+                                                                const int32_t *norm_part, float *out) {
   const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (i >= rows) return;
   float v;
   if (categorical) {
-    v = wave_support_expectation(logits + (size_t)i * V, V, norm_flag[0] == 0);
+    v = wave_support_expectation(logits + (size_t)i * V, V, !norm_ok(norm_part, norm_parts(rows), 0));
   } else {
     v = logits[(size_t)i * V];
   }
   if ((threadIdx.x & 63) == 0) out[i] = h_inverse(v);
 }
 
-__global__ void set_word_kernel(int32_t *w, int32_t v) { *w = v; }
 
 // CRoots::prepare / prepare_no_noise (cnode.cpp:321-358): expand each root over its legal list
 // (an empty list means every action, cnode.cpp:101-107), optional Dirichlet mix
@@ -709,7 +723,7 @@ int lzm_create(int B, int A, int max_sims, int flags, lzm_handle **out) {
   TRY(hipMalloc(&h->off, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->diag, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->hint, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
-  TRY(hipMalloc(&h->norm_flag, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->norm_flag, sizeof(int32_t) * 2 * norm_parts(B)) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMemset(h->diag, 0, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMemset(h->hint, 0, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMemset(h->pathlen, 0, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
@@ -919,10 +933,7 @@ int lzm_backprop(lzm_handle *h, int cur, float discount, float *minmax, const fl
 static int launch_norm_check(lzm_handle *hflag_owner, int32_t *flag, const float *a, const float *b, int rows, int V,
                              hipStream_t s) {
   (void)hflag_owner;
-  hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, flag, 1);
-  hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, flag + 1, 1);
-  const int waves = 2 * rows;
-  hipLaunchKernelGGL(normalized_check_kernel, dim3((waves * 64 + 255) / 256), dim3(256), 0, s, a, b, rows, V, flag);
+  hipLaunchKernelGGL(normalized_check_kernel, dim3(norm_parts(rows)), dim3(256), 0, s, a, b, rows, V, flag);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
@@ -962,6 +973,7 @@ int lzm_decode_backprop(lzm_handle *h, int cur, float discount, float *minmax, c
 }
 
 static int32_t *g_scratch_flag = nullptr;
+static int g_scratch_parts = 0;
 static std::mutex g_scratch_mu;
 
 int lzm_inverse_scalar_transform(const float *logits, int rows, int V, int categorical, float *out, void *stream) {
@@ -969,14 +981,17 @@ int lzm_inverse_scalar_transform(const float *logits, int rows, int V, int categ
   hipStream_t s = (hipStream_t)stream;
   {
     std::lock_guard<std::mutex> lk(g_scratch_mu);
-    if (!g_scratch_flag) LZM_HIP(hipMalloc(&g_scratch_flag, 64));
+    if (g_scratch_parts < norm_parts(rows)) {
+      // (grows only outside graph capture in practice: the first call sizes it)
+      if (g_scratch_flag) LZM_HIP(hipFree(g_scratch_flag));
+      g_scratch_flag = nullptr;
+      LZM_HIP(hipMalloc(&g_scratch_flag, sizeof(int32_t) * 2 * norm_parts(rows)));
+      g_scratch_parts = norm_parts(rows);
+    }
   }
-  if (categorical) {
-    hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, g_scratch_flag, 1);
-    hipLaunchKernelGGL(set_word_kernel, dim3(1), dim3(1), 0, s, g_scratch_flag + 1, 1);
-    hipLaunchKernelGGL(normalized_check_kernel, dim3((2 * rows * 64 + 255) / 256), dim3(256), 0, s, logits, logits,
-                       rows, V, g_scratch_flag);
-  }
+  if (categorical)
+    hipLaunchKernelGGL(normalized_check_kernel, dim3(norm_parts(rows)), dim3(256), 0, s, logits, logits, rows, V,
+                       g_scratch_flag);
   hipLaunchKernelGGL(inverse_transform_kernel, dim3((rows * 64 + 255) / 256), dim3(256), 0, s, logits, rows, V,
                      categorical, g_scratch_flag, out);
   LZM_CHECK_LAUNCH();
