@@ -264,6 +264,31 @@ int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const floa
                    const float *pool, const int32_t *x, const int32_t *action, float *out_latent, float *out_r,
                    float *out_h, void *stream);
 
+/* The MLP heads of the conv recurrent step in one launch (lzm_heads.h): reward hidden from
+ * r [B][Kr] (optionally relu(r * r_scale + r_shift), the EfficientZero value-prefix BatchNorm),
+ * value / policy hiddens from the head planes hd [B][Khd] (value planes at 0, policy planes at
+ * off_policy), then the three output layers. Replaces, per simulation, the fc_reward_head /
+ * fc_value / fc_policy MLPs of muzero_model.py:505-530, efficientzero_model.py:526-574 and
+ * common.py:854-881 (BatchNorm folded). w1t float[3][8][32][32][4], b1[96], w2t float[32][Vr+Vv+A],
+ * b2[Vr+Vv+A] as packed by lightzero_amd.conv_infer; outputs reward [B][Vr], value [B][Vv],
+ * policy [B][A]. */
+int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const float *r_scale, const float *r_shift,
+                   const float *hd, const float *w1t, const float *b1, const float *w2t, const float *b2, int Vr,
+                   int Vv, int A, float *reward, float *value, float *policy, void *stream);
+
+/* EfficientZero reward LSTM, input side (lzm_lstm.h): xin[b] = [r[b] | hpool[x[b]][b]] — the leaf's
+ * hidden-state gather and the concat ahead of the gate GEMM. Replaces the per-simulation gathers of
+ * the LSTM state lists (mcts_ctree.py:756-775) and the nn.LSTM input assembly
+ * (efficientzero_model.py:526-574). r [B][Kr], hpool [slots][B][H], xin [B][Kr + H]; Kr, H % 4 == 0. */
+int lzm_ez_lstm_input(int B, int Kr, int H, const float *r, const float *hpool, const int32_t *x, float *xin,
+                      void *stream);
+
+/* EfficientZero reward LSTM, cell side: gates [B][4H] (= xin W^T + b, nn.LSTM order i, f, g, o),
+ * c0 = cpool[x[b]][b]; writes h1 / c1 [B][H] and the next state slot hslot / cslot [B][H], zeroed
+ * where search_len[b] % horizon == 0 (mcts_ctree.py:810-813). */
+int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *cpool, const int32_t *x, const int32_t *search_len,
+                     int horizon, float *h1, float *c1, float *hslot, float *cslot, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

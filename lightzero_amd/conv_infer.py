@@ -26,7 +26,8 @@ head 1x1) is ONE hand-written HIP launch per simulation, one workgroup per env w
 activations in LDS and f32 MFMA convolutions (csrc/lzm_conv.h, lzm_conv_trunk): it reads the leaf
 latent straight from the search's latent pool and writes the next latent straight into the next
 pool slot (`step_from_pool`), so the gather and the pool filing kernels disappear too. The head
-MLPs and the EfficientZero LSTM cell stay batched GEMMs over the envs.
+MLPs (reward, value, policy; both layers, ReLUs, the EZ value-prefix BatchNorm) are ONE more
+launch (csrc/lzm_heads.h, lzm_conv_heads); the EfficientZero LSTM cell stays a batched GEMM.
 """
 import numpy as np
 import torch
@@ -168,11 +169,41 @@ class FoldedConvNet:
         _lib.check(L.lzm_conv_trunk_prepare(self.n_dres, self.n_pres, self.r_ch, self.h_ch,
                                             raw.ctypes.data, host.ctypes.data), "lzm_conv_trunk_prepare")
         blob = torch.from_numpy(host).to(dev)
+        heads = self._pack_heads()
         if self.native is None:
             self.native = blob
             self.actmap = t["dyn_actmap"]  # [A, 64, 8, 8], re-folded in place
+            self.heads = heads
         else:
             self.native.copy_(blob)
+            if heads is not None:
+                for k, v in heads.items():
+                    if torch.is_tensor(v):
+                        self.heads[k].copy_(v)
+
+    def _pack_heads(self):
+        """lzm_conv_heads layouts (csrc/lzm_heads.h) of the folded head MLPs, or None if they do
+        not fit the kernel: w1t [3][8][32][32][4] over the three hidden layers (reward from r,
+        value / policy from the value / policy planes), w2t [32][Vr + Vv + A]."""
+        t = self.t
+        rw1, vw1 = t["rh_w1"], t["ph_w1"]
+        Kr, fv = rw1.shape[1], self.hv * 64
+        Khd = vw1.shape[1]
+        fp = Khd - fv
+        if rw1.shape[0] != 32 or vw1.shape[0] != 64 or Kr > 1024 or fv > 1024 or fp > 1024 or fp <= 0 \
+                or Kr % 4 or fv % 4 or Khd > 2048:
+            return None
+        dev = rw1.device
+        W = torch.zeros(96, 1024, dtype=torch.float32, device=dev)
+        W[0:32, :Kr] = rw1
+        W[32:64, :fv] = vw1[:32, :fv]
+        W[64:96, :fp] = vw1[32:, fv:]
+        w1t = W.reshape(3, 32, 8, 32, 4).permute(0, 2, 3, 1, 4).contiguous()  # [head][part][k4][col][4]
+        b1 = torch.cat([t["rh_b1"], t["ph_b1"]]).contiguous()
+        w2t = torch.cat([t["rh_w2"], t["v_w2"], t["p_w2"]], dim=0).t().contiguous()
+        b2 = torch.cat([t["rh_b2"], t["v_b2"], t["p_b2"]]).contiguous()
+        return dict(w1t=w1t, b1=b1, w2t=w2t, b2=b2, Kr=Kr, Khd=Khd, off_policy=fv, Vr=t["rh_w2"].shape[0],
+                    Vv=t["v_w2"].shape[0], A=t["p_w2"].shape[0])
 
     def _trunk(self, pool, x, action, out_latent):
         """lzm_conv_trunk: (reward planes [B, r_ch*64], head planes [B, h_ch*64]); next latent -> out_latent"""
@@ -190,6 +221,23 @@ class FoldedConvNet:
         is written to out_latent ([B, 64, 8, 8], e.g. the next pool slot). Native trunk only."""
         r, h = self._trunk(pool, x, action, out_latent)
         return self._heads(r, h, out_latent, hidden)
+
+    def step_from_pool_lstm(self, pool, x, action, out_latent, hpool, cpool, k, search_len, horizon):
+        """EfficientZero step on the pools: leaf latent pool[x[b]][b] and LSTM state (hpool, cpool)[x[b]][b]
+        ([S+1, B, H] each). The next latent goes to out_latent, the next LSTM state — zeroed where
+        search_len % horizon == 0 (mcts_ctree.py:810-813) — to hpool[k + 1] / cpool[k + 1]
+        (csrc/lzm_lstm.h around the rocBLAS gate GEMM). Native trunk only."""
+        r, hd = self._trunk(pool, x, action, out_latent)
+        t, P = self.t, _lib.ptr
+        B, H = r.shape[0], hpool.shape[2]
+        xin = torch.empty((B, r.shape[1] + H), dtype=torch.float32, device=r.device)
+        _lib.call("lzm_ez_lstm_input", B, r.shape[1], H, P(r), P(hpool), P(x), P(xin), _lib.stream_ptr())
+        gates = torch.addmm(t["lstm_b"], xin, t["lstm_w"].t())
+        h1 = torch.empty((B, H), dtype=torch.float32, device=r.device)
+        c1 = torch.empty_like(h1)
+        _lib.call("lzm_ez_lstm_cell", B, H, P(gates), P(cpool), P(x), P(search_len), int(horizon), P(h1), P(c1),
+                  P(hpool[k + 1]), P(cpool[k + 1]), _lib.stream_ptr())
+        return self._head_mlps(r, hd, out_latent, h1, c1)
 
     def initial_inference(self, obs):
         return self.model.initial_inference(obs)
@@ -230,6 +278,35 @@ class FoldedConvNet:
             i, f, g, o = gates.chunk(4, dim=1)
             c1 = torch.sigmoid(f) * c0 + torch.sigmoid(i) * torch.tanh(g)
             h1 = torch.sigmoid(o) * torch.tanh(c1)
+        else:
+            h1 = c1 = None
+        return self._head_mlps(r, hd, nxt, h1, c1)
+
+    def _head_mlps(self, r, hd, nxt, h1, c1):
+        """reward / value / policy MLPs (EZ: the reward head reads the LSTM output h1)"""
+        t = self.t
+        B = r.shape[0]
+        hp = getattr(self, "heads", None)
+        if hp is not None and r.is_cuda:
+            # every head MLP in one launch (csrc/lzm_heads.h)
+            inp = h1.contiguous() if self.ez else r
+            reward = torch.empty((B, hp["Vr"]), dtype=torch.float32, device=r.device)
+            value = torch.empty((B, hp["Vv"]), dtype=torch.float32, device=r.device)
+            policy = torch.empty((B, hp["A"]), dtype=torch.float32, device=r.device)
+            P = _lib.ptr
+            _lib.call("lzm_conv_heads", B, inp.shape[1], hp["Khd"], hp["off_policy"], P(inp),
+                      P(t["vp_s"]) if self.ez else None, P(t["vp_t"]) if self.ez else None, P(hd.contiguous()),
+                      P(hp["w1t"]), P(hp["b1"]), P(hp["w2t"]), P(hp["b2"]), hp["Vr"], hp["Vv"], hp["A"], P(reward),
+                      P(value), P(policy), _lib.stream_ptr())
+            out = _Out()
+            out.latent_state, out.value, out.policy_logits = nxt, value, policy
+            if self.ez:
+                out.value_prefix = reward
+                out.reward_hidden_state = (h1.unsqueeze(0), c1.unsqueeze(0))
+            else:
+                out.reward = reward
+            return out
+        if self.ez:
             r = torch.addcmul(t["vp_t"], h1, t["vp_s"]).relu_()
         r = F.linear(r, t["rh_w1"], t["rh_b1"]).relu_()
         reward = F.linear(r, t["rh_w2"], t["rh_b2"])

@@ -37,6 +37,8 @@
 #include "lzm_search_mlp.h"
 #include "lzm_search_res.h"
 #include "lzm_conv.h"
+#include "lzm_heads.h"
+#include "lzm_lstm.h"
 
 namespace lzm {
 
@@ -268,7 +270,59 @@ __global__ __launch_bounds__(256) void backprop_kernel(BackpropArgs p) {
 
 // InverseScalarTransform (scaling_transform.py:118-128) of one row by one wave:
 // softmax (unless `raw`), expectation over support [-(V-1)/2 .. (V-1)/2], then h^-1.
+// Register form for V <= 64 * NPL: the row is loaded once, every load in flight together (the loop
+// form re-reads it in three passes with one memory latency per iteration). Same per-lane order and
+// the same reductions, so the same bits.
+template <int NPL>
+__device__ inline float wave_support_expectation_reg(const float *row, int V, bool softmax) {
+  const int lane = threadIdx.x & 63;
+  const float half = (float)((V - 1) / 2);
+  float x[NPL];
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int j = lane + 64 * q;
+    x[q] = j < V ? row[j] : 0.0f;
+  }
+  if (!softmax) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int q = 0; q < NPL; ++q)
+      if (lane + 64 * q < V) acc += x[q] * ((float)(lane + 64 * q) - half);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+    return acc;
+  }
+  float mx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q)
+    if (lane + 64 * q < V) mx = fmaxf(mx, x[q]);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+  float sum = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q)
+    if (lane + 64 * q < V) sum += expf(x[q] - mx);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  float acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q)
+    if (lane + 64 * q < V) acc += (expf(x[q] - mx) / sum) * ((float)(lane + 64 * q) - half);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  return acc;
+}
+
+__device__ inline float wave_support_expectation_loop(const float *row, int V, bool softmax);
+
 __device__ inline float wave_support_expectation(const float *row, int V, bool softmax) {
+  if (V <= 64 * 2) return wave_support_expectation_reg<2>(row, V, softmax);
+  if (V <= 64 * 10) return wave_support_expectation_reg<10>(row, V, softmax);
+  if (V <= 64 * 16) return wave_support_expectation_reg<16>(row, V, softmax);
+  return wave_support_expectation_loop(row, V, softmax);
+}
+
+__device__ inline float wave_support_expectation_loop(const float *row, int V, bool softmax) {
   const int lane = threadIdx.x & 63;
   const float half = (float)((V - 1) / 2);
   if (!softmax) {
@@ -297,6 +351,18 @@ __device__ inline float wave_support_expectation(const float *row, int V, bool s
 __device__ inline float wave_row_sum(const float *row, int V) {
   const int lane = threadIdx.x & 63;
   float s = 0.0f;
+  if (V <= 64 * 10) {
+    // every load in flight together; same per-lane order as the loop
+    float x[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) x[q] = lane + 64 * q < V ? row[lane + 64 * q] : 0.0f;
+#pragma unroll
+    for (int q = 0; q < 10; ++q)
+      if (lane + 64 * q < V) s += x[q];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+    return s;
+  }
   for (int j = lane; j < V; j += 64) s += row[j];
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
@@ -367,11 +433,25 @@ __global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, cons
   }
   r = h_inverse(r);
   v = h_inverse(v);
-  if (lane != 0) return;
-  if (p.out_decoded) {
+  if (p.out_decoded && lane == 0) {
     p.out_decoded[2 * i] = r;
     p.out_decoded[2 * i + 1] = v;
   }
+  if (t.A <= 64) {
+    // one lane per child / path level, bit-identical to the serial form below (lzm_tree.h)
+    const int len = t.pathlen[i];
+    const int leaf = t.path[(size_t)len * t.B + i];
+    const int tp = p.to_play[i];
+    const int is_reset = (EZ && p.horizon > 0 && len % p.horizon == 0) ? 1 : 0;
+    if (p.out_is_reset && lane == 0) p.out_is_reset[i] = is_reset;
+    expand_wave(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, EZ ? is_reset : -1);
+    if (EZ)
+      backup_wave_ez(t, i, i, t.B, p.minmax + i, tp, v, p.disc);
+    else
+      backup_wave(t, i, i, t.B, p.minmax + i, tp, v, p.disc);
+    return;
+  }
+  if (lane != 0) return;
   const int len = t.pathlen[i];
   const int leaf = t.path[(size_t)len * t.B + i];
   int is_reset = 0;
@@ -2005,3 +2085,59 @@ int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const floa
 }
 
 }  // extern "C"
+
+extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const float *r_scale,
+                              const float *r_shift, const float *hd, const float *w1t, const float *b1,
+                              const float *w2t, const float *b2, int Vr, int Vv, int A, float *reward, float *value,
+                              float *policy, void *stream) {
+  if (B <= 0 || Kr <= 0 || Kr > kHdRMax || Khd <= 0 || Khd > kHdHMax || off_policy <= 0 || off_policy >= Khd ||
+      Khd - off_policy > kHdKMax || off_policy > kHdKMax || Vr <= 0 || Vv <= 0 || A <= 0 || Vr > kHdCols * kHdThreads || Vv > kHdCols * kHdThreads ||
+      A > kHdCols * kHdThreads || !r || !hd || !w1t ||
+      !b1 || !w2t || !b2 || !reward || !value || !policy || (!r_scale) != (!r_shift) || ((uintptr_t)w1t & 15) ||
+      (Kr & 3) || (Khd & 3) || (off_policy & 3)) {
+    set_err("lzm_conv_heads: bad arguments (Kr <= 1024, head planes <= 2048, K per head <= 1024, supports <= 768, 16-B aligned w1t)");
+    return LZM_ERR_ARG;
+  }
+  HeadsArgs p;
+  p.B = B; p.Kr = Kr; p.Khd = Khd;
+  p.r = r; p.r_scale = r_scale; p.r_shift = r_shift; p.hd = hd;
+  p.src[0] = 0; p.off[0] = 0; p.K[0] = Kr;
+  p.src[1] = 1; p.off[1] = 0; p.K[1] = off_policy;
+  p.src[2] = 1; p.off[2] = off_policy; p.K[2] = Khd - off_policy;
+  p.w1t = w1t; p.b1 = b1; p.w2t = w2t; p.b2 = b2;
+  p.Vr = Vr; p.Vv = Vv; p.A = A;
+  p.reward = reward; p.value = value; p.policy = policy;
+  hipLaunchKernelGGL(conv_heads_kernel, dim3((B + kHdEnvs - 1) / kHdEnvs, 3), dim3(kHdThreads), 0, (hipStream_t)stream, p);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" int lzm_ez_lstm_input(int B, int Kr, int H, const float *r, const float *hpool, const int32_t *x, float *xin,
+                                 void *stream) {
+  if (B <= 0 || Kr <= 0 || H <= 0 || (Kr & 3) || (H & 3) || !r || !hpool || !x || !xin ||
+      (((uintptr_t)r | (uintptr_t)hpool | (uintptr_t)xin) & 15)) {
+    set_err("lzm_ez_lstm_input: bad arguments (Kr, H multiples of 4, 16-B aligned buffers)");
+    return LZM_ERR_ARG;
+  }
+  const long long n = (long long)B * ((Kr + H) >> 2);
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(ez_lstm_input_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, Kr, H, r, hpool, x, xin);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *cpool, const int32_t *x,
+                                const int32_t *search_len, int horizon, float *h1, float *c1, float *hslot,
+                                float *cslot, void *stream) {
+  if (B <= 0 || H <= 0 || (H & 3) || !gates || !cpool || !x || !search_len || !h1 || !c1 || !hslot || !cslot ||
+      (((uintptr_t)gates | (uintptr_t)cpool | (uintptr_t)h1 | (uintptr_t)c1 | (uintptr_t)hslot | (uintptr_t)cslot) & 15)) {
+    set_err("lzm_ez_lstm_cell: bad arguments (H multiple of 4, 16-B aligned buffers)");
+    return LZM_ERR_ARG;
+  }
+  const long long n = (long long)B * (H >> 2);
+  const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(ez_lstm_cell_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, H, gates, cpool, x,
+                     search_len, horizon, h1, c1, hslot, cslot);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}

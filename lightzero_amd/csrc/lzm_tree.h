@@ -439,13 +439,14 @@ __device__ inline void backup(const TreeView &t, int i, float4 *mm_ptr, int to_p
 // Bit-identical: pmax is a max (order-free), the prior denominator is summed in action order by a
 // readlane chain, every other quantity is per child.
 __device__ inline void expand_wave(const TreeView &t, int i, int leaf, int to_play, int latent, float reward,
-                                   const float *logits) {
+                                   const float *logits, int is_reset = -1) {
   const int lane = threadIdx.x & 63;
   const int A = t.A;
   if (lane == 0) {
     NodeMeta m = t.meta[nidx(t, leaf, i)];
     m.latent = latent;
     m.to_play = to_play;
+    if (is_reset >= 0) m.is_reset = is_reset;  // EfficientZero (is_reset < 0: MuZero, untouched)
     t.meta[nidx(t, leaf, i)] = m;
     t.stat[nidx(t, leaf, i)].reward = reward;
   }
@@ -519,6 +520,74 @@ __device__ inline void backup_wave(const TreeView &t, int i, int li, int ps, flo
       const float v = node_value(s);
       if (t.val) t.val[nidx(t, node, i)] = v;
       const float q = (to_play == -1) ? s.reward + disc * v : s.reward + disc * -v;
+      qmax = fmaxf(qmax, q);
+      qmin = fminf(qmin, q);
+    }
+  }
+  qmax = wave_max_dpp(qmax);
+  qmin = -wave_max_dpp(-qmin);
+  if (lane == 0) {
+    float4 mm = *mm_ptr;
+    if (qmax > mm.x) mm.x = qmax;
+    if (qmin < mm.y) mm.y = qmin;
+    *mm_ptr = mm;
+  }
+}
+
+// backup_slice<true> with one lane per path level (EfficientZero cbackpropagate,
+// ctree_efficientzero/lib/cnode.cpp:482-575). Per level: true_reward = value_prefix - parent's
+// value_prefix feeds the min-max update, its is_reset form (the node's own value_prefix when the
+// parent is reset) feeds the bootstrap chain. The chain runs leaf to root by readlane in the
+// reference's order; the rest is per level; min-max by an order-free max / min (exact).
+__device__ inline void backup_wave_ez(const TreeView &t, int i, int li, int ps, float4 *mm_ptr, int to_play,
+                                      float value, float disc) {
+  const int lane = threadIdx.x & 63;
+  const int len = t.pathlen[li];
+  float b = value;  // wave-uniform chain value
+  float qmax = -INFINITY, qmin = INFINITY;
+  for (int g0 = len; g0 >= 0; g0 -= 64) {
+    const int l = g0 - lane;  // lane j holds level g0 - j (leaf-most first)
+    const bool act = l >= 0;
+    int node = 0, ntp = 0;
+    NodeStat s;
+    s.visit = 0; s.value_sum = 0.0f; s.prior = 0.0f; s.reward = 0.0f;
+    float tq = 0.0f, tc = 0.0f;  // true reward for the min-max update / for the chain
+    if (act) {
+      node = t.path[(size_t)l * ps + li];
+      s = t.stat[nidx(t, node, i)];
+      ntp = t.meta[nidx(t, node, i)].to_play;
+      float pvp = 0.0f;
+      int reset = 0;
+      if (l >= 1) {
+        const int pn = t.path[(size_t)(l - 1) * ps + li];
+        pvp = t.stat[nidx(t, pn, i)].reward;
+        reset = t.meta[nidx(t, pn, i)].is_reset;
+      }
+      tq = s.reward - pvp;
+      tc = (reset == 1) ? s.reward : tq;
+    }
+    const int nlev = g0 + 1 < 64 ? g0 + 1 : 64;
+    float bl = 0.0f;
+    for (int j = 0; j < nlev; ++j) {
+      if (lane == j) bl = b;
+      const float tr = readlane_f(tc, j);
+      if (to_play == -1) {
+        b = tr + disc * b;
+      } else {
+        const int nj = __builtin_amdgcn_readlane(ntp, j);
+        b = (nj != to_play) ? (tr + disc * b) : (-tr + disc * b);
+      }
+    }
+    if (act) {
+      if (to_play == -1 || ntp == to_play)
+        s.value_sum += bl;
+      else
+        s.value_sum += -bl;
+      s.visit += 1;
+      t.stat[nidx(t, node, i)] = s;
+      const float v = node_value(s);
+      if (t.val) t.val[nidx(t, node, i)] = v;
+      const float q = tq + disc * v;
       qmax = fmaxf(qmax, q);
       qmin = fminf(qmin, q);
     }

@@ -292,12 +292,14 @@ class EfficientZeroMCTSCtree(object):
         native = _native_trunk(model, buf)
         for k in range(S):
             t.traverse(buf.mm, buf.seeds[k:k + 1], buf.vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
-            t.gather(buf.extra[0], Hl, buf.extra_in[0])
-            t.gather(buf.extra[1], Hl, buf.extra_in[1])
-            hidden = (buf.extra_in[0].unsqueeze(0), buf.extra_in[1].unsqueeze(0))
             if native:
-                out = model.step_from_pool(buf.pool, t.x, t.action, buf.pool[k + 1], hidden)
+                # the LSTM state is gathered from / filed (reset-masked) into the state pools on the device
+                out = model.step_from_pool_lstm(buf.pool, t.x, t.action, buf.pool[k + 1], buf.extra[0], buf.extra[1],
+                                                k, t.search_len, horizon)
             else:
+                t.gather(buf.extra[0], Hl, buf.extra_in[0])
+                t.gather(buf.extra[1], Hl, buf.extra_in[1])
+                hidden = (buf.extra_in[0].unsqueeze(0), buf.extra_in[1].unsqueeze(0))
                 t.gather(buf.pool, row, buf.net_in)
                 out = model.recurrent_inference(buf.net_in, hidden, t.action64)
             logits = out.policy_logits.float().contiguous()
@@ -310,6 +312,8 @@ class EfficientZeroMCTSCtree(object):
                               out_decoded=None if rec is None else rec.decoded[k])
             if rec is not None:
                 rec.is_reset[k].copy_(t.is_reset)
+            if native:
+                continue  # lzm_ez_lstm_cell already filed the masked state
             # reset the LSTM state of roots whose search_len % horizon == 0 (mcts_ctree.py:810-816)
             keep = (1 - t.is_reset).to(torch.float32).unsqueeze(1)
             hc, hh = out.reward_hidden_state

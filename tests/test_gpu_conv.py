@@ -197,3 +197,36 @@ def test_native_trunk_matches_module(kind):
         o2 = net.recurrent_inference(leaf, hc, act) if kind == "ez" else net.recurrent_inference(leaf, act)
         assert torch.equal(slot, o2.latent_state) and torch.equal(o1.value, o2.value)
         assert torch.equal(o1.policy_logits, o2.policy_logits)
+
+
+def test_native_lstm_step_matches_module():
+    """EZ on the pools: trunk + lzm_ez_lstm_input / rocBLAS gates / lzm_ez_lstm_cell + heads == the
+    module's recurrent_inference on the gathered inputs (fp32, rtol 1e-4 / atol 1e-5), and the next
+    state slots hold the new state zeroed where search_len % horizon == 0 (mcts_ctree.py:810-813)."""
+    from lightzero_amd.conv_infer import FoldedConvNet
+    model = conv_model("ez", 6)
+    net = FoldedConvNet(model)
+    assert net.native is not None, "native trunk not packed on the GPU"
+    B, slots, H = 37, 4, 512
+    g = torch.Generator(device=DEV).manual_seed(2)
+    pool = torch.relu(torch.randn(slots, B, 64, 8, 8, generator=g, device=DEV))
+    hpool = torch.randn(slots + 1, B, H, generator=g, device=DEV) * 0.5
+    cpool = torch.randn(slots + 1, B, H, generator=g, device=DEV) * 0.5
+    x = torch.randint(0, slots, (B,), generator=g, device=DEV).to(torch.int32)
+    act = torch.randint(0, model.action_space_size, (B,), generator=g, device=DEV)
+    slen = torch.randint(1, 13, (B,), generator=g, device=DEV).to(torch.int32)
+    rows = torch.arange(B, device=DEV)
+    xl = x.long()
+    with torch.no_grad():
+        ref = model.recurrent_inference(pool[xl, rows], (hpool[xl, rows].unsqueeze(0), cpool[xl, rows].unsqueeze(0)),
+                                        act)
+        slot = torch.empty(B, 64, 8, 8, device=DEV)
+        got = net.step_from_pool_lstm(pool, x, act.to(torch.int32), slot, hpool, cpool, slots - 1, slen, 5)
+    for name in ("value_prefix", "value", "policy_logits"):
+        torch.testing.assert_close(getattr(got, name), getattr(ref, name), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(slot, ref.latent_state, rtol=1e-4, atol=1e-5)
+    keep = (slen % 5 != 0).float().unsqueeze(1)
+    h1, c1 = (s.reshape(B, H) for s in ref.reward_hidden_state)
+    torch.testing.assert_close(hpool[slots], h1 * keep, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(cpool[slots], c1 * keep, rtol=1e-4, atol=1e-5)
+    assert torch.all(hpool[slots][slen % 5 == 0] == 0) and torch.all(cpool[slots][slen % 5 == 0] == 0)
