@@ -276,6 +276,21 @@ int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const
                    const float *hd, const float *w1t, const float *b1, const float *w2t, const float *b2, int Vr,
                    int Vv, int A, float *reward, float *value, float *policy, void *stream);
 
+/* lzm_decode_backprop of simulation `cur` fused with lzm_traverse of the next simulation (parity /
+ * glibc mode only): one launch in which the wave that backs up root i then walks root i again
+ * (same requests, draws and outputs as the two separate calls). Replaces the pair
+ * batch_backpropagate(sim) + batch_traverse(sim + 1) of mcts_ctree.py:255-321 / :756-827
+ * (cnode.cpp:480-500, :755-824). Arguments: those of lzm_decode_backprop, then those of lzm_traverse
+ * (the next traverse's seed; its outputs overwrite the current request buffers). */
+int lzm_decode_backprop_traverse(lzm_handle *h, int current_latent_state_index, float discount, float *minmax,
+                                 const float *reward_logits, const float *value_logits, int support_len,
+                                 int categorical, const float *policy_logits, const int32_t *to_play,
+                                 int lstm_horizon, int32_t *out_is_reset, const float *next_latent, float *pool_slot,
+                                 int64_t row_elems, float *out_decoded, int pb_c_base, float pb_c_init,
+                                 const uint32_t *seed, const int32_t *virtual_to_play_in, int32_t *out_x,
+                                 int32_t *out_y, int32_t *out_last_action, int64_t *out_last_action_i64,
+                                 int32_t *out_virtual_to_play, int32_t *out_search_len, void *stream);
+
 /* EfficientZero reward LSTM, input side (lzm_lstm.h): xin[b] = [r[b] | hpool[x[b]][b]] — the leaf's
  * hidden-state gather and the concat ahead of the gate GEMM. Replaces the per-simulation gathers of
  * the LSTM state lists (mcts_ctree.py:756-775) and the nn.LSTM input assembly

@@ -410,12 +410,11 @@ __device__ inline bool norm_ok(const int32_t *part, int nparts, int head) {
   return __ballot(bad) == 0ull;
 }
 
+// decode + expand + backup of root i by one wave (all 64 lanes call it)
 template <bool EZ>
-__global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, const int32_t *norm_part) {
+__device__ inline void decode_root(const DecodeArgs &p, const int32_t *norm_part, int i) {
   const TreeView &t = p.t;
   const int lane = threadIdx.x & 63;
-  const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per root
-  if (i >= t.B) return;
   // new latent row into the pool slot (mcts_ctree.py:305)
   if (p.next_latent && p.pool_slot) {
     const float *src = p.next_latent + (size_t)i * p.row_elems;
@@ -460,6 +459,12 @@ __global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, cons
   const int tp = p.to_play[i];
   expand_leaf(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, is_reset, EZ);
   backup<EZ>(t, i, p.minmax + i, tp, v, p.disc);
+}
+
+template <bool EZ>
+__global__ __launch_bounds__(256) void decode_backprop_kernel(DecodeArgs p, const int32_t *norm_part) {
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;  // one wave per root
+  if (i < p.t.B) decode_root<EZ>(p, norm_part, i);
 }
 
 __global__ __launch_bounds__(256) void inverse_transform_kernel(const float *logits, int rows, int V, int categorical,
@@ -634,6 +639,33 @@ __global__ void debug_glibc_kernel(uint32_t seed, int n, int32_t *out, const uin
 }  // namespace lzm
 
 #include "lzm_traverse_lb.h"  // uses block_players above
+
+namespace lzm {
+
+// Simulation k's decode + expand + backup fused with simulation k + 1's traverse (generic search
+// path, parity mode): the wave that backs up root i walks root i again at once, over the records it
+// has just written (warm in this CU's caches) and without a launch of its own. The walk is the
+// look-back traverse's (lzm_traverse_lb.h), so requests and draws are those of the separate launches.
+template <bool EZ>
+__global__ __launch_bounds__(kTlbThreads) void decode_traverse_kernel(DecodeArgs p, const int32_t *norm_part,
+                                                                      TraverseLbArgs q) {
+  __shared__ uint32_t s_z0[31], s_pow[31];
+  __shared__ int s_epoch;
+  int players;
+  const unsigned long long epoch = traverse_lb_setup(q, s_z0, s_pow, &s_epoch, &players);
+  const int i = blockIdx.x * (kTlbThreads / 64) + (threadIdx.x >> 6);
+  if (i < p.t.B) {
+    decode_root<EZ>(p, norm_part, i);
+    // the backup's stores (other lanes of this wave) complete before the walk reads them; the walk
+    // runs on the same CU, so workgroup scope suffices (agent scope would write back the L2)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    traverse_lb_root<EZ>(q, i, s_z0, epoch, players);
+  }
+  traverse_lb_finish(q, epoch);
+}
+
+}  // namespace lzm
 
 // ============================================================================ host side
 using namespace lzm;
@@ -1048,6 +1080,65 @@ int lzm_decode_backprop(lzm_handle *h, int cur, float discount, float *minmax, c
   const int32_t *nf = categorical ? h->norm_flag : nullptr;
   if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(decode_backprop_kernel<true>, g, b, 0, s, p, nf);
   else hipLaunchKernelGGL(decode_backprop_kernel<false>, g, b, 0, s, p, nf);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_decode_backprop_traverse(lzm_handle *h, int cur, float discount, float *minmax, const float *reward_logits,
+                                 const float *value_logits, int support_len, int categorical,
+                                 const float *policy_logits, const int32_t *to_play, int lstm_horizon,
+                                 int32_t *out_is_reset, const float *next_latent, float *pool_slot, int64_t row_elems,
+                                 float *out_decoded, int pb_c_base, float pb_c_init, const uint32_t *seed,
+                                 const int32_t *vtp_in, int32_t *out_x, int32_t *out_y, int32_t *out_a,
+                                 int64_t *out_a64, int32_t *out_vtp, int32_t *out_len, void *stream) {
+  if (!h || !minmax || !reward_logits || !value_logits || !policy_logits || !to_play || support_len <= 0 || !seed ||
+      !vtp_in || !out_x || !out_y || !out_a || !out_vtp || !out_len) {
+    set_err("lzm_decode_backprop_traverse: null argument");
+    return LZM_ERR_ARG;
+  }
+  if (categorical && support_len % 2 == 0) {
+    set_err("lzm_decode_backprop_traverse: categorical support length must be odd (2*support_scale+1)");
+    return LZM_ERR_ARG;
+  }
+  if (pb_c_base <= 0) {
+    set_err("lzm_decode_backprop_traverse: pb_c_base must be positive");
+    return LZM_ERR_ARG;
+  }
+  if (h->flags & LZM_RNG_FAST) {
+    set_err("lzm_decode_backprop_traverse: parity (glibc) mode only; use lzm_decode_backprop + lzm_traverse");
+    return LZM_ERR_ARG;
+  }
+  int rc = check_cur(h, cur);
+  if (rc != LZM_OK) return rc;
+  rc = fill_lut(h, pb_c_base, pb_c_init);
+  if (rc != LZM_OK) return rc;
+  rc = ensure_coef(h, h->B * h->depth_cap + 64);
+  if (rc != LZM_OK) return rc;
+  rc = ensure_flags(h, 1, 1);
+  if (rc != LZM_OK) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (categorical) {
+    rc = launch_norm_check(h, h->norm_flag, reward_logits, value_logits, h->B, support_len, s);
+    if (rc != LZM_OK) return rc;
+  }
+  DecodeArgs p;
+  p.t = view(h);
+  p.minmax = (float4 *)minmax;
+  p.reward_logits = reward_logits; p.value_logits = value_logits; p.policy_logits = policy_logits;
+  p.to_play = to_play; p.out_is_reset = out_is_reset; p.next_latent = next_latent; p.pool_slot = pool_slot;
+  p.row_elems = row_elems; p.V = support_len; p.categorical = categorical; p.cur = cur; p.horizon = lstm_horizon;
+  p.disc = discount; p.out_decoded = out_decoded;
+  TraverseLbArgs q;
+  q.t = p.t; q.minmax = (const float4 *)minmax; q.seed = seed; q.vtp_in = vtp_in;
+  q.out_x = out_x; q.out_y = out_y; q.out_a = out_a; q.out_vtp = out_vtp; q.out_len = out_len;
+  q.out_a64 = (long long *)out_a64; q.disc = discount;
+  q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
+  q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag;
+  const int per = kTlbThreads / 64;
+  dim3 g((h->B + per - 1) / per), b(kTlbThreads);
+  const int32_t *nf = categorical ? h->norm_flag : nullptr;
+  if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(decode_traverse_kernel<true>, g, b, 0, s, p, nf, q);
+  else hipLaunchKernelGGL(decode_traverse_kernel<false>, g, b, 0, s, p, nf, q);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }

@@ -38,104 +38,124 @@ struct TraverseLbArgs {
   int32_t *diag;              // [0] passes (1), [1] spin timeouts (must stay 0)
 };
 
-template <bool EZ>
-__global__ __launch_bounds__(kTlbThreads) void traverse_lookback_kernel(TraverseLbArgs p) {
-  const TreeView &t = p.t;
-  const int tid = threadIdx.x, lane = tid & 63, B = t.B;
-  const int i = blockIdx.x * (kTlbThreads / 64) + (tid >> 6);
-  __shared__ uint32_t s_z0[31], s_pow[31];
-  __shared__ int s_epoch;
-  const int players = block_players(p.vtp_in, B);
+// Workgroup-level part of a look-back traverse (every thread calls it): the seeded glibc state and
+// the launch epoch in LDS. Returns the epoch; *players = the batch's player count.
+__device__ inline unsigned long long traverse_lb_setup(const TraverseLbArgs &p, uint32_t *s_z0, uint32_t *s_pow,
+                                                       int *s_epoch, int *players) {
+  const int tid = threadIdx.x;
+  *players = block_players(p.vtp_in, p.t.B);
   const uint32_t seed = *p.seed;
   if (tid < 31) s_pow[tid] = p.pow16807[tid];
-  if (tid == 0) s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) *s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   seed_state_parallel(seed, s_pow, s_z0);
   __syncthreads();
-  const unsigned long long epoch = (unsigned long long)(uint32_t)s_epoch;
-  if (i < B) {
-    const float4 mm = p.minmax[i];
-    const int vtp0 = p.vtp_in[i];
-    TieInfo ti;
-    auto nodraw = [](int) -> uint32_t { return 0u; };
-    Descent d = descend_wave<EZ, true>(t, i, i, B, mm, players, vtp0, p.disc, nodraw, &ti);
-    if (lane == 0 && ti.status != 2)
-      __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ti.status != 0) {
-      // draw offset: the depths of every earlier root (wave-wide look-back, bounded spin)
-      int base = 0;
-      for (int q = lane; q < i; q += 64) {
-        unsigned long long v;
-        long long spins = 0;
-        while (true) {
-          v = __hip_atomic_load(&p.flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((v >> 32) == epoch) break;
-          if (++spins > (1ll << 22)) {
-            atomicAdd(p.diag + 1, 1);
-            v = 0;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+  return (unsigned long long)(uint32_t)*s_epoch;
+}
+
+// One root's walk by one wave (all 64 lanes): draw-free classification, depth published at once,
+// look-back only when a draw value is needed (see the header comment).
+template <bool EZ>
+__device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const uint32_t *s_z0, unsigned long long epoch,
+                                        int players) {
+  const TreeView &t = p.t;
+  const int lane = threadIdx.x & 63, B = t.B;
+  const float4 mm = p.minmax[i];
+  const int vtp0 = p.vtp_in[i];
+  TieInfo ti;
+  auto nodraw = [](int) -> uint32_t { return 0u; };
+  Descent d = descend_wave<EZ, true>(t, i, i, B, mm, players, vtp0, p.disc, nodraw, &ti);
+  if (lane == 0 && ti.status != 2)
+    __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ti.status != 0) {
+    // draw offset: the depths of every earlier root (wave-wide look-back, bounded spin)
+    int base = 0;
+    for (int q = lane; q < i; q += 64) {
+      unsigned long long v;
+      long long spins = 0;
+      while (true) {
+        v = __hip_atomic_load(&p.flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 32) == epoch) break;
+        if (++spins > (1ll << 22)) {
+          atomicAdd(p.diag + 1, 1);
+          v = 0;
+          break;
         }
-        base += (int)(v & 0xffffffffu);
+        __builtin_amdgcn_s_sleep(1);
       }
+      base += (int)(v & 0xffffffffu);
+    }
 #pragma unroll
-      for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
-      const uint32_t *coef = p.coef;
-      const int npos = p.coef_positions;
-      int32_t *diag = p.diag;
-      if (ti.status == 1) {
-        // a tie among unexpanded children: the draw picks the leaf, the depth stays
-        const uint32_t rr = glibc_draw(coef, npos, s_z0, base + ti.level, diag);
-        unsigned long long m = ti.mask;
-        int kk = (int)(rr % (uint32_t)__popcll(m));
-        for (; kk > 0; --kk) m &= m - 1;
-        const int jsel = __ffsll((long long)m) - 1;
-        const int parent = t.path[(size_t)ti.level * B + i];
-        const int action = legal_at(t, i, parent, jsel);
-        if (lane == 0) {
-          t.path_act[(size_t)ti.level * B + i] = action;
-          t.path[(size_t)(ti.level + 1) * B + i] = 1 + t.A * t.meta[nidx(t, parent, i)].latent + action;
-        }
-        d.action = action;
-        d.leaf = 1 + t.A * t.meta[nidx(t, parent, i)].latent + action;
-      } else {
-        // the depth depends on the draws: walk with them, then publish
-        auto draw = [coef, npos, diag, base](int level) -> uint32_t {
-          return glibc_draw(coef, npos, s_z0, base + level, diag);
-        };
-        d = descend_wave<EZ, false>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr);
-        if (lane == 0)
-          __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+    for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
+    const uint32_t *coef = p.coef;
+    const int npos = p.coef_positions;
+    int32_t *diag = p.diag;
+    if (ti.status == 1) {
+      // a tie among unexpanded children: the draw picks the leaf, the depth stays
+      const uint32_t rr = glibc_draw(coef, npos, s_z0, base + ti.level, diag);
+      unsigned long long m = ti.mask;
+      int kk = (int)(rr % (uint32_t)__popcll(m));
+      for (; kk > 0; --kk) m &= m - 1;
+      const int jsel = __ffsll((long long)m) - 1;
+      const int parent = t.path[(size_t)ti.level * B + i];
+      const int action = legal_at(t, i, parent, jsel);
+      if (lane == 0) {
+        t.path_act[(size_t)ti.level * B + i] = action;
+        t.path[(size_t)(ti.level + 1) * B + i] = 1 + t.A * t.meta[nidx(t, parent, i)].latent + action;
       }
-    }
-    if (lane == 0) {
-      p.out_x[i] = d.x;
-      p.out_y[i] = i;
-      p.out_a[i] = d.action;
-      if (p.out_a64) p.out_a64[i] = d.action;
-      p.out_vtp[i] = d.vtp;
-      p.out_len[i] = d.len;
-      t.pathlen[i] = d.len;
-    }
-    // best_action along the final path (cnode.cpp:806)
-    for (int l = lane; l < d.len; l += 64) {
-      const int node = t.path[(size_t)l * B + i];
-      t.meta[nidx(t, node, i)].best = t.path_act[(size_t)l * B + i];
+      d.action = action;
+      d.leaf = 1 + t.A * t.meta[nidx(t, parent, i)].latent + action;
+    } else {
+      // the depth depends on the draws: walk with them, then publish
+      auto draw = [coef, npos, diag, base, s_z0](int level) -> uint32_t {
+        return glibc_draw(coef, npos, s_z0, base + level, diag);
+      };
+      d = descend_wave<EZ, false>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr);
+      if (lane == 0)
+        __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  // the last workgroup to finish advances the epoch for the next launch
+  if (lane == 0) {
+    p.out_x[i] = d.x;
+    p.out_y[i] = i;
+    p.out_a[i] = d.action;
+    if (p.out_a64) p.out_a64[i] = d.action;
+    p.out_vtp[i] = d.vtp;
+    p.out_len[i] = d.len;
+    t.pathlen[i] = d.len;
+  }
+  // best_action along the final path (cnode.cpp:806)
+  for (int l = lane; l < d.len; l += 64) {
+    const int node = t.path[(size_t)l * B + i];
+    t.meta[nidx(t, node, i)].best = t.path_act[(size_t)l * B + i];
+  }
+}
+
+// The last workgroup to finish advances the epoch for the next launch (every thread calls it). No
+// release fence: nothing inside the launch reads data behind this counter (the draw counts travel
+// in the atomic flag words; the kernel boundary orders everything else), and on gfx950 an
+// agent-scope release is an L2 writeback (buffer_wbl2) per workgroup.
+__device__ inline void traverse_lb_finish(const TraverseLbArgs &p, unsigned long long epoch) {
   __syncthreads();
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     if (blockIdx.x == 0) p.diag[0] = 1;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const uint32_t done = atomicAdd(p.epoch + 1, 1u);
     if (done == gridDim.x - 1) {
       p.epoch[1] = 0;
       __hip_atomic_store(p.epoch, (uint32_t)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+template <bool EZ>
+__global__ __launch_bounds__(kTlbThreads) void traverse_lookback_kernel(TraverseLbArgs p) {
+  __shared__ uint32_t s_z0[31], s_pow[31];
+  __shared__ int s_epoch;
+  int players;
+  const unsigned long long epoch = traverse_lb_setup(p, s_z0, s_pow, &s_epoch, &players);
+  const int i = blockIdx.x * (kTlbThreads / 64) + (threadIdx.x >> 6);
+  if (i < p.t.B) traverse_lb_root<EZ>(p, i, s_z0, epoch, players);
+  traverse_lb_finish(p, epoch);
 }
 
 }  // namespace lzm

@@ -15,6 +15,7 @@ bit for bit in the default parity mode (glibc rand() stream seeded per traverse,
 draw per tree level), see lzm_kernels.hip.
 """
 import copy
+import os
 from typing import Any, List, Union
 
 import numpy as np
@@ -104,6 +105,14 @@ def _step_net(mcts, model):
     return model
 
 
+def _fuse_traverse(cfg, t):
+    """fold each simulation's traverse into the previous simulation's decode launch (parity mode with
+    the look-back traverse; cfg.fuse_traverse, default off: measured even with the two launches at
+    the conv configs; LZM_FUSE=0 forces it off)"""
+    return (cfg.get('fuse_traverse', False) and not t.fast_rng and os.environ.get("LZM_FUSE", "1") != "0"
+            and os.environ.get("LZM_TRAVERSE", "") != "serial")
+
+
 def _native_trunk(net, buf):
     """the step net runs the lzm_conv_trunk kernel straight on the latent pool"""
     return getattr(net, "native", None) is not None and tuple(buf.pool.shape[2:]) == (64, 8, 8)
@@ -171,8 +180,10 @@ class MuZeroMCTSCtree(object):
         new_minmax(t.B, cfg.value_delta_max, t.device, out=mm)
         model = _step_net(self, model)
         native = _native_trunk(model, buf)
+        fuse = _fuse_traverse(cfg, t)
         for k in range(S):
-            t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+            if k == 0 or not fuse:
+                t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
             if native:  # leaf latents read from the pool and the next latents filed by the trunk kernel
                 out = model.step_from_pool(buf.pool, t.x, t.action, buf.pool[k + 1])
             else:
@@ -181,10 +192,16 @@ class MuZeroMCTSCtree(object):
             logits = out.policy_logits.float().contiguous()
             if rec is not None:
                 rec.step(k, t, logits)
-            t.decode_backprop(k + 1, disc, mm, out.reward.float().contiguous(), out.value.float().contiguous(), cat,
-                              logits, t.vtp, next_latent=None if native else out.latent_state.float().contiguous(),
-                              pool_slot=None if native else buf.pool[k + 1], row_elems=0 if native else row,
-                              out_decoded=None if rec is None else rec.decoded[k])
+            kw = dict(next_latent=None if native else out.latent_state.float().contiguous(),
+                      pool_slot=None if native else buf.pool[k + 1], row_elems=0 if native else row,
+                      out_decoded=None if rec is None else rec.decoded[k])
+            if fuse and k + 1 < S:  # this simulation's backup and the next one's traverse in one launch
+                t.decode_backprop_traverse(k + 1, disc, mm, out.reward.float().contiguous(),
+                                           out.value.float().contiguous(), cat, logits, t.vtp, seeds[k + 1:k + 2],
+                                           vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), **kw)
+            else:
+                t.decode_backprop(k + 1, disc, mm, out.reward.float().contiguous(), out.value.float().contiguous(),
+                                  cat, logits, t.vtp, **kw)
 
     def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
                to_play_batch: Union[int, List[Any]], seeds: torch.Tensor = None) -> None:
@@ -290,8 +307,10 @@ class EfficientZeroMCTSCtree(object):
         new_minmax(B, cfg.value_delta_max, t.device, out=buf.mm)
         model = _step_net(self, model)
         native = _native_trunk(model, buf)
+        fuse = _fuse_traverse(cfg, t)
         for k in range(S):
-            t.traverse(buf.mm, buf.seeds[k:k + 1], buf.vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+            if k == 0 or not fuse:
+                t.traverse(buf.mm, buf.seeds[k:k + 1], buf.vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
             if native:
                 # the LSTM state is gathered from / filed (reset-masked) into the state pools on the device
                 out = model.step_from_pool_lstm(buf.pool, t.x, t.action, buf.pool[k + 1], buf.extra[0], buf.extra[1],
@@ -305,11 +324,17 @@ class EfficientZeroMCTSCtree(object):
             logits = out.policy_logits.float().contiguous()
             if rec is not None:
                 rec.step(k, t, logits)
-            t.decode_backprop(k + 1, disc, buf.mm, out.value_prefix.float().contiguous(), out.value.float().contiguous(),
-                              cat, logits, t.vtp, lstm_horizon=horizon, out_is_reset=t.is_reset,
-                              next_latent=None if native else out.latent_state.float().contiguous(),
-                              pool_slot=None if native else buf.pool[k + 1], row_elems=0 if native else row,
-                              out_decoded=None if rec is None else rec.decoded[k])
+            kw = dict(lstm_horizon=horizon, out_is_reset=t.is_reset,
+                      next_latent=None if native else out.latent_state.float().contiguous(),
+                      pool_slot=None if native else buf.pool[k + 1], row_elems=0 if native else row,
+                      out_decoded=None if rec is None else rec.decoded[k])
+            if fuse and k + 1 < S:  # this simulation's backup and the next one's traverse in one launch
+                t.decode_backprop_traverse(k + 1, disc, buf.mm, out.value_prefix.float().contiguous(),
+                                           out.value.float().contiguous(), cat, logits, t.vtp, buf.seeds[k + 1:k + 2],
+                                           buf.vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), **kw)
+            else:
+                t.decode_backprop(k + 1, disc, buf.mm, out.value_prefix.float().contiguous(),
+                                  out.value.float().contiguous(), cat, logits, t.vtp, **kw)
             if rec is not None:
                 rec.is_reset[k].copy_(t.is_reset)
             if native:

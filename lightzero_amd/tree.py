@@ -132,6 +132,19 @@ class DeviceTree:
              ptr(value_logits), int(V), int(bool(categorical)), ptr(policy_logits), ptr(to_play), int(lstm_horizon),
              ptr(out_is_reset), ptr(next_latent), ptr(pool_slot), int(row_elems), ptr(out_decoded), stream_ptr(stream))
 
+    def decode_backprop_traverse(self, cur, discount, minmax, reward_logits, value_logits, categorical, policy_logits,
+                                 to_play, seed, vtp_in, pb_c_base=19652, pb_c_init=1.25, lstm_horizon=0,
+                                 out_is_reset=None, next_latent=None, pool_slot=None, row_elems=0, out_decoded=None,
+                                 stream=None):
+        """decode_backprop of simulation `cur` and the traverse of the next one in one launch (parity
+        mode); the traverse outputs overwrite x / y / action / vtp / search_len."""
+        V = reward_logits.shape[-1] if categorical else 1
+        call("lzm_decode_backprop_traverse", self.h, int(cur), float(discount), ptr(minmax), ptr(reward_logits),
+             ptr(value_logits), int(V), int(bool(categorical)), ptr(policy_logits), ptr(to_play), int(lstm_horizon),
+             ptr(out_is_reset), ptr(next_latent), ptr(pool_slot), int(row_elems), ptr(out_decoded), int(pb_c_base),
+             float(pb_c_init), ptr(seed), ptr(vtp_in), ptr(self.x), ptr(self.y), ptr(self.action), ptr(self.action64),
+             ptr(self.vtp), ptr(self.search_len), stream_ptr(stream))
+
     def search_mlp(self, dims, weights, S, minmax, seeds, vtp_in, pool, pb_c_base=19652, pb_c_init=1.25,
                    discount=0.997, rec=None, stream=None):
         """One launch for the whole search (lzm_search_mlp); rec: optional _Recorder-like object."""
