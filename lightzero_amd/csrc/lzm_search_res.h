@@ -892,7 +892,8 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __syncthreads();
   if (p.phase && tid < 64 && s_phase[tid]) atomicAdd(p.phase + tid, s_phase[tid]);
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    // the last workgroup advances the epoch; no release fence (an L2 writeback per workgroup on
+    // gfx950): the kernel boundary orders the write-back above for every later reader
     const uint32_t done = atomicAdd(p.epoch + 1, 1u);
     if (done == (uint32_t)G - 1) {
       p.epoch[1] = 0;
