@@ -291,6 +291,18 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int current_latent_state_index, 
                                  int32_t *out_y, int32_t *out_last_action, int64_t *out_last_action_i64,
                                  int32_t *out_virtual_to_play, int32_t *out_search_len, void *stream);
 
+/* MuZeroModelMLP.initial_inference in one launch (lzm_initial.h): representation (Linear O->H + BN,
+ * GELU(tanh), Linear H->H, SimNorm over groups of `group`) and prediction (two Linear H->H + BN +
+ * ReLU; value head Linear H->F + BN + ReLU, Linear F->V; policy head Linear H->F + BN + ReLU,
+ * Linear F->A) for B observations [B][O]. Replaces model.initial_inference in the collect step
+ * (muzero.py:617-690; muzero_model_mlp.py:145-177, common.py:467-517, :883-971). `weights` (device)
+ * holds eight BN-folded layers W[K][N] + bias[N]; `offsets` (host, 16 entries) their float offsets
+ * in the order R1 w, R1 b, R2 w, R2 b, P1, P2, V1, V2, Q1, Q2. Outputs latent [B][H], value logits
+ * [B][V], policy logits [B][A]. */
+int lzm_mlp_initial_inference(int B, int O, int H, int F, int V, int A, int group, const float *obs,
+                              const float *weights, const int64_t *offsets, float *latent, float *value, float *policy,
+                              void *stream);
+
 /* EfficientZero reward LSTM, input side (lzm_lstm.h): xin[b] = [r[b] | hpool[x[b]][b]] — the leaf's
  * hidden-state gather and the concat ahead of the gate GEMM. Replaces the per-simulation gathers of
  * the LSTM state lists (mcts_ctree.py:756-775) and the nn.LSTM input assembly

@@ -16,6 +16,7 @@ values, root latents and policy logits). `step_counter` counts the steps (device
 """
 import torch
 
+from .initial import fused_initial_or_none
 from .mcts_ctree import MuZeroMCTSCtree
 from .utils import EasyDict
 
@@ -23,8 +24,10 @@ from .utils import EasyDict
 class DeviceSearchStep:
     def __init__(self, model, num_envs, num_simulations, legal_actions, obs_shape, device, noise_weight=0.25,
                  discount_factor=0.997, support_scale=300, seed=0, rng_mode="glibc", graph=True, cfg_extra=None,
-                 epilogue=None):
+                 epilogue=None, fused_initial=True):
         self.model = model.eval()
+        # initial_inference as one HIP launch when the model is a MuZeroModelMLP (lightzero_amd.initial)
+        self.initial = fused_initial_or_none(self.model) if fused_initial else None
         self.B, self.S = int(num_envs), int(num_simulations)
         self.device = torch.device(device)
         self.noise_weight = float(noise_weight)
@@ -65,7 +68,7 @@ class DeviceSearchStep:
             try:
                 if self.roots is None:
                     self.roots = self.mcts_cls.roots(self.B, self.legal)
-                out = self.model.initial_inference(self.obs)
+                out = (self.initial or self.model).initial_inference(self.obs)
                 seeds = ((self._base + self._count * self.S + self._ar) % 1000000).to(torch.int32)
                 self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
                                           self.to_play)

@@ -39,6 +39,7 @@
 #include "lzm_conv.h"
 #include "lzm_heads.h"
 #include "lzm_lstm.h"
+#include "lzm_initial.h"
 
 namespace lzm {
 
@@ -2229,6 +2230,29 @@ extern "C" int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *c
   const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(ez_lstm_cell_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, H, gates, cpool, x,
                      search_len, horizon, h1, c1, hslot, cslot);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" int lzm_mlp_initial_inference(int B, int O, int H, int F, int V, int A, int group, const float *obs,
+                                         const float *weights, const int64_t *offsets, float *latent, float *value,
+                                         float *policy, void *stream) {
+  if (B <= 0 || O <= 0 || O > kIiMaxW || H <= 0 || H > kIiMaxW || F <= 0 || F > 256 || V <= 0 || V > kIiMaxW ||
+      A <= 0 || A > kIiMaxW || group <= 0 || H % group || !obs || !weights || !offsets || !latent || !value ||
+      !policy) {
+    set_err("lzm_mlp_initial_inference: bad arguments (widths <= 1024, head hidden <= 256, H % group == 0)");
+    return LZM_ERR_ARG;
+  }
+  IiArgs p;
+  p.B = B; p.O = O; p.H = H; p.F = F; p.V = V; p.A = A; p.group = group;
+  p.obs = obs;
+  for (int l = 0; l < kIiLayers; ++l) {
+    p.w[l] = l < 8 ? weights + offsets[2 * l] : nullptr;
+    p.b[l] = l < 8 ? weights + offsets[2 * l + 1] : nullptr;
+  }
+  p.latent = latent; p.value = value; p.policy = policy;
+  hipLaunchKernelGGL(initial_inference_kernel, dim3((B + kIiEnvs - 1) / kIiEnvs), dim3(kIiThreads), 0,
+                     (hipStream_t)stream, p);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
