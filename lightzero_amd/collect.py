@@ -47,6 +47,7 @@ class DeviceSearchStep:
         self._count = torch.zeros(1, dtype=torch.int64, device=dev)
         self._base = (1000003 * int(seed)) % 1000000
         self._ar = torch.arange(self.S, dtype=torch.int64, device=dev)
+        self._seed_base = self._ar + self._base  # usec_k = (base + count * S + k) mod 10^6
         self.graph = None
         self.use_graph = bool(graph)
         self.epilogue = epilogue  # fn(out dict), enqueued after the search inside the same graph
@@ -69,7 +70,7 @@ class DeviceSearchStep:
                 if self.roots is None:
                     self.roots = self.mcts_cls.roots(self.B, self.legal)
                 out = (self.initial or self.model).initial_inference(self.obs)
-                seeds = ((self._base + self._count * self.S + self._ar) % 1000000).to(torch.int32)
+                seeds = torch.remainder(torch.add(self._seed_base, self._count, alpha=self.S), 1000000).to(torch.int32)
                 self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
                                           self.to_play)
                 self.mcts.search(self.roots, self.model, out.latent_state, self.to_play, seeds=seeds)

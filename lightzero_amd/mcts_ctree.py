@@ -42,6 +42,12 @@ def _to_play_tensor(to_play_batch, B, device):
     return torch.as_tensor(np.asarray(to_play_batch, dtype=np.int32).reshape(B), device=device)
 
 
+def _usable_i32(x, n, device):
+    """a contiguous int32 device tensor of n elements on `device` (readable by a kernel as is)"""
+    return (isinstance(x, torch.Tensor) and x.dtype == torch.int32 and x.is_contiguous() and x.numel() == n
+            and x.device == torch.device(device))
+
+
 def _latent_tensor(x, device):
     if isinstance(x, torch.Tensor):
         return x.to(device=device, dtype=torch.float32)
@@ -232,7 +238,10 @@ class MuZeroMCTSCtree(object):
                 packed, dims = fz
                 cfg = self._cfg
                 new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
-                t.search_mlp(dims, packed, S, buf.mm, buf.seeds, buf.vtp_in, buf.pool, int(cfg.pb_c_base),
+                # the one-launch search reads device seeds / to_play in place (no staging copies)
+                sd = seeds if _usable_i32(seeds, S, dev) and rec is None else buf.seeds
+                vt = to_play_batch if _usable_i32(to_play_batch, B, dev) else buf.vtp_in
+                t.search_mlp(dims, packed, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base),
                              float(cfg.pb_c_init), float(np.float32(cfg.discount_factor)), rec=rec)
             elif rec is None and self._cfg.get('use_hip_graph', False):
                 self._graph_search(t, model, buf, S, row)
