@@ -164,6 +164,10 @@ def kernel_timing(step, n_search=3):
     def timed(name, fn):
         def w(self, *a, **k):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if hasattr(torch.cuda, "_sleep"):
+                # keep the stream busy while the host enqueues e0, the launch and e1, so the events
+                # bracket the kernel alone (not the host-side launch latency)
+                torch.cuda._sleep(200000)
             e0.record()
             fn(self, *a, **k)
             e1.record()
@@ -176,14 +180,20 @@ def kernel_timing(step, n_search=3):
     mcts._cfg.use_hip_graph = False
     for n in names:
         setattr(mc.DeviceTree, n, timed(n, orig[n]))
-    mcts.record = True
     # a graph replay runs no Python: time the captured body eagerly (same kernels, same inputs)
     run = step.step._body if isinstance(step, (GraphStep, CollectStep)) else step
     try:
+        # d-bar from one recorded search (recording adds per-simulation stores to the fused kernel,
+        # so the timed searches below run without it, as the bench step does)
+        mcts.record = True
+        run()
+        if mcts.last_record is not None and not acc["traverse"]:
+            depth.append(mcts.last_record.search_len.clone())
+        mcts.record = False
+        for v in acc.values():
+            v.clear()
         for _ in range(n_search):
             run()
-            if mcts.last_record is not None and not acc["traverse"]:
-                depth.append(mcts.last_record.search_len.clone())
         torch.cuda.synchronize()
     finally:
         for n in names:
