@@ -291,6 +291,16 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int current_latent_state_index, 
                                  int32_t *out_y, int32_t *out_last_action, int64_t *out_last_action_i64,
                                  int32_t *out_virtual_to_play, int32_t *out_search_len, void *stream);
 
+/* ReZero search-with-reuse inputs for the following lzm_traverse / lzm_backprop /
+ * lzm_decode_backprop(_traverse) calls on this handle (device arrays [B], kept by pointer; null /
+ * null turns it off). With them set the traverse scores the root's true_action child by
+ * carm_score and ends the walk there (x = -1 when that child is already expanded), and the backup
+ * skips the expansion of such roots and backs up reuse_value for them and for roots that stopped
+ * at the unexpanded true-action child. Replaces batch_traverse_with_reuse /
+ * batch_backpropagate_with_reuse (mz_tree.pyx:84-107; ctree_muzero/lib/cnode.cpp:502-546,
+ * 598-642, 702-749, 827-927). MuZero trees, parity mode, look-back traverse only. */
+int lzm_set_reuse(lzm_handle *h, const int32_t *true_action, const float *reuse_value);
+
 /* MuZeroModelMLP.initial_inference in one launch (lzm_initial.h): representation (Linear O->H + BN,
  * GELU(tanh), Linear H->H, SimNorm over groups of `group`) and prediction (two Linear H->H + BN +
  * ReLU; value head Linear H->F + BN + ReLU, Linear F->V; policy head Linear H->F + BN + ReLU,

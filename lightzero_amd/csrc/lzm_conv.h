@@ -156,7 +156,8 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const ConvTrunkLayout L = conv_trunk_layout(a.n_dres, a.n_pres);
   for (int i = tid; i < 3 * kCvBuf; i += kCvThreads) cv_lds[i] = 0.f;  // zero borders
   __syncthreads();
-  const float *src = a.pool + ((a.x ? (int64_t)a.x[b] * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
+  // x = -1 (a search-with-reuse root that needs no inference): any row will do, its output is unused
+  const float *src = a.pool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
   for (int i = tid; i < kCvCh * kCvPix / 4; i += kCvThreads) {
     const float4 v = reinterpret_cast<const float4 *>(src)[i];
     const int c = (4 * i) >> 6, p = (4 * i) & 63;

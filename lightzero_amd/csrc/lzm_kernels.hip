@@ -256,17 +256,38 @@ struct BackpropArgs {
   const int32_t *to_play, *is_reset;
   int cur;
   float disc;
+  const int32_t *reuse_action;  // optional (MuZero): search-with-reuse, see reuse_leaf
+  const float *reuse_value;
 };
+
+// cbatch_backpropagate_with_reuse (ctree_muzero/lib/cnode.cpp:502-546) for root i whose walk ended
+// at `leaf` after `len` levels: no inference when the walk stopped on an expanded node (the root
+// child of the true action: no expand, back up the reuse value); a walk that stopped at the
+// unexpanded true-action child expands it but backs up the reuse value too.
+__device__ inline void reuse_leaf(const TreeView &t, int i, int leaf, int len, const int32_t *ra, const float *rv,
+                                  bool *no_inference, float *value) {
+  *no_inference = false;
+  if (!ra) return;
+  const bool expanded = t.meta[nidx(t, leaf, i)].latent >= 0;
+  const bool reuse = !expanded && len == 1 && t.path_act[i] == ra[i];
+  if (expanded || reuse) *value = rv[i];
+  *no_inference = expanded;
+}
 
 template <bool EZ>
 __global__ __launch_bounds__(256) void backprop_kernel(BackpropArgs p) {
   const TreeView &t = p.t;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= t.B) return;
-  const int leaf = t.path[(size_t)t.pathlen[i] * t.B + i];
+  const int len = t.pathlen[i];
+  const int leaf = t.path[(size_t)len * t.B + i];
   const int tp = p.to_play[i];
-  expand_leaf(t, i, leaf, tp, p.cur, p.rewards[i], p.logits + (size_t)i * t.A, p.is_reset ? p.is_reset[i] : 0, EZ);
-  backup<EZ>(t, i, p.minmax + i, tp, p.values[i], p.disc);
+  float v = p.values[i];
+  bool no_inf;
+  reuse_leaf(t, i, leaf, len, EZ ? nullptr : p.reuse_action, p.reuse_value, &no_inf, &v);
+  if (!no_inf)
+    expand_leaf(t, i, leaf, tp, p.cur, p.rewards[i], p.logits + (size_t)i * t.A, p.is_reset ? p.is_reset[i] : 0, EZ);
+  backup<EZ>(t, i, p.minmax + i, tp, v, p.disc);
 }
 
 // InverseScalarTransform (scaling_transform.py:118-128) of one row by one wave:
@@ -382,6 +403,8 @@ struct DecodeArgs {
   int V, categorical, cur, horizon;
   float disc;
   float *out_decoded;  // [B][2] {reward, value} after h^-1, optional
+  const int32_t *reuse_action;  // optional (MuZero): search-with-reuse, see reuse_leaf
+  const float *reuse_value;
 };
 
 // ensure_softmax (scaling_transform.py:36-62): softmax is skipped only when EVERY row of the
@@ -444,7 +467,9 @@ __device__ inline void decode_root(const DecodeArgs &p, const int32_t *norm_part
     const int tp = p.to_play[i];
     const int is_reset = (EZ && p.horizon > 0 && len % p.horizon == 0) ? 1 : 0;
     if (p.out_is_reset && lane == 0) p.out_is_reset[i] = is_reset;
-    expand_wave(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, EZ ? is_reset : -1);
+    bool no_inf;
+    reuse_leaf(t, i, leaf, len, EZ ? nullptr : p.reuse_action, p.reuse_value, &no_inf, &v);
+    if (!no_inf) expand_wave(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, EZ ? is_reset : -1);
     if (EZ)
       backup_wave_ez(t, i, i, t.B, p.minmax + i, tp, v, p.disc);
     else
@@ -458,7 +483,9 @@ __device__ inline void decode_root(const DecodeArgs &p, const int32_t *norm_part
   if (EZ && p.horizon > 0) is_reset = (len % p.horizon == 0) ? 1 : 0;
   if (p.out_is_reset) p.out_is_reset[i] = is_reset;
   const int tp = p.to_play[i];
-  expand_leaf(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, is_reset, EZ);
+  bool no_inf;
+  reuse_leaf(t, i, leaf, len, EZ ? nullptr : p.reuse_action, p.reuse_value, &no_inf, &v);
+  if (!no_inf) expand_leaf(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, is_reset, EZ);
   backup<EZ>(t, i, p.minmax + i, tp, v, p.disc);
 }
 
@@ -705,6 +732,8 @@ struct lzm_handle {
   uint32_t *epoch = nullptr;               // [2] launch epoch, done counter
   int32_t *search_diag = nullptr;          // [2]
   unsigned long long *phase = nullptr;     // [64] diagnostic phase cycles (LZM_PHASE_TIMING=1)
+  const int32_t *reuse_action = nullptr;   // lzm_set_reuse: search-with-reuse inputs (device, [B])
+  const float *reuse_value = nullptr;
 };
 
 // Jump matrices of glibc random_r: row m of J_first expresses z[344+m] (the m-th rand()
@@ -963,11 +992,16 @@ int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, 
   p.disc = discount;
   const bool ez = h->flags & LZM_TREE_EZ;
   hipStream_t s = (hipStream_t)stream;
+  const bool serial = getenv("LZM_TRAVERSE") && strcmp(getenv("LZM_TRAVERSE"), "serial") == 0;
+  if (h->reuse_action && (ez || (h->flags & LZM_RNG_FAST) || serial)) {
+    set_err("lzm_traverse: search-with-reuse needs a MuZero tree in parity mode with the look-back traverse");
+    return LZM_ERR_ARG;
+  }
   if (h->flags & LZM_RNG_FAST) {
     dim3 g((h->B + 255) / 256), b(256);
     if (ez) hipLaunchKernelGGL(traverse_fast_kernel<true>, g, b, 0, s, p);
     else hipLaunchKernelGGL(traverse_fast_kernel<false>, g, b, 0, s, p);
-  } else if (!(getenv("LZM_TRAVERSE") && strcmp(getenv("LZM_TRAVERSE"), "serial") == 0)) {
+  } else if (!serial) {
     // one wave per root, decoupled look-back of the draw offsets (lzm_traverse_lb.h)
     rc = ensure_coef(h, h->B * h->depth_cap + 64);
     if (rc != LZM_OK) return rc;
@@ -979,6 +1013,7 @@ int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, 
     q.out_a64 = p.out_a64; q.disc = discount;
     q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
     q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag;
+    q.reuse_action = h->reuse_action; q.reuse_value = h->reuse_value;
     const int per = kTlbThreads / 64;
     dim3 g((h->B + per - 1) / per), b(kTlbThreads);
     if (ez) hipLaunchKernelGGL(traverse_lookback_kernel<true>, g, b, 0, s, q);
@@ -1036,6 +1071,7 @@ int lzm_backprop(lzm_handle *h, int cur, float discount, float *minmax, const fl
   p.rewards = rewards; p.values = values; p.logits = logits; p.to_play = to_play; p.is_reset = is_reset;
   p.cur = cur;
   p.disc = discount;
+  p.reuse_action = h->reuse_action; p.reuse_value = h->reuse_value;
   dim3 g((h->B + 255) / 256), b(256);
   if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(backprop_kernel<true>, g, b, 0, (hipStream_t)stream, p);
   else hipLaunchKernelGGL(backprop_kernel<false>, g, b, 0, (hipStream_t)stream, p);
@@ -1077,6 +1113,7 @@ int lzm_decode_backprop(lzm_handle *h, int cur, float discount, float *minmax, c
   p.to_play = to_play; p.out_is_reset = out_is_reset; p.next_latent = next_latent; p.pool_slot = pool_slot;
   p.row_elems = row_elems; p.V = support_len; p.categorical = categorical; p.cur = cur; p.horizon = lstm_horizon;
   p.disc = discount; p.out_decoded = out_decoded;
+  p.reuse_action = h->reuse_action; p.reuse_value = h->reuse_value;
   dim3 g((h->B * 64 + 255) / 256), b(256);
   const int32_t *nf = categorical ? h->norm_flag : nullptr;
   if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(decode_backprop_kernel<true>, g, b, 0, s, p, nf);
@@ -1129,12 +1166,14 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int cur, float discount, float *
   p.to_play = to_play; p.out_is_reset = out_is_reset; p.next_latent = next_latent; p.pool_slot = pool_slot;
   p.row_elems = row_elems; p.V = support_len; p.categorical = categorical; p.cur = cur; p.horizon = lstm_horizon;
   p.disc = discount; p.out_decoded = out_decoded;
+  p.reuse_action = h->reuse_action; p.reuse_value = h->reuse_value;
   TraverseLbArgs q;
   q.t = p.t; q.minmax = (const float4 *)minmax; q.seed = seed; q.vtp_in = vtp_in;
   q.out_x = out_x; q.out_y = out_y; q.out_a = out_a; q.out_vtp = out_vtp; q.out_len = out_len;
   q.out_a64 = (long long *)out_a64; q.disc = discount;
   q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
   q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag;
+  q.reuse_action = h->reuse_action; q.reuse_value = h->reuse_value;
   const int per = kTlbThreads / 64;
   dim3 g((h->B + per - 1) / per), b(kTlbThreads);
   const int32_t *nf = categorical ? h->norm_flag : nullptr;
@@ -2254,5 +2293,19 @@ extern "C" int lzm_mlp_initial_inference(int B, int O, int H, int F, int V, int 
   hipLaunchKernelGGL(initial_inference_kernel, dim3((B + kIiEnvs - 1) / kIiEnvs), dim3(kIiThreads), 0,
                      (hipStream_t)stream, p);
   LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" int lzm_set_reuse(lzm_handle *h, const int32_t *true_action, const float *reuse_value) {
+  if (!h || (!true_action) != (!reuse_value)) {
+    set_err("lzm_set_reuse: both arrays or neither");
+    return LZM_ERR_ARG;
+  }
+  if (true_action && (h->flags & LZM_TREE_EZ)) {
+    set_err("lzm_set_reuse: MuZero trees only (the EfficientZero reuse search is not built)");
+    return LZM_ERR_ARG;
+  }
+  h->reuse_action = true_action;
+  h->reuse_value = reuse_value;
   return LZM_OK;
 }

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(256) void ez_lstm_input_kernel(int B, int Kr, int H
     if (k < Kr4)
       v = reinterpret_cast<const float4 *>(r)[(size_t)b * Kr4 + k];
     else
-      v = reinterpret_cast<const float4 *>(hpool)[((size_t)x[b] * B + b) * H4 + (k - Kr4)];
+      v = reinterpret_cast<const float4 *>(hpool)[((size_t)max(x[b], 0) * B + b) * H4 + (k - Kr4)];
     reinterpret_cast<float4 *>(xin)[q] = v;
   }
 }
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void ez_lstm_cell_kernel(int B, int H, const f
     const int b = (int)(q / H4), j = (int)(q - (long long)b * H4);
     const float4 *g4 = reinterpret_cast<const float4 *>(gates) + (size_t)b * 4 * H4;
     const float4 gi = g4[j], gf = g4[H4 + j], gg = g4[2 * H4 + j], go = g4[3 * H4 + j];
-    const float4 c0 = reinterpret_cast<const float4 *>(cpool)[((size_t)x[b] * B + b) * H4 + j];
+    const float4 c0 = reinterpret_cast<const float4 *>(cpool)[((size_t)max(x[b], 0) * B + b) * H4 + j];
     float4 c, h;
 #define LZM_LSTM_LANE(m)                                                          \
   c.m = lstm_sigmoid(gf.m) * c0.m + lstm_sigmoid(gi.m) * tanhf(gg.m);             \

@@ -36,6 +36,8 @@ struct TraverseLbArgs {
   unsigned long long *flags;  // [B] {epoch, depth}
   uint32_t *epoch;            // [2] epoch, done counter
   int32_t *diag;              // [0] passes (1), [1] spin timeouts (must stay 0)
+  const int32_t *reuse_action;  // optional [B] ReZero true actions (search-with-reuse), with
+  const float *reuse_value;     // [B] their reuse values; null: plain search
 };
 
 // Workgroup-level part of a look-back traverse (every thread calls it): the seeded glibc state and
@@ -64,7 +66,9 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
   const int vtp0 = p.vtp_in[i];
   TieInfo ti;
   auto nodraw = [](int) -> uint32_t { return 0u; };
-  Descent d = descend_wave<EZ, true>(t, i, i, B, mm, players, vtp0, p.disc, nodraw, &ti);
+  const int ta = p.reuse_action ? p.reuse_action[i] : -1;
+  const float rv = p.reuse_action ? p.reuse_value[i] : 0.0f;
+  Descent d = descend_wave<EZ, true>(t, i, i, B, mm, players, vtp0, p.disc, nodraw, &ti, ta, rv);
   if (lane == 0 && ti.status != 2)
     __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (ti.status != 0) {
@@ -110,7 +114,7 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
       auto draw = [coef, npos, diag, base, s_z0](int level) -> uint32_t {
         return glibc_draw(coef, npos, s_z0, base + level, diag);
       };
-      d = descend_wave<EZ, false>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr);
+      d = descend_wave<EZ, false>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr, ta, rv);
       if (lane == 0)
         __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -239,10 +239,16 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
 // maximum score and r its first position: the running max only ever resets at the first position
 // reaching a new maximum, so the last reset is at r and from then on the running max is M.
 // Every lane returns the same Descent; lane 0 writes the path. All 64 lanes must call it.
+// true_action >= 0: ReZero search-with-reuse at the root (cbatch_traverse_with_reuse,
+// ctree_muzero/lib/cnode.cpp:827-927): the true action's child is scored by carm_score (:702-749:
+// its value term uses reuse_value instead of the child's value, and a visited child scores the
+// value term alone), and choosing it ends the walk there even if the child is expanded (x = -1).
 template <bool EZ, bool CLASSIFY, typename Draw>
 __device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps, float4 mm, int players, int vtp,
-                                       float disc, Draw draw, TieInfo *tie) {
+                                       float disc, Draw draw, TieInfo *tie, int true_action = -1,
+                                       float reuse_value = 0.0f) {
   const int lane = threadIdx.x & 63;
+  bool reuse_stop = false;
   int node = 0, is_root = 1, len = 0, last_action = -1, parent = 0;
   float parent_q = 0.0f;
   NodeStat s = t.stat[nidx(t, 0, i)];
@@ -286,15 +292,17 @@ __device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps,
     float pb_c = L.x;
     pb_c *= (t.pbt && c.visit <= N) ? t.pbt[N * (N + 1) / 2 + c.visit] : (L.y / (float)(c.visit + 1));
     const float prior_score = pb_c * c.prior;
+    const bool arm = len == 0 && true_action >= 0 && a == true_action;  // carm_score at the root
+    const float cq = arm ? reuse_value : cv;
     float vs;
     if (c.visit == 0)
       vs = mean_q;
     else
-      vs = (players == 1) ? tr + disc * cv : tr + disc * (-cv);
+      vs = (players == 1) ? tr + disc * cq : tr + disc * (-cq);
     vs = mm_normalize(mm, vs);
     if (vs < 0) vs = 0;
     if (vs > 1) vs = 1;
-    const float score = prior_score + vs;
+    const float score = (arm && c.visit > 0) ? vs : prior_score + vs;
     const float M = wave_max_dpp(valid ? score : -INFINITY);
     const int r = __ffsll((long long)__ballot(valid && score == M)) - 1;
     const uint64_t mask = __ballot(valid && lane > r && score >= M - 0.000001f) | (1ull << r);
@@ -331,10 +339,14 @@ __device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps,
     ++len;
     s = t.stat[nidx(t, node, i)];
     m = t.meta[nidx(t, node, i)];
+    if (len == 1 && true_action >= 0 && action == true_action) {
+      reuse_stop = true;  // cnode.cpp:888-891
+      break;
+    }
   }
   Descent d;
   d.len = len;
-  d.x = t.meta[nidx(t, parent, i)].latent;
+  d.x = (reuse_stop && m.latent >= 0) ? -1 : t.meta[nidx(t, parent, i)].latent;
   d.action = last_action;
   d.vtp = vtp;
   d.leaf = node;

@@ -171,7 +171,7 @@ class _RootsBase:
 
 
 def _traverse(roots, pb_c_base, pb_c_init, discount_factor, min_max_stats_lst, results, virtual_to_play_batch,
-              seed=None):
+              seed=None, reuse=None):
     if not isinstance(pb_c_base, (int, np.integer)):
         raise TypeError("an integer is required for pb_c_base")
     _require_list("virtual_to_play_batch", virtual_to_play_batch)
@@ -182,11 +182,21 @@ def _traverse(roots, pb_c_base, pb_c_init, discount_factor, min_max_stats_lst, r
     mm = min_max_stats_lst._device(dev)
     vtp = torch.tensor(np.asarray(virtual_to_play_batch, np.int32)[:t.B], device=dev)
     s = seed_tensor(next_seed() if seed is None else seed, dev)
+    if reuse is None and getattr(t, "_reuse", None) is not None:
+        t.set_reuse(None)
+    if reuse is not None:
+        t.set_reuse(*reuse)
     t.traverse(mm, s, vtp, int(pb_c_base), _f32(pb_c_init), _f32(discount_factor))
     out = torch.stack([t.x, t.y, t.action, t.vtp, t.search_len]).cpu().numpy()
     results._search_lens = out[4].tolist()
     results._tree = t
-    return out[0].tolist(), out[1].tolist(), out[2].tolist(), out[3].tolist()
+    y = out[1]
+    if reuse is not None:
+        # latent_state_index_in_batch as the reference reports it: the parent's batch_index, i.e. its
+        # position among the envs that ran inference in the parent's simulation (cnode.cpp:920)
+        bidx = getattr(roots, "_batch_index", {})
+        y = np.array([bidx[x][i] if x > 0 and x in bidx else i for i, x in enumerate(out[0])], np.int64)
+    return out[0].tolist(), y.tolist(), out[2].tolist(), out[3].tolist()
 
 
 def _backprop(current_latent_state_index, discount_factor, value_prefixs, values, policies, min_max_stats_lst,
@@ -208,3 +218,57 @@ def _backprop(current_latent_state_index, discount_factor, value_prefixs, values
     t.backprop(cur, _f32(discount_factor), min_max_stats_lst._device(dev), g(np.asarray(value_prefixs).reshape(B), np.float32),
                g(np.asarray(values).reshape(B), np.float32), g(np.asarray(policies, np.float32).reshape(B, t.A), np.float32),
                g(np.asarray(to_play_batch, np.int32).reshape(B), np.int32), rs)
+
+
+def _traverse_with_reuse(roots, pb_c_base, pb_c_init, discount_factor, min_max_stats_lst, results,
+                         virtual_to_play_batch, true_action, reuse_value):
+    """batch_traverse_with_reuse (mz_tree.pyx:102-107)."""
+    _require_list("true_action", true_action)
+    _require_list("reuse_value", reuse_value)
+    t = roots.tree
+    if t is None:
+        raise RuntimeError("batch_traverse_with_reuse: roots not prepared")
+    B = t.B
+    ta = torch.from_numpy(np.asarray(true_action[:B], np.int32)).to(t.device)
+    rv = torch.from_numpy(np.asarray(reuse_value[:B], np.float32)).to(t.device)
+    x, y, a, vtp = _traverse(roots, pb_c_base, pb_c_init, discount_factor, min_max_stats_lst, results,
+                             virtual_to_play_batch, reuse=(ta, rv))
+    results._roots = roots
+    return x, y, a, vtp
+
+
+def _backprop_with_reuse(current_latent_state_index, discount_factor, value_prefixs, values, policies,
+                         min_max_stats_lst, results, to_play_batch, no_inference_lst, reuse_lst, reuse_value_lst):
+    """batch_backpropagate_with_reuse (mz_tree.pyx:84-93): the outputs arrive compacted to the envs
+    that ran inference (every env not in no_inference_lst, in env order); they are scattered back
+    to env rows, the device backup derives the no-inference / reuse cases from the tree itself
+    (the same rule the caller used to build the two lists) and reads the reuse values."""
+    for n, v in (("no_inference_lst", no_inference_lst), ("reuse_lst", reuse_lst),
+                 ("reuse_value_lst", reuse_value_lst)):
+        _require_list(n, v)
+    t = getattr(results, "_tree", None)
+    if t is None or getattr(t, "_reuse", None) is None:
+        raise RuntimeError("batch_backpropagate_with_reuse: results do not come from batch_traverse_with_reuse")
+    B, A = t.B, t.A
+    skip = set(int(i) for i in no_inference_lst if int(i) >= 0)
+    inf = [i for i in range(B) if i not in skip]
+    if len(values) != len(inf) or len(value_prefixs) != len(inf) or len(policies) != len(inf):
+        raise ValueError("batch_backpropagate_with_reuse: output lists must cover exactly the inferred envs")
+    full_r = np.zeros(B, np.float32)
+    full_v = np.zeros(B, np.float32)
+    full_p = np.zeros((B, A), np.float32)
+    if inf:
+        full_r[inf] = np.asarray(value_prefixs, np.float32)
+        full_v[inf] = np.asarray(values, np.float32)
+        full_p[inf] = np.asarray(policies, np.float32).reshape(len(inf), A)
+    rv = torch.from_numpy(np.asarray(reuse_value_lst[:B], np.float32)).to(t.device)
+    t.set_reuse(t._reuse[0], rv)
+    cur = int(current_latent_state_index)
+    roots = getattr(results, "_roots", None)
+    if roots is not None:
+        if not hasattr(roots, "_batch_index"):
+            roots._batch_index = {}
+        roots._batch_index[cur] = {i: n for n, i in enumerate(inf)}
+    _backprop(cur, discount_factor, full_r.tolist(), full_v.tolist(), full_p.tolist(), min_max_stats_lst, results,
+              to_play_batch)
+    t.set_reuse(None)

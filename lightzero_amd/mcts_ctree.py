@@ -178,8 +178,10 @@ class MuZeroMCTSCtree(object):
             return None
         return packed, dims
 
-    def _loop(self, t, model, buf, mm, vtp_in, seeds, S, row, rec=None):
-        """The S simulations (mcts_ctree.py:255-321), all enqueued on the current stream."""
+    def _loop(self, t, model, buf, mm, vtp_in, seeds, S, row, rec=None, infer=None):
+        """The S simulations (mcts_ctree.py:255-321), all enqueued on the current stream.
+        infer: optional device int64 [S], per simulation the number of roots that ran inference
+        (search-with-reuse: roots whose walk stopped on an expanded node report x = -1)."""
         cfg = self._cfg
         disc = float(np.float32(cfg.discount_factor))
         cat = self._categorical()
@@ -190,6 +192,8 @@ class MuZeroMCTSCtree(object):
         for k in range(S):
             if k == 0 or not fuse:
                 t.traverse(mm, seeds[k:k + 1], vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+            if infer is not None:
+                infer[k] = (t.x >= 0).sum()
             if native:  # leaf latents read from the pool and the next latents filed by the trunk kernel
                 out = model.step_from_pool(buf.pool, t.x, t.action, buf.pool[k + 1])
             else:
@@ -249,6 +253,55 @@ class MuZeroMCTSCtree(object):
                 self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, rec)
             roots._last_minmax = buf.mm
             self.last_record = rec
+
+    def search_with_reuse(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
+                          to_play_batch: Union[int, List[Any]], true_action_list=None, reuse_value_list=None,
+                          seeds: torch.Tensor = None):
+        """ReZero search with value reuse (mcts_ctree.py:323-420; arXiv 2404.16364): at the root the
+        true action's child is scored with the reuse value (carm_score) and choosing it ends the
+        walk; roots stopping on an already expanded node skip the network and back up their reuse
+        value, roots stopping at the unexpanded true-action child are expanded but back up the
+        reuse value too. Runs the generic device loop with the reuse inputs on the tree handle
+        (lzm_set_reuse); the network is evaluated for every root (rows of skipped roots unused).
+        Returns (length, average_infer) as the reference: roots that ran inference in the last
+        simulation, and inferences per simulation."""
+        if true_action_list is None or reuse_value_list is None:
+            raise TypeError("search_with_reuse needs true_action_list and reuse_value_list")
+        with torch.no_grad():
+            model.eval()
+            t = roots.tree
+            if t is None:
+                raise RuntimeError("search_with_reuse: roots must be prepared (Roots.prepare / prepare_no_noise) first")
+            if t.fast_rng:
+                raise ValueError("search_with_reuse: parity (glibc) mode only")
+            B, S = roots.num, int(self._cfg.num_simulations)
+            t.reserve(S)
+            t.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
+            dev = t.device
+            lat0 = _latent_tensor(latent_state_roots, dev)
+            shape = lat0.shape[1:]
+            row = int(np.prod(shape)) if len(shape) else 1
+            buf = self._buf.get(B, S, shape, dev)
+            buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
+            buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
+            buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
+            ta = torch.as_tensor(np.asarray(true_action_list, np.int32).reshape(B) if not torch.is_tensor(
+                true_action_list) else true_action_list, device=dev)
+            rv = torch.as_tensor(np.asarray(reuse_value_list, np.float32).reshape(B) if not torch.is_tensor(
+                reuse_value_list) else reuse_value_list, device=dev)
+            rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
+            if rec is not None:
+                rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
+            infer = torch.zeros(S, dtype=torch.int64, device=dev)
+            t.set_reuse(ta, rv)
+            try:
+                self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, rec, infer=infer)
+            finally:
+                t.set_reuse(None)
+            roots._last_minmax = buf.mm
+            self.last_record = rec
+            counts = infer.cpu().numpy()
+        return int(counts[-1]) if S else 0, float(counts.sum()) / max(S, 1)
 
     def _graph_search(self, t, model, buf, S, row):
         """Replays the whole S-simulation loop as one HIP graph (captured once per tree handle,

@@ -111,6 +111,18 @@ class DeviceTree:
         call("lzm_roots_prepare", self.h, ptr(legal), ptr(count), ptr(noises), float(noise_weight), ptr(rewards),
              ptr(logits), ptr(to_play), stream_ptr(stream))
 
+    def set_reuse(self, true_action=None, reuse_value=None):
+        """ReZero search-with-reuse inputs for the following traverse / backprop calls (device int32 /
+        float32 [B]; None clears). The tensors are kept alive here: the handle keeps their pointers."""
+        if true_action is None:
+            self._reuse = None
+            call("lzm_set_reuse", self.h, None, None)
+            return
+        ta = true_action.to(device=self.device, dtype=torch.int32).reshape(self.B).contiguous()
+        rv = reuse_value.to(device=self.device, dtype=torch.float32).reshape(self.B).contiguous()
+        self._reuse = (ta, rv)
+        call("lzm_set_reuse", self.h, ptr(ta), ptr(rv))
+
     def traverse(self, minmax, seed, vtp_in, pb_c_base=19652, pb_c_init=1.25, discount=0.997, stream=None):
         """seed: 1-element device tensor (int32/uint32 bits)."""
         call("lzm_traverse", self.h, int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax), ptr(seed),
