@@ -271,10 +271,12 @@ int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const floa
  * fc_value / fc_policy MLPs of muzero_model.py:505-530, efficientzero_model.py:526-574 and
  * common.py:854-881 (BatchNorm folded). w1t float[3][8][32][32][4], b1[96], w2t float[32][Vr+Vv+A],
  * b2[Vr+Vv+A] as packed by lightzero_amd.conv_infer; outputs reward [B][Vr], value [B][Vv],
- * policy [B][A]. */
+ * policy [B][A]. norm_words (nullable, int32 [2 * ceil(B / 2)]): also write ensure_softmax's
+ * verdict for the reward and value rows (scaling_transform.py:36-62) in the layout
+ * lzm_decode_backprop reads after lzm_set_norm_words, so it launches no check of its own. */
 int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const float *r_scale, const float *r_shift,
                    const float *hd, const float *w1t, const float *b1, const float *w2t, const float *b2, int Vr,
-                   int Vv, int A, float *reward, float *value, float *policy, void *stream);
+                   int Vv, int A, float *reward, float *value, float *policy, int32_t *norm_words, void *stream);
 
 /* lzm_decode_backprop of simulation `cur` fused with lzm_traverse of the next simulation (parity /
  * glibc mode only): one launch in which the wave that backs up root i then walks root i again
@@ -290,6 +292,10 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int current_latent_state_index, 
                                  const uint32_t *seed, const int32_t *virtual_to_play_in, int32_t *out_x,
                                  int32_t *out_y, int32_t *out_last_action, int64_t *out_last_action_i64,
                                  int32_t *out_virtual_to_play, int32_t *out_search_len, void *stream);
+
+/* Verdict words for the following lzm_decode_backprop(_traverse) calls on this handle: written by
+ * lzm_conv_heads(norm_words) for the same outputs; null restores the decode's own check launch. */
+int lzm_set_norm_words(lzm_handle *h, const int32_t *words);
 
 /* ReZero search-with-reuse inputs for the following lzm_traverse / lzm_backprop /
  * lzm_decode_backprop(_traverse) calls on this handle (device arrays [B], kept by pointer; null /

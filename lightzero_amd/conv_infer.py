@@ -297,7 +297,7 @@ class FoldedConvNet:
             _lib.call("lzm_conv_heads", B, inp.shape[1], hp["Khd"], hp["off_policy"], P(inp),
                       P(t["vp_s"]) if self.ez else None, P(t["vp_t"]) if self.ez else None, P(hd.contiguous()),
                       P(hp["w1t"]), P(hp["b1"]), P(hp["w2t"]), P(hp["b2"]), hp["Vr"], hp["Vv"], hp["A"], P(reward),
-                      P(value), P(policy), _lib.stream_ptr())
+                      P(value), P(policy), P(getattr(self, "norm_out", None)), _lib.stream_ptr())
             out = _Out()
             out.latent_state, out.value, out.policy_logits = nxt, value, policy
             if self.ez:

@@ -42,6 +42,8 @@ struct HeadsArgs {
   const float *w2t, *b2;               // [32][N2], [N2]
   int Vr, Vv, A;
   float *reward, *value, *policy;      // [B][Vr], [B][Vv], [B][A]
+  int32_t *norm_words;                 // optional: ensure_softmax verdict words (see below)
+  int norm_nparts;                     // norm_parts(B) word pairs the consumer ANDs
 };
 
 __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
@@ -138,6 +140,9 @@ __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
   __syncthreads();
   // ---- output layer: kHdCols columns of this head per thread, 32-deep dot per env
   float *out = head == 0 ? p.reward : (head == 1 ? p.value : p.policy);
+  float rsum[kHdEnvs];  // this thread's share of each row's sum (verdict words below)
+#pragma unroll
+  for (int e = 0; e < kHdEnvs; ++e) rsum[e] = 0.0f;
 #pragma unroll
   for (int cc = 0; cc < kHdCols; ++cc) {
     const int jj = tid + cc * kHdThreads;
@@ -151,6 +156,33 @@ __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
       for (int e = 0; e < kHdEnvs; ++e) acc[e] = __fmaf_rn(s_hid[e][k], w2[cc][k], acc[e]);
     }
     for (int e = 0; e < ne; ++e) out[(size_t)(e0 + e) * wd + jj] = acc[e] + b2[cc];
+#pragma unroll
+    for (int e = 0; e < kHdEnvs; ++e) rsum[e] += acc[e] + b2[cc];
+  }
+  // ensure_softmax's verdict (scaling_transform.py:36-62) for the reward and value rows this
+  // workgroup wrote, in the word layout normalized_check_kernel uses (lzm_kernels.hip): word pair q,
+  // head h is 0 iff a row of that head fails allclose(sum, 1); pairs nb.. are set to 1 here so the
+  // consumer's AND over norm_parts(B) pairs sees exactly these verdicts. Saves one launch per step.
+  if (p.norm_words && head < 2) {
+    __shared__ float s_sum[kHdEnvs][kHdThreads / 64];
+#pragma unroll
+    for (int e = 0; e < kHdEnvs; ++e) {
+      float v = rsum[e];
+#pragma unroll
+      for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+      if ((tid & 63) == 0) s_sum[e][tid >> 6] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int ok = 1;
+      for (int e = 0; e < ne; ++e) {
+        const float sm = (s_sum[e][0] + s_sum[e][1]) + (s_sum[e][2] + s_sum[e][3]);
+        if (!(fabsf(sm - 1.0f) <= 1e-5f + 1e-5f)) ok = 0;
+      }
+      const int nb = gridDim.x;
+      p.norm_words[2 * blockIdx.x + head] = ok;
+      if (nb + (int)blockIdx.x < p.norm_nparts) p.norm_words[2 * (nb + blockIdx.x) + head] = 1;
+    }
   }
 }
 

@@ -732,6 +732,7 @@ struct lzm_handle {
   uint32_t *epoch = nullptr;               // [2] launch epoch, done counter
   int32_t *search_diag = nullptr;          // [2]
   unsigned long long *phase = nullptr;     // [64] diagnostic phase cycles (LZM_PHASE_TIMING=1)
+  const int32_t *ext_norm = nullptr;       // lzm_set_norm_words: verdict words written by lzm_conv_heads
   const int32_t *reuse_action = nullptr;   // lzm_set_reuse: search-with-reuse inputs (device, [B])
   const float *reuse_value = nullptr;
 };
@@ -1102,7 +1103,7 @@ int lzm_decode_backprop(lzm_handle *h, int cur, float discount, float *minmax, c
   int rc = check_cur(h, cur);
   if (rc != LZM_OK) return rc;
   hipStream_t s = (hipStream_t)stream;
-  if (categorical) {
+  if (categorical && !h->ext_norm) {
     rc = launch_norm_check(h, h->norm_flag, reward_logits, value_logits, h->B, support_len, s);
     if (rc != LZM_OK) return rc;
   }
@@ -1115,7 +1116,7 @@ int lzm_decode_backprop(lzm_handle *h, int cur, float discount, float *minmax, c
   p.disc = discount; p.out_decoded = out_decoded;
   p.reuse_action = h->reuse_action; p.reuse_value = h->reuse_value;
   dim3 g((h->B * 64 + 255) / 256), b(256);
-  const int32_t *nf = categorical ? h->norm_flag : nullptr;
+  const int32_t *nf = categorical ? (h->ext_norm ? h->ext_norm : h->norm_flag) : nullptr;
   if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(decode_backprop_kernel<true>, g, b, 0, s, p, nf);
   else hipLaunchKernelGGL(decode_backprop_kernel<false>, g, b, 0, s, p, nf);
   LZM_CHECK_LAUNCH();
@@ -1155,7 +1156,7 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int cur, float discount, float *
   rc = ensure_flags(h, 1, 1);
   if (rc != LZM_OK) return rc;
   hipStream_t s = (hipStream_t)stream;
-  if (categorical) {
+  if (categorical && !h->ext_norm) {
     rc = launch_norm_check(h, h->norm_flag, reward_logits, value_logits, h->B, support_len, s);
     if (rc != LZM_OK) return rc;
   }
@@ -1176,7 +1177,7 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int cur, float discount, float *
   q.reuse_action = h->reuse_action; q.reuse_value = h->reuse_value;
   const int per = kTlbThreads / 64;
   dim3 g((h->B + per - 1) / per), b(kTlbThreads);
-  const int32_t *nf = categorical ? h->norm_flag : nullptr;
+  const int32_t *nf = categorical ? (h->ext_norm ? h->ext_norm : h->norm_flag) : nullptr;
   if (h->flags & LZM_TREE_EZ) hipLaunchKernelGGL(decode_traverse_kernel<true>, g, b, 0, s, p, nf, q);
   else hipLaunchKernelGGL(decode_traverse_kernel<false>, g, b, 0, s, p, nf, q);
   LZM_CHECK_LAUNCH();
@@ -2220,7 +2221,7 @@ int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const floa
 extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const float *r_scale,
                               const float *r_shift, const float *hd, const float *w1t, const float *b1,
                               const float *w2t, const float *b2, int Vr, int Vv, int A, float *reward, float *value,
-                              float *policy, void *stream) {
+                              float *policy, int32_t *norm_words, void *stream) {
   if (B <= 0 || Kr <= 0 || Kr > kHdRMax || Khd <= 0 || Khd > kHdHMax || off_policy <= 0 || off_policy >= Khd ||
       Khd - off_policy > kHdKMax || off_policy > kHdKMax || Vr <= 0 || Vv <= 0 || A <= 0 || Vr > kHdCols * kHdThreads || Vv > kHdCols * kHdThreads ||
       A > kHdCols * kHdThreads || !r || !hd || !w1t ||
@@ -2238,6 +2239,7 @@ extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const floa
   p.w1t = w1t; p.b1 = b1; p.w2t = w2t; p.b2 = b2;
   p.Vr = Vr; p.Vv = Vv; p.A = A;
   p.reward = reward; p.value = value; p.policy = policy;
+  p.norm_words = norm_words; p.norm_nparts = norm_parts(B);
   hipLaunchKernelGGL(conv_heads_kernel, dim3((B + kHdEnvs - 1) / kHdEnvs, 3), dim3(kHdThreads), 0, (hipStream_t)stream, p);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
@@ -2307,5 +2309,11 @@ extern "C" int lzm_set_reuse(lzm_handle *h, const int32_t *true_action, const fl
   }
   h->reuse_action = true_action;
   h->reuse_value = reuse_value;
+  return LZM_OK;
+}
+
+extern "C" int lzm_set_norm_words(lzm_handle *h, const int32_t *words) {
+  if (!h) return LZM_ERR_ARG;
+  h->ext_norm = words;
   return LZM_OK;
 }

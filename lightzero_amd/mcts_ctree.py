@@ -119,6 +119,32 @@ def _fuse_traverse(cfg, t):
             and os.environ.get("LZM_TRAVERSE", "") != "serial")
 
 
+class _HeadVerdicts:
+    """The native conv step's head kernel writes ensure_softmax's verdict words for the tree's
+    decode (one launch fewer per simulation); set for the duration of a loop."""
+
+    def __init__(self, t, net, buf, on):
+        self.t, self.net, self.on = t, net, on
+        if on:
+            n = 2 * ((t.B + 1) // 2)
+            w = getattr(buf, "norm_words", None)
+            if w is None or w.numel() != n or w.device != t.device:
+                buf.norm_words = torch.ones(n, dtype=torch.int32, device=t.device)
+            self.words = buf.norm_words
+
+    def __enter__(self):
+        if self.on:
+            self.net.norm_out = self.words
+            self.t.set_norm_words(self.words)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            self.net.norm_out = None
+            self.t.set_norm_words(None)
+        return False
+
+
 def _native_trunk(net, buf):
     """the step net runs the lzm_conv_trunk kernel straight on the latent pool"""
     return getattr(net, "native", None) is not None and tuple(buf.pool.shape[2:]) == (64, 8, 8)
@@ -188,6 +214,11 @@ class MuZeroMCTSCtree(object):
         new_minmax(t.B, cfg.value_delta_max, t.device, out=mm)
         model = _step_net(self, model)
         native = _native_trunk(model, buf)
+        with _HeadVerdicts(t, model, buf, native and cat and getattr(model, "heads", None) is not None):
+            self._sims(t, model, buf, mm, vtp_in, seeds, S, row, rec, infer, native, cat, disc)
+
+    def _sims(self, t, model, buf, mm, vtp_in, seeds, S, row, rec, infer, native, cat, disc):
+        cfg = self._cfg
         fuse = _fuse_traverse(cfg, t)
         for k in range(S):
             if k == 0 or not fuse:
@@ -369,6 +400,12 @@ class EfficientZeroMCTSCtree(object):
         new_minmax(B, cfg.value_delta_max, t.device, out=buf.mm)
         model = _step_net(self, model)
         native = _native_trunk(model, buf)
+        with _HeadVerdicts(t, model, buf, native and cat and getattr(model, "heads", None) is not None):
+            self._sims(t, model, buf, S, row, Hl, rec, native, cat, disc, horizon)
+
+    def _sims(self, t, model, buf, S, row, Hl, rec, native, cat, disc, horizon):
+        cfg = self._cfg
+        B = t.B
         fuse = _fuse_traverse(cfg, t)
         for k in range(S):
             if k == 0 or not fuse:

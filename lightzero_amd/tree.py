@@ -111,6 +111,12 @@ class DeviceTree:
         call("lzm_roots_prepare", self.h, ptr(legal), ptr(count), ptr(noises), float(noise_weight), ptr(rewards),
              ptr(logits), ptr(to_play), stream_ptr(stream))
 
+    def set_norm_words(self, words=None):
+        """int32 device [2 * ceil(B / 2)] ensure_softmax verdict words that the step's head kernel
+        writes (lzm_conv_heads); decode_backprop then skips its own check. None restores it."""
+        self._norm_words = words
+        call("lzm_set_norm_words", self.h, ptr(words))
+
     def set_reuse(self, true_action=None, reuse_value=None):
         """ReZero search-with-reuse inputs for the following traverse / backprop calls (device int32 /
         float32 [B]; None clears). The tensors are kept alive here: the handle keeps their pointers."""
