@@ -8,8 +8,8 @@
 //   value hidden    vh = relu(W_v1 hd[value planes] + b),  policy hidden ph = relu(W_p1 hd[policy planes] + b)
 //   value logits    W_v2 vh + b (support Vv),  policy logits W_p2 ph + b (A)
 // with every BatchNorm folded on the host (conv_infer.py). As separate GEMMs these are six tiny
-// launches plus two ReLU passes per simulation. Here the grid is (env blocks of 4) x (3 heads):
-// 192 workgroups at B = 256, so the launch spreads over most CUs instead of one per 8 envs
+// launches plus two ReLU passes per simulation. Here the grid is (env blocks of 2) x (3 heads):
+// 384 workgroups at B = 256 (8.7 us; blocks of 4: 13 us), instead of one workgroup per 8 envs
 // (32 workgroups measured 38.6 us, L2-latency bound on the serial weight stream). Every thread
 // issues all of its weight loads (128 + 96 registers) before the first wait, so the weights cost one
 // L2 round trip, not one per loop batch (13.0 -> see DESIGN.md 6.3). A workgroup stages its head's
@@ -25,7 +25,7 @@
 
 namespace lzm {
 
-constexpr int kHdEnvs = 4;     // envs per workgroup
+constexpr int kHdEnvs = 2;     // envs per workgroup
 constexpr int kHdThreads = 256;
 constexpr int kHdParts = 8;    // K split of the first layer, one per 32-lane half wave
 constexpr int kHdKMax = 1024;  // K per head (8 parts of 128)
