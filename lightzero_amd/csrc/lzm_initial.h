@@ -6,7 +6,8 @@
 // then prediction (common.py:883-971: two Linear+BN+ReLU, value head Linear+BN+ReLU -> Linear to
 // the support, policy head Linear+BN+ReLU -> Linear to A). As PyTorch modules that is ~20 launches
 // (GEMMs, eval BatchNorm, activations, softmax) of a few microseconds each around tiny matrices; at
-// the bench shape it was ~1/8 of the whole collect step. Here one workgroup takes kIiEnvs envs,
+// the bench shape it was ~1/8 of the whole collect step. Here one workgroup takes kIiEnvs envs (1:
+// 256 workgroups at B = 256, 18.6 us; 4 envs per workgroup: 24 us),
 // keeps their activations in LDS and runs every layer (BatchNorm folded on the host in float64):
 // a layer of N outputs over K inputs maps thread t to column t % N and K slice t / N (N < 256) or
 // to columns t, t + 256, ... (N >= 256); K slices are summed in slice order (deterministic).
@@ -19,7 +20,7 @@
 namespace lzm {
 
 constexpr int kIiThreads = 256;
-constexpr int kIiEnvs = 4;
+constexpr int kIiEnvs = 1;
 constexpr int kIiMaxW = 1024;  // widest activation row kept in LDS (support <= 1024)
 constexpr int kIiLayers = 9;   // R1 R2 | P1 P2 | V1 V2 | Q1 Q2 (+ spare)
 
