@@ -85,6 +85,9 @@ CASES = [
     (64, 50, 9, 64, False, 1, False),   # cap = 460 nodes: slice stays in HBM
     (256, 50, 2, 128, False, 1, True),
     (96, 30, 4, 64, True, 2, True),
+    (1, 10, 2, 128, False, 1, False),    # edge sizes: one root; a long search; a batch past one root per CU
+    (8, 100, 2, 128, False, 1, False),
+    (1024, 20, 2, 128, False, 1, False),
 ]
 
 

@@ -27,6 +27,11 @@ DEV = torch.device("cuda", 0)
     (64, 30, 9, 2, True, False),
     (256, 50, 2, 1, False, True),
     (128, 25, 5, 2, True, True),
+    # edge sizes: one root / one action / one simulation, a long search (capacity growth), a wide batch
+    (1, 1, 1, 1, False, False),
+    (1, 64, 2, 1, False, False),
+    (33, 100, 3, 2, True, False),
+    (1024, 20, 2, 1, False, False),
 ])
 def test_search_bit_exact_vs_host_loop(B, S, A, players, quant, fast):
     g = run_scripted_search_gpu(B, S, A, seed=B + S, players=players, quant=quant, fast_rng=fast)
