@@ -252,3 +252,42 @@ def test_fused_decode_traverse_equals_separate(kind):
         assert np.array_equal(a[key], b[key]), key
     for key in ("x", "action", "search_len"):
         assert np.array_equal(a["rec"][key], b["rec"][key]), key
+
+
+@pytest.mark.parametrize("B", [37, 256])
+def test_heads_kernel_verdict_words(B):
+    """lzm_conv_heads(norm_words): word pair q / head h is 1 iff every reward (h = 0) / value (h = 1)
+    row of env block q sums to 1 within allclose(1e-5, 1e-5) (ensure_softmax,
+    scaling_transform.py:36-62); pairs past the blocks are 1. Checked with output layers that
+    give exactly normalised rows (zero weights, bias 1/V) and with random ones."""
+    from lightzero_amd import _lib
+    g = torch.Generator(device=DEV).manual_seed(3)
+    Kr, Khd, fv, Vr, Vv, A = 1024, 2048, 1024, 601, 601, 4
+    r = torch.rand(B, Kr, generator=g, device=DEV)
+    hd = torch.rand(B, Khd, generator=g, device=DEV)
+    w1t = torch.randn(3, 8, 32, 32, 4, generator=g, device=DEV) * 0.01
+    b1 = torch.randn(96, generator=g, device=DEV) * 0.1
+    nparts = (B + 1) // 2
+    P = _lib.ptr
+    for normalised in (True, False):
+        if normalised:
+            w2t = torch.zeros(32, Vr + Vv + A, device=DEV)
+            b2 = torch.cat([torch.full((Vr,), 1.0 / Vr), torch.full((Vv,), 1.0 / Vv), torch.zeros(A)]).to(DEV)
+        else:
+            w2t = torch.randn(32, Vr + Vv + A, generator=g, device=DEV)
+            b2 = torch.randn(Vr + Vv + A, generator=g, device=DEV)
+        outs = [torch.empty(B, n, device=DEV) for n in (Vr, Vv, A)]
+        words = torch.full((2 * nparts,), -7, dtype=torch.int32, device=DEV)
+        _lib.call("lzm_conv_heads", B, Kr, Khd, fv, P(r), None, None, P(hd), P(w1t), P(b1), P(w2t), P(b2), Vr, Vv, A,
+                  P(outs[0]), P(outs[1]), P(outs[2]), P(words), _lib.stream_ptr())
+        torch.cuda.synchronize()
+        w = words.cpu().numpy().reshape(nparts, 2)
+        sums = [outs[h].sum(dim=1).cpu().numpy() for h in (0, 1)]
+        nb = (B + 1) // 2  # env blocks of 2
+        for h in (0, 1):
+            ok = np.abs(sums[h] - 1.0) <= 2e-5
+            exp = np.ones(nparts, np.int32)
+            for q in range(nb):
+                exp[q] = int(ok[2 * q:2 * q + 2].all())
+            assert np.array_equal(w[:, h], exp), (normalised, h)
+        assert w.all() == normalised
