@@ -293,6 +293,11 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int current_latent_state_index, 
                                  int32_t *out_y, int32_t *out_last_action, int64_t *out_last_action_i64,
                                  int32_t *out_virtual_to_play, int32_t *out_search_len, void *stream);
 
+/* The S traverse seeds of one collect step, usec_k = (base + count * S + k) mod 10^6 with the step
+ * counter read on the device (int64 [1]); the deterministic stand-in for the reference's per-call
+ * srand(tv_usec) (common_lib/utils.cpp:25) used by lightzero_amd.collect.DeviceSearchStep. */
+int lzm_seed_sequence(const int64_t *count, int64_t base, int S, int32_t *seeds, void *stream);
+
 /* Verdict words for the following lzm_decode_backprop(_traverse) calls on this handle: written by
  * lzm_conv_heads(norm_words) for the same outputs; null restores the decode's own check launch. */
 int lzm_set_norm_words(lzm_handle *h, const int32_t *words);

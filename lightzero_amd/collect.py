@@ -16,6 +16,7 @@ values, root latents and policy logits). `step_counter` counts the steps (device
 """
 import torch
 
+from . import _lib
 from .initial import fused_initial_or_none
 from .mcts_ctree import MuZeroMCTSCtree
 from .utils import EasyDict
@@ -47,7 +48,6 @@ class DeviceSearchStep:
         self._count = torch.zeros(1, dtype=torch.int64, device=dev)
         self._base = (1000003 * int(seed)) % 1000000
         self._ar = torch.arange(self.S, dtype=torch.int64, device=dev)
-        self._seed_base = self._ar + self._base  # usec_k = (base + count * S + k) mod 10^6
         self.graph = None
         self.use_graph = bool(graph)
         self.epilogue = epilogue  # fn(out dict), enqueued after the search inside the same graph
@@ -69,8 +69,14 @@ class DeviceSearchStep:
             try:
                 if self.roots is None:
                     self.roots = self.mcts_cls.roots(self.B, self.legal)
-                out = (self.initial or self.model).initial_inference(self.obs)
-                seeds = torch.remainder(torch.add(self._seed_base, self._count, alpha=self.S), 1000000).to(torch.int32)
+                pool0 = self._root_slot()
+                if self.initial is not None and pool0 is not None:
+                    out = self.initial.initial_inference(self.obs, latent_out=pool0)  # search skips its copy
+                else:
+                    out = (self.initial or self.model).initial_inference(self.obs)
+                seeds = torch.empty(self.S, dtype=torch.int32, device=self.device)
+                _lib.call("lzm_seed_sequence", _lib.ptr(self._count), self._base, self.S, _lib.ptr(seeds),
+                          _lib.stream_ptr())
                 self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
                                           self.to_play)
                 self.mcts.search(self.roots, self.model, out.latent_state, self.to_play, seeds=seeds)
@@ -84,6 +90,12 @@ class DeviceSearchStep:
                 return res
             finally:
                 self.mcts_cls.rng_mode = old
+
+    def _root_slot(self):
+        """the search's root latent slot (pool[0]) once its buffers exist, else None"""
+        buf = getattr(self.mcts, "_buf", None)
+        pool = getattr(buf, "pool", None) if buf is not None and buf.key is not None else None
+        return pool[0] if pool is not None and pool.shape[1] == self.B else None
 
     def build_graph(self):
         """Warm up (allocations: tree handle, glibc tables, packed weights, torch workspaces) and

@@ -2317,3 +2317,22 @@ extern "C" int lzm_set_norm_words(lzm_handle *h, const int32_t *words) {
   h->ext_norm = words;
   return LZM_OK;
 }
+
+// Traverse seeds of one collect step (SURVEY.md §8(d) rule, lightzero_amd.collect.DeviceSearchStep):
+// seeds[k] = (base + count * S + k) mod 10^6, count read on the device (a captured graph replays it).
+__global__ void seed_sequence_kernel(const int64_t *count, long long base, int S, int32_t *seeds) {
+  const long long c = *count;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < S; k += gridDim.x * blockDim.x)
+    seeds[k] = (int32_t)((base + c * (long long)S + k) % 1000000ll);
+}
+
+extern "C" int lzm_seed_sequence(const int64_t *count, int64_t base, int S, int32_t *seeds, void *stream) {
+  if (!count || !seeds || S <= 0 || base < 0) {
+    set_err("lzm_seed_sequence: bad arguments");
+    return LZM_ERR_ARG;
+  }
+  hipLaunchKernelGGL(seed_sequence_kernel, dim3((S + 255) / 256), dim3(256), 0, (hipStream_t)stream, count,
+                     (long long)base, S, seeds);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}

@@ -76,7 +76,9 @@ class FusedInitialInference:
         self.dims = dims
         self.key = ver
 
-    def initial_inference(self, obs):
+    def initial_inference(self, obs, latent_out=None):
+        """latent_out: optional float32 [B, H] (contiguous) to write the latent into (e.g. a search's
+        root slot, so the search does not copy it)."""
         self._pack()
         d = self.dims
         x = obs.reshape(obs.shape[0], -1)
@@ -86,7 +88,9 @@ class FusedInitialInference:
         if x.shape[1] != d["obs"]:
             raise ValueError(f"observation width {x.shape[1]} != {d['obs']}")
         kw = dict(dtype=torch.float32, device=x.device)
-        latent = torch.empty((B, d["hidden"]), **kw)
+        latent = torch.empty((B, d["hidden"]), **kw) if latent_out is None else latent_out.reshape(B, d["hidden"])
+        if latent_out is not None and (not latent.is_contiguous() or latent.dtype != torch.float32):
+            raise ValueError("latent_out must be a contiguous float32 [B, H] tensor")
         value = torch.empty((B, d["support"]), **kw)
         policy = torch.empty((B, d["actions"]), **kw)
         _lib.call("lzm_mlp_initial_inference", B, d["obs"], d["hidden"], d["head_hidden"], d["support"], d["actions"],

@@ -262,7 +262,8 @@ class MuZeroMCTSCtree(object):
             shape = lat0.shape[1:]
             row = int(np.prod(shape)) if len(shape) else 1
             buf = self._buf.get(B, S, shape, dev)
-            buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
+            if lat0.data_ptr() != buf.pool[0].data_ptr():  # (the collect step writes it in place)
+                buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
             buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
             rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
