@@ -293,6 +293,10 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int current_latent_state_index, 
                                  int32_t *out_y, int32_t *out_last_action, int64_t *out_last_action_i64,
                                  int32_t *out_virtual_to_play, int32_t *out_search_len, void *stream);
 
+/* lzm_get_distributions and lzm_get_values in one launch (get_distributions / get_values,
+ * cnode.cpp:369-417): dist int32 [B][A] (legal order, -1 padded), values float [B]. */
+int lzm_get_root_outputs(lzm_handle *h, int32_t *dist, float *values, void *stream);
+
 /* The S traverse seeds of one collect step, usec_k = (base + count * S + k) mod 10^6 with the step
  * counter read on the device (int64 [1]); the deterministic stand-in for the reference's per-call
  * srand(tv_usec) (common_lib/utils.cpp:25) used by lightzero_amd.collect.DeviceSearchStep. */

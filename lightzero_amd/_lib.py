@@ -64,6 +64,7 @@ SIGNATURES = {
     "lzm_conv_heads": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "lzm_set_norm_words": [_vp, _vp],
     "lzm_seed_sequence": [_vp, _i64, _i, _vp, _vp],
+    "lzm_get_root_outputs": [_vp, _vp, _vp, _vp],
     "lzm_mlp_prepare": [_i, _i, _i, _i, _i, _vp, _vp, _vp],
     "lzm_search_mlp": [_vp, _i, _i, _i, _i, _vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_diagnostics": [_vp, _vp, _vp],

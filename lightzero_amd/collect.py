@@ -81,7 +81,7 @@ class DeviceSearchStep:
                                           self.to_play)
                 self.mcts.search(self.roots, self.model, out.latent_state, self.to_play, seeds=seeds)
                 t = self.roots.tree
-                dist, values = t.distributions(), t.values()
+                dist, values = t.root_outputs()
                 res = dict(distributions=dist, values=values, latent_state=out.latent_state,
                            policy_logits=out.policy_logits)
                 if self.epilogue is not None:

@@ -613,6 +613,20 @@ __global__ void distributions_kernel(TreeView t, int32_t *out) {
   }
 }
 
+// get_distributions and get_values in one pass (the collect step reads both every env step)
+__global__ void root_outputs_kernel(TreeView t, int32_t *dist, float *values) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= t.B) return;
+  const NodeStat rs = t.stat[i];
+  const NodeMeta rm = t.meta[i];
+  for (int j = 0; j < t.A; ++j) {
+    int v = -1;
+    if (rm.latent >= 0 && j < t.nlegal[i]) v = t.stat[nidx(t, 1 + t.A * rm.latent + t.legal[(size_t)i * t.A + j], i)].visit;
+    dist[(size_t)i * t.A + j] = v;
+  }
+  values[i] = node_value(rs);
+}
+
 __global__ void values_kernel(TreeView t, float *out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < t.B) out[i] = node_value(t.stat[i]);
@@ -2333,6 +2347,17 @@ extern "C" int lzm_seed_sequence(const int64_t *count, int64_t base, int S, int3
   }
   hipLaunchKernelGGL(seed_sequence_kernel, dim3((S + 255) / 256), dim3(256), 0, (hipStream_t)stream, count,
                      (long long)base, S, seeds);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" int lzm_get_root_outputs(lzm_handle *h, int32_t *dist, float *values, void *stream) {
+  if (!h || !dist || !values) {
+    set_err("lzm_get_root_outputs: null argument");
+    return LZM_ERR_ARG;
+  }
+  hipLaunchKernelGGL(root_outputs_kernel, dim3((h->B + 255) / 256), dim3(256), 0, (hipStream_t)stream, view(h), dist,
+                     values);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }

@@ -187,6 +187,13 @@ class DeviceTree:
         call("lzm_get_values", self.h, ptr(out), stream_ptr(stream))
         return out
 
+    def root_outputs(self, stream=None):
+        """(distributions(), values()) from one launch"""
+        dist = torch.empty((self.B, self.A), dtype=torch.int32, device=self.device)
+        vals = torch.empty(self.B, dtype=torch.float32, device=self.device)
+        call("lzm_get_root_outputs", self.h, ptr(dist), ptr(vals), stream_ptr(stream))
+        return dist, vals
+
     def trajectories(self, tmax=64, stream=None):
         out = torch.empty((self.B, tmax), dtype=torch.int32, device=self.device)
         call("lzm_get_trajectories", self.h, ptr(out), int(tmax), stream_ptr(stream))

@@ -157,3 +157,30 @@ def test_efficientzero_search_runs_and_conserves_visits():
     d = roots.get_distributions()
     assert all(sum(row) == S for row in d)
     assert np.isfinite(roots.get_values()).all()
+
+
+def test_root_outputs_equal_separate_reads():
+    """DeviceTree.root_outputs (lzm_get_root_outputs, one launch) == distributions() and values()"""
+    from lightzero_amd.mcts_ctree import MuZeroMCTSCtree
+    from lightzero_amd.tree import SequentialSeeds, set_seed_source
+    from lightzero_amd.utils import EasyDict
+    from tests.helpers import NOISE_W, ScriptedTables, make_scripted_model
+    B, S, A = 40, 15, 5
+    tab = ScriptedTables(B, S, A, 4, players=2, quant=True)
+    cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV,
+                        model=dict(support_scale=300, categorical_distribution=False)))
+    mcts = MuZeroMCTSCtree(cfg)
+    legal = [list(range(A)) if i % 3 else [0, 2, 4] for i in range(B)]
+    roots = MuZeroMCTSCtree.roots(B, legal)
+    noises = [tab.noises[i, :len(legal[i])].tolist() for i in range(B)]
+    roots.prepare(float(NOISE_W), noises, [0.0] * B, tab.root_logits.tolist(), tab.to_play.tolist())
+    set_seed_source(SequentialSeeds(4))
+    try:
+        mcts.search(roots, make_scripted_model(tab, DEV), tab.lat0, tab.to_play.tolist())
+    finally:
+        set_seed_source(None)
+    t = roots.tree
+    d, v = t.root_outputs()
+    assert torch.equal(d, t.distributions()) and torch.equal(v, t.values())
+    assert (d[0 * 3 + 0] >= 0).sum() == 3  # a ragged root reports its 3 legal children, -1 padded
+    roots.clear()
