@@ -96,6 +96,9 @@ class GraphStep:
         out = self.step.step()
         self.last = (out["distributions"], out["values"], None)
 
+    def tree(self):
+        return self.step.roots.tree
+
 
 class CollectStep:
     """One env step of the device collector for every env: search + select_action + CartPole step +
@@ -114,6 +117,9 @@ class CollectStep:
         self.col.step()
         out = self.col.search.out
         self.last = (out["distributions"], out["values"], None)
+
+    def tree(self):
+        return self.col.search.roots.tree
 
 
 class GpuStep:
@@ -147,7 +153,11 @@ class GpuStep:
             self.mcts.search(roots, self.model, out.latent_state, self.to_play)
             t = roots.tree
             self.last = (t.distributions(), t.values(), t.search_len)
+            self._tree = t
             roots.clear()
+
+    def tree(self):
+        return self._tree
 
 
 def kernel_timing(step, n_search=3):
@@ -354,9 +364,11 @@ def main():
     el = slowest_rank_seconds(time.perf_counter() - t0, world, device)
     value = whole_job_rate(B, S, args.steps, world, el)
 
-    # sanity: every root received exactly S visits
+    # sanity: every root received exactly S visits, and no search reported a broken tie-break
+    # stream (look-back timeout / draw-table overflow: lzm_check_errors raises)
     dsum = step.last[0].sum(dim=1)
     assert bool((dsum == S).all()), "visit counts do not sum to num_simulations"
+    tie_errors = step.tree().check_errors()
 
     roofline = None
     cpu = None
@@ -418,7 +430,7 @@ def main():
                            "hip_graph": (args.step != "python") if args.path == "fused" else bool(args.graph),
                            "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
-                "roofline": roofline, "cpu_baseline": cpu}
+                "tie_stream_errors": int(sum(tie_errors)), "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

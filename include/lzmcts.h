@@ -162,6 +162,14 @@ int lzm_search_mlp_kind(int B, int actions, int hidden, int head_hidden, int sup
  * an expanded child)} accumulated over the handle's fused searches. */
 int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream);
 
+/* Post-search integrity check (host-synchronous on `stream`): the sticky error counters of every
+ * search path on the handle — {look-back spin timeouts, draw positions beyond the coefficient
+ * table, serial-traverse fixed-point failures, fused-search errors} into out_host[4] (nullable).
+ * Returns LZM_ERR_STATE when any is non-zero (the parity-mode tie-break stream then differs from
+ * the reference's); clear != 0 resets them. No reference counterpart: the reference's draws are
+ * serial on one host thread (cnode.cpp:770, :590) and cannot fail this way. */
+int lzm_check_errors(lzm_handle *h, int32_t *out_host, int clear, void *stream);
+
 /* Diagnostics: traverse passes used by the last parity-mode traverse (device int32[1]). */
 int lzm_last_traverse_passes(lzm_handle *h, int32_t *out, void *stream);
 

@@ -103,6 +103,7 @@ class AlphaZeroMCTS:
         self.seed = int(seed) & 0xffffffff
         self._count = torch.zeros(1, dtype=torch.int64, device=self.device)
         self._ctx = {}  # B -> per-batch buffers (and graphs)
+        self.graph_cache_size = 4  # captured graphs kept per batch size
 
     # ------------------------------------------------------------------ per-batch buffers
     def _buffers(self, B):
@@ -153,8 +154,13 @@ class AlphaZeroMCTS:
             self._body(B, pv, temperature, sample)
             return
         c = self._buffers(B)
-        key = (id(pv), float(temperature), bool(sample))
+        # a bound method is a new object on every attribute access (net.compute_policy_value):
+        # key on the function and its instance, so the same callable replays its graph
+        key = (id(getattr(pv, "__func__", pv)), id(getattr(pv, "__self__", None)), float(temperature), bool(sample))
         g = c["graphs"].get(key)
+        if g is not None and (g[1] is not getattr(pv, "__func__", pv) or g[2] is not getattr(pv, "__self__", None)):
+            del c["graphs"][key]  # ids reused by new objects
+            g = None
         if g is None:
             side = torch.cuda.Stream(device=self.device)
             side.wait_stream(torch.cuda.current_stream(self.device))
@@ -165,8 +171,12 @@ class AlphaZeroMCTS:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._body(B, pv, temperature, sample)
-            c["graphs"][key] = (g, pv)  # keep pv alive: the key holds its id
+            # keep the function and instance alive (the key holds their ids); bounded LRU
+            c["graphs"][key] = (g, getattr(pv, "__func__", pv), getattr(pv, "__self__", None))
+            while len(c["graphs"]) > self.graph_cache_size:
+                c["graphs"].pop(next(iter(c["graphs"])))
         else:
+            c["graphs"][key] = c["graphs"].pop(key)  # most recently used last
             g = g[0]
         g.replay()
 

@@ -114,12 +114,22 @@ class DeviceSearchStep:
         with torch.cuda.graph(self.graph):
             self.out = self._body()
 
+    def refresh_weights(self):
+        """Re-pack the network for the captured kernels if its parameters changed (e.g. a learner
+        update): both caches re-pack IN PLACE, so the captured graph reads the new weights. A graph
+        replay runs no Python, so this host-side version check runs before every replay."""
+        if self.initial is not None:
+            self.initial._pack()
+        if self.roots is not None and self.roots.tree is not None:
+            self.mcts._fused(self.model, self.roots.tree)
+
     def step(self):
         """One collect-time search pass over the current inputs; returns the static output dict."""
         if not self.use_graph:
             self.out = self._body()
             return self.out
         self.build_graph()
+        self.refresh_weights()
         self.graph.replay()
         return self.out
 

@@ -106,6 +106,7 @@ class DeviceCollector:
             for _ in range(self.poll_every):
                 self.step()
             counts = self.ep_count.cpu().numpy().astype(np.int64)
+            self.search.roots.tree.check_errors()  # (already synchronised) tie-break stream intact
             new = counts - self._consumed
             if (new >= self.E).any():  # the running episode reuses slot ep_count % E
                 raise RuntimeError("episode slots overwritten before collection: raise episode_slots or lower "

@@ -29,6 +29,9 @@ pool slot (`step_from_pool`), so the gather and the pool filing kernels disappea
 MLPs (reward, value, policy; both layers, ReLUs, the EZ value-prefix BatchNorm) are ONE more
 launch (csrc/lzm_heads.h, lzm_conv_heads); the EfficientZero LSTM cell stays a batched GEMM.
 """
+import weakref
+from collections import OrderedDict
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -329,19 +332,29 @@ class _Out:
 
 
 class FoldedCache:
-    """FoldedConvNet per model (None for models it does not recognise)."""
+    """FoldedConvNet per model (None for models it does not recognise); a small LRU keyed by model
+    identity, re-folded in place when the model's parameters change (FoldedConvNet.refresh)."""
 
-    def __init__(self):
-        self._id = None
-        self._net = None
+    def __init__(self, cap=4):
+        self.cap = int(cap)
+        self._d = OrderedDict()  # id(model) -> (model weakref, FoldedConvNet or None)
 
     def get(self, model):
-        if id(model) != self._id:
-            self._id = id(model)
+        k = id(model)
+        e = self._d.get(k)
+        if e is not None and e[0]() is not model:  # a dead model's id was reused
+            del self._d[k]
+            e = None
+        if e is None:
             try:
-                self._net = FoldedConvNet(model) if hasattr(model, "latent_hw") else None
+                net = FoldedConvNet(model) if hasattr(model, "latent_hw") else None
             except (NotFoldable, AttributeError):
-                self._net = None
-        elif self._net is not None:
-            self._net.refresh()
-        return self._net
+                net = None
+            e = (weakref.ref(model), net)
+            self._d[k] = e
+            while len(self._d) > self.cap:
+                self._d.popitem(last=False)
+        elif e[1] is not None:
+            e[1].refresh()
+        self._d.move_to_end(k)
+        return e[1]

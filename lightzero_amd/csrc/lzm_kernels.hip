@@ -55,7 +55,8 @@ struct TraverseArgs {
   const uint32_t *jfirst;  // [kMaxWG][31]
   const uint32_t *jnext;   // [kMaxWG][31]
   int32_t *off;            // [B]
-  int32_t *diag;           // [0] passes, [1] overflow-error
+  int32_t *diag;           // [0] passes
+  int32_t *err;            // sticky error counters (lzm_check_errors): [2] fixed point not reached
   int32_t *hint;           // [0] stream length used by the previous call
   float disc;
 };
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(1024) void traverse_glibc_kernel(TraverseArgs p) {
       break;
     }
     if (passes > B + 2) {  // cannot happen: the fixed point is reached in <= B+1 passes
-      if (tid == 0) p.diag[1] = 1;
+      if (tid == 0) atomicAdd(p.err + 2, 1);
       break;
     }
   }
@@ -730,6 +731,7 @@ struct lzm_handle {
   NodeMeta *meta = nullptr;
   int32_t *legal = nullptr, *nlegal = nullptr, *path = nullptr, *path_act = nullptr, *pathlen = nullptr;
   int32_t *off = nullptr, *diag = nullptr, *hint = nullptr, *norm_flag = nullptr;
+  int32_t *err = nullptr;  // [4] sticky error counters of the generic path (lzm_check_errors)
   uint32_t *stream = nullptr;
   int stream_cap = 0;
   float2 *lut = nullptr;
@@ -879,6 +881,8 @@ int lzm_create(int B, int A, int max_sims, int flags, lzm_handle **out) {
   TRY(hipMalloc(&h->pathlen, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->off, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->diag, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->err, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMemset(h->err, 0, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->hint, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->norm_flag, sizeof(int32_t) * 2 * norm_parts(B)) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMemset(h->diag, 0, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
@@ -900,7 +904,7 @@ int lzm_create(int B, int A, int max_sims, int flags, lzm_handle **out) {
 int lzm_destroy(lzm_handle *h) {
   if (!h) return LZM_OK;
   free_tree(h);
-  dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag);
+  dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag); dfree(h->err);
   dfree(h->hint); dfree(h->norm_flag); dfree(h->jmat);
   dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag); dfree(h->phase);
   delete h;
@@ -1003,6 +1007,7 @@ int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, 
   p.jnext = h->jmat + kMaxWG * 31;
   p.off = h->off;
   p.diag = h->diag;
+  p.err = h->err;
   p.hint = h->hint;
   p.disc = discount;
   const bool ez = h->flags & LZM_TREE_EZ;
@@ -1027,7 +1032,7 @@ int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, 
     q.out_x = out_x; q.out_y = out_y; q.out_a = out_a; q.out_vtp = out_vtp; q.out_len = out_len;
     q.out_a64 = p.out_a64; q.disc = discount;
     q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
-    q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag;
+    q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag; q.err = h->err;
     q.reuse_action = h->reuse_action; q.reuse_value = h->reuse_value;
     const int per = kTlbThreads / 64;
     dim3 g((h->B + per - 1) / per), b(kTlbThreads);
@@ -1187,7 +1192,7 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int cur, float discount, float *
   q.out_x = out_x; q.out_y = out_y; q.out_a = out_a; q.out_vtp = out_vtp; q.out_len = out_len;
   q.out_a64 = (long long *)out_a64; q.disc = discount;
   q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
-  q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag;
+  q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag; q.err = h->err;
   q.reuse_action = h->reuse_action; q.reuse_value = h->reuse_value;
   const int per = kTlbThreads / 64;
   dim3 g((h->B + per - 1) / per), b(kTlbThreads);
@@ -1821,6 +1826,34 @@ int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream) {
     return LZM_OK;
   }
   LZM_HIP(hipMemcpyAsync(out, h->search_diag, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return LZM_OK;
+}
+
+// Sticky error counters of every search path on this handle (a look-back spin that
+// times out, or a draw position beyond the coefficient table, would otherwise leave a silently
+// wrong tie-break stream). Synchronises `stream`; out_host (nullable) gets {look-back timeouts,
+// draw-table overflows, traverse fixed-point failures, fused-search errors}.
+int lzm_check_errors(lzm_handle *h, int32_t *out_host, int clear, void *stream) {
+  if (!h) return LZM_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  int32_t w[4] = {0, 0, 0, 0};
+  LZM_HIP(hipMemcpyAsync(w, h->err, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (h->search_diag) LZM_HIP(hipMemcpyAsync(w + 3, h->search_diag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  LZM_HIP(hipStreamSynchronize(s));
+  if (out_host) memcpy(out_host, w, sizeof(w));
+  const bool bad = w[0] || w[1] || w[2] || w[3];
+  if (bad && clear) {
+    LZM_HIP(hipMemsetAsync(h->err, 0, 4 * sizeof(int32_t), s));
+    if (h->search_diag) LZM_HIP(hipMemsetAsync(h->search_diag, 0, sizeof(int32_t), s));
+    LZM_HIP(hipStreamSynchronize(s));
+  }
+  if (bad) {
+    snprintf(g_err, sizeof(g_err),
+             "search tie-break stream invalid: %d look-back timeouts, %d draw-table overflows, %d traverse "
+             "fixed-point failures, %d fused-search errors (results differ from the reference)",
+             w[0], w[1], w[2], w[3]);
+    return LZM_ERR_STATE;
+  }
   return LZM_OK;
 }
 

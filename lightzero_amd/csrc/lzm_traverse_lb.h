@@ -35,7 +35,9 @@ struct TraverseLbArgs {
   const uint32_t *pow16807;   // [31]
   unsigned long long *flags;  // [B] {epoch, depth}
   uint32_t *epoch;            // [2] epoch, done counter
-  int32_t *diag;              // [0] passes (1), [1] spin timeouts (must stay 0)
+  int32_t *diag;              // [0] passes (1)
+  int32_t *err;               // sticky error counters (lzm_check_errors): [0] look-back spin timeouts,
+                              // [1] draw positions beyond the coefficient table
   const int32_t *reuse_action;  // optional [B] ReZero true actions (search-with-reuse), with
   const float *reuse_value;     // [B] their reuse values; null: plain search
 };
@@ -81,7 +83,7 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
         v = __hip_atomic_load(&p.flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((v >> 32) == epoch) break;
         if (++spins > (1ll << 22)) {
-          atomicAdd(p.diag + 1, 1);
+          atomicAdd(p.err, 1);
           v = 0;
           break;
         }
@@ -93,7 +95,7 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
     for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
     const uint32_t *coef = p.coef;
     const int npos = p.coef_positions;
-    int32_t *diag = p.diag;
+    int32_t *diag = p.err + 1;
     if (ti.status == 1) {
       // a tie among unexpanded children: the draw picks the leaf, the depth stays
       const uint32_t rr = glibc_draw(coef, npos, s_z0, base + ti.level, diag);

@@ -9,6 +9,9 @@ packer walks ``dynamics_network.fc_dynamics(_1|_2)``, ``fc_reward_head`` and
 ``prediction_network.fc_{prediction_common,value_head,policy_head}`` and accepts any nesting of
 Linear / BatchNorm1d / ReLU inside them (DI-engine's MLP nests fc blocks).
 """
+import weakref
+from collections import OrderedDict
+
 import torch
 import torch.nn as nn
 
@@ -118,28 +121,46 @@ def pack_muzero_mlp(model, device):
     return flat, dims
 
 
-def prepare_kernel_weights(flat, dims):
-    """Packed network -> the search kernel's lane-order layout (lzm_mlp_prepare, on the current stream)."""
+def prepare_kernel_weights(flat, dims, out=None):
+    """Packed network -> the search kernel's lane-order layout (lzm_mlp_prepare, on the current stream);
+    out: optional existing buffer of the right size to refill in place."""
     args = (dims["hidden"], dims["actions"], dims["head_hidden"], dims["support"], int(dims["res"]))
     n = _lib.load().lzm_mlp_kernel_floats(*args)
-    out = torch.empty(n, dtype=torch.float32, device=flat.device)
+    if out is None or out.numel() != n or out.device != flat.device:
+        out = torch.empty(n, dtype=torch.float32, device=flat.device)
     _lib.call("lzm_mlp_prepare", *args, _lib.ptr(flat), _lib.ptr(out), _lib.stream_ptr())
     return out
 
 
 class PackedCache:
-    """Kernel-layout weights of a model; re-packs only when the model's parameters or buffers
-    change (tensor version counters)."""
+    """Kernel-layout weights per model (small LRU keyed by model identity and device). Re-packs only
+    when the model's parameters or buffers change (tensor version counters), and then IN PLACE, so a
+    HIP graph that captured a search over these weights keeps reading the current ones."""
 
-    def __init__(self):
-        self.key = None
-        self.value = None
+    def __init__(self, cap=4):
+        self.cap = int(cap)
+        self._d = OrderedDict()  # (id(model), device) -> [model weakref, version, weights, dims]
+
+    @staticmethod
+    def _version(model):
+        return tuple(t._version for t in list(model.parameters()) + list(model.buffers()))
 
     def get(self, model, device):
-        ver = tuple(t._version for t in list(model.parameters()) + list(model.buffers()))
-        key = (id(model), str(device), ver)
-        if key != self.key:
+        key = (id(model), str(device))
+        e = self._d.get(key)
+        if e is not None and e[0]() is not model:  # a dead model's id was reused
+            del self._d[key]
+            e = None
+        ver = self._version(model)
+        if e is None:
             flat, dims = pack_muzero_mlp(model, device)
-            self.value = (prepare_kernel_weights(flat, dims), dims)
-            self.key = key
-        return self.value
+            e = [weakref.ref(model), ver, prepare_kernel_weights(flat, dims), dims]
+            self._d[key] = e
+            while len(self._d) > self.cap:
+                self._d.popitem(last=False)
+        elif e[1] != ver:
+            flat, dims = pack_muzero_mlp(model, device)
+            e[2] = prepare_kernel_weights(flat, dims, out=e[2] if dims == e[3] else None)
+            e[1], e[3] = ver, dims
+        self._d.move_to_end(key)
+        return e[2], e[3]

@@ -16,6 +16,8 @@ draw per tree level), see lzm_kernels.hip.
 """
 import copy
 import os
+import weakref
+from collections import OrderedDict
 from typing import Any, List, Union
 
 import numpy as np
@@ -111,6 +113,58 @@ def _step_net(mcts, model):
     return model
 
 
+class _GraphEntry:
+    """One captured search: the graph together with everything its kernels point at — the
+    buffers the inputs are copied into, the (folded) network whose weights it reads — so none of
+    them can be freed or rebuilt while the graph may replay."""
+
+    def __init__(self, graph, buf, net, model, tree):
+        self.graph, self.buf, self.net = graph, buf, net
+        self.model_ref, self.tree_ref = weakref.ref(model), weakref.ref(tree)
+
+    def valid_for(self, model, tree):
+        return self.model_ref() is model and self.tree_ref() is tree and tree.h is not None
+
+    def replay(self):
+        if self.net is not None and hasattr(self.net, "refresh"):
+            self.net.refresh()  # re-fold in place if the parameters changed since capture
+        self.graph.replay()
+
+
+class _GraphCache:
+    """LRU of captured searches keyed by (tree uid, tree generation, model, B, S, latent shape);
+    entries whose tree or model died are dropped on lookup, the oldest beyond `cap` evicted."""
+
+    def __init__(self, cap=4):
+        self.cap = int(cap)
+        self._d = OrderedDict()
+
+    def __len__(self):
+        return len(self._d)
+
+    def get(self, key, model, tree):
+        e = self._d.get(key)
+        if e is None:
+            return None
+        if not e.valid_for(model, tree):
+            del self._d[key]
+            return None
+        self._d.move_to_end(key)
+        return e
+
+    def put(self, key, entry):
+        self._d[key] = entry
+        self._d.move_to_end(key)
+        for k in [k for k, e in self._d.items() if e.tree_ref() is None or e.model_ref() is None]:
+            del self._d[k]
+        while len(self._d) > self.cap:
+            self._d.popitem(last=False)
+
+
+def _graph_key(t, model, B, S, shape, extra=()):
+    return (t.uid, t.generation, id(model), B, S, tuple(shape), tuple(extra))
+
+
 def _fuse_traverse(cfg, t):
     """fold each simulation's traverse into the previous simulation's decode launch (parity mode with
     the look-back traverse; cfg.fuse_traverse, default off: measured even with the two launches at
@@ -176,7 +230,7 @@ class MuZeroMCTSCtree(object):
             self._cfg.model.support_scale, self._cfg.device, self._cfg.model.categorical_distribution
         )
         self._buf = _SearchBuffers()
-        self._graphs = {}
+        self._graphs = _GraphCache(int(self._cfg.get('graph_cache_size', 4)))
         self._packed = PackedCache()
         self._folded = FoldedCache()
 
@@ -204,15 +258,16 @@ class MuZeroMCTSCtree(object):
             return None
         return packed, dims
 
-    def _loop(self, t, model, buf, mm, vtp_in, seeds, S, row, rec=None, infer=None):
+    def _loop(self, t, model, buf, mm, vtp_in, seeds, S, row, rec=None, infer=None, net=None):
         """The S simulations (mcts_ctree.py:255-321), all enqueued on the current stream.
         infer: optional device int64 [S], per simulation the number of roots that ran inference
-        (search-with-reuse: roots whose walk stopped on an expanded node report x = -1)."""
+        (search-with-reuse: roots whose walk stopped on an expanded node report x = -1).
+        net: the step network to run (default: _step_net(model))."""
         cfg = self._cfg
         disc = float(np.float32(cfg.discount_factor))
         cat = self._categorical()
         new_minmax(t.B, cfg.value_delta_max, t.device, out=mm)
-        model = _step_net(self, model)
+        model = _step_net(self, model) if net is None else net
         native = _native_trunk(model, buf)
         with _HeadVerdicts(t, model, buf, native and cat and getattr(model, "heads", None) is not None):
             self._sims(t, model, buf, mm, vtp_in, seeds, S, row, rec, infer, native, cat, disc)
@@ -261,15 +316,19 @@ class MuZeroMCTSCtree(object):
             lat0 = _latent_tensor(latent_state_roots, dev)
             shape = lat0.shape[1:]
             row = int(np.prod(shape)) if len(shape) else 1
-            buf = self._buf.get(B, S, shape, dev)
+            rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
+            fz = self._fused(model, t)
+            graph = fz is None and rec is None and self._cfg.get('use_hip_graph', False)
+            gkey = _graph_key(t, model, B, S, shape) if graph else None
+            entry = self._graphs.get(gkey, model, t) if graph else None
+            # a captured search owns its buffers (they are what its kernels point at)
+            buf = entry.buf if entry is not None else (_SearchBuffers() if graph else self._buf).get(B, S, shape, dev)
             if lat0.data_ptr() != buf.pool[0].data_ptr():  # (the collect step writes it in place)
                 buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
             buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
-            rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
             if rec is not None:
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
-            fz = self._fused(model, t)
             if fz is not None:
                 packed, dims = fz
                 cfg = self._cfg
@@ -279,8 +338,11 @@ class MuZeroMCTSCtree(object):
                 vt = to_play_batch if _usable_i32(to_play_batch, B, dev) else buf.vtp_in
                 t.search_mlp(dims, packed, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base),
                              float(cfg.pb_c_init), float(np.float32(cfg.discount_factor)), rec=rec)
-            elif rec is None and self._cfg.get('use_hip_graph', False):
-                self._graph_search(t, model, buf, S, row)
+            elif graph:
+                if entry is None:
+                    entry = self._capture(t, model, buf, S, row)
+                    self._graphs.put(gkey, entry)
+                entry.replay()
             else:
                 self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, rec)
             roots._last_minmax = buf.mm
@@ -335,25 +397,21 @@ class MuZeroMCTSCtree(object):
             counts = infer.cpu().numpy()
         return int(counts[-1]) if S else 0, float(counts.sum()) / max(S, 1)
 
-    def _graph_search(self, t, model, buf, S, row):
-        """Replays the whole S-simulation loop as one HIP graph (captured once per tree handle,
-        model and shape; inputs are the static buffers filled just before)."""
-        key = (t.h.value, t.generation, id(model), buf.key)
-        g = self._graphs.get(key)
-        if g is None:
-            # warm up every kernel and library handle on a scratch tree (must not touch `t`)
-            scratch = DeviceTree(t.B, t.A, max(S, t.sims_capacity), ez=t.ez, fast_rng=t.fast_rng, device=t.device)
-            scratch.copy_roots_from(t)
-            scratch.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
-            self._loop(scratch, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row)
-            torch.cuda.synchronize(t.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row)
-            self._graphs[key] = g
-            scratch.close()
-        _step_net(self, model)  # re-fold in place if the parameters changed since capture
-        g.replay()
+    def _capture(self, t, model, buf, S, row):
+        """Captures the whole S-simulation loop as one HIP graph over `buf` (the static buffers
+        filled just before) and the network _step_net picks now; the entry keeps both alive."""
+        net = _step_net(self, model)
+        # warm up every kernel and library handle on a scratch tree (must not touch `t`)
+        scratch = DeviceTree(t.B, t.A, max(S, t.sims_capacity), ez=t.ez, fast_rng=t.fast_rng, device=t.device)
+        scratch.copy_roots_from(t)
+        scratch.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
+        self._loop(scratch, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, net=net)
+        torch.cuda.synchronize(t.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, net=net)
+        scratch.close()
+        return _GraphEntry(g, buf, net if net is not model else None, model, t)
 
 
 class EfficientZeroMCTSCtree(object):
@@ -382,7 +440,7 @@ class EfficientZeroMCTSCtree(object):
             self._cfg.model.support_scale, self._cfg.device, self._cfg.model.categorical_distribution
         )
         self._buf = _SearchBuffers()
-        self._graphs = {}
+        self._graphs = _GraphCache(int(self._cfg.get('graph_cache_size', 4)))
         self._folded = FoldedCache()
 
     rng_mode = 'glibc'
@@ -391,7 +449,7 @@ class EfficientZeroMCTSCtree(object):
     def roots(cls: int, active_collect_env_num: int, legal_actions: List[Any]) -> "ez_tree.Roots":
         return ez_tree.Roots(active_collect_env_num, legal_actions, fast_rng=(cls.rng_mode == 'philox'))
 
-    def _loop(self, t, model, buf, S, row, Hl, rec=None):
+    def _loop(self, t, model, buf, S, row, Hl, rec=None, net=None):
         """The S simulations (mcts_ctree.py:756-827), all enqueued on the current stream."""
         cfg = self._cfg
         disc = float(np.float32(cfg.discount_factor))
@@ -399,7 +457,7 @@ class EfficientZeroMCTSCtree(object):
         cat = bool(cfg.model.get('categorical_distribution', True))
         B = t.B
         new_minmax(B, cfg.value_delta_max, t.device, out=buf.mm)
-        model = _step_net(self, model)
+        model = _step_net(self, model) if net is None else net
         native = _native_trunk(model, buf)
         with _HeadVerdicts(t, model, buf, native and cat and getattr(model, "heads", None) is not None):
             self._sims(t, model, buf, S, row, Hl, rec, native, cat, disc, horizon)
@@ -466,38 +524,41 @@ class EfficientZeroMCTSCtree(object):
             hc0 = _latent_tensor(reward_hidden_state_roots[0], dev).reshape(B, -1)
             hh0 = _latent_tensor(reward_hidden_state_roots[1], dev).reshape(B, -1)
             Hl = hc0.shape[1]
-            buf = self._buf.get(B, S, shape, dev, extra=(Hl, Hl))
+            rec = None
+            graph = self._cfg.get('use_hip_graph', False) and not getattr(self, "record", False)
+            gkey = _graph_key(t, model, B, S, shape, (Hl, Hl)) if graph else None
+            entry = self._graphs.get(gkey, model, t) if graph else None
+            buf = entry.buf if entry is not None else (_SearchBuffers() if graph else self._buf).get(
+                B, S, shape, dev, extra=(Hl, Hl))
             buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             buf.extra[0][0].copy_(hc0)
             buf.extra[1][0].copy_(hh0)
             buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
             buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
-            rec = None
             if getattr(self, "record", False):
                 rec = _Recorder(S, B, t.A, dev)
                 rec.is_reset = torch.zeros((S, B), dtype=torch.int32, device=dev)
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
-            if rec is None and self._cfg.get('use_hip_graph', False):
-                self._graph_search(t, model, buf, S, row, Hl)
+            if graph:
+                if entry is None:
+                    entry = self._capture(t, model, buf, S, row, Hl)
+                    self._graphs.put(gkey, entry)
+                entry.replay()
             else:
                 self._loop(t, model, buf, S, row, Hl, rec)
             roots._last_minmax = buf.mm
             self.last_record = rec
 
-    def _graph_search(self, t, model, buf, S, row, Hl):
-        """The S-simulation loop replayed as one HIP graph (see MuZeroMCTSCtree._graph_search)."""
-        key = (t.h.value, t.generation, id(model), buf.key)
-        g = self._graphs.get(key)
-        if g is None:
-            scratch = DeviceTree(t.B, t.A, max(S, t.sims_capacity), ez=t.ez, fast_rng=t.fast_rng, device=t.device)
-            scratch.copy_roots_from(t)
-            scratch.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
-            self._loop(scratch, model, buf, S, row, Hl)
-            torch.cuda.synchronize(t.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._loop(t, model, buf, S, row, Hl)
-            self._graphs[key] = g
-            scratch.close()
-        _step_net(self, model)  # re-fold in place if the parameters changed since capture
-        g.replay()
+    def _capture(self, t, model, buf, S, row, Hl):
+        """The S-simulation loop captured as one HIP graph (see MuZeroMCTSCtree._capture)."""
+        net = _step_net(self, model)
+        scratch = DeviceTree(t.B, t.A, max(S, t.sims_capacity), ez=t.ez, fast_rng=t.fast_rng, device=t.device)
+        scratch.copy_roots_from(t)
+        scratch.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
+        self._loop(scratch, model, buf, S, row, Hl, net=net)
+        torch.cuda.synchronize(t.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._loop(t, model, buf, S, row, Hl, net=net)
+        scratch.close()
+        return _GraphEntry(g, buf, net if net is not model else None, model, t)

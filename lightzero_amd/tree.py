@@ -5,6 +5,7 @@ Host-side owner of the structures the reference keeps in ``CRoots`` + ``CSearchR
 every method enqueues work on the current torch stream and never synchronises.
 """
 import ctypes
+import itertools
 import threading
 import time
 
@@ -50,9 +51,13 @@ class SequentialSeeds:
 
 
 # ----------------------------------------------------------------------------- handle
+_uids = itertools.count(1)
+
+
 class DeviceTree:
     def __init__(self, num_roots, action_space, max_sims=64, ez=False, fast_rng=False, device=None):
         _lib.require_gpu()
+        self.uid = next(_uids)  # never reused (a handle address can be, after lzm_destroy)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.B, self.A = int(num_roots), int(action_space)
         self.ez, self.fast_rng = bool(ez), bool(fast_rng)
@@ -171,6 +176,15 @@ class DeviceTree:
              ptr(weights), int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax), ptr(seeds),
              ptr(vtp_in), ptr(pool), r("x"), r("action"), r("search_len"), r("decoded"), r("policy_logits"),
              stream_ptr(stream))
+
+    def check_errors(self, clear=True, stream=None):
+        """Post-search integrity check (synchronises the stream): raises LzmError when a look-back
+        spin timed out or a draw fell outside the coefficient table on any search path of this
+        handle, i.e. when the parity-mode tie-break stream may differ from the reference's.
+        Returns the four counters otherwise (all zero)."""
+        out = (ctypes.c_int32 * 4)()
+        call("lzm_check_errors", self.h, out, int(bool(clear)), stream_ptr(stream))
+        return list(out)
 
     def search_diagnostics(self):
         out = torch.zeros(2, dtype=torch.int32, device=self.device)
