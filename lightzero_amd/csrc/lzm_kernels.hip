@@ -1567,11 +1567,12 @@ size_t plan_res(SearchArgs &p, ResNet &n, const lzm_handle *h, int S, int A) {
   n.off_l2n = (int)o; o += round4((size_t)S + 2);
   n.off_nq = (int)o; o += round4((size_t)2 * (S + 2));
   n.off_cs = (int)o; o += (size_t)4 * h->cap;
+  n.off_dec = (int)o; o += round4((size_t)S + 2);
   p.off_misc = o; o += round4((size_t)S + 32);
   n.off_wd1 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
   n.off_wd2 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
   // static LDS of the kernel: activations (two rows), biases, scalars (below 2 KiB)
-  constexpr size_t kResStatic = (kRHid + 2 * (6 * kRHid + kRF + 2 * kRF + kRMaxA) + kResBiasFloats) * 4 + 2048;
+  constexpr size_t kResStatic = (kRHid + 4 * kRHid + 2 * (4 * kRHid + kRF + 2 * kRF + kRMaxA) + kResBiasFloats) * 4 + 2048;
   constexpr size_t kResMax = 160 * 1024 - kResStatic;
   // pUCT visit table (optional: the descent divides without it)
   const size_t tri = round4((size_t)h->lut_n * (h->lut_n + 1) / 2);
@@ -1581,15 +1582,8 @@ size_t plan_res(SearchArgs &p, ResNet &n, const lzm_handle *h, int S, int A) {
   return o * sizeof(float) <= kResMax ? o * sizeof(float) : 0;
 }
 void res_net(ResNet &n, const float *wres, int A) {
-  auto blk = [&](int b) { return wres + res_block_offset(b, A); };
-  for (int q = 0; q < 6; ++q) n.d[q] = reinterpret_cast<const float4 *>(blk(kRbD + q));
-  n.rh = reinterpret_cast<const float4 *>(blk(kRbRH));
-  n.vph = reinterpret_cast<const float4 *>(blk(kRbVPH));
-  n.rs = reinterpret_cast<const float4 *>(blk(kRbRS));
-  n.vs = reinterpret_cast<const float4 *>(blk(kRbVS));
-  n.po = reinterpret_cast<const float4 *>(blk(kRbPO));
-  n.bd = blk(kRbBD); n.brh = blk(kRbBRH); n.bvph = blk(kRbBVPH); n.brs = blk(kRbBRS); n.bvs = blk(kRbBVS);
-  n.bpo = blk(kRbBPO); n.act = blk(kRbAct);
+  (void)A;
+  n.w = wres;
 }
 }  // namespace
 
@@ -1746,18 +1740,26 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     if (lds) {
       res_net(n, weights + round4(kernel_layout(kls, nkl, lay_w, lay_b)), A);
       const char *sm = getenv("LZM_RES_SELECT");
-      n.select_mode = sm ? atoi(sm) : 1;  // measured: 1 < 0 < 2 < 3
+      // measured: 4 < 1 < 0 < 2 < 3; 4 is 1 with descend_small for A <= 2
+      n.select_mode = sm ? atoi(sm) : (A <= 2 ? 4 : 1);
       // LZM_RES_SPEC=1 (parity mode): evaluate two-way leaf ties speculatively as a second network
       // row instead of waiting for the look-back (measured slower: every simulation pays the row)
+      const char *sl = getenv("LZM_RES_LATE");
+      n.late_draw = sl ? atoi(sl) : 1;
       const char *se = getenv("LZM_RES_SPEC");
       const bool spec = !fast && se && atoi(se) == 1;
-      const void *fn = spec ? (const void *)search_res_kernel<2> : (const void *)search_res_kernel<1>;
-      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      // production: selection mode, RNG and stamps fixed at compile time (modes 1 and 4); phase
+      // timing compiles the stamps in; the other selection modes (experiments) read it at run time
+      const int md = (n.select_mode == 4 && A > 2) ? 1 : n.select_mode;
+      void (*fn)(SearchArgs, ResNet) =
+          spec                  ? search_res_kernel<2, 1, 0, false>
+          : (md != 1 && md != 4) ? search_res_kernel<1, -1, -1, true>
+          : q.phase             ? (md == 4 ? search_res_kernel<1, 4, -1, true> : search_res_kernel<1, 1, -1, true>)
+          : md == 4             ? (fast ? search_res_kernel<1, 4, 1, false> : search_res_kernel<1, 4, 0, false>)
+                                : (fast ? search_res_kernel<1, 1, 1, false> : search_res_kernel<1, 1, 0, false>);
+      hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       if (e == hipSuccess) {
-        if (!spec)
-          hipLaunchKernelGGL(search_res_kernel<1>, dim3(G), dim3(kRT), lds, (hipStream_t)stream, q, n);
-        else
-          hipLaunchKernelGGL(search_res_kernel<2>, dim3(G), dim3(kRT), lds, (hipStream_t)stream, q, n);
+        hipLaunchKernelGGL(fn, dim3(G), dim3(kRT), lds, (hipStream_t)stream, q, n);
         e = hipGetLastError();
       }
       LZM_HIP(e);

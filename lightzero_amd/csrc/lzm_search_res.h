@@ -57,12 +57,15 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 // then the biases ([6][128] D, [32] RH, [64] VPH, [604] RS, [604] VS, [32] PO) and the one-hot
 // action rows of fc_dynamics[0], [A][128].
 struct ResNet {
-  const float4 *d[6];  // fc_dynamics[0] (latent rows), fc_dynamics[1], fc_dynamics_2[0..1], fc_prediction_common[0..1]
-  const float4 *rh, *vph, *rs, *vs, *po;
-  const float *bd, *brh, *bvph, *brs, *bvs, *bpo, *act;
+  // the resident layout (one base pointer: every block offset but the action rows' is a
+  // compile-time constant, res_block_offset; the kernel derives the block addresses, which keeps
+  // ~30 scalar registers of block pointers out of the simulation loop)
+  const float *w;
   // LDS float offsets beyond SearchArgs' tree plan
-  int off_act, off_wd1, off_wd2, off_l2n, off_nq, off_cs;
+  int off_act, off_wd1, off_wd2, off_l2n, off_nq, off_cs, off_dec;
   int select_mode;  // LZM_RES_SELECT (experiments): how the walk runs, see the simulation loop
+  int late_draw;    // NR = 1: two-way leaf ties run the dynamics layers for both candidates before the
+                    // look-back wait (LZM_RES_LATE, default 1)
 };
 
 // floats of the bias blocks ([6][128] D, [32] RH, [64] VPH, [604] RS, [604] VS, [32] PO)
@@ -90,6 +93,12 @@ __host__ __device__ inline size_t res_block_offset(int b, int A) {
   for (int q = 0; q < b; ++q) o += res_block_floats(q, A);
   return o;
 }
+
+// block b of the resident layout (b < kRbAct: a compile-time offset)
+__device__ __forceinline__ const float4 *res_blk4(const ResNet &n, int b) {
+  return reinterpret_cast<const float4 *>(n.w + res_block_offset(b, 0));
+}
+__device__ __forceinline__ const float *res_blk(const ResNet &n, int b, int A) { return n.w + res_block_offset(b, A); }
 
 // Packed-network source of resident float d of block b: packed layer index (lzm_kernels.hip
 // mlp_shapes order: 0,1 fc_dynamics, 2,3 fc_dynamics_2, 4,5 reward head, 6,7 prediction common,
@@ -180,6 +189,19 @@ __device__ __forceinline__ void support_logits(const float *h, const float4 *P, 
   z2 = (t + dpp_f<0xB1>(t)) + (tid < 2 * kRTail ? bias[2 * kRT + (tid >> 1)] : 0.0f);
 }
 
+// Two-action selection outcome of an expanded node when it does not depend on the walk (all
+// children visited, or a single legal child): 0 / 1 = the legal position cselect_child picks,
+// 3 = a tie between the two visited children (a draw decides), 2 = depends on the walk's mean-q
+// (an unvisited child scores the normalised parent mean-q). Same operations as the walk's scores.
+__device__ __forceinline__ int a2_decision(float4 c0, float4 c1, int n) {
+  if (n < 2) return 0;
+  if (!__float_as_int(c0.w) || !__float_as_int(c1.w)) return 2;
+  const float s0 = c0.x + c0.y, s1 = c1.x + c1.y;
+  const float M = fmaxf(s0, s1);
+  const int r = (s0 == M) ? 0 : 1;
+  return (r == 0 && s1 >= M - 0.000001f) ? 3 : r;
+}
+
 // ---- selection split in two (MuZero, tree slice in LDS, one root):
 // (1) every expanded node's pUCT terms that do not depend on the walk, one thread per node
 //     (cucb_score, cnode.cpp:655-699: prior_score, and for visited children the normalised,
@@ -188,8 +210,9 @@ __device__ __forceinline__ void support_logits(const float *h, const float4 *P, 
 //     what unvisited children score) and the argmax / tie list per level.
 // Same float operations in the same order as descend_wave, so the same bits.
 // nq[latent] = {total_q, total_v}; cs[child node] = {prior_score, value term, child latent, visited}
+// dec (nullable, A == 2): each node's walk-independent outcome (a2_decision) for descend_a2.
 __device__ inline void precompute_terms(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
-                                        float4 mm, int players, float disc) {
+                                        float4 mm, int players, float disc, int *dec = nullptr) {
   for (int L = threadIdx.x; L < nlat; L += kRT) {
     const int n = lat2node[L];
     if (n < 0) continue;
@@ -201,6 +224,7 @@ __device__ inline void precompute_terms(const TreeView &t, int nlat, const int *
     const float2 Lx = t.lut[N];
     float total_q = 0.0f;
     int total_v = 0;
+    float4 c01[2];
     for (int j = 0; j < nleg; ++j) {
       const int c = base + legal_at(t, 0, n, j);
       const NodeStat cst = t.stat[c];
@@ -218,9 +242,13 @@ __device__ inline void precompute_terms(const TreeView &t, int nlat, const int *
       }
       float pb_c = Lx.x;
       pb_c *= (t.pbt && cst.visit <= N) ? t.pbt[N * (N + 1) / 2 + cst.visit] : (Lx.y / (float)(cst.visit + 1));
-      cs[c] = make_float4(pb_c * cst.prior, vv, __int_as_float(t.meta[c].latent), __int_as_float(cst.visit > 0 ? 1 : 0));
+      const float4 term = make_float4(pb_c * cst.prior, vv, __int_as_float(t.meta[c].latent),
+                                      __int_as_float(cst.visit > 0 ? 1 : 0));
+      cs[c] = term;
+      if (j < 2) c01[j] = term;
     }
     nq[L] = make_float2(total_q, __int_as_float(total_v));
+    if (dec) dec[L] = (t.A == 2 && nleg >= 1) ? a2_decision(c01[0], c01[nleg > 1 ? 1 : 0], nleg) : 2;
   }
 }
 
@@ -309,6 +337,271 @@ __device__ inline Descent descend_terms(const TreeView &t, const float2 *nq, con
     plat = lat;
     lat = __builtin_amdgcn_readlane(__float_as_int(c.z), jsel);
   }
+  Descent d;
+  d.len = len;
+  d.x = plat;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
+// descend_terms for small action spaces (A <= AM <= 4): every lane of the wave evaluates the level
+// (all AM children's terms as broadcast LDS reads, the max / first index / tie list as a short
+// unrolled chain of per-lane compares), so a level is one round of LDS reads and a few dozen
+// dependent VALU operations — no DPP reduction, ballots or readlanes on the chain. The root's legal
+// actions (rleg, nleg) are passed in registers. Same float operations and tie rule as descend_terms
+// (SURVEY.md A7 closed form), so the same bits; every lane returns the same Descent.
+template <int AM, bool CLASSIFY, typename Draw>
+__device__ inline Descent descend_small(const TreeView &t, const float2 *nq, const float4 *cs, float4 mm, int vtp,
+                                        int players, const int *rleg, int nleg, Draw draw, TieInfo *tie,
+                                        WalkState *resume = nullptr, WalkState *at_tie = nullptr) {
+  const int lane = threadIdx.x & 63;
+  const int A = t.A;
+  WalkState w0 = resume ? *resume : walk_start(t, vtp);
+  int node = w0.node, is_root = w0.is_root, len = w0.len, last_action = w0.last_action, plat = w0.plat;
+  float parent_q = w0.parent_q;
+  int lat = w0.lat;
+  vtp = w0.vtp;
+  if (lane == 0 && !resume) t.path[0] = 0;
+  if (CLASSIFY) tie->status = 0;
+  while (lat >= 0 && len < t.depth_cap - 1) {
+    if (CLASSIFY && at_tie) {
+      at_tie->node = node; at_tie->lat = lat; at_tie->len = len; at_tie->plat = plat;
+      at_tie->last_action = last_action; at_tie->is_root = is_root; at_tie->vtp = vtp; at_tie->parent_q = parent_q;
+    }
+    const bool root = node == 0;
+    const int n = root ? nleg : A;
+    const int base = 1 + A * lat;
+    int act[AM];
+    float4 c[AM];
+#pragma unroll
+    for (int j = 0; j < AM; ++j) {
+      act[j] = root ? rleg[j] : j;
+      c[j] = j < n ? cs[base + act[j]] : make_float4(0.0f, 0.0f, __int_as_float(-1), __int_as_float(0));
+    }
+    const float2 q = nq[lat];
+    const int total_v = __float_as_int(q.y);
+    float mean_q;
+    if (is_root && total_v > 0)
+      mean_q = q.x / (float)total_v;
+    else
+      mean_q = (parent_q + q.x) / (float)(total_v + 1);
+    is_root = 0;
+    parent_q = mean_q;
+    float vu = mm_normalize(mm, mean_q);
+    if (vu < 0) vu = 0;
+    if (vu > 1) vu = 1;
+    float sc[AM];
+    float M = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < AM; ++j) {
+      sc[j] = c[j].x + (__float_as_int(c[j].w) ? c[j].y : vu);
+      if (j < n) M = fmaxf(M, sc[j]);
+    }
+    int r = 0;
+#pragma unroll
+    for (int j = AM - 1; j >= 0; --j)
+      if (j < n && sc[j] == M) r = j;
+    const float thr = M - 0.000001f;
+    unsigned mask = 1u << r;
+#pragma unroll
+    for (int j = 1; j < AM; ++j)
+      if (j < n && j > r && sc[j] >= thr) mask |= 1u << j;
+    const int nl = __popc(mask);
+    if (CLASSIFY && nl > 1) {
+      bool all_leaves = true;
+#pragma unroll
+      for (int j = 0; j < AM; ++j)
+        if (((mask >> j) & 1u) && __float_as_int(c[j].z) >= 0) all_leaves = false;
+      if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+      tie->status = all_leaves ? 1 : 2;
+      tie->level = len;
+      tie->mask = mask;
+      Descent d;
+      d.len = len + 1;
+      d.x = lat;
+      d.action = -1;
+      d.vtp = vtp;
+      d.leaf = -1;
+      return d;
+    }
+    int jsel = r;
+    if (!CLASSIFY) {
+      const uint32_t rr = draw(len);
+      int kk = (int)(rr % (uint32_t)nl);
+      unsigned m_ = mask;
+      for (; kk > 0; --kk) m_ &= m_ - 1;
+      jsel = __ffs(m_) - 1;
+    }
+    int action = act[0], nlat = __float_as_int(c[0].z);
+#pragma unroll
+    for (int j = 1; j < AM; ++j)
+      if (jsel == j) {
+        action = act[j];
+        nlat = __float_as_int(c[j].z);
+      }
+    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+    node = base + action;
+    last_action = action;
+    if (lane == 0) {
+      t.path_act[len] = action;
+      t.path[len + 1] = node;
+    }
+    ++len;
+    plat = lat;
+    lat = nlat;
+  }
+  Descent d;
+  d.len = len;
+  d.x = plat;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
+// descend_small for exactly two actions, written for the shortest dependent chain per level. The
+// terms phase precomputes each node's walk-independent outcome (dec[latent], a2_decision); where
+// it is known the level is a pointer chase — the next node's terms are read while this level's
+// mean-q division (needed further down only) completes. Only a node with an unvisited child waits
+// for its normalised mean-q. The normaliser's divisor is fixed per walk (mm_normalize's branches
+// become one division); same float operations as descend_terms, so the same bits.
+__device__ __forceinline__ float mm_norm_fixed(bool scale, float lo, float div, float v) {
+  return scale ? (v - lo) / div : v;
+}
+
+// OPT (experiments): bit 0 collects the path in lanes (one store at the end instead of two LDS
+// stores per level), bit 1 reads the next level's node data before this level's mean-q division.
+template <bool CLASSIFY, typename Draw, int OPT = 0>
+__device__ inline Descent descend_a2(const TreeView &t, const float2 *nq, const int *dec, const float4 *cs, float4 mm,
+                                     int vtp, int players, const int *rleg, int nleg, Draw draw, TieInfo *tie,
+                                     WalkState *resume = nullptr, WalkState *at_tie = nullptr,
+                                     float2 *chain = nullptr) {
+  const int lane = threadIdx.x & 63;
+  const float delta = mm.x - mm.y;
+  const bool scale = delta > 0;
+  const float div = (delta < mm.z) ? mm.z : delta;
+  const float lo = mm.y;
+  WalkState w0 = resume ? *resume : walk_start(t, vtp);
+  int node = w0.node, len = w0.len, last_action = w0.last_action, plat = w0.plat, lat = w0.lat;
+  float parent_q = w0.parent_q;
+  bool is_root = w0.is_root;
+  vtp = w0.vtp;
+  if (lane == 0 && !resume) t.path[0] = 0;
+  if (CLASSIFY) tie->status = 0;
+  const int dmax = t.depth_cap - 1;
+  const bool lanes_path = (OPT & 1) && t.depth_cap <= 64;
+  const int len0 = len;
+  int pnode = 0, pact = 0;
+  auto flush = [&]() {
+    if (lanes_path) {
+      if (lane > len0 && lane <= len) t.path[lane] = pnode;
+      if (lane >= len0 && lane < len) t.path_act[lane] = pact;
+    }
+  };
+  int a0 = 0, a1 = 0, n = 2;
+  float4 c0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), c1 = c0;
+  float2 q = make_float2(0.0f, 0.0f);
+  int dl = 2;
+  auto fetch = [&](int nd, int lt) {
+    const bool root = nd == 0;  // (only the first level of a walk from the root)
+    a0 = root ? rleg[0] : 0;
+    a1 = root ? rleg[1] : 1;
+    n = root ? nleg : 2;
+    const int base = 1 + 2 * lt;
+    c0 = cs[base + a0];
+    c1 = cs[base + (n > 1 ? a1 : a0)];
+    q = nq[lt];
+    dl = dec[lt];
+  };
+  if ((OPT & 2) && lat >= 0) fetch(node, lat);
+  // OPT & 4: the mean-q chain is evaluated lazily — a level whose outcome is known only records
+  // its (total_q, total_v) in chain[]; the divisions run (in level order, the same operations)
+  // when a level needs its normalised mean-q or a tie needs parent_q
+  const bool lazy = (OPT & 4) && chain != nullptr;
+  const bool root0 = is_root;
+  int pend = len;
+  auto settle = [&](int upto) {
+    for (int l = pend; l < upto; ++l) {
+      const float2 cq = chain[l];
+      const int tv = __float_as_int(cq.y);
+      parent_q = (l == len0 && root0 && tv > 0) ? cq.x / (float)tv : (parent_q + cq.x) / (float)(tv + 1);
+    }
+    pend = upto > pend ? upto : pend;
+  };
+  while (lat >= 0 && len < dmax) {
+    if (!(OPT & 2)) fetch(node, lat);
+    const int base = 1 + 2 * lat;
+    const int total_v = __float_as_int(q.y);
+    const float qx = q.x;
+    int jsel = dl;
+    bool tie2 = dl == 3;
+    float mean_q = 0.0f;
+    if (lazy && (dl == 2 || (CLASSIFY && dl == 3))) settle(len);
+    const bool rootq = (lazy ? (len == len0 && root0) : is_root) && total_v > 0;
+    if ((!(OPT & 2) && !lazy) || dl == 2) mean_q = rootq ? qx / (float)total_v : (parent_q + qx) / (float)(total_v + 1);
+    if (dl == 2) {
+      float vu = mm_norm_fixed(scale, lo, div, mean_q);
+      if (vu < 0) vu = 0;
+      if (vu > 1) vu = 1;
+      const float s0 = c0.x + (__float_as_int(c0.w) ? c0.y : vu);
+      const float s1 = c1.x + (__float_as_int(c1.w) ? c1.y : vu);
+      const float M = fmaxf(s0, s1);
+      jsel = (s0 == M) ? 0 : 1;
+      tie2 = jsel == 0 && s1 >= M - 0.000001f;
+    }
+    if (CLASSIFY && tie2) {
+      if (at_tie) {
+        at_tie->node = node; at_tie->lat = lat; at_tie->len = len; at_tie->plat = plat;
+        at_tie->last_action = last_action; at_tie->is_root = is_root; at_tie->vtp = vtp; at_tie->parent_q = parent_q;
+      }
+      flush();
+      if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+      const bool all_leaves = __float_as_int(c0.z) < 0 && __float_as_int(c1.z) < 0;
+      tie->status = all_leaves ? 1 : 2;
+      tie->level = len;
+      tie->mask = 3ull;
+      Descent d;
+      d.len = len + 1;
+      d.x = lat;
+      d.action = -1;
+      d.vtp = vtp;
+      d.leaf = -1;
+      return d;
+    }
+    if (!CLASSIFY && tie2) jsel = (int)(draw(len) % 2u);
+    const int action = jsel ? a1 : a0;
+    const int nlat = __float_as_int(jsel ? c1.z : c0.z);
+    const int nnode = base + action;
+    if (OPT & 2) {
+      if (nlat >= 0) fetch(nnode, nlat);
+      if (dl != 2) mean_q = rootq ? qx / (float)total_v : (parent_q + qx) / (float)(total_v + 1);
+    }
+    is_root = false;
+    if (!lazy) {
+      parent_q = mean_q;
+    } else if (dl == 2) {
+      parent_q = mean_q;
+      pend = len + 1;
+    } else if (lane == 0) {
+      chain[len] = make_float2(qx, __int_as_float(total_v));
+    }
+    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
+    node = nnode;
+    last_action = action;
+    if (lanes_path) {
+      pact = lane == len ? action : pact;
+      pnode = lane == len + 1 ? node : pnode;
+    } else if (lane == 0) {
+      t.path_act[len] = action;
+      t.path[len + 1] = node;
+    }
+    ++len;
+    plat = lat;
+    lat = nlat;
+  }
+  flush();
   Descent d;
   d.len = len;
   d.x = plat;
@@ -500,8 +793,14 @@ __device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, uns
 }
 
 // NR = 2 (parity mode): the network carries a second, speculative row for two-way leaf ties.
-template <int NR>
+// SMODE: the selection mode at compile time (-1: n.select_mode at run time, experiments); RNG:
+// 0 glibc, 1 Philox, -1 p.fast at run time; STAMPS: phase stamps compiled in (LZM_PHASE_TIMING).
+// Production launches fix all three, so the unused paths cost neither code nor registers.
+template <int NR, int SMODE, int RNG, bool STAMPS>
 __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) void search_res_kernel(SearchArgs p, ResNet n) {
+  if (!STAMPS) p.phase = nullptr;
+  if (RNG >= 0) p.fast = RNG;
+  if (SMODE >= 0) n.select_mode = SMODE;
   extern __shared__ float4 smem4[];
   float *smem = reinterpret_cast<float *>(smem4);
   const int tid = threadIdx.x, g = blockIdx.x, G = gridDim.x, lane = tid & 63, wid = tid >> 6;
@@ -551,6 +850,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // latent -> node map of the expanded nodes (children of latent L sit at 1 + A L)
   int *L2N = reinterpret_cast<int *>(smem + n.off_l2n);
   float2 *NQ = reinterpret_cast<float2 *>(smem + n.off_nq);
+  int *DEC = reinterpret_cast<int *>(smem + n.off_dec);
   float4 *CS = reinterpret_cast<float4 *>(smem + n.off_cs);
   // A search starts from prepared roots: only the root is expanded, with latent 0 (cnode.cpp:
   // 301-358); simulation k gives its leaf latent k + 1. (Nodes past the root's children may hold a
@@ -574,51 +874,59 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // ---- network residency: LDS layers, action rows, register layers and biases
   // activations and biases at static LDS addresses: lane-dependent addresses then share a few base
   // registers and fold the arrays' offsets into the instructions' immediates
-  __shared__ float4 s_acts[(kRHid + NR * (6 * kRHid + kRF + 2 * kRF + kRMaxA)) / 4];
+  // T1 / NL hold two rows even at NR = 1: the two candidates of a leaf tie run the dynamics
+  // layers side by side while the draw offset is still unknown (see the simulation loop)
+  __shared__ float4 s_acts[(kRHid + 4 * kRHid + NR * (4 * kRHid + kRF + 2 * kRF + kRMaxA)) / 4];
   __shared__ float4 s_bias[kResBiasFloats / 4];
-  float *X0 = reinterpret_cast<float *>(s_acts), *T1 = X0 + kRHid, *NL = T1 + NR * kRHid, *T2 = NL + NR * kRHid,
+  float *X0 = reinterpret_cast<float *>(s_acts), *T1 = X0 + kRHid, *NL = T1 + 2 * kRHid, *T2 = NL + 2 * kRHid,
         *T3 = T2 + NR * kRHid, *U2 = T3 + NR * kRHid, *U3 = U2 + NR * kRHid, *RHo = U3 + NR * kRHid,
         *HV = RHo + NR * kRF, *LG = HV + NR * 2 * kRF;
   float *ACT = smem + n.off_act;
   const float4 *WD1 = reinterpret_cast<const float4 *>(smem + n.off_wd1);
   const float4 *WD2 = reinterpret_cast<const float4 *>(smem + n.off_wd2);
   for (int e = tid; e < kRSlotsD * kRT; e += kRT) {
-    reinterpret_cast<float4 *>(smem + n.off_wd1)[e] = n.d[1][e];
-    reinterpret_cast<float4 *>(smem + n.off_wd2)[e] = n.d[2][e];
+    reinterpret_cast<float4 *>(smem + n.off_wd1)[e] = res_blk4(n, kRbD + 1)[e];
+    reinterpret_cast<float4 *>(smem + n.off_wd2)[e] = res_blk4(n, kRbD + 2)[e];
   }
-  for (int e = tid; e < A * kRHid; e += kRT) ACT[e] = n.act[e];
+  for (int e = tid; e < A * kRHid; e += kRT) ACT[e] = res_blk(n, kRbAct, A)[e];
   float4 wD3[kRSlotsD], wD4[kRSlotsD], wRS[kRSlotsS], wRH[kRSlotsRH], wVPH[kRSlotsVPH], wPO[1];
-  res_fetch<kRSlotsD>(n.d[3], wD3);
-  res_fetch<kRSlotsD>(n.d[4], wD4);
-  res_fetch<kRSlotsS>(n.rs, wRS);
-  res_fetch<kRSlotsRH>(n.rh, wRH);
-  res_fetch<kRSlotsVPH>(n.vph, wVPH);
-  res_fetch<kRSlotsPO>(n.po, wPO);
+  res_fetch<kRSlotsD>(res_blk4(n, kRbD + 3), wD3);
+  res_fetch<kRSlotsD>(res_blk4(n, kRbD + 4), wD4);
+  res_fetch<kRSlotsS>(res_blk4(n, kRbRS), wRS);
+  res_fetch<kRSlotsRH>(res_blk4(n, kRbRH), wRH);
+  res_fetch<kRSlotsVPH>(res_blk4(n, kRbVPH), wVPH);
+  res_fetch<kRSlotsPO>(res_blk4(n, kRbPO), wPO);
   const int cD = tid >> 1, pD = tid & 1, cRH = tid >> 3, pRH = tid & 7, cVP = tid >> 2, pVP = tid & 3, cPO = tid >> 3;
   // biases live in LDS (registers are the scarce resource): the bias blocks are contiguous
   float *BB = reinterpret_cast<float *>(s_bias);
-  for (int e = tid; e < kResBiasFloats; e += kRT) BB[e] = n.bd[e];
+  for (int e = tid; e < kResBiasFloats; e += kRT) BB[e] = res_blk(n, kRbBD, A)[e];
   const float *BD = BB, *BRH = BD + 6 * kRHid, *BVP = BRH + kRF, *BRS = BVP + 2 * kRF,
               *BVS = BRS + ((kRV + 3) & ~3), *BPO = BVS + ((kRV + 3) & ~3);
   // the streamed buffer: fc_dynamics[0] for the first simulation
   float4 P[kRSlotsS];
-  res_fetch<kRSlotsD>(n.d[0], P);
+  res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
 #pragma unroll
   for (int j = kRSlotsD; j < kRSlotsS; ++j) P[j] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   __syncthreads();
   const int players = s_players;
   const unsigned long long epoch = (unsigned long long)(uint32_t)s_epoch;
+  // the root's legal actions in registers (descend_small)
+  int rleg[2];
+  const int nleg = t.nlegal[0];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) rleg[j] = j < A ? t.legal[j] : 0;
   LZM_STAMP(10);
 
   for (int k = 0; k < p.S; ++k) {
     const uint32_t seed = s_seeds[k];
     if (!p.fast) seed_state_parallel(seed, s_pow, s_z0);
     // ---- selection, part 1: every expanded node's walk-independent pUCT terms (all threads)
-    // 0: descend_wave; 1 (default): terms + wave walk; 2: terms + lane walk; 3: descend_slice
-    const int smode = n.select_mode;
-    if (smode == 1 || smode == 2) {
+    // 0: descend_wave; 1: terms + wave walk; 2: terms + lane walk; 3: descend_slice; 4 (default):
+    // terms + descend_small when A <= 2, else as 1
+    const int smode = (n.select_mode == 4 && A > 2) ? 1 : n.select_mode;
+    if (smode == 1 || smode == 2 || smode == 4) {
       __syncthreads();  // the previous simulation's backup (wave 0) is complete
-      precompute_terms(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc);
+      precompute_terms(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, smode == 4 ? DEC : nullptr);
       __syncthreads();
     }
     LZM_STAMP(12);
@@ -631,7 +939,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           return o.x >> 1;
         };
         Descent d;
-        if (smode == 1) {
+        if (smode == 4) {
+          d = descend_a2<false>(t, NQ, DEC, CS, mm, s_vtp, players, rleg, nleg, draw, nullptr);
+        } else if (smode == 1) {
           d = descend_terms<false>(t, NQ, CS, mm, s_vtp, players, draw, nullptr);
         } else if (smode == 0) {
           d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp, p.disc, draw, nullptr);
@@ -644,7 +954,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         TieInfo ti;
         auto nodraw = [](int) -> uint32_t { return 0u; };
         Descent d;
-        if (smode == 1) {
+        if (smode == 4) {
+          WalkState ws;
+          d = descend_a2<true>(t, NQ, DEC, CS, mm, s_vtp, players, rleg, nleg, nodraw, &ti, nullptr, &ws);
+          LZM_STAMP(13);
+          if (lane == 0 && ti.status == 2) s_walk = ws;
+        } else if (smode == 1) {
           WalkState ws;
           d = descend_terms<true>(t, NQ, CS, mm, s_vtp, players, nodraw, &ti, nullptr, &ws);
           if (lane == 0 && ti.status == 2) s_walk = ws;
@@ -667,7 +982,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
     LZM_STAMP(0);
     const int status = s_status;
-    if (status == 2 && smode == 1) {
+    if (status == 2 && (smode == 1 || smode == 4)) {
       // the depth depends on a draw: look back now, then resume the walk at the tie with the draws
       // (exact semantics; the draws of the forced levels above the tie are never read)
       const int base = lookback_sum(p, k, g, G, epoch, s_part);
@@ -680,7 +995,11 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
           return glibc_draw(coef, npos, s_z0, base + level, diag);
         };
         WalkState ws = s_walk;
-        Descent d = descend_terms<false>(t, NQ, CS, s_mm, s_vtp, players, draw, nullptr, &ws);
+        Descent d;
+        if (smode == 4)
+          d = descend_a2<false>(t, NQ, DEC, CS, s_mm, s_vtp, players, rleg, nleg, draw, nullptr, &ws);
+        else
+          d = descend_terms<false>(t, NQ, CS, s_mm, s_vtp, players, draw, nullptr, &ws);
         if (lane == 0) {
           s_len[0] = d.len; s_x = d.x; s_act = d.action;
           __hip_atomic_store(&p.flags[(size_t)k * G + g], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
@@ -722,13 +1041,17 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // Rows: row r carries the network for action act_r. A tie between exactly two unexpanded
     // children (status 1) is evaluated speculatively for both (NR = 2) and resolved after the
     // network, when the predecessors' draw counts have long been published; other ties wait here.
-    bool spec = false;
+    // NR = 1, late draw: a two-way leaf tie runs the two dynamics layers for both candidates (two
+    // rows, shared weight reads) and only then waits for the look-back, which by then has mostly
+    // been published; the draw picks the next-latent row the rest of the network reads.
+    bool spec = false, late = false;
     int act_r[2];
     if (status == 1) {
       const unsigned long long m = s_tmask;
       const int parent = t.path[s_tlevel];
-      if (NR == 2 && __popcll(m) == 2) {
-        spec = true;
+      if (__popcll(m) == 2 && (NR == 2 || n.late_draw)) {
+        spec = NR == 2;
+        late = NR == 1;
         act_r[0] = legal_at(t, 0, parent, __ffsll((long long)m) - 1);
         act_r[1] = legal_at(t, 0, parent, __ffsll((long long)(m & (m - 1))) - 1);
       } else {
@@ -737,19 +1060,27 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __syncthreads();
       }
     }
-    if (!spec) act_r[0] = act_r[1] = s_act;
+    if (!spec && !late) act_r[0] = act_r[1] = s_act;
     LZM_SUBSTAMP(17);
     __builtin_amdgcn_sched_barrier(0);
-    res_fetch<kRSlotsD>(n.d[5], P);  // fc_prediction_common[1], three steps on
+    res_fetch<kRSlotsD>(res_blk4(n, kRbD + 5), P);  // fc_prediction_common[1], three steps on
     // + the action's one-hot row, bias, ReLU (muzero_model_mlp.py:188-190)
     if (pD == 0) {
 #pragma unroll
-      for (int r = 0; r < NR; ++r) T1[r * kRHid + cD] = fmaxf((z0 + ACT[act_r[r] * kRHid + cD]) + BD[cD], 0.0f);
+      for (int r = 0; r < 2; ++r)
+        if (r < NR || late) T1[r * kRHid + cD] = fmaxf((z0 + ACT[act_r[r] * kRHid + cD]) + BD[cD], 0.0f);
     }
     __syncthreads();
     LZM_SUBSTAMP(18);
     // ---- fc_dynamics[1] (LDS weights) + latent residual -> next latent
-    {
+    if (NR == 1 && late) {
+      float z[2];
+      dense128n<2>(T1, [&](int j) { return WD1[j * kRT + tid]; }, z);
+      if (pD == 0) {
+#pragma unroll
+        for (int r = 0; r < 2; ++r) NL[r * kRHid + cD] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[cD];
+      }
+    } else {
       float z[NR];
       dense128n<NR>(T1, [&](int j) { return WD1[j * kRT + tid]; }, z);
       if (pD == 0) {
@@ -758,14 +1089,21 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
     __syncthreads();
+    if (NR == 1 && late) {
+      const int base = lookback_sum(p, k, g, G, epoch, s_part);
+      if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+      __syncthreads();
+    }
+    // the next latent row the rest of the network reads (NR = 1: the late draw's pick)
+    const float *NLb = NL + ((NR == 1 && late && s_act == act_r[1]) ? kRHid : 0);
     LZM_STAMP(3);
     // The reward chain (fc_dynamics_2 -> reward head) and the prediction chain (prediction
     // common -> value / policy heads) both start from the next latent: one step per layer pair.
     // ---- [fc_dynamics_2[0] (LDS) | fc_prediction_common[0] (registers)]
     {
       float z2[NR], z6[NR];
-      dense128n<NR>(NL, [&](int j) { return WD2[j * kRT + tid]; }, z2);
-      dense128n<NR>(NL, [&](int j) { return wD4[j]; }, z6);
+      dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2);
+      dense128n<NR>(NLb, [&](int j) { return wD4[j]; }, z6);
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -781,7 +1119,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       float z7[NR], z3[NR];
       dense128n<NR>(U2, [&](int j) { return P[j]; }, z7);
       __builtin_amdgcn_sched_barrier(0);
-      res_fetch<kRSlotsS>(n.vs, P);  // the value support head, two steps on
+      res_fetch<kRSlotsS>(res_blk4(n, kRbVS), P);  // the value support head, two steps on
       dense128n<NR>(T2, [&](int j) { return wD3[j]; }, z3);
       if (pD == 0) {
 #pragma unroll
@@ -833,7 +1171,8 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      res_fetch<kRSlotsD>(n.d[0], P);  // fc_dynamics[0] for the next simulation
+      res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // fc_dynamics[0] for the next simulation
+      LZM_STAMP(15);
       support_decode_n<2 * NR>(zz, s_red, dec);
     }
     LZM_STAMP(6);
@@ -850,7 +1189,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // file the next latent (mcts_ctree.py:305): pool[k + 1][i]
     if (tid < kRHid / 4)
       reinterpret_cast<float4 *>(p.pool + ((size_t)(k + 1) * B + i) * kRHid)[tid] =
-          reinterpret_cast<const float4 *>(NL + row * kRHid)[tid];
+          reinterpret_cast<const float4 *>(NLb + row * kRHid)[tid];
     if (p.rec_x && tid == 0) {
       p.rec_x[(size_t)k * B + i] = s_x;
       p.rec_a[(size_t)k * B + i] = s_act;
@@ -869,6 +1208,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (players > 1)
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
       expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA);
+      LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
     }

@@ -18,7 +18,7 @@ from lightzero_amd import _lib  # noqa: E402
 
 NAMES = ["select", "offsets+lookback", "gather", "dynamics", "reward head+decode", "pred trunk",
          "value head+decode", "policy head", "file latents", "expand+backup", "stage-in", "write-back",
-         "select terms (res)"]
+         "select terms (res)", "walk (res, of select)", "expand (res, of e+b)", "support logits (res)"]
 
 
 def main():
@@ -47,7 +47,7 @@ def main():
     torch.cuda.synchronize()
     _lib.load().lzm_debug_phase_cycles(t.h, buf, 0)
     G = -(-a.envs // R)
-    per = np.array(buf[:13], dtype=np.float64) / (n * G)
+    per = np.array(buf[:16], dtype=np.float64) / (n * G)
     tot = per.sum()
     print(f"per workgroup per search (cycles), R={R}, G={G}, sims={a.sims}:")
     for name, c in zip(NAMES, per):
