@@ -27,7 +27,9 @@ __device__ __constant__ static const uint64_t kExp2fTab[32] = {
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
 
-__device__ inline float glibc_expf(float x) {
+// tab: the 2^(k/32) table (kExp2fTab, or a copy of it in LDS: a kernel that keeps global loads
+// in flight across the call then waits only for this LDS read, not for every outstanding load).
+__device__ inline float glibc_expf(float x, const uint64_t *tab = kExp2fTab) {
   const double kInvLn2N = 0x1.71547652b82fep+5;  // 32/ln2
   const double kShift = 0x1.8p+52;
   const double C0 = 0x1.c6af84b912394p-20, C1 = 0x1.ebfce50fac4f3p-13, C2 = 0x1.62e42ff0c52d6p-6;
@@ -44,7 +46,7 @@ __device__ inline float glibc_expf(float x) {
   uint64_t ki = (uint64_t)__double_as_longlong(kd);
   kd -= kShift;
   double r = __fma_rn(kInvLn2N, xd, -kd);
-  uint64_t t = kExp2fTab[ki % 32];
+  uint64_t t = tab[ki % 32];
   t += ki << 47;
   double s = __longlong_as_double((long long)t);
   double z = __fma_rn(C0, r, C1);

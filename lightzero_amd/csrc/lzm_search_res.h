@@ -211,11 +211,10 @@ __device__ __forceinline__ int a2_decision(float4 c0, float4 c1, int n) {
 // Same float operations in the same order as descend_wave, so the same bits.
 // nq[latent] = {total_q, total_v}; cs[child node] = {prior_score, value term, child latent, visited}
 // dec (nullable, A == 2): each node's walk-independent outcome (a2_decision) for descend_a2.
-__device__ inline void precompute_terms(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
-                                        float4 mm, int players, float disc, int *dec = nullptr) {
-  for (int L = threadIdx.x; L < nlat; L += kRT) {
-    const int n = lat2node[L];
-    if (n < 0) continue;
+// node_terms: one expanded node n (latent L), by the calling thread.
+__device__ inline void node_terms(const TreeView &t, int L, int n, float2 *nq, float4 *cs, float4 mm, int players,
+                                  float disc, int *dec) {
+  {
     const NodeStat s = t.stat[n];
     const int nleg = legal_n(t, 0, n);
     const int base = 1 + t.A * L;
@@ -249,6 +248,13 @@ __device__ inline void precompute_terms(const TreeView &t, int nlat, const int *
     }
     nq[L] = make_float2(total_q, __int_as_float(total_v));
     if (dec) dec[L] = (t.A == 2 && nleg >= 1) ? a2_decision(c01[0], c01[nleg > 1 ? 1 : 0], nleg) : 2;
+  }
+}
+__device__ inline void precompute_terms(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
+                                        float4 mm, int players, float disc, int *dec = nullptr) {
+  for (int L = threadIdx.x; L < nlat; L += kRT) {
+    const int n = lat2node[L];
+    if (n >= 0) node_terms(t, L, n, nq, cs, mm, players, disc, dec);
   }
 }
 
@@ -815,6 +821,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ WalkState s_walk;
   __shared__ float4 s_mm;
   __shared__ float s_red[12 * 2 * NR];
+  __shared__ uint64_t s_exptab[32];  // glibc_expf's table: expand reads it from LDS (no vmcnt wait
+                                     // on the weight prefetch in flight)
+  if (threadIdx.x < 32) s_exptab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __shared__ unsigned long long s_phase[64];
   if (p.phase && tid < 64) s_phase[tid] = 0ull;
 
@@ -1207,7 +1216,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       int vtp = s_vtp;
       if (players > 1)
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
-      expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA);
+      expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA, -1, s_exptab);
       LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);

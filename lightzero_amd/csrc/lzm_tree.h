@@ -451,7 +451,7 @@ __device__ inline void backup(const TreeView &t, int i, float4 *mm_ptr, int to_p
 // Bit-identical: pmax is a max (order-free), the prior denominator is summed in action order by a
 // readlane chain, every other quantity is per child.
 __device__ inline void expand_wave(const TreeView &t, int i, int leaf, int to_play, int latent, float reward,
-                                   const float *logits, int is_reset = -1) {
+                                   const float *logits, int is_reset = -1, const uint64_t *exptab = kExp2fTab) {
   const int lane = threadIdx.x & 63;
   const int A = t.A;
   if (lane == 0) {
@@ -465,7 +465,7 @@ __device__ inline void expand_wave(const TreeView &t, int i, int leaf, int to_pl
   const bool act = lane < A;
   const float lg = act ? logits[lane] : -INFINITY;
   const float pmax = fmaxf(kFloatMin, wave_max_dpp(lg));
-  const float e = act ? glibc_expf(lg - pmax) : 0.0f;
+  const float e = act ? glibc_expf(lg - pmax, exptab) : 0.0f;
   float sum = 0.0f;
   for (int a = 0; a < A; ++a) sum += readlane_f(e, a);
   if (act) {
