@@ -617,6 +617,80 @@ __device__ inline Descent descend_a2(const TreeView &t, const float2 *nq, const 
   return d;
 }
 
+// descend_a2 with the walk state cut to what a decided level needs: the root level runs through
+// descend_a2's general body (legal list, root mean-q rule); below it a level whose outcome is
+// known (dec 0 / 1) is a pointer chase plus the mean-q division for the next level, and any other
+// level (an unvisited child or a tie) hands the walk back to descend_a2 at that level's state
+// (same operations either way, so the same bits). vtp flips per level are applied at the end.
+template <bool CLASSIFY, typename Draw>
+__device__ inline Descent descend_a2f(const TreeView &t, const float2 *nq, const int *dec, const float4 *cs, float4 mm,
+                                      int vtp, int players, const int *rleg, int nleg, Draw draw, TieInfo *tie,
+                                      WalkState *at_tie = nullptr) {
+  const int lane = threadIdx.x & 63;
+  // root level: the general body for one level
+  WalkState w = walk_start(t, vtp);
+  if (w.lat < 0 || t.depth_cap <= 1) return descend_a2<CLASSIFY>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, draw, tie,
+                                                                  nullptr, at_tie);
+  {
+    const int dl = dec[w.lat];
+    if (dl >= 2) return descend_a2<CLASSIFY>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, draw, tie, nullptr, at_tie);
+    const float2 q = nq[w.lat];
+    const int action = rleg[dl];
+    const float4 c = cs[1 + 2 * w.lat + action];
+    const int tv = __float_as_int(q.y);
+    w.parent_q = tv > 0 ? q.x / (float)tv : (0.0f + q.x) / (float)(tv + 1);
+    if (lane == 0) {
+      t.path[0] = 0;
+      t.path_act[0] = action;
+      t.path[1] = 1 + 2 * w.lat + action;
+    }
+    w.node = 1 + 2 * w.lat + action;
+    w.last_action = action;
+    w.plat = w.lat;
+    w.lat = __float_as_int(c.z);
+    w.len = 1;
+    w.is_root = 0;
+  }
+  // non-root levels: two children at legal positions 0 / 1
+  int lat = w.lat, node = w.node, len = w.len, plat = w.plat, last_action = w.last_action;
+  float parent_q = w.parent_q;
+  const int dmax = t.depth_cap - 1;
+  int dl = 2;
+  while (lat >= 0 && len < dmax) {
+    dl = dec[lat];
+    if (dl >= 2) break;
+    const float2 q = nq[lat];
+    const float4 c = cs[1 + 2 * lat + dl];
+    const int nnode = 1 + 2 * lat + dl;
+    if (lane == 0) {
+      t.path_act[len] = dl;
+      t.path[len + 1] = nnode;
+    }
+    parent_q = (parent_q + q.x) / (float)(__float_as_int(q.y) + 1);
+    last_action = dl;
+    node = nnode;
+    plat = lat;
+    lat = __float_as_int(c.z);
+    ++len;
+  }
+  if (players > 1 && (len & 1)) vtp = (vtp == 1) ? 2 : 1;
+  if (lat >= 0 && len < dmax) {
+    // an undecided level: continue with the general body from this level's state
+    WalkState r;
+    r.node = node; r.lat = lat; r.len = len; r.plat = plat; r.last_action = last_action; r.is_root = 0;
+    r.vtp = vtp; r.parent_q = parent_q;
+    return descend_a2<CLASSIFY>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, draw, tie, &r, at_tie);
+  }
+  if (CLASSIFY) tie->status = 0;
+  Descent d;
+  d.len = len;
+  d.x = plat;
+  d.action = last_action;
+  d.vtp = vtp;
+  d.leaf = node;
+  return d;
+}
+
 // descend_terms by one lane: the reference's sequential tie-list scan (cselect_child,
 // cnode.cpp:551-596) over the precomputed terms, no cross-lane operations.
 template <bool CLASSIFY, typename Draw>
@@ -949,7 +1023,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         };
         Descent d;
         if (smode == 4) {
-          d = descend_a2<false>(t, NQ, DEC, CS, mm, s_vtp, players, rleg, nleg, draw, nullptr);
+          d = descend_a2f<false>(t, NQ, DEC, CS, mm, s_vtp, players, rleg, nleg, draw, nullptr);
         } else if (smode == 1) {
           d = descend_terms<false>(t, NQ, CS, mm, s_vtp, players, draw, nullptr);
         } else if (smode == 0) {
@@ -965,7 +1039,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         Descent d;
         if (smode == 4) {
           WalkState ws;
-          d = descend_a2<true>(t, NQ, DEC, CS, mm, s_vtp, players, rleg, nleg, nodraw, &ti, nullptr, &ws);
+          d = descend_a2f<true>(t, NQ, DEC, CS, mm, s_vtp, players, rleg, nleg, nodraw, &ti, &ws);
           LZM_STAMP(13);
           if (lane == 0 && ti.status == 2) s_walk = ws;
         } else if (smode == 1) {

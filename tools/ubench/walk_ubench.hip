@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       } else {
         Descent d = V == 0 ? descend_small<2, true>(t, nq, cs, mm, vtp, players, rleg, nleg, nodraw, &ti)
                   : V == 1 ? descend_a2<true, decltype(nodraw), 0>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, nodraw, &ti)
-                  : V == 3 ? descend_a2<true, decltype(nodraw), 1>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, nodraw, &ti)
+                  : V == 3 ? descend_a2f<true>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, nodraw, &ti)
                   : V == 4 ? descend_a2<true, decltype(nodraw), 4>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, nodraw, &ti,
                                                                    nullptr, nullptr, chain)
                            : descend_a2<true, decltype(nodraw), 5>(t, nq, dec, cs, mm, vtp, players, rleg, nleg, nodraw, &ti,
@@ -147,7 +147,6 @@ int main() {
   run<0, 1>(dcs, dnq, dc, dout, dpin, G, dmm, dgi);
   run<0, 2>(dcs, dnq, dc, dout, dpin, G, dmm, dgi);
   run<0, 3>(dcs, dnq, dc, dout, dpin, G, dmm, dgi);
-  run<0, 4>(dcs, dnq, dc, dout, dpin, G, dmm, dgi);
-  run<0, 5>(dcs, dnq, dc, dout, dpin, G, dmm, dgi);
+
   return 0;
 }
