@@ -290,6 +290,66 @@ def algorithmic_bytes(B, A, H, V, dbar):
     return {"traverse": trav, "decode_backprop": dec}
 
 
+def load_reference_ctree():
+    """The reference's own compiled ctree (LightZero ctree_muzero, built from its sources by
+    oracle/build_ref.sh into oracle/_ref; git-ignored, travels with the tree), or None. Only this
+    CPU-baseline leg loads it: it is the thing timed beside the GPU, never part of the product."""
+    import glob
+    import importlib.util
+    paths = sorted(glob.glob(os.path.join(REPO, "oracle", "_ref", "mz_tree*.so")))
+    if not paths:
+        return None
+    try:
+        spec = importlib.util.spec_from_file_location("mz_tree", paths[0])
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod
+    except (ImportError, OSError):
+        return None
+
+
+def cpu_reference_ctree_search(mod, B, S, model_cpu, secs, threads):
+    """The reference's search loop on the host (mcts_ctree.py:245-321 with device='cpu'): the
+    reference's compiled ctree (batch_traverse / batch_backpropagate on Python lists), the same
+    network on torch CPU, InverseScalarTransform. Returns (sims/s, searches run, seconds)."""
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    obs = torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32))
+    support = torch.arange(-300, 301, dtype=torch.float64).unsqueeze(0)
+
+    def inv(logits):
+        p = torch.softmax(logits, dim=1)
+        v = p.mul_(support).sum(1, keepdim=True)
+        tmp = (torch.sqrt(1 + 4 * 0.001 * (torch.abs(v) + 1 + 0.001)) - 1) / (2 * 0.001)
+        return (torch.sign(v) * (tmp * tmp - 1)).float()
+
+    legal = [[0, 1] for _ in range(B)]
+    to_play = [-1] * B
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            out = model_cpu.initial_inference(obs)
+            roots = mod.Roots(B, legal)
+            noises = rng.dirichlet([0.3, 0.3], size=B).astype(np.float32).tolist()
+            roots.prepare(0.25, noises, [0.0] * B, out.policy_logits.numpy().tolist(), to_play)
+            pool = [out.latent_state.numpy()]
+            mms = mod.MinMaxStatsList(B)
+            mms.set_delta(0.01)
+            for k in range(S):
+                results = mod.ResultsWrapper(num=B)
+                x, y, a, vtp = mod.batch_traverse(roots, 19652, 1.25, 0.997, mms, results, to_play)
+                lat = torch.from_numpy(np.asarray([pool[ix][iy] for ix, iy in zip(x, y)]))
+                o = model_cpu.recurrent_inference(lat, torch.from_numpy(np.asarray(a)).long())
+                pool.append(o.latent_state.numpy())
+                mod.batch_backpropagate(k + 1, 0.997, inv(o.reward).numpy().reshape(-1).tolist(),
+                                        inv(o.value).numpy().reshape(-1).tolist(), o.policy_logits.numpy().tolist(),
+                                        mms, results, vtp)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return n * B * S / el, n, el
+
+
 def cpu_reference_search(B, S, model_cpu, secs, threads):
     """The reference's architecture on the host: oracle ctree (restated cnode.cpp) + the same
     network on torch CPU + InverseScalarTransform + list glue, as mcts_ctree.py:228-321 runs
@@ -414,10 +474,18 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cores = min(16, os.cpu_count() or 1)
             model_cpu = build_model(torch.device("cpu"), args.zero_heads, seed=0)
-            v, n, secs = cpu_reference_search(B, S, model_cpu, args.cpu_baseline_secs, cores)
-            cpu = {"value": round(v, 1), "unit": "sims/s", "cores": cores, "kind": "port",
-                   "sample": f"{n} full searches (B={B}, S={S}, same MLP on torch-CPU, oracle ctree restatement, "
-                             f"{secs:.1f}s)"}
+            ref = load_reference_ctree()
+            if ref is not None:
+                # the reference's compiled ctree (single-threaded, as in LightZero) driving the same
+                # network on `cores` torch threads
+                v, n, secs = cpu_reference_ctree_search(ref, B, S, model_cpu, args.cpu_baseline_secs, cores)
+                kind, what = "reference", "LightZero ctree_muzero compiled from the reference sources"
+            else:
+                v, n, secs = cpu_reference_search(B, S, model_cpu, args.cpu_baseline_secs, cores)
+                kind, what = "port", "oracle ctree restatement"
+            cpu = {"value": round(v, 1), "unit": "sims/s", "cores": cores, "kind": kind,
+                   "sample": f"{n} full searches (B={B}, S={S}, mcts_ctree.py search loop, {what}, same MLP on "
+                             f"torch-CPU with {cores} threads, {secs:.1f}s)"}
     if rank == 0:
         line = {"metric": "MCTS simulations/sec (whole node), 256 parallel envs x 50 sims/step",
                 "value": round(value, 1), "unit": "sims/s", "n_gpus": world, "steps": args.steps,
