@@ -1,0 +1,17 @@
+# GPU: the round's profile set for the fused bench (usage: bash tools/profile_round.sh r01)
+#   kernel trace + stats of the default bench command, the bench line, and PMC passes
+#   (each counter group in its own pass, kernel-trace only: FETCH_SIZE, WRITE_SIZE, TCC hit/miss)
+set -e
+tag=${1:-r01}
+out=gpurun_out/prof_$tag
+mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o fused --output-format csv -- \
+  python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $out/bench_traced.log 2>&1
+i=0
+for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $out/pmc_$i -o pmc --output-format csv -- \
+    python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $out/pmc_$i.log 2>&1
+done
+timeout -k 10 300 python3 bench.py > $out/bench.json 2>&1
