@@ -429,6 +429,8 @@ def main():
     dsum = step.last[0].sum(dim=1)
     assert bool((dsum == S).all()), "visit counts do not sum to num_simulations"
     tie_errors = step.tree().check_errors()
+    # fused kernels: {integrity errors, ties resolved serially, ties whose depth was published early}
+    sdiag = step.tree().search_diagnostics()[:3] if args.path == "fused" else None
 
     roofline = None
     cpu = None
@@ -498,7 +500,7 @@ def main():
                            "hip_graph": (args.step != "python") if args.path == "fused" else bool(args.graph),
                            "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
-                "tie_stream_errors": int(sum(tie_errors)), "roofline": roofline, "cpu_baseline": cpu}
+                "tie_stream_errors": int(sum(tie_errors)), "search_diag": sdiag, "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

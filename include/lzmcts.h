@@ -158,8 +158,10 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
  * network: 1 = network-resident (search_res_kernel, lzm_search_res.h: the config-2 shape with one
  * root per workgroup), 0 = weight-streaming (search_mlp_kernel). Host-only, no GPU work. */
 int lzm_search_mlp_kind(int B, int actions, int hidden, int head_hidden, int support, int res_dynamics);
-/* int32[2]: {look-back spin timeouts (must stay 0), slices resolved serially (ties that reached
- * an expanded child)} accumulated over the handle's fused searches. */
+/* int32[4]: {integrity errors: look-back spin timeouts and speculation mismatches (must stay 0),
+ * slices resolved serially (ties that reached an expanded child, depth unknown until the draw),
+ * such ties whose depth was published early (every draw outcome gives the same depth),
+ * speculation mismatches (must stay 0)} accumulated over the handle's fused searches. */
 int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream);
 
 /* Post-search integrity check (host-synchronous on `stream`): the sticky error counters of every

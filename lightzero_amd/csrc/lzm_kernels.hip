@@ -1425,8 +1425,8 @@ int ensure_flags(lzm_handle *h, int sims, int G) {
     LZM_HIP(hipMalloc(&h->epoch, 2 * sizeof(uint32_t)));
     const uint32_t init[2] = {1u, 0u};
     LZM_HIP(hipMemcpy(h->epoch, init, sizeof(init), hipMemcpyHostToDevice));
-    LZM_HIP(hipMalloc(&h->search_diag, 2 * sizeof(int32_t)));
-    LZM_HIP(hipMemset(h->search_diag, 0, 2 * sizeof(int32_t)));
+    LZM_HIP(hipMalloc(&h->search_diag, 4 * sizeof(int32_t)));
+    LZM_HIP(hipMemset(h->search_diag, 0, 4 * sizeof(int32_t)));
   }
   if (h->flag_sims >= sims) return LZM_OK;
   dfree(h->lb_flags);
@@ -1746,6 +1746,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
       // row instead of waiting for the look-back (measured slower: every simulation pays the row)
       const char *sl = getenv("LZM_RES_LATE");
       n.late_draw = sl ? atoi(sl) : 1;
+      const char *sd = getenv("LZM_RES_SPEC_DEPTH");
+      n.spec_depth = sd ? atoi(sd) : 1;
       const char *se = getenv("LZM_RES_SPEC");
       const bool spec = !fast && se && atoi(se) == 1;
       // production: selection mode, RNG and stamps fixed at compile time (modes 1 and 4); phase
@@ -1753,7 +1755,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
       const int md = (n.select_mode == 4 && A > 2) ? 1 : n.select_mode;
       void (*fn)(SearchArgs, ResNet) =
           spec                  ? search_res_kernel<2, 1, 0, false>
-          : (md != 1 && md != 4) ? search_res_kernel<1, -1, -1, true>
+          : (md != 1 && md != 4) || !n.spec_depth ? search_res_kernel<1, -1, -1, true>
           : q.phase             ? (md == 4 ? search_res_kernel<1, 4, -1, true> : search_res_kernel<1, 1, -1, true>)
           : md == 4             ? (fast ? search_res_kernel<1, 4, 1, false> : search_res_kernel<1, 4, 0, false>)
                                 : (fast ? search_res_kernel<1, 1, 1, false> : search_res_kernel<1, 1, 0, false>);
@@ -1824,10 +1826,10 @@ int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset) {
 int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream) {
   if (!h || !out) return LZM_ERR_ARG;
   if (!h->search_diag) {
-    LZM_HIP(hipMemsetAsync(out, 0, 2 * sizeof(int32_t), (hipStream_t)stream));
+    LZM_HIP(hipMemsetAsync(out, 0, 4 * sizeof(int32_t), (hipStream_t)stream));
     return LZM_OK;
   }
-  LZM_HIP(hipMemcpyAsync(out, h->search_diag, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  LZM_HIP(hipMemcpyAsync(out, h->search_diag, 4 * sizeof(int32_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return LZM_OK;
 }
 

@@ -66,6 +66,8 @@ struct ResNet {
   int select_mode;  // LZM_RES_SELECT (experiments): how the walk runs, see the simulation loop
   int late_draw;    // NR = 1: two-way leaf ties run the dynamics layers for both candidates before the
                     // look-back wait (LZM_RES_LATE, default 1)
+  int spec_depth;   // status-2 ties: publish the depth early when every draw outcome gives the same
+                    // depth (speculate_depth_a2; LZM_RES_SPEC_DEPTH, default 1)
 };
 
 // floats of the bias blocks ([6][128] D, [32] RH, [64] VPH, [604] RS, [604] VS, [32] PO)
@@ -617,6 +619,60 @@ __device__ inline Descent descend_a2(const TreeView &t, const float2 *nq, const 
   return d;
 }
 
+// Depth speculation for a classification walk stopped at a tie between children of which one is
+// expanded (status 2, A == 2): lane `pattern` continues the walk from the tie's state taking, at the
+// i-th tie on its way, the child that draw parity bit i of `pattern` selects (rr % 2 picks legal
+// position 0 or 1); returns that walk's depth (Descent::len), or -1 when it meets more than 6 ties.
+// If all 64 patterns give one depth, the root's draw count is known before any of its draw values:
+// it is published at once and the path is resolved after the look-back (same walk, same bits).
+// Same per-level operations as descend_a2.
+__device__ inline int speculate_depth_a2(const TreeView &t, const float2 *nq, const int *dec, const float4 *cs,
+                                         float4 mm, const int *rleg, int nleg, const WalkState &w, int pattern) {
+  const float delta = mm.x - mm.y;
+  const bool scale = delta > 0;
+  const float div = (delta < mm.z) ? mm.z : delta;
+  const float lo = mm.y;
+  int node = w.node, len = w.len, lat = w.lat, used = 0;
+  bool is_root = w.is_root;
+  float parent_q = w.parent_q;
+  const int dmax = t.depth_cap - 1;
+  while (lat >= 0 && len < dmax) {
+    const bool root = node == 0;
+    const int a0 = root ? rleg[0] : 0, a1 = root ? rleg[1] : 1, n = root ? nleg : 2;
+    const int base = 1 + 2 * lat;
+    const float4 c0 = cs[base + a0];
+    const float4 c1 = cs[base + (n > 1 ? a1 : a0)];
+    const float2 q = nq[lat];
+    const int dl = dec[lat];
+    const int total_v = __float_as_int(q.y);
+    const float mean_q = (is_root && total_v > 0) ? q.x / (float)total_v : (parent_q + q.x) / (float)(total_v + 1);
+    int jsel = dl;
+    bool tie2 = dl == 3;
+    if (dl == 2) {
+      float vu = mm_norm_fixed(scale, lo, div, mean_q);
+      if (vu < 0) vu = 0;
+      if (vu > 1) vu = 1;
+      const float s0 = c0.x + (__float_as_int(c0.w) ? c0.y : vu);
+      const float s1 = c1.x + (__float_as_int(c1.w) ? c1.y : vu);
+      const float M = fmaxf(s0, s1);
+      jsel = (s0 == M) ? 0 : 1;
+      tie2 = jsel == 0 && s1 >= M - 0.000001f;
+    }
+    if (tie2) {
+      if (__float_as_int(c0.z) < 0 && __float_as_int(c1.z) < 0) return len + 1;  // either way a leaf
+      if (used == 6) return -1;
+      jsel = (pattern >> used) & 1;
+      ++used;
+    }
+    is_root = false;
+    parent_q = mean_q;
+    node = base + (jsel ? a1 : a0);
+    lat = __float_as_int(jsel ? c1.z : c0.z);
+    ++len;
+  }
+  return len;
+}
+
 // descend_a2 with the walk state cut to what a decided level needs: the root level runs through
 // descend_a2's general body (legal list, root mean-q rule); below it a level whose outcome is
 // known (dec 0 / 1) is a pointer chase plus the mean-q division for the next level, and any other
@@ -881,6 +937,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (!STAMPS) p.phase = nullptr;
   if (RNG >= 0) p.fast = RNG;
   if (SMODE >= 0) n.select_mode = SMODE;
+  if (SMODE == 4 && RNG == 0 && !STAMPS) n.spec_depth = 1;  // production parity kernel
   extern __shared__ float4 smem4[];
   float *smem = reinterpret_cast<float *>(smem4);
   const int tid = threadIdx.x, g = blockIdx.x, G = gridDim.x, lane = tid & 63, wid = tid >> 6;
@@ -1065,12 +1122,25 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
     LZM_STAMP(0);
     const int status = s_status;
-    if (status == 2 && (smode == 1 || smode == 4)) {
+    if (__builtin_expect(status == 2 && (smode == 1 || smode == 4), 0)) {
       // the depth depends on a draw: look back now, then resume the walk at the tie with the draws
-      // (exact semantics; the draws of the forced levels above the tie are never read)
+      // (exact semantics; the draws of the forced levels above the tie are never read). First
+      // (A == 2), when every draw outcome gives the same depth (speculate_depth_a2), publish it at
+      // once so that the roots after this one need not wait for this root's look-back (st = 3).
+      int st = 2, d0 = -1;
+      if (smode == 4 && n.spec_depth && wid == 0) {
+        const int de = speculate_depth_a2(t, NQ, DEC, CS, s_mm, rleg, nleg, s_walk, lane);
+        d0 = __builtin_amdgcn_readfirstlane(de);
+        if (d0 >= 0 && __ballot(de != d0) == 0ull) {
+          st = 3;
+          if (lane == 0)
+            __hip_atomic_store(&p.flags[(size_t)k * G + g], (epoch << 32) | (unsigned)d0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
       const int base = lookback_sum(p, k, g, G, epoch, s_part);
       if (wid == 0) {
-        if (lane == 0) atomicAdd(p.diag + 1, 1);
+        if (lane == 0) atomicAdd(p.diag + (st == 2 ? 1 : 2), 1);
         const uint32_t *coef = p.coef;
         const int npos = p.coef_positions;
         int32_t *diag = p.diag;
@@ -1084,9 +1154,15 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         else
           d = descend_terms<false>(t, NQ, CS, s_mm, s_vtp, players, draw, nullptr, &ws);
         if (lane == 0) {
+          if (st == 3 && d.len != d0) {
+            // cannot happen (the speculation walked every draw outcome); counted as an integrity error
+            atomicAdd(p.diag, 1);
+            atomicAdd(p.diag + 3, 1);
+          }
           s_len[0] = d.len; s_x = d.x; s_act = d.action;
-          __hip_atomic_store(&p.flags[(size_t)k * G + g], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
+          if (st == 2)
+            __hip_atomic_store(&p.flags[(size_t)k * G + g], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       __syncthreads();

@@ -187,7 +187,7 @@ class DeviceTree:
         return list(out)
 
     def search_diagnostics(self):
-        out = torch.zeros(2, dtype=torch.int32, device=self.device)
+        out = torch.zeros(4, dtype=torch.int32, device=self.device)
         call("lzm_search_diagnostics", self.h, ptr(out), stream_ptr())
         return out.cpu().tolist()
 

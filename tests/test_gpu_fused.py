@@ -112,12 +112,20 @@ def test_fused_roots_per_workgroup(case, roots, monkeypatch):
 # the config-2 shape takes the network-resident kernel (lzm_search_res.h); the same cases through
 # the weight-streaming kernel (LZM_FUSED_RES=0) and the speculative two-row variant (LZM_RES_SPEC=1)
 @pytest.mark.parametrize("env", ["LZM_FUSED_RES=0", "LZM_RES_SPEC=1", "LZM_RES_SELECT=0", "LZM_RES_SELECT=2",
-                                 "LZM_RES_SELECT=3"])
+                                 "LZM_RES_SELECT=3", "LZM_RES_SPEC_DEPTH=0"])
 @pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[4]], ids=_case_id)
 def test_fused_kernel_variants(case, env, monkeypatch):
     k, v = env.split("=")
     monkeypatch.setenv(k, v)
     check_tree_exact(case)
+
+
+def test_zero_heads_depth_speculation_exercised():
+    """Zero-init heads tie between visited children often: the resident kernel publishes such a
+    root's depth early when every draw outcome gives the same depth (speculate_depth_a2), and the
+    tree stays bit-exact with the oracle (check_tree_exact)."""
+    r = check_tree_exact(CASES[1])
+    assert r["diag"][2] > 0, "no tie was resolved through depth speculation"
 
 
 def test_resident_kernel_serves_config2():
@@ -132,7 +140,8 @@ def check_tree_exact(case):
     B, S, A, H, zero, players, fast = case
     r = fused_search(B, S, A, H, zero, players, fast, seed=B + S + A)
     rec = r["rec"]
-    assert r["diag"][0] == 0, "look-back spin timeout"
+    assert r["diag"][0] == 0, "look-back spin timeout or depth speculation mismatch"
+    assert r["diag"][3] == 0, "depth speculation mismatch"
     ot = OracleTree(B, A, S, fast_rng=fast)
     ot.set_delta(VDM)
     ot.prepare(NOISE_W, r["noises"], np.zeros(B, np.float32), r["logits0"], r["to_play"])
@@ -145,6 +154,7 @@ def check_tree_exact(case):
     assert np.array_equal(r["dist"], ot.distributions())
     assert np.array_equal(r["values"], ot.values())
     assert np.array_equal(r["traj"], ot.trajectories(S + 2))
+    return r
 
 
 # support 601 decodes from registers across the workgroup; support 21 (< 512 lanes) through LDS
