@@ -1740,8 +1740,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     if (lds) {
       res_net(n, weights + round4(kernel_layout(kls, nkl, lay_w, lay_b)), A);
       const char *sm = getenv("LZM_RES_SELECT");
-      // measured: 4 < 1 < 0 < 2 < 3; 4 is 1 with descend_small for A <= 2
-      n.select_mode = sm ? atoi(sm) : (A <= 2 ? 4 : 1);
+      // measured: 4 < 1 < 0 < 2 < 3; 4 is 1 with the two-action walk for A == 2
+      n.select_mode = sm ? atoi(sm) : (A == 2 ? 4 : 1);
       // LZM_RES_SPEC=1 (parity mode): evaluate two-way leaf ties speculatively as a second network
       // row instead of waiting for the look-back (measured slower: every simulation pays the row)
       const char *sl = getenv("LZM_RES_LATE");
@@ -1752,7 +1752,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
       const bool spec = !fast && se && atoi(se) == 1;
       // production: selection mode, RNG and stamps fixed at compile time (modes 1 and 4); phase
       // timing compiles the stamps in; the other selection modes (experiments) read it at run time
-      const int md = (n.select_mode == 4 && A > 2) ? 1 : n.select_mode;
+      const int md = (n.select_mode == 4 && A != 2) ? 1 : n.select_mode;
       void (*fn)(SearchArgs, ResNet) =
           spec                  ? search_res_kernel<2, 1, 0, false>
           : (md != 1 && md != 4) || !n.spec_depth ? search_res_kernel<1, -1, -1, true>

@@ -144,12 +144,12 @@ __host__ __device__ inline void res_source(int b, size_t d, int A, int *layer, i
 }
 
 // NS float4 slots of a resident block into registers (buffer loads: the slot offset is scalar)
-template <int NS>
+template <int NS, int J0 = 0, int J1 = NS>
 __device__ __forceinline__ void res_fetch(const float4 *blk, float4 *dst) {
   const __amdgpu_buffer_rsrc_t r = wave_rsrc(blk, NS * kRT * 16);
   const int vo = (int)threadIdx.x * 16;
 #pragma unroll
-  for (int j = 0; j < NS; ++j) {
+  for (int j = J0; j < J1; ++j) {
     const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, vo, j * kRT * 16, 0);
     dst[j] = make_float4(v.x, v.y, v.z, v.w);
   }
@@ -257,6 +257,65 @@ __device__ inline void precompute_terms(const TreeView &t, int nlat, const int *
   for (int L = threadIdx.x; L < nlat; L += kRT) {
     const int n = lat2node[L];
     if (n >= 0) node_terms(t, L, n, nq, cs, mm, players, disc, dec);
+  }
+}
+
+// node_terms for two actions, written for few LDS round trips: a child's slot depends on the latent
+// only (1 + 2 L + legal position; the root, latent 0, takes its legal actions from registers), so
+// both children's records are read with the latent -> node map, the node's visit count next, then
+// the pb_c table row; every read is unconditional and the branches are selects. Same float
+// operations in the same order as node_terms (so the same bits), and also dec[L].
+__device__ inline void precompute_terms_a2(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
+                                           float4 mm, int players, float disc, int *dec, const int *rleg,
+                                           int nleg_root) {
+  for (int L = threadIdx.x; L < nlat; L += kRT) {
+    const int n = lat2node[L];
+    const bool root = L == 0;
+    const int nleg = root ? nleg_root : 2;
+    const int base = 1 + 2 * L;
+    const int c0 = base + (root ? rleg[0] : 0);
+    const int c1 = base + (root ? rleg[nleg > 1 ? 1 : 0] : 1);
+    const NodeStat s0 = t.stat[c0], s1 = t.stat[c1];
+    const float v0 = t.val[c0], v1 = t.val[c1];
+    const int l0 = t.meta[c0].latent, l1 = t.meta[c1].latent;
+    if (n < 0) continue;
+    int N = t.stat[n].visit - 1;
+    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
+    const float2 Lx = t.lut[N];
+    const int row = N * (N + 1) / 2;
+    const bool p0 = t.pbt && s0.visit <= N, p1 = t.pbt && s1.visit <= N;
+    const float f0 = p0 ? t.pbt[row + s0.visit] : (Lx.y / (float)(s0.visit + 1));
+    const float f1 = p1 ? t.pbt[row + s1.visit] : (Lx.y / (float)(s1.visit + 1));
+    float total_q = 0.0f;
+    int total_v = 0;
+    float vv0 = 0.0f, vv1 = 0.0f;
+    if (s0.visit > 0) {
+      total_q += s0.reward + disc * v0;
+      ++total_v;
+      float v = (players == 1) ? s0.reward + disc * v0 : s0.reward + disc * (-v0);
+      v = mm_normalize(mm, v);
+      if (v < 0) v = 0;
+      if (v > 1) v = 1;
+      vv0 = v;
+    }
+    if (nleg > 1 && s1.visit > 0) {
+      total_q += s1.reward + disc * v1;
+      ++total_v;
+      float v = (players == 1) ? s1.reward + disc * v1 : s1.reward + disc * (-v1);
+      v = mm_normalize(mm, v);
+      if (v < 0) v = 0;
+      if (v > 1) v = 1;
+      vv1 = v;
+    }
+    float pb0 = Lx.x, pb1 = Lx.x;
+    pb0 *= f0;
+    pb1 *= f1;
+    const float4 t0 = make_float4(pb0 * s0.prior, vv0, __int_as_float(l0), __int_as_float(s0.visit > 0 ? 1 : 0));
+    const float4 t1 = make_float4(pb1 * s1.prior, vv1, __int_as_float(l1), __int_as_float(s1.visit > 0 ? 1 : 0));
+    if (nleg > 0) cs[c0] = t0;
+    if (nleg > 1) cs[c1] = t1;
+    nq[L] = make_float2(total_q, __int_as_float(total_v));
+    dec[L] = nleg >= 1 ? a2_decision(t0, nleg > 1 ? t1 : t0, nleg) : 2;
   }
 }
 
@@ -826,14 +885,21 @@ __device__ inline Descent descend_terms_lane(const TreeView &t, const float2 *nq
 }
 
 // NR rows of a 128 x 128 layer (inputs x + r * 128): each weight read once for all rows.
-template <int NR, typename WF>
-__device__ __forceinline__ void dense128n(const float *x, WF w, float *z) {
+struct NoSide {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+// side(j) runs at the top of slot j: a weight prefetch spread over the layer, one or two buffer
+// loads per slot, instead of a burst that stalls the wave at issue (the texture path takes a
+// 1 KiB wave-load per 16 cycles and four waves share it)
+template <int NR, typename WF, typename SF = NoSide>
+__device__ __forceinline__ void dense128n(const float *x, WF w, float *z, SF side = SF()) {
   const int p = threadIdx.x & 1;
   float a[NR][4];
 #pragma unroll
   for (int r = 0; r < NR; ++r) a[r][0] = a[r][1] = a[r][2] = a[r][3] = 0.0f;
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
+    side(j);
     const float4 q = w(j);
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
@@ -1063,10 +1129,13 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // ---- selection, part 1: every expanded node's walk-independent pUCT terms (all threads)
     // 0: descend_wave; 1: terms + wave walk; 2: terms + lane walk; 3: descend_slice; 4 (default):
     // terms + descend_small when A <= 2, else as 1
-    const int smode = (n.select_mode == 4 && A > 2) ? 1 : n.select_mode;
+    const int smode = (n.select_mode == 4 && A != 2) ? 1 : n.select_mode;
     if (smode == 1 || smode == 2 || smode == 4) {
       __syncthreads();  // the previous simulation's backup (wave 0) is complete
-      precompute_terms(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, smode == 4 ? DEC : nullptr);
+      if (smode == 4)
+        precompute_terms_a2(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, DEC, rleg, nleg);
+      else
+        precompute_terms(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, smode == 4 ? DEC : nullptr);
       __syncthreads();
     }
     LZM_STAMP(12);
@@ -1222,7 +1291,6 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (!spec && !late) act_r[0] = act_r[1] = s_act;
     LZM_SUBSTAMP(17);
     __builtin_amdgcn_sched_barrier(0);
-    res_fetch<kRSlotsD>(res_blk4(n, kRbD + 5), P);  // fc_prediction_common[1], three steps on
     // + the action's one-hot row, bias, ReLU (muzero_model_mlp.py:188-190)
     if (pD == 0) {
 #pragma unroll
@@ -1261,7 +1329,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // ---- [fc_dynamics_2[0] (LDS) | fc_prediction_common[0] (registers)]
     {
       float z2[NR], z6[NR];
-      dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2);
+      // fc_prediction_common[1] into P (used by the next pair), one slot per slot of this layer
+      const __amdgpu_buffer_rsrc_t rd5 = wave_rsrc(res_blk4(n, kRbD + 5), kRSlotsD * kRT * 16);
+      dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2, [&](int j) {
+        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rd5, tid * 16, j * kRT * 16, 0);
+        P[j] = make_float4(v.x, v.y, v.z, v.w);
+      });
       dense128n<NR>(NLb, [&](int j) { return wD4[j]; }, z6);
       if (pD == 0) {
 #pragma unroll
@@ -1277,9 +1350,21 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     {
       float z7[NR], z3[NR];
       dense128n<NR>(U2, [&](int j) { return P[j]; }, z7);
+      // the value support head into P (two steps on): half before this layer, half after it (a
+      // 20-load burst stalls the wave at issue)
       __builtin_amdgcn_sched_barrier(0);
-      res_fetch<kRSlotsS>(res_blk4(n, kRbVS), P);  // the value support head, two steps on
+      const __amdgpu_buffer_rsrc_t rvs = wave_rsrc(res_blk4(n, kRbVS), kRSlotsS * kRT * 16);
+      auto fetch_vs = [&](int q0, int q1) {
+#pragma unroll
+        for (int q = q0; q < q1; ++q) {
+          const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rvs, tid * 16, q * kRT * 16, 0);
+          P[q] = make_float4(v.x, v.y, v.z, v.w);
+        }
+      };
+      fetch_vs(0, kRSlotsS / 2);
       dense128n<NR>(T2, [&](int j) { return wD3[j]; }, z3);
+      __builtin_amdgcn_sched_barrier(0);
+      fetch_vs(kRSlotsS / 2, kRSlotsS);
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -1330,7 +1415,6 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __builtin_amdgcn_sched_barrier(0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // fc_dynamics[0] for the next simulation
       LZM_STAMP(15);
       support_decode_n<2 * NR>(zz, s_red, dec);
     }
@@ -1359,6 +1443,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       p.rec_dec[((size_t)k * B + i) * 2 + 1] = vdec;
       for (int a = 0; a < A; ++a) p.rec_logits[((size_t)k * B + i) * A + a] = LG[row * kRMaxA + a];
     }
+    // fc_dynamics[0] for the next simulation: waves 1-3 fetch now (they idle through the expand
+    // and backup), wave 0 after its backup
+    if (wid != 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
     // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500), wave 0
     if (wid == 0) {
       const int len = s_len[0];
@@ -1370,6 +1457,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
+      res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
     }
     LZM_STAMP(9);
   }
