@@ -157,19 +157,30 @@ __device__ __forceinline__ void res_fetch(const float4 *blk, float4 *dst) {
 
 // Partial dot product of 4*NJ consecutive inputs x4[0..NJ) with weights w(j): four independent
 // FMA chains (k mod 4), summed as (c0 + c1) + (c2 + c3).
+// (LZM_PK_FMA: the chains in pairs, v_pk_fma_f32 — each half rounds exactly like v_fma_f32)
+#ifndef LZM_PK_FMA
+#define LZM_PK_FMA 1
+#endif
+typedef float lzm_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void fma4(float4 v, float4 q, float *a) {
+#if LZM_PK_FMA
+  lzm_f2 lo = {a[0], a[1]}, hi = {a[2], a[3]};
+  lo = __builtin_elementwise_fma((lzm_f2){v.x, v.y}, (lzm_f2){q.x, q.y}, lo);
+  hi = __builtin_elementwise_fma((lzm_f2){v.z, v.w}, (lzm_f2){q.z, q.w}, hi);
+  a[0] = lo.x; a[1] = lo.y; a[2] = hi.x; a[3] = hi.y;
+#else
+  a[0] = __fmaf_rn(v.x, q.x, a[0]);
+  a[1] = __fmaf_rn(v.y, q.y, a[1]);
+  a[2] = __fmaf_rn(v.z, q.z, a[2]);
+  a[3] = __fmaf_rn(v.w, q.w, a[3]);
+#endif
+}
 template <int NJ, typename WF>
 __device__ __forceinline__ float dot4(const float4 *x4, WF w) {
-  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+  float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const float4 v = x4[j];
-    const float4 q = w(j);
-    a0 = __fmaf_rn(v.x, q.x, a0);
-    a1 = __fmaf_rn(v.y, q.y, a1);
-    a2 = __fmaf_rn(v.z, q.z, a2);
-    a3 = __fmaf_rn(v.w, q.w, a3);
-  }
-  return (a0 + a1) + (a2 + a3);
+  for (int j = 0; j < NJ; ++j) fma4(x4[j], w(j), a);
+  return (a[0] + a[1]) + (a[2] + a[3]);
 }
 
 // Full pre-activation of this lane's column of a 128 x 128 layer (both lanes of a pair get it).
@@ -902,13 +913,7 @@ __device__ __forceinline__ void dense128n(const float *x, WF w, float *z, SF sid
     side(j);
     const float4 q = w(j);
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const float4 v = reinterpret_cast<const float4 *>(x + r * kRHid)[16 * p + j];
-      a[r][0] = __fmaf_rn(v.x, q.x, a[r][0]);
-      a[r][1] = __fmaf_rn(v.y, q.y, a[r][1]);
-      a[r][2] = __fmaf_rn(v.z, q.z, a[r][2]);
-      a[r][3] = __fmaf_rn(v.w, q.w, a[r][3]);
-    }
+    for (int r = 0; r < NR; ++r) fma4(reinterpret_cast<const float4 *>(x + r * kRHid)[16 * p + j], q, a[r]);
   }
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
