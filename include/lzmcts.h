@@ -163,6 +163,9 @@ int lzm_search_mlp_kind(int B, int actions, int hidden, int head_hidden, int sup
  * such ties whose depth was published early (every draw outcome gives the same depth),
  * speculation mismatches (must stay 0)} accumulated over the handle's fused searches. */
 int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream);
+/* Diagnostics: uint64[n] (n <= 1024), shader-clock cycles workgroup g of the resident kernel spent
+ * waiting in the parity-mode look-back, summed over launches; zeros unless LZM_PHASE_TIMING=1. */
+int lzm_debug_root_wait_cycles(lzm_handle *h, uint64_t *out_host, int n, int reset);
 
 /* Post-search integrity check (host-synchronous on `stream`): the sticky error counters of every
  * search path on the handle — {look-back spin timeouts, draw positions beyond the coefficient

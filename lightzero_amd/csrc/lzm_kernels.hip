@@ -1554,32 +1554,13 @@ __global__ void mlp_res_swizzle_kernel(const float *packed, ResSrc src, int A, f
 }
 // LDS plan of search_res_kernel (float offsets, 16-B aligned); returns bytes, or 0 if it does not fit
 size_t plan_res(SearchArgs &p, ResNet &n, const lzm_handle *h, int S, int A) {
-  size_t o = 0;
+  const ResPlan q = res_plan(h->cap, h->lut_n, h->depth_cap, S, A);
+  n.plan = q;
   p.tree_in_lds = 1;
-  p.off_stat = o; o += (size_t)h->cap * 4;
-  p.off_meta = o; o += (size_t)h->cap * 4;
-  p.off_lut = o; o += round4((size_t)2 * h->lut_n);
-  p.off_legal = o; o += round4((size_t)A + 1);
-  p.off_val = o; o += round4((size_t)h->cap);
-  p.off_path = o; o += round4((size_t)h->depth_cap);
-  p.off_pact = o; o += round4((size_t)h->depth_cap);
-  n.off_act = (int)o; o += (size_t)A * kRHid;
-  n.off_l2n = (int)o; o += round4((size_t)S + 2);
-  n.off_nq = (int)o; o += round4((size_t)2 * (S + 2));
-  n.off_cs = (int)o; o += (size_t)4 * h->cap;
-  n.off_dec = (int)o; o += round4((size_t)S + 2);
-  p.off_misc = o; o += round4((size_t)S + 32);
-  n.off_wd1 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
-  n.off_wd2 = (int)o; o += (size_t)kRSlotsD * kRT * 4;
-  // static LDS of the kernel: activations (two rows), biases, scalars (below 2 KiB)
-  constexpr size_t kResStatic = (kRHid + 4 * kRHid + 2 * (4 * kRHid + kRF + 2 * kRF + kRMaxA) + kResBiasFloats) * 4 + 2048;
-  constexpr size_t kResMax = 160 * 1024 - kResStatic;
-  // pUCT visit table (optional: the descent divides without it)
-  const size_t tri = round4((size_t)h->lut_n * (h->lut_n + 1) / 2);
-  p.pbt_rows = ((o + tri) * sizeof(float) <= kResMax && tri <= 8192) ? h->lut_n : 0;
-  p.off_pbt = o;
-  if (p.pbt_rows) o += tri;
-  return o * sizeof(float) <= kResMax ? o * sizeof(float) : 0;
+  p.off_stat = q.stat; p.off_meta = q.meta; p.off_lut = q.lut; p.off_legal = q.legal; p.off_val = q.val;
+  p.off_path = q.path; p.off_pact = q.pact; p.off_misc = q.misc; p.off_pbt = q.pbt;
+  p.pbt_rows = q.pbt_rows;
+  return (size_t)q.floats * sizeof(float) <= (size_t)kResMaxBytes ? (size_t)q.floats * sizeof(float) : 0;
 }
 void res_net(ResNet &n, const float *wres, int A) {
   (void)A;
@@ -1725,8 +1706,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
   p.flags = h->lb_flags; p.epoch = h->epoch; p.diag = h->search_diag; p.fast = fast ? 1 : 0;
   if (!h->phase && getenv("LZM_PHASE_TIMING") && atoi(getenv("LZM_PHASE_TIMING")) > 0) {
-    LZM_HIP(hipMalloc(&h->phase, 64 * sizeof(unsigned long long)));
-    LZM_HIP(hipMemset(h->phase, 0, 64 * sizeof(unsigned long long)));
+    LZM_HIP(hipMalloc(&h->phase, (64 + 1024) * sizeof(unsigned long long)));
+    LZM_HIP(hipMemset(h->phase, 0, (64 + 1024) * sizeof(unsigned long long)));
   }
   p.phase = h->phase;
   p.diag_mode = getenv("LZM_DIAG_MODE") ? atoi(getenv("LZM_DIAG_MODE")) : 0;  // timing experiments only
@@ -1820,6 +1801,20 @@ int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset) {
   LZM_HIP(hipDeviceSynchronize());
   LZM_HIP(hipMemcpy(out_host, h->phase, 64 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   if (reset) LZM_HIP(hipMemset(h->phase, 0, 64 * sizeof(unsigned long long)));
+  return LZM_OK;
+}
+
+// Diagnostics (LZM_PHASE_TIMING=1, resident kernel): shader-clock cycles each workgroup spent in
+// the parity-mode look-back wait, summed over launches (phase[64 + g], up to 1024 workgroups).
+int lzm_debug_root_wait_cycles(lzm_handle *h, uint64_t *out_host, int n, int reset) {
+  if (!h || !out_host || n < 0 || n > 1024) return LZM_ERR_ARG;
+  if (!h->phase) {
+    memset(out_host, 0, n * sizeof(uint64_t));
+    return LZM_OK;
+  }
+  LZM_HIP(hipDeviceSynchronize());
+  LZM_HIP(hipMemcpy(out_host, h->phase + 64, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (reset) LZM_HIP(hipMemset(h->phase + 64, 0, 1024 * sizeof(unsigned long long)));
   return LZM_OK;
 }
 

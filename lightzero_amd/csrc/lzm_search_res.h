@@ -56,13 +56,17 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 //   PO (32 -> A policy output): one slot: W[4 (l & 7) ..][l >> 3], l >> 3 < A
 // then the biases ([6][128] D, [32] RH, [64] VPH, [604] RS, [604] VS, [32] PO) and the one-hot
 // action rows of fc_dynamics[0], [A][128].
+// dynamic LDS plan of the resident kernel (float offsets; res_plan below)
+struct ResPlan {
+  int wd1, wd2, stat, meta, lut, legal, val, path, pact, act, l2n, nq, cs, dec, misc, pbt, pbt_rows, floats;
+};
 struct ResNet {
   // the resident layout (one base pointer: every block offset but the action rows' is a
   // compile-time constant, res_block_offset; the kernel derives the block addresses, which keeps
   // ~30 scalar registers of block pointers out of the simulation loop)
   const float *w;
   // LDS float offsets beyond SearchArgs' tree plan
-  int off_act, off_wd1, off_wd2, off_l2n, off_nq, off_cs, off_dec;
+  ResPlan plan;      // dynamic LDS plan (res_plan)
   int select_mode;  // LZM_RES_SELECT (experiments): how the walk runs, see the simulation loop
   int late_draw;    // NR = 1: two-way leaf ties run the dynamics layers for both candidates before the
                     // look-back wait (LZM_RES_LATE, default 1)
@@ -1003,10 +1007,46 @@ __device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, uns
 // SMODE: the selection mode at compile time (-1: n.select_mode at run time, experiments); RNG:
 // 0 glibc, 1 Philox, -1 p.fast at run time; STAMPS: phase stamps compiled in (LZM_PHASE_TIMING).
 // Production launches fix all three, so the unused paths cost neither code nor registers.
+// The kernel's dynamic LDS plan (float offsets from the dynamic base): the two LDS weight layers
+// first (their slot addresses become instruction immediates), then the tree slice, the selection
+// tables and the optional pUCT visit table. cap / lut_n / depth_cap: the handle's capacities;
+// S: simulations the selection tables hold. (A compile-time plan for the production handle, which
+// frees ~45 scalar registers of offsets, measured even: the scalar spills are not on the path.)
+// static LDS of the kernel: activations (two rows), biases, scalars (below 2 KiB)
+constexpr int kResStaticBytes = (kRHid + 4 * kRHid + 2 * (4 * kRHid + kRF + 2 * kRF + kRMaxA) + kResBiasFloats) * 4 + 2048;
+constexpr int kResMaxBytes = 160 * 1024 - kResStaticBytes;
+__host__ __device__ constexpr int res_round4(int x) { return (x + 3) & ~3; }
+__host__ __device__ constexpr ResPlan res_plan(int cap, int lut_n, int depth_cap, int S, int A) {
+  ResPlan q{};
+  int o = 0;
+  q.wd1 = o; o += kRSlotsD * kRT * 4;
+  q.wd2 = o; o += kRSlotsD * kRT * 4;
+  q.stat = o; o += cap * 4;
+  q.meta = o; o += cap * 4;
+  q.lut = o; o += res_round4(2 * lut_n);
+  q.legal = o; o += res_round4(A + 1);
+  q.val = o; o += res_round4(cap);
+  q.path = o; o += res_round4(depth_cap);
+  q.pact = o; o += res_round4(depth_cap);
+  q.act = o; o += A * kRHid;
+  q.l2n = o; o += res_round4(S + 2);
+  q.nq = o; o += res_round4(2 * (S + 2));
+  q.cs = o; o += 4 * cap;
+  q.dec = o; o += res_round4(S + 2);
+  q.misc = o; o += res_round4(S + 32);
+  const int tri = res_round4(lut_n * (lut_n + 1) / 2);
+  q.pbt = o;
+  q.pbt_rows = ((o + tri) * 4 <= kResMaxBytes && tri <= 8192) ? lut_n : 0;
+  if (q.pbt_rows) o += tri;
+  q.floats = o;
+  return q;
+}
+
 template <int NR, int SMODE, int RNG, bool STAMPS>
 __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) void search_res_kernel(SearchArgs p, ResNet n) {
   if (!STAMPS) p.phase = nullptr;
   if (RNG >= 0) p.fast = RNG;
+  const ResPlan L = n.plan;
   if (SMODE >= 0) n.select_mode = SMODE;
   if (SMODE == 4 && RNG == 0 && !STAMPS) n.spec_depth = 1;  // production parity kernel
   extern __shared__ float4 smem4[];
@@ -1028,19 +1068,20 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (threadIdx.x < 32) s_exptab[threadIdx.x] = kExp2fTab[threadIdx.x];
   __shared__ unsigned long long s_phase[64];
   if (p.phase && tid < 64) s_phase[tid] = 0ull;
+  unsigned long long s_wait = 0ull;  // (thread 0) look-back wait cycles, diagnostics
 
   // ---- tree slice into LDS (node records, value cache, pUCT tables, legal list, path)
   TreeView t;
   t.A = A; t.cap = p.cap; t.lut_n = p.lut_n; t.depth_cap = p.depth_cap; t.B = 1;
-  t.path = reinterpret_cast<int32_t *>(smem + p.off_path);
-  t.path_act = reinterpret_cast<int32_t *>(smem + p.off_pact);
+  t.path = reinterpret_cast<int32_t *>(smem + L.path);
+  t.path_act = reinterpret_cast<int32_t *>(smem + L.pact);
   t.pathlen = s_len;
   {
-    NodeStat *ls = reinterpret_cast<NodeStat *>(smem + p.off_stat);
-    NodeMeta *lm = reinterpret_cast<NodeMeta *>(smem + p.off_meta);
-    float2 *llut = reinterpret_cast<float2 *>(smem + p.off_lut);
-    int32_t *llegal = reinterpret_cast<int32_t *>(smem + p.off_legal);
-    float *lval = smem + p.off_val;
+    NodeStat *ls = reinterpret_cast<NodeStat *>(smem + L.stat);
+    NodeMeta *lm = reinterpret_cast<NodeMeta *>(smem + L.meta);
+    float2 *llut = reinterpret_cast<float2 *>(smem + L.lut);
+    int32_t *llegal = reinterpret_cast<int32_t *>(smem + L.legal);
+    float *lval = smem + L.val;
     for (int e = tid; e < p.cap; e += kRT) {
       const NodeStat s = p.stat[(size_t)e * B + i];
       ls[e] = s;
@@ -1048,7 +1089,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       lval[e] = node_value(s);
     }
     for (int e = tid; e < p.lut_n; e += kRT) llut[e] = p.lut[e];
-    float *lpbt = smem + p.off_pbt;
+    float *lpbt = smem + L.pbt;
     for (int r = 0; r < p.pbt_rows; ++r) {
       const float y = p.lut[r].y;
       for (int v = tid; v <= r; v += kRT) lpbt[r * (r + 1) / 2 + v] = y / (float)(v + 1);
@@ -1059,10 +1100,10 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     t.pbt = p.pbt_rows ? lpbt : nullptr;
   }
   // latent -> node map of the expanded nodes (children of latent L sit at 1 + A L)
-  int *L2N = reinterpret_cast<int *>(smem + n.off_l2n);
-  float2 *NQ = reinterpret_cast<float2 *>(smem + n.off_nq);
-  int *DEC = reinterpret_cast<int *>(smem + n.off_dec);
-  float4 *CS = reinterpret_cast<float4 *>(smem + n.off_cs);
+  int *L2N = reinterpret_cast<int *>(smem + L.l2n);
+  float2 *NQ = reinterpret_cast<float2 *>(smem + L.nq);
+  int *DEC = reinterpret_cast<int *>(smem + L.dec);
+  float4 *CS = reinterpret_cast<float4 *>(smem + L.cs);
   // A search starts from prepared roots: only the root is expanded, with latent 0 (cnode.cpp:
   // 301-358); simulation k gives its leaf latent k + 1. (Nodes past the root's children may hold a
   // previous search's records: never scan them.)
@@ -1076,7 +1117,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     s_players = (m == -1) ? 1 : 2;
     s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  uint32_t *s_seeds = reinterpret_cast<uint32_t *>(smem + p.off_misc);
+  uint32_t *s_seeds = reinterpret_cast<uint32_t *>(smem + L.misc);
   uint32_t *s_pow = s_seeds + p.S;
   for (int e = tid; e < p.S; e += kRT) s_seeds[e] = p.seeds[e];
   if (!p.fast)
@@ -1092,12 +1133,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float *X0 = reinterpret_cast<float *>(s_acts), *T1 = X0 + kRHid, *NL = T1 + 2 * kRHid, *T2 = NL + 2 * kRHid,
         *T3 = T2 + NR * kRHid, *U2 = T3 + NR * kRHid, *U3 = U2 + NR * kRHid, *RHo = U3 + NR * kRHid,
         *HV = RHo + NR * kRF, *LG = HV + NR * 2 * kRF;
-  float *ACT = smem + n.off_act;
-  const float4 *WD1 = reinterpret_cast<const float4 *>(smem + n.off_wd1);
-  const float4 *WD2 = reinterpret_cast<const float4 *>(smem + n.off_wd2);
+  float *ACT = smem + L.act;
+  const float4 *WD1 = reinterpret_cast<const float4 *>(smem + L.wd1);
+  const float4 *WD2 = reinterpret_cast<const float4 *>(smem + L.wd2);
   for (int e = tid; e < kRSlotsD * kRT; e += kRT) {
-    reinterpret_cast<float4 *>(smem + n.off_wd1)[e] = res_blk4(n, kRbD + 1)[e];
-    reinterpret_cast<float4 *>(smem + n.off_wd2)[e] = res_blk4(n, kRbD + 2)[e];
+    reinterpret_cast<float4 *>(smem + L.wd1)[e] = res_blk4(n, kRbD + 1)[e];
+    reinterpret_cast<float4 *>(smem + L.wd2)[e] = res_blk4(n, kRbD + 2)[e];
   }
   for (int e = tid; e < A * kRHid; e += kRT) ACT[e] = res_blk(n, kRbAct, A)[e];
   float4 wD3[kRSlotsD], wD4[kRSlotsD], wRS[kRSlotsS], wRH[kRSlotsRH], wVPH[kRSlotsVPH], wPO[1];
@@ -1144,6 +1185,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       __syncthreads();
     }
     LZM_STAMP(12);
+    if (wid != 0 && k > 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // (see the expand)
     // ---- selection, part 2: the walk (wave 0, one lane per child)
     if (wid == 0) {
       const float4 mm = s_mm;
@@ -1322,7 +1364,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     __syncthreads();
     if (NR == 1 && late) {
+      const unsigned long long w0_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
       const int base = lookback_sum(p, k, g, G, epoch, s_part);
+      if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
       if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
       __syncthreads();
     }
@@ -1448,9 +1492,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       p.rec_dec[((size_t)k * B + i) * 2 + 1] = vdec;
       for (int a = 0; a < A; ++a) p.rec_logits[((size_t)k * B + i) * A + a] = LG[row * kRMaxA + a];
     }
-    // fc_dynamics[0] for the next simulation: waves 1-3 fetch now (they idle through the expand
-    // and backup), wave 0 after its backup
-    if (wid != 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
+    // fc_dynamics[0] for the next simulation: wave 0 now, alone on the texture path (16 loads
+    // issue in a few hundred cycles), waves 1-3 during the next walk, which only wave 0 runs
+    if (wid == 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
     // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500), wave 0
     if (wid == 0) {
       const int len = s_len[0];
@@ -1462,7 +1506,6 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
-      res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
     }
     LZM_STAMP(9);
   }
@@ -1483,6 +1526,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   __syncthreads();
   if (p.phase && tid < 64 && s_phase[tid]) atomicAdd(p.phase + tid, s_phase[tid]);
+  if (p.phase && tid == 0 && g < 1024) atomicAdd(p.phase + 64 + g, s_wait);
   if (tid == 0) {
     // the last workgroup advances the epoch; no release fence (an L2 writeback per workgroup on
     // gfx950): the kernel boundary orders the write-back above for every later reader

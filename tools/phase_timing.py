@@ -41,6 +41,7 @@ def main():
     t = next(iter(POOL._free.values()))[0]
     buf = (ctypes.c_uint64 * 64)()
     _lib.load().lzm_debug_phase_cycles(t.h, buf, 1)
+    _lib.load().lzm_debug_root_wait_cycles(t.h, buf, 0, 1)
     n = 3
     for _ in range(n):
         step()
@@ -56,6 +57,16 @@ def main():
     sub = np.array(buf[16:64], dtype=np.float64) / (n * G * a.sims)
     print("sub-stamps per simulation (cycles; index = stamp id - 16, meaning per kernel):")
     print("  " + "  ".join(f"{q}:{c:.0f}" for q, c in enumerate(sub) if c > 0))
+    # per-workgroup look-back wait (resident kernel, parity mode): by root range and by XCD (g % 8)
+    wait = (ctypes.c_uint64 * 1024)()
+    _lib.load().lzm_debug_root_wait_cycles(t.h, wait, 1024, 0)
+    w = np.array(wait[:G], dtype=np.float64) / (n * a.sims)
+    if w.sum() > 0:
+        print("look-back wait per simulation (cycles), by root range:")
+        for q in range(8):
+            lo, hi = q * G // 8, (q + 1) * G // 8
+            print(f"  roots {lo:4d}-{hi - 1:4d}: mean {w[lo:hi].mean():7.0f}  max {w[lo:hi].max():7.0f}")
+        print("by XCD (g % 8): " + "  ".join(f"{x}:{w[x::8].mean():.0f}" for x in range(8)))
 
 
 if __name__ == "__main__":
