@@ -1003,6 +1003,37 @@ __device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, uns
   return (part[0] + part[1]) + (part[2] + part[3]);
 }
 
+// lookback_sum by wave 0 alone, for G <= 256 workgroups: lane l polls roots l, l + 64, ... (all
+// loads in flight at once), the sum by DPP (exact: float sums of integers < 2^24), no LDS and no
+// barrier. Returns the sum in every lane of wave 0.
+__device__ inline int lookback_sum_w0(const SearchArgs &p, int k, int g, int G, unsigned long long epoch) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long ok = epoch << 32;  // a published flag of depth 0
+  unsigned long long v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = lane + 64 * j;
+    v[j] = q < g ? __hip_atomic_load(&p.flags[(size_t)k * G + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ok;
+  }
+  float sum = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = lane + 64 * j;
+    long long spins = 0;
+    while ((v[j] >> 32) != epoch) {
+      if (++spins > (1ll << 22)) {
+        atomicAdd(p.diag, 1);
+        v[j] = ok;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v[j] = __hip_atomic_load(&p.flags[(size_t)k * G + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    sum += (float)(int)(v[j] & 0xffffffffu);
+  }
+  return (int)wave_sum(sum);
+}
+
 // NR = 2 (parity mode): the network carries a second, speculative row for two-way leaf ties.
 // SMODE: the selection mode at compile time (-1: n.select_mode at run time, experiments); RNG:
 // 0 glibc, 1 Philox, -1 p.fast at run time; STAMPS: phase stamps compiled in (LZM_PHASE_TIMING).
@@ -1365,9 +1396,17 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
     if (NR == 1 && late) {
       const unsigned long long w0_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
-      const int base = lookback_sum(p, k, g, G, epoch, s_part);
-      if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
-      if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+      if (G <= kRT) {
+        if (wid == 0) {
+          const int base = lookback_sum_w0(p, k, g, G, epoch);
+          if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
+          if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+        }
+      } else {
+        const int base = lookback_sum(p, k, g, G, epoch, s_part);
+        if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
+        if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+      }
       __syncthreads();
     }
     // the next latent row the rest of the network reads (NR = 1: the late draw's pick)

@@ -67,6 +67,7 @@ def main():
             lo, hi = q * G // 8, (q + 1) * G // 8
             print(f"  roots {lo:4d}-{hi - 1:4d}: mean {w[lo:hi].mean():7.0f}  max {w[lo:hi].max():7.0f}")
         print("by XCD (g % 8): " + "  ".join(f"{x}:{w[x::8].mean():.0f}" for x in range(8)))
+        print("roots 0-7: " + "  ".join(f"{x}:{w[x]:.0f}" for x in range(min(8, G))))
 
 
 if __name__ == "__main__":
