@@ -154,6 +154,18 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
                    int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
                    const uint32_t *seeds, const int32_t *virtual_to_play, float *latent_pool, int32_t *rec_x,
                    int32_t *rec_a, int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream);
+/* Collect-step mode of the next lzm_search_mlp calls on h (sticky; host state only, so a captured
+ * launch keeps the values it was launched with; pass nulls / 0 to clear). Replaces the small
+ * launches around one collect-time search (lightzero_amd.collect.DeviceSearchStep,
+ * muzero.py:617-690): count (device int64) non-null: the traverse seeds are
+ * (base + *count * S + k) mod 10^6 (lzm_seed_sequence's rule; the `seeds` argument may be null)
+ * and, if increment, *count is incremented after the search; root_dist (int32[B*A]) / root_values (float[B])
+ * non-null: the search also writes lzm_get_root_outputs' outputs; fresh_minmax: every root starts
+ * from fresh min-max bounds (lzm_minmax_init with value_delta_max) instead of reading `minmax`.
+ * The network-resident kernel does all of it in-kernel; the weight-streaming kernel adds one
+ * launch before and one after. Replaces the glue of mcts_ctree.py:245-321 + muzero.py:660-690. */
+int lzm_search_set_step(lzm_handle *h, int64_t *count, int64_t base, int increment, int32_t *root_dist,
+                        float *root_values, int fresh_minmax, float value_delta_max);
 /* Which kernel lzm_search_mlp launches for a batch of B roots with `actions` actions and this
  * network: 1 = network-resident (search_res_kernel, lzm_search_res.h: the config-2 shape with one
  * root per workgroup), 0 = weight-streaming (search_mlp_kernel). Host-only, no GPU work. */

@@ -69,6 +69,7 @@ SIGNATURES = {
     "lzm_search_mlp": [_vp, _i, _i, _i, _i, _vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_diagnostics": [_vp, _vp, _vp],
     "lzm_debug_root_wait_cycles": [_vp, _vp, _i, _i],
+    "lzm_search_set_step": [_vp, _vp, _i64, _i, _vp, _vp, _i, _f],
     "lzm_check_errors": [_vp, _vp, _i, _vp],
     "lzm_debug_expf": [_vp, _vp, _i64, _vp],
     "lzm_debug_glibc_rand": [_u32, _i, _vp, _vp],

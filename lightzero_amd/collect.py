@@ -16,7 +16,6 @@ values, root latents and policy logits). `step_counter` counts the steps (device
 """
 import torch
 
-from . import _lib
 from .initial import fused_initial_or_none
 from .mcts_ctree import MuZeroMCTSCtree
 from .utils import EasyDict
@@ -74,19 +73,22 @@ class DeviceSearchStep:
                     out = self.initial.initial_inference(self.obs, latent_out=pool0)  # search skips its copy
                 else:
                     out = (self.initial or self.model).initial_inference(self.obs)
-                seeds = torch.empty(self.S, dtype=torch.int32, device=self.device)
-                _lib.call("lzm_seed_sequence", _lib.ptr(self._count), self._base, self.S, _lib.ptr(seeds),
-                          _lib.stream_ptr())
                 self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
                                           self.to_play)
-                self.mcts.search(self.roots, self.model, out.latent_state, self.to_play, seeds=seeds)
+                # the seeds (from the step counter), fresh min-max bounds, the root outputs and the
+                # counter increment run inside the search (the one-launch search: in its kernel)
                 t = self.roots.tree
-                dist, values = t.root_outputs()
+                dist = torch.empty((self.B, t.A), dtype=torch.int32, device=self.device)
+                values = torch.empty(self.B, dtype=torch.float32, device=self.device)
+                # (an epilogue reads the counter of this step: it advances after the epilogue)
+                self.mcts.search(self.roots, self.model, out.latent_state, self.to_play,
+                                 step=dict(count=self._count, base=self._base, dist=dist, values=values,
+                                           increment=self.epilogue is None))
                 res = dict(distributions=dist, values=values, latent_state=out.latent_state,
                            policy_logits=out.policy_logits)
                 if self.epilogue is not None:
                     self.epilogue(res)
-                self._count.add_(1)
+                    self._count.add_(1)
                 return res
             finally:
                 self.mcts_cls.rng_mode = old

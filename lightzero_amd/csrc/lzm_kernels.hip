@@ -583,6 +583,15 @@ __global__ void minmax_init_kernel(float4 *mm, int n, float delta) {
   if (i < n) mm[i] = make_float4(kFloatMin, kFloatMax, delta, 0.0f);
 }
 
+// collect-step mode on the weight-streaming path (the network-resident kernel does both in-kernel):
+// seeds of this step (seed_sequence_kernel's rule) and, optionally, fresh min-max bounds ...
+__global__ void step_prologue_kernel(const int64_t *count, long long base, int S, int32_t *seeds, float4 *mm, int n,
+                                     int fresh, float delta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (count && i < S) seeds[i] = (int32_t)((base + *count * (long long)S + i) % 1000000ll);
+  if (fresh && i < n) mm[i] = make_float4(kFloatMin, kFloatMax, delta, 0.0f);
+}
+
 __global__ void gather_kernel(const float *pool, long long row, int B, const int32_t *x, float *out) {
   const long long total = (long long)B * row;
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
@@ -626,6 +635,21 @@ __global__ void root_outputs_kernel(TreeView t, int32_t *dist, float *values) {
     dist[(size_t)i * t.A + j] = v;
   }
   values[i] = node_value(rs);
+}
+
+// ... and after the search: the root outputs (root_outputs_kernel) and the step counter
+__global__ void step_epilogue_kernel(TreeView t, int32_t *dist, float *values, int64_t *count) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (dist && i < t.B) {
+    const NodeMeta rm = t.meta[i];
+    for (int j = 0; j < t.A; ++j) {
+      int v = -1;
+      if (rm.latent >= 0 && j < t.nlegal[i]) v = t.stat[nidx(t, 1 + t.A * rm.latent + t.legal[(size_t)i * t.A + j], i)].visit;
+      dist[(size_t)i * t.A + j] = v;
+    }
+  }
+  if (values && i < t.B) values[i] = node_value(t.stat[i]);
+  if (count && i == 0) *count += 1;
 }
 
 __global__ void values_kernel(TreeView t, float *out) {
@@ -746,7 +770,17 @@ struct lzm_handle {
   unsigned long long *lb_flags = nullptr;  // [flag_sims][G] look-back words
   int flag_sims = 0;
   uint32_t *epoch = nullptr;               // [2] launch epoch, done counter
-  int32_t *search_diag = nullptr;          // [2]
+  int32_t *search_diag = nullptr;          // [4]
+  // collect-step mode of the fused search (lzm_search_set_step)
+  int64_t *step_count = nullptr;
+  int step_inc = 0;
+  long long step_base = 0;
+  int step_fresh = 0;
+  float step_delta = 0.0f;
+  int32_t *step_dist = nullptr;
+  float *step_vals = nullptr;
+  int32_t *step_seeds = nullptr;  // [sims] the weight-streaming path's staged seeds
+  int step_seeds_n = 0;
   unsigned long long *phase = nullptr;     // [64] diagnostic phase cycles (LZM_PHASE_TIMING=1)
   const int32_t *ext_norm = nullptr;       // lzm_set_norm_words: verdict words written by lzm_conv_heads
   const int32_t *reuse_action = nullptr;   // lzm_set_reuse: search-with-reuse inputs (device, [B])
@@ -906,7 +940,7 @@ int lzm_destroy(lzm_handle *h) {
   free_tree(h);
   dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag); dfree(h->err);
   dfree(h->hint); dfree(h->norm_flag); dfree(h->jmat);
-  dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag); dfree(h->phase);
+  dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag); dfree(h->phase); dfree(h->step_seeds);
   delete h;
   return LZM_OK;
 }
@@ -1651,7 +1685,7 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
                    int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
                    const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, int32_t *rec_x, int32_t *rec_a,
                    int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream) {
-  if (!h || !weights || !minmax || !seeds || !vtp_in || !latent_pool || num_simulations <= 0) {
+  if (!h || !weights || !minmax || (!seeds && !h->step_count) || !vtp_in || !latent_pool || num_simulations <= 0) {
     set_err("lzm_search_mlp: null argument or no simulations");
     return LZM_ERR_ARG;
   }
@@ -1715,6 +1749,8 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   if (R == 1 && res_enabled() && res_shape_ok(H, A, F, V, res_dynamics)) {
     // the network-resident kernel (lzm_search_res.h); its weights follow the generic layout
     SearchArgs q = p;
+    q.step_count = h->step_count; q.step_inc = h->step_inc; q.step_base = h->step_base; q.mm_fresh = h->step_fresh; q.mm_delta = h->step_delta;
+    q.out_dist = h->step_dist; q.out_values = h->step_vals;
     ResNet n;
     memset(&n, 0, sizeof(n));
     const size_t lds = plan_res(q, n, h, S, A);
@@ -1780,6 +1816,21 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
     snprintf(g_err, sizeof(g_err), "lzm_search_mlp: %zu B of LDS needed (network too wide)", lds);
     return LZM_ERR_ARG;
   }
+  // collect-step mode: the prologue (seeds, fresh min-max) and epilogue (root outputs, counter)
+  // as one launch each around the search
+  if (h->step_count || h->step_fresh) {
+    if (h->step_count && h->step_seeds_n < S) {
+      dfree(h->step_seeds);
+      h->step_seeds = nullptr;
+      LZM_HIP(hipMalloc(&h->step_seeds, (size_t)h->sims_cap * sizeof(int32_t)));
+      h->step_seeds_n = h->sims_cap;
+    }
+    const int n = std::max(S, h->B);
+    hipLaunchKernelGGL(step_prologue_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->step_count,
+                       h->step_base, S, h->step_seeds, (float4 *)minmax, h->B, h->step_fresh, h->step_delta);
+    LZM_CHECK_LAUNCH();
+    if (h->step_count) p.seeds = reinterpret_cast<const uint32_t *>(h->step_seeds);
+  }
   hipError_t e;
   switch (R) {
     case 1: e = launch_search_r<1>(p, G, lds, (hipStream_t)stream); break;
@@ -1789,6 +1840,26 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   }
   LZM_HIP(e);
   LZM_CHECK_LAUNCH();
+  if ((h->step_count && h->step_inc) || h->step_dist || h->step_vals) {
+    hipLaunchKernelGGL(step_epilogue_kernel, dim3((h->B + 255) / 256), dim3(256), 0, (hipStream_t)stream, view(h),
+                       h->step_dist, h->step_vals, h->step_inc ? h->step_count : nullptr);
+    LZM_CHECK_LAUNCH();
+  }
+  return LZM_OK;
+}
+
+// Collect-step mode of lzm_search_mlp (sticky on the handle, host state only: a captured launch
+// keeps the values it was launched with). See include/lzmcts.h.
+int lzm_search_set_step(lzm_handle *h, int64_t *count, int64_t base, int increment, int32_t *root_dist,
+                        float *root_values, int fresh_minmax, float value_delta_max) {
+  if (!h || base < 0) return LZM_ERR_ARG;
+  h->step_count = count;
+  h->step_inc = increment ? 1 : 0;
+  h->step_base = (long long)base;
+  h->step_dist = root_dist;
+  h->step_vals = root_values;
+  h->step_fresh = fresh_minmax ? 1 : 0;
+  h->step_delta = value_delta_max;
   return LZM_OK;
 }
 

@@ -89,6 +89,18 @@ struct SearchArgs {
   size_t off_stat, off_meta, off_lut, off_legal, off_path, off_pact, off_x0, off_x1, off_x2, off_n, off_h, off_logit, off_part,
       off_misc, off_val, off_pbt;
   int pbt_rows;  // rows N of the pUCT visit table in LDS (0: none)
+  // collect-step mode (lzm_search_set_step; the network-resident kernel runs it in-kernel):
+  // step_count != null: seeds[k] = (step_base + *step_count * S + k) mod 10^6 instead of `seeds`,
+  // and (step_inc) the last workgroup increments *step_count; mm_fresh: every root starts from fresh
+  // min-max bounds (delta mm_delta); out_dist / out_values: the root outputs of
+  // lzm_get_root_outputs, written by each root's workgroup after the search
+  int64_t *step_count;
+  int step_inc;  // the last workgroup increments *step_count
+  long long step_base;
+  int mm_fresh;
+  float mm_delta;
+  int32_t *out_dist;
+  float *out_values;
 };
 
 // ------------------------------------------------------------------------------ LDS helpers

@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int e = tid; e < p.S + 2; e += kRT) L2N[e] = e == 0 ? 0 : -1;
   if (tid == 0) s_nlat = 1;
   if (tid == 0) {
-    s_mm = p.minmax[i];
+    s_mm = p.mm_fresh ? make_float4(kFloatMin, kFloatMax, p.mm_delta, 0.0f) : p.minmax[i];
     s_vtp = p.vtp_in[i];
     int m = INT_MIN;
     for (int q = 0; q < B; ++q) m = max(m, p.vtp_in[q]);
@@ -1150,7 +1150,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   uint32_t *s_seeds = reinterpret_cast<uint32_t *>(smem + L.misc);
   uint32_t *s_pow = s_seeds + p.S;
-  for (int e = tid; e < p.S; e += kRT) s_seeds[e] = p.seeds[e];
+  if (p.step_count) {
+    const long long c = *p.step_count;  // (read before the last workgroup's increment below)
+    for (int e = tid; e < p.S; e += kRT) s_seeds[e] = (uint32_t)((p.step_base + c * (long long)p.S + e) % 1000000ll);
+  } else {
+    for (int e = tid; e < p.S; e += kRT) s_seeds[e] = p.seeds[e];
+  }
   if (!p.fast)
     for (int e = tid; e < 31; e += kRT) s_pow[e] = p.pow16807[e];
 
@@ -1563,6 +1568,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     p.minmax[i] = s_mm;
     p.pathlen[i] = s_len[0];
   }
+  // root outputs (root_outputs_kernel's values: visit counts per legal action, the root's value)
+  if (p.out_dist && tid < A) {
+    const int rl = t.meta[0].latent;
+    p.out_dist[(size_t)i * A + tid] = (rl >= 0 && tid < t.nlegal[0]) ? t.stat[1 + A * rl + t.legal[tid]].visit : -1;
+  }
+  if (p.out_values && tid == 0) p.out_values[i] = node_value(t.stat[0]);
   __syncthreads();
   if (p.phase && tid < 64 && s_phase[tid]) atomicAdd(p.phase + tid, s_phase[tid]);
   if (p.phase && tid == 0 && g < 1024) atomicAdd(p.phase + 64 + g, s_wait);
@@ -1573,6 +1584,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (done == (uint32_t)G - 1) {
       p.epoch[1] = 0;
       __hip_atomic_store(p.epoch, (uint32_t)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.step_count && p.step_inc) *p.step_count += 1;  // every workgroup has read it (its seeds)
     }
   }
 }

@@ -23,6 +23,7 @@ from typing import Any, List, Union
 import numpy as np
 import torch
 
+from . import _lib
 from .ctree import ez_tree, mz_tree
 from .conv_infer import FoldedCache
 from .fused import NotPackable, PackedCache
@@ -300,10 +301,17 @@ class MuZeroMCTSCtree(object):
                                   cat, logits, t.vtp, **kw)
 
     def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
-               to_play_batch: Union[int, List[Any]], seeds: torch.Tensor = None) -> None:
+               to_play_batch: Union[int, List[Any]], seeds: torch.Tensor = None, step: dict = None) -> None:
         """seeds (not in the reference): optional device int32 [num_simulations] traverse seeds
         (the srand(tv_usec) values, uint32 bits) instead of the host seed source — keeps the call
-        free of host copies (HIP-graph capture, lightzero_amd.collect)."""
+        free of host copies (HIP-graph capture, lightzero_amd.collect).
+        step (not in the reference; lightzero_amd.collect): dict(count=int64 device counter,
+        base=int, dist=int32 [B, A], values=float32 [B], increment=True) — the collect step's glue
+        in the search itself: seeds (base + count * S + k) mod 10^6 (`seeds` ignored), count
+        incremented (unless increment=False), the
+        root outputs (get_distributions / get_values as device tensors) written to dist / values,
+        fresh min-max bounds. The one-launch search does all of it in its kernel
+        (lzm_search_set_step); other paths run the same steps as separate launches."""
         with torch.no_grad():
             model.eval()
             t = roots.tree
@@ -325,19 +333,39 @@ class MuZeroMCTSCtree(object):
             buf = entry.buf if entry is not None else (_SearchBuffers() if graph else self._buf).get(B, S, shape, dev)
             if lat0.data_ptr() != buf.pool[0].data_ptr():  # (the collect step writes it in place)
                 buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
-            buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
-            buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
+            # the one-launch search reads device seeds / to_play in place (no staging copies)
+            in_place = fz is not None and rec is None
+            step_in_kernel = step is not None and in_place
+            vt = to_play_batch if in_place and _usable_i32(to_play_batch, B, dev) else None
+            if vt is None:
+                buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
+                vt = buf.vtp_in
+            sd = None
+            if step is not None and not step_in_kernel:
+                _lib.call("lzm_seed_sequence", _lib.ptr(step["count"]), int(step["base"]), S, _lib.ptr(buf.seeds),
+                          _lib.stream_ptr())
+                sd = buf.seeds
+            elif step is None:
+                sd = seeds if in_place and _usable_i32(seeds, S, dev) else None
+                if sd is None:
+                    buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
+                    sd = buf.seeds
             if rec is not None:
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
             if fz is not None:
                 packed, dims = fz
                 cfg = self._cfg
-                new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
-                # the one-launch search reads device seeds / to_play in place (no staging copies)
-                sd = seeds if _usable_i32(seeds, S, dev) and rec is None else buf.seeds
-                vt = to_play_batch if _usable_i32(to_play_batch, B, dev) else buf.vtp_in
-                t.search_mlp(dims, packed, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base),
-                             float(cfg.pb_c_init), float(np.float32(cfg.discount_factor)), rec=rec)
+                if step_in_kernel:
+                    t.set_step(step["count"], int(step["base"]), step.get("increment", True), step["dist"],
+                               step["values"], True, cfg.value_delta_max)
+                else:
+                    new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
+                try:
+                    t.search_mlp(dims, packed, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base),
+                                 float(cfg.pb_c_init), float(np.float32(cfg.discount_factor)), rec=rec)
+                finally:
+                    if step_in_kernel:
+                        t.set_step()
             elif graph:
                 if entry is None:
                     entry = self._capture(t, model, buf, S, row)
@@ -345,6 +373,11 @@ class MuZeroMCTSCtree(object):
                 entry.replay()
             else:
                 self._loop(t, model, buf, buf.mm, buf.vtp_in, buf.seeds, S, row, rec)
+            if step is not None and not step_in_kernel:
+                _lib.call("lzm_get_root_outputs", t.h, _lib.ptr(step["dist"]), _lib.ptr(step["values"]),
+                          _lib.stream_ptr())
+                if step.get("increment", True):
+                    step["count"].add_(1)
             roots._last_minmax = buf.mm
             self.last_record = rec
 

@@ -177,6 +177,15 @@ class DeviceTree:
              ptr(vtp_in), ptr(pool), r("x"), r("action"), r("search_len"), r("decoded"), r("policy_logits"),
              stream_ptr(stream))
 
+    def set_step(self, count=None, base=0, increment=True, dist=None, values=None, fresh_minmax=False,
+                 value_delta_max=0.0):
+        """Collect-step mode of the next search_mlp calls (lzm_search_set_step; host state only):
+        device seeds from the int64 step counter `count` (incremented by the search if
+        `increment`), root outputs into `dist` / `values`, fresh min-max bounds. set_step() clears
+        it."""
+        call("lzm_search_set_step", self.h, ptr(count), int(base), int(bool(increment)), ptr(dist), ptr(values),
+             int(bool(fresh_minmax)), float(np.float32(value_delta_max)))
+
     def check_errors(self, clear=True, stream=None):
         """Post-search integrity check (synchronises the stream): raises LzmError when a look-back
         spin timed out or a draw fell outside the coefficient table on any search path of this

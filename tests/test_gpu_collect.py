@@ -51,8 +51,13 @@ def _reference_steps(model, obs_list, noises_list, B, S, seed, legal):
     return outs
 
 
+# the collect-step glue (seeds from the step counter, fresh min-max, root outputs, counter) runs
+# inside the network-resident kernel, and around the weight-streaming kernel (LZM_FUSED_RES=0)
+@pytest.mark.parametrize("env", ["", "LZM_FUSED_RES=0"])
 @pytest.mark.parametrize("graph", [False, True])
-def test_device_search_step_matches_python_search(graph):
+def test_device_search_step_matches_python_search(graph, env, monkeypatch):
+    if env:
+        monkeypatch.setenv(*env.split("="))
     from lightzero_amd.collect import DeviceSearchStep
     B, S, seed = 64, 30, 7
     legal = [[0, 1]] * B
@@ -69,3 +74,4 @@ def test_device_search_step_matches_python_search(graph):
         assert np.array_equal(d, ref[k][0]), f"step {k}: visit counts differ"
         assert np.array_equal(v, ref[k][1]), f"step {k}: root values differ"
         assert (d.sum(axis=1) == S).all()
+        assert int(step.step_counter.item()) == k + 1

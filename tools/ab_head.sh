@@ -1,0 +1,7 @@
+set -e
+out=gpurun_out/ab_step; mkdir -p $out
+for rep in 1 2; do
+  (cd _ab_head && timeout -k 10 200 python bench.py --no-cpu-baseline --steps 30 > ../$out/head_$rep.json 2>&1)
+  timeout -k 10 200 python bench.py --no-cpu-baseline --steps 30 > $out/cur_$rep.json 2>&1
+done
+for f in $out/*.json; do python3 -c "import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);print('$f', d['value'], d['ms_per_step'], d['roofline']['launch_us'])"; done
