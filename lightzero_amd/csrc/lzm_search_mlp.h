@@ -578,6 +578,19 @@ __device__ inline void seed_state_parallel(uint32_t seed, const uint32_t *pw, ui
 
 // TL: the workgroup's tree slice (node records, pUCT table, root legal lists) is staged in LDS
 // for the whole search; otherwise the nodes stay in HBM (large action spaces x simulations).
+// The pUCT visit table lpbt[n (n + 1) / 2 + v] = lut[n].y / (v + 1) for v <= n < rows, one entry
+// per thread: every lut load is independent (one memory round trip, not one per row).
+__device__ inline void build_pbt(const float2 *lut, int rows, float *lpbt, int tid, int nthreads) {
+  const int total = rows * (rows + 1) / 2;
+  for (int e = tid; e < total; e += nthreads) {
+    int n = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+    while (n > 0 && n * (n + 1) / 2 > e) --n;
+    while ((n + 1) * (n + 2) / 2 <= e) ++n;
+    const int v = e - n * (n + 1) / 2;
+    lpbt[e] = lut[n].y / (float)(v + 1);
+  }
+}
+
 template <int R, bool TL>
 __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
   extern __shared__ float4 smem4[];
@@ -627,10 +640,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
       lval[e] = li < nr ? node_value(p.stat[(size_t)node * B + i0 + li]) : 0.0f;
     }
     float *lpbt = smem + p.off_pbt;
-    for (int n = 0; n < p.pbt_rows; ++n) {
-      const float y = p.lut[n].y;
-      for (int v = tid; v <= n; v += kThreads) lpbt[n * (n + 1) / 2 + v] = y / (float)(v + 1);
-    }
+    build_pbt(p.lut, p.pbt_rows, lpbt, tid, kThreads);
     t.val = lval;
     t.pbt = p.pbt_rows ? lpbt : nullptr;
     for (int e = tid; e < R * A; e += kThreads) llegal[e] = (e / A < nr) ? p.legal[(size_t)i0 * A + e] : 0;

@@ -1086,6 +1086,15 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int B = p.B, A = p.A;
   const int i = g;  // one root per workgroup
   unsigned long long stamp_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
+  unsigned long long isub_ = stamp_;  // init sub-stamps (diagnostics)
+#define LZM_ISTAMP(n)                                                      \
+  do {                                                                     \
+    if (p.phase && tid == 0) {                                             \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();       \
+      s_phase[n] += (now_ - isub_) * (unsigned long long)p.S;              \
+      isub_ = now_;                                                        \
+    }                                                                      \
+  } while (0)
 
   __shared__ uint32_t s_z0[31];
   __shared__ int s_players, s_epoch, s_x, s_act, s_status, s_tlevel, s_vtp;
@@ -1121,15 +1130,13 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     for (int e = tid; e < p.lut_n; e += kRT) llut[e] = p.lut[e];
     float *lpbt = smem + L.pbt;
-    for (int r = 0; r < p.pbt_rows; ++r) {
-      const float y = p.lut[r].y;
-      for (int v = tid; v <= r; v += kRT) lpbt[r * (r + 1) / 2 + v] = y / (float)(v + 1);
-    }
+    build_pbt(p.lut, p.pbt_rows, lpbt, tid, kRT);
     for (int e = tid; e < A; e += kRT) llegal[e] = p.legal[(size_t)i * A + e];
     if (tid == 0) llegal[A] = p.nlegal[i];
     t.stat = ls; t.meta = lm; t.lut = llut; t.legal = llegal; t.nlegal = llegal + A; t.val = lval;
     t.pbt = p.pbt_rows ? lpbt : nullptr;
   }
+  LZM_ISTAMP(24);
   // latent -> node map of the expanded nodes (children of latent L sit at 1 + A L)
   int *L2N = reinterpret_cast<int *>(smem + L.l2n);
   float2 *NQ = reinterpret_cast<float2 *>(smem + L.nq);
@@ -1143,10 +1150,16 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (tid == 0) {
     s_mm = p.mm_fresh ? make_float4(kFloatMin, kFloatMax, p.mm_delta, 0.0f) : p.minmax[i];
     s_vtp = p.vtp_in[i];
-    int m = INT_MIN;
-    for (int q = 0; q < B; ++q) m = max(m, p.vtp_in[q]);
-    s_players = (m == -1) ? 1 : 2;
     s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wid == 0) {
+    // players: 2 unless every root's to_play is -1 (max over the batch), by wave 0 with all its
+    // loads in flight (a serial loop over B was ~30 K cycles of the launch)
+    int m = INT_MIN;
+    for (int q = lane; q < B; q += 64) m = max(m, p.vtp_in[q]);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+    if (lane == 0) s_players = (m == -1) ? 1 : 2;
   }
   uint32_t *s_seeds = reinterpret_cast<uint32_t *>(smem + L.misc);
   uint32_t *s_pow = s_seeds + p.S;
@@ -1159,6 +1172,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if (!p.fast)
     for (int e = tid; e < 31; e += kRT) s_pow[e] = p.pow16807[e];
 
+  LZM_ISTAMP(25);
   // ---- network residency: LDS layers, action rows, register layers and biases
   // activations and biases at static LDS addresses: lane-dependent addresses then share a few base
   // registers and fold the arrays' offsets into the instructions' immediates
@@ -1172,11 +1186,19 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float *ACT = smem + L.act;
   const float4 *WD1 = reinterpret_cast<const float4 *>(smem + L.wd1);
   const float4 *WD2 = reinterpret_cast<const float4 *>(smem + L.wd2);
-  for (int e = tid; e < kRSlotsD * kRT; e += kRT) {
-    reinterpret_cast<float4 *>(smem + L.wd1)[e] = res_blk4(n, kRbD + 1)[e];
-    reinterpret_cast<float4 *>(smem + L.wd2)[e] = res_blk4(n, kRbD + 2)[e];
+  {
+    // the two LDS layers, each thread's 16 + 16 slots loaded before any is stored (one round trip
+    // per block instead of one per slot: the registers are free before the weights arrive)
+    float4 st[kRSlotsD];
+    res_fetch<kRSlotsD>(res_blk4(n, kRbD + 1), st);
+#pragma unroll
+    for (int j = 0; j < kRSlotsD; ++j) reinterpret_cast<float4 *>(smem + L.wd1)[j * kRT + tid] = st[j];
+    res_fetch<kRSlotsD>(res_blk4(n, kRbD + 2), st);
+#pragma unroll
+    for (int j = 0; j < kRSlotsD; ++j) reinterpret_cast<float4 *>(smem + L.wd2)[j * kRT + tid] = st[j];
   }
   for (int e = tid; e < A * kRHid; e += kRT) ACT[e] = res_blk(n, kRbAct, A)[e];
+  LZM_ISTAMP(26);
   float4 wD3[kRSlotsD], wD4[kRSlotsD], wRS[kRSlotsS], wRH[kRSlotsRH], wVPH[kRSlotsVPH], wPO[1];
   res_fetch<kRSlotsD>(res_blk4(n, kRbD + 3), wD3);
   res_fetch<kRSlotsD>(res_blk4(n, kRbD + 4), wD4);
@@ -1185,9 +1207,19 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   res_fetch<kRSlotsVPH>(res_blk4(n, kRbVPH), wVPH);
   res_fetch<kRSlotsPO>(res_blk4(n, kRbPO), wPO);
   const int cD = tid >> 1, pD = tid & 1, cRH = tid >> 3, pRH = tid & 7, cVP = tid >> 2, pVP = tid & 3, cPO = tid >> 3;
+  LZM_ISTAMP(27);
   // biases live in LDS (registers are the scarce resource): the bias blocks are contiguous
   float *BB = reinterpret_cast<float *>(s_bias);
-  for (int e = tid; e < kResBiasFloats; e += kRT) BB[e] = res_blk(n, kRbBD, A)[e];
+  {
+    constexpr int kNB = (kResBiasFloats + kRT - 1) / kRT;
+    float bv[kNB];
+    const float *bsrc = res_blk(n, kRbBD, A);
+#pragma unroll
+    for (int j = 0; j < kNB; ++j) bv[j] = j * kRT + tid < kResBiasFloats ? bsrc[j * kRT + tid] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < kNB; ++j)
+      if (j * kRT + tid < kResBiasFloats) BB[j * kRT + tid] = bv[j];
+  }
   const float *BD = BB, *BRH = BD + 6 * kRHid, *BVP = BRH + kRF, *BRS = BVP + 2 * kRF,
               *BVS = BRS + ((kRV + 3) & ~3), *BPO = BVS + ((kRV + 3) & ~3);
   // the streamed buffer: fc_dynamics[0] for the first simulation
@@ -1203,6 +1235,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int nleg = t.nlegal[0];
 #pragma unroll
   for (int j = 0; j < 2; ++j) rleg[j] = j < A ? t.legal[j] : 0;
+  LZM_ISTAMP(28);
   LZM_STAMP(10);
 
   for (int k = 0; k < p.S; ++k) {
