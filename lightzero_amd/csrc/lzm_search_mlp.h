@@ -665,11 +665,14 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     s_mm[tid] = p.minmax[i0 + tid];
     s_vtp[tid] = p.vtp_in[i0 + tid];
   }
-  if (tid == 0) {
+  if (tid == 0) s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid < 64) {
+    // players (cnode.cpp:776-781) by wave 0, every load in flight at once
     int m = INT_MIN;
-    for (int i = 0; i < B; ++i) m = max(m, p.vtp_in[i]);
-    s_players = (m == -1) ? 1 : 2;
-    s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int q = tid; q < B; q += 64) m = max(m, p.vtp_in[q]);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+    if (tid == 0) s_players = (m == -1) ? 1 : 2;
   }
   __syncthreads();
   const int players = s_players;
