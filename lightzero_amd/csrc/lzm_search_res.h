@@ -900,6 +900,9 @@ __device__ inline Descent descend_terms_lane(const TreeView &t, const float2 *nq
 }
 
 // NR rows of a 128 x 128 layer (inputs x + r * 128): each weight read once for all rows.
+#ifndef LZM_RES_STAGE_WD1
+#define LZM_RES_STAGE_WD1 1
+#endif
 struct NoSide {
   __device__ __forceinline__ void operator()(int) const {}
 };
@@ -1381,6 +1384,13 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
     // ---- fc_dynamics[0], latent rows (streamed weights in P): shared by the speculative rows
     const float z0 = dense128(X0, [&](int j) { return P[j]; });
+#if LZM_RES_STAGE_WD1
+    // the stream buffer is free until the next pair's prefetch: stage fc_dynamics[1]'s LDS slots in
+    // it now, so the layer below reads registers (its LDS reads in flight during the action rows)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < kRSlotsD; ++j) P[j] = WD1[j * kRT + tid];
+#endif
     LZM_SUBSTAMP(16);
     // Rows: row r carries the network for action act_r. A tie between exactly two unexpanded
     // children (status 1) is evaluated speculatively for both (NR = 2) and resolved after the
@@ -1418,14 +1428,22 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // ---- fc_dynamics[1] (LDS weights) + latent residual -> next latent
     if (NR == 1 && late) {
       float z[2];
+#if LZM_RES_STAGE_WD1
+      dense128n<2>(T1, [&](int j) { return P[j]; }, z);
+#else
       dense128n<2>(T1, [&](int j) { return WD1[j * kRT + tid]; }, z);
+#endif
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) NL[r * kRHid + cD] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[cD];
       }
     } else {
       float z[NR];
+#if LZM_RES_STAGE_WD1
+      dense128n<NR>(T1, [&](int j) { return P[j]; }, z);
+#else
       dense128n<NR>(T1, [&](int j) { return WD1[j * kRT + tid]; }, z);
+#endif
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) NL[r * kRHid + cD] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[cD];
