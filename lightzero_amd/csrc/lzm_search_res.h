@@ -1573,10 +1573,11 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float rdec = (NR == 2 && row) ? dec[2 * NR - 2] : dec[0];  // static indices: no scratch
     const float vdec = (NR == 2 && row) ? dec[2 * NR - 1] : dec[1];
     LZM_STAMP(7);
-    // file the next latent (mcts_ctree.py:305): pool[k + 1][i]
-    if (tid < kRHid / 4)
-      reinterpret_cast<float4 *>(p.pool + ((size_t)(k + 1) * B + i) * kRHid)[tid] =
-          reinterpret_cast<const float4 *>(NLb + row * kRHid)[tid];
+    if (p.phase && tid == 0) sub_ = __builtin_amdgcn_s_memtime();
+    // file the next latent (mcts_ctree.py:305): pool[k + 1][i], by wave 1 (wave 0 expands)
+    if (tid >= 64 && tid < 64 + kRHid / 4)
+      reinterpret_cast<float4 *>(p.pool + ((size_t)(k + 1) * B + i) * kRHid)[tid - 64] =
+          reinterpret_cast<const float4 *>(NLb + row * kRHid)[tid - 64];
     if (p.rec_x && tid == 0) {
       p.rec_x[(size_t)k * B + i] = s_x;
       p.rec_a[(size_t)k * B + i] = s_act;
@@ -1589,7 +1590,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     // fc_dynamics[0] for the next simulation: wave 0 now, alone on the texture path (16 loads
     // issue in a few hundred cycles), waves 1-3 during the next walk, which only wave 0 runs
+    LZM_SUBSTAMP(29);
     if (wid == 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
+    LZM_SUBSTAMP(30);
     // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500), wave 0
     if (wid == 0) {
       const int len = s_len[0];
@@ -1597,6 +1600,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       int vtp = s_vtp;
       if (players > 1)
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
+      LZM_SUBSTAMP(31);
       expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA, -1, s_exptab);
       LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
