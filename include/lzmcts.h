@@ -282,12 +282,24 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
  * into lzm_conv_trunk_floats() floats (copy to the device, 16-byte aligned).
  * lzm_conv_trunk: input latent of env b = pool[(x[b] * B + b) * 4096 ..] (x nullable: pool[b * 4096]);
  * actmap float[A][64][64] (action planes' conv + dynamics bias), action int32[B];
- * outputs out_latent float[B][4096], out_r float[B][r_ch*64], out_h float[B][h_ch*64]. */
+ * outputs out_latent float[B][4096], out_r float[B][r_ch*64], out_h float[B][h_ch*64].
+ * The unsuffixed entry points run the exact-f32 matrix path (LZM_CONV_F32); the _p forms take the
+ * precision: LZM_CONV_F32 (v_mfma_f32_32x32x2_f32) or LZM_CONV_BF16X3 (each f32 operand split into
+ * three bf16 terms, six products per K on v_mfma_f32_16x16x32_bf16: f32-level error at 2.7x fewer
+ * matrix cycles). A blob packed for one precision must be run with the same precision. */
+#define LZM_CONV_F32 0
+#define LZM_CONV_BF16X3 1
 int64_t lzm_conv_trunk_floats(int n_dres, int n_pres);
 int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const float *raw, float *out_host);
 int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,
                    const float *pool, const int32_t *x, const int32_t *action, float *out_latent, float *out_r,
                    float *out_h, void *stream);
+int64_t lzm_conv_trunk_floats_p(int n_dres, int n_pres, int precision);
+int lzm_conv_trunk_prepare_p(int precision, int n_dres, int n_pres, int r_ch, int h_ch, const float *raw,
+                             float *out_host);
+int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
+                     const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
+                     float *out_latent, float *out_r, float *out_h, void *stream);
 
 /* The MLP heads of the conv recurrent step in one launch (lzm_heads.h): reward hidden from
  * r [B][Kr] (optionally relu(r * r_scale + r_shift), the EfficientZero value-prefix BatchNorm),

@@ -92,10 +92,13 @@ SIGNATURES = {
     "lzm_conv_trunk_floats": [_i, _i],
     "lzm_conv_trunk_prepare": [_i, _i, _i, _i, _vp, _vp],
     "lzm_conv_trunk": [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_conv_trunk_floats_p": [_i, _i, _i],
+    "lzm_conv_trunk_prepare_p": [_i, _i, _i, _i, _i, _vp, _vp],
+    "lzm_conv_trunk_p": [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
             "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64,
-            "lzm_conv_trunk_floats": ctypes.c_int64}
+            "lzm_conv_trunk_floats": ctypes.c_int64, "lzm_conv_trunk_floats_p": ctypes.c_int64}
 
 _lib = None
 

@@ -23,12 +23,15 @@ tensors change (version counters), so captured HIP graphs keep valid pointers.
 
 On the GPU the convolutional trunk (dynamics conv, residual blocks, reward 1x1, prediction blocks,
 head 1x1) is ONE hand-written HIP launch per simulation, one workgroup per env with the
-activations in LDS and f32 MFMA convolutions (csrc/lzm_conv.h, lzm_conv_trunk): it reads the leaf
+activations in LDS and split-bf16 MFMA convolutions (csrc/lzm_conv.h, lzm_conv_trunk_p; each f32
+operand as three bf16 terms, six products per K — f32-level error on the bf16 matrix path; the
+exact-f32 MFMA kernel stays selectable, precision='f32'): it reads the leaf
 latent straight from the search's latent pool and writes the next latent straight into the next
 pool slot (`step_from_pool`), so the gather and the pool filing kernels disappear too. The head
 MLPs (reward, value, policy; both layers, ReLUs, the EZ value-prefix BatchNorm) are ONE more
 launch (csrc/lzm_heads.h, lzm_conv_heads); the EfficientZero LSTM cell stays a batched GEMM.
 """
+import os
 import weakref
 from collections import OrderedDict
 
@@ -121,7 +124,16 @@ def fold_tensors(model):
 class FoldedConvNet:
     """recurrent_inference of a conv MuZeroModel / EfficientZeroModel with every BN folded."""
 
-    def __init__(self, model):
+    PRECISIONS = {"f32": 0, "bf16x3": 1}  # LZM_CONV_F32 / LZM_CONV_BF16X3 (include/lzmcts.h)
+
+    def __init__(self, model, precision=None):
+        """precision of the native trunk: 'bf16x3' (default: f32 operands split into three bf16
+        terms, six products per K on the bf16 matrix path, f32-level error) or 'f32' (the exact
+        f32 matrix path); LZM_CONV_PRECISION overrides the default."""
+        precision = precision or os.environ.get("LZM_CONV_PRECISION", "bf16x3")
+        if precision not in self.PRECISIONS:
+            raise ValueError(f"conv trunk precision {precision!r}: expected one of {sorted(self.PRECISIONS)}")
+        self.precision = precision
         self.model = model
         self.ez = hasattr(model.dynamics_network, "lstm")
         self.A = model.dynamics_network.action_encoding_dim
@@ -166,11 +178,12 @@ class FoldedConvNet:
         parts += [t["head_w"], t["head_b"]]
         raw = np.ascontiguousarray(torch.cat([p.reshape(-1) for p in parts]).cpu().numpy(), dtype=np.float32)
         L = _lib.load()
-        n = L.lzm_conv_trunk_floats(self.n_dres, self.n_pres)
+        prec = self.PRECISIONS[self.precision]
+        n = L.lzm_conv_trunk_floats_p(self.n_dres, self.n_pres, prec)
         host = np.zeros(n, np.float32)
         self.r_ch, self.h_ch = int(t["rw_w"].shape[0]), int(t["head_w"].shape[0])
-        _lib.check(L.lzm_conv_trunk_prepare(self.n_dres, self.n_pres, self.r_ch, self.h_ch,
-                                            raw.ctypes.data, host.ctypes.data), "lzm_conv_trunk_prepare")
+        _lib.check(L.lzm_conv_trunk_prepare_p(prec, self.n_dres, self.n_pres, self.r_ch, self.h_ch,
+                                              raw.ctypes.data, host.ctypes.data), "lzm_conv_trunk_prepare_p")
         blob = torch.from_numpy(host).to(dev)
         heads = self._pack_heads()
         if self.native is None:
@@ -214,7 +227,8 @@ class FoldedConvNet:
         act = action if action.dtype == torch.int32 else action.to(torch.int32)
         r = torch.empty((B, self.r_ch * 64), dtype=torch.float32, device=out_latent.device)
         h = torch.empty((B, self.h_ch * 64), dtype=torch.float32, device=out_latent.device)
-        _lib.call("lzm_conv_trunk", B, self.n_dres, self.n_pres, self.r_ch, self.h_ch, _lib.ptr(self.native),
+        _lib.call("lzm_conv_trunk_p", self.PRECISIONS[self.precision], B, self.n_dres, self.n_pres, self.r_ch,
+                  self.h_ch, _lib.ptr(self.native),
                   _lib.ptr(self.actmap), _lib.ptr(pool), _lib.ptr(x), _lib.ptr(act.contiguous()), _lib.ptr(out_latent),
                   _lib.ptr(r), _lib.ptr(h), _lib.stream_ptr())
         return r, h

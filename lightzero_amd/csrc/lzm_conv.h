@@ -200,6 +200,339 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
                            abase);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Split-bf16 trunk (precision 1, the default): the same network on v_mfma_f32_16x16x32_bf16.
+//
+// Every f32 operand x is held as three bf16 terms x = h + m + l (h = bf16(x), m = bf16(x - h),
+// l = bf16(x - h - m); each subtraction is exact, so h + m carries 16 significant bits and h + m + l
+// the full 24 in all but carry cases). A product is summed from the six terms whose magnitude is
+// >= 2^-16 of h_a h_b: l_a h_b, h_a l_b, m_a m_b, m_a h_b, h_a m_b, h_a h_b (the dropped m l, l m, l l
+// terms are <= 2^-24 relative: f32 round-off). The bf16 matrix rate is 16x the f32 one
+// (MI355X_MICROARCH.md constants: 16x16x32 bf16 16 cycles vs 32x32x2 f32 64 cycles, 16x the K), so
+// six products per K are 2.7x fewer matrix cycles than the exact-f32 kernel above.
+//
+// Layout. Wave w owns out-channels 16w..16w+15 for all 64 pixels (four 16-pixel M tiles), so the four
+// waves stream disjoint weights (221 KB per 3x3 layer per workgroup, vs 295 KB when two waves of
+// the f32 tiling share a half). K = tap-major (9 taps) x 64 in-channels, in 18 chunks of 32.
+// Activations live in LDS as the three bf16 planes of each buffer, [100 bordered positions][64 ch],
+// 16-B chunk c of position ps stored at chunk c ^ ((ps % 10) & 7): the A-fragment reads (lane:
+// pixel l&15 of the tile, channels 8(l>>4)..+7 of the chunk, one ds_read_b128) are then
+// conflict-free for every tap (checked over the four lane groups of ds_read_b128).
+// B fragments come from the host-packed [wave][chunk][term][lane][8 bf16] layout, one 1 KiB
+// dwordx4 wave-load per term, a ring of kBxRing chunks issued kBxAhead ahead.
+constexpr int kBxComp = 100 * 64;                  // bf16 per term plane
+constexpr int kBxBuf = 3 * kBxComp;                // bf16 per activation buffer (h, m, l); two buffers
+constexpr int kBx3Frag = 4 * 18 * 3 * 64 * 4;      // floats: [wave][chunk][term][lane][8 bf16]
+constexpr int kBx1Frag = 2 * 2 * 3 * 64 * 4;       // 1x1 64->32: [wave 0..1][chunk][term][lane][8 bf16]
+constexpr int kBxBlock = 2 * kBx3Frag + 2 * kCvCh;
+constexpr int kBxAhead = 3;  // default weight read-ahead (chunks)
+
+typedef __bf16 bxv8 __attribute__((ext_vector_type(8)));
+typedef float bxf4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline uint16_t bx_rn(float x) {  // f32 -> bf16, round to nearest even (finite x)
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__host__ __device__ inline float bx_f(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float x;
+  memcpy(&x, &u, 4);
+  return x;
+}
+__host__ __device__ inline void bx_split(float x, uint16_t &h, uint16_t &m, uint16_t &l) {
+  h = bx_rn(x);
+  const float r = x - bx_f(h);
+  m = bx_rn(r);
+  l = bx_rn(r - bx_f(m));
+}
+
+// the same split on the device with the hardware conversion (v_cvt_pk_bf16_f32, round to nearest even)
+__device__ __forceinline__ void bx_split_d(float x, uint16_t &h, uint16_t &m, uint16_t &l) {
+  const __bf16 hb = (__bf16)x;
+  const float r = x - (float)hb;
+  const __bf16 mb = (__bf16)r;
+  const __bf16 lb = (__bf16)(r - (float)mb);
+  h = __builtin_bit_cast(uint16_t, hb);
+  m = __builtin_bit_cast(uint16_t, mb);
+  l = __builtin_bit_cast(uint16_t, lb);
+}
+
+__host__ __device__ inline ConvTrunkLayout conv_trunk_layout_p(int n_dres, int n_pres, int precision) {
+  if (precision == 0) return conv_trunk_layout(n_dres, n_pres);
+  ConvTrunkLayout L;
+  int o = 0;
+  L.dyn = o; o += kBx3Frag;
+  L.dres = o; o += n_dres * kBxBlock;
+  L.rw = o; o += kBx1Frag;
+  L.rb = o; o += 32;
+  L.pres = o; o += n_pres * kBxBlock;
+  L.hw = o; o += kBx1Frag;
+  L.hb = o; o += 32;
+  L.total = o;
+  return L;
+}
+
+// element offset (bf16) of (bordered position ps, channel c) inside one term plane
+__device__ __forceinline__ int bx_at(int ps, int c) { return ps * 64 + ((((c >> 3) ^ (ps % 10)) & 7) << 3) + (c & 7); }
+
+__device__ __forceinline__ float bx_load(const uint16_t *buf, int ps, int c) {
+  const int o = bx_at(ps, c);
+  return (bx_f(buf[o]) + bx_f(buf[kBxComp + o])) + bx_f(buf[2 * kBxComp + o]);
+}
+
+__device__ __forceinline__ void bx_store(uint16_t *buf, int ps, int c, float v) {
+  uint16_t h, m, l;
+  bx_split_d(v, h, m, l);
+  const int o = bx_at(ps, c);
+  buf[o] = h;
+  buf[kBxComp + o] = m;
+  buf[2 * kBxComp + o] = l;
+}
+
+__device__ __forceinline__ bxv8 bx_as(uint4 u) { return __builtin_bit_cast(bxv8, u); }
+
+// Weight ring of one wave: RING chunks x 3 terms (one uint4 per lane each).
+template <int AHEAD>
+struct BxRing {
+  uint4 w[AHEAD + 1][3];
+};
+
+template <int AHEAD, int DIAG>
+__device__ __forceinline__ void bx_load_w(BxRing<AHEAD> &r, const uint4 *__restrict__ wf, int s, int lane) {
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+    r.w[s % (AHEAD + 1)][q] = DIAG == 1 ? uint4{(uint32_t)(lane + s), 1u, 2u, 3u} : wf[(s * 3 + q) * 64 + lane];
+}
+
+// a conv's first chunks of weights; issued early (before the previous layer's epilogue and barrier)
+template <int NCH, int AHEAD, int DIAG>
+__device__ __forceinline__ void bx_prefetch(BxRing<AHEAD> &r, const uint4 *__restrict__ wf, int lane) {
+#pragma unroll
+  for (int s = 0; s < (NCH < AHEAD ? NCH : AHEAD); ++s) bx_load_w<AHEAD, DIAG>(r, wf, s, lane);
+}
+
+// one convolution for this wave's 16 out-channels x 64 pixels: NCH = 18 chunks (3x3) or 2 (1x1), its
+// first AHEAD chunks already in the ring (bx_prefetch). DIAG = 1: no weight loads (timing
+// experiments only, results invalid). Software pipeline, in issue order (the scheduling barriers keep
+// the compiler from sinking loads next to their first use): weights of chunk s + AHEAD, activations
+// of chunk s + 1, then chunk s's 24 MFMAs.
+template <int NCH, int AHEAD, int DIAG>
+__device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restrict__ wf, BxRing<AHEAD> &r, int lane,
+                                        bxf4 (&acc)[4]) {
+  uint4 a[2][4][3];
+  const int px = lane & 7, g = lane >> 4;
+  // lane's pixel in tile t: p = 16t + (lane & 15), plane row py = 2t + ((lane >> 3) & 1), column px; tap
+  // (dy, dx) reads bordered position (py + dy) * 10 + px + dx
+  const int lbase = ((lane >> 3) & 1) * 10 + px;
+  auto load_a = [&](int s) {
+    const int tap = NCH == 2 ? 4 : s >> 1, j = NCH == 2 ? s : s & 1;
+    const int dy = tap / 3, dx = tap % 3;
+    const int chunk = ((4 * j + g) ^ (px + dx)) & 7;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int ps = lbase + (2 * t + dy) * 10 + dx;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        a[s & 1][t][q] = *reinterpret_cast<const uint4 *>(in + q * kBxComp + ps * 64 + chunk * 8);
+    }
+  };
+  load_a(0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = bxf4{0.f, 0.f, 0.f, 0.f};
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int s = 0; s < NCH; ++s) {
+    if (s + AHEAD < NCH) bx_load_w<AHEAD, DIAG>(r, wf, s + AHEAD, lane);
+    if (s + 1 < NCH) load_a(s + 1);
+    const uint4 *w = r.w[s % (AHEAD + 1)];
+    const uint4(&x)[4][3] = a[s & 1];
+    // small terms first: l_a h_b, h_a l_b, m_a m_b, m_a h_b, h_a m_b, h_a h_b
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][0]), bx_as(w[2]), acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][1]), bx_as(w[1]), acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][1]), bx_as(w[0]), acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][0]), bx_as(w[1]), acc[t], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
+    // issue the next chunks' loads in the MFMA gaps (an MFMA holds the vector issue for half its
+    // cycles): weights first (they have the longest way), then one activation read per MFMA
+    const int nw = (s + AHEAD < NCH && DIAG != 1) ? 3 : 0, na = s + 1 < NCH ? 12 : 0;
+#pragma unroll
+    for (int k = 0; k < nw; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+    }
+#pragma unroll
+    for (int k = 0; k < na; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    }
+#pragma unroll
+    for (int k = 0; k < 24 - nw - na; ++k) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Accumulator (t, r) of a lane is out-channel c = 16 wave + (lane & 15) at pixel
+// p = 16t + 4 (lane >> 4) + r: plane row 2t + (lane >> 5), column 4 ((lane >> 4) & 1) + r. The same lane
+// owns the same (c, p) in every layer, so a residual block's input stays in that lane's registers
+// (exact f32) and is added in the block's second epilogue without an LDS round trip.
+__device__ __forceinline__ int bx_ep_pos(int lane, int t, int r) {
+  return (2 * t + (lane >> 5) + 1) * 10 + 4 * ((lane >> 4) & 1) + r + 1;
+}
+
+// 3x3 epilogue: v = relu(acc + bias [+ amap] [+ xres]) -> split LDS planes of `out`; KEEP: xres = v
+__device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out, float bc, bool use_am,
+                                             const float4 (&am)[4], float (&xres)[16], bool add_res, bool keep,
+                                             int lane, int c) {
+  const int cb = c >> 3, ce = c & 7;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ps = bx_ep_pos(lane, t, r);
+      float v = acc[t][r] + bc;
+      if (use_am) v += r == 0 ? am[t].x : r == 1 ? am[t].y : r == 2 ? am[t].z : am[t].w;
+      if (add_res) v += xres[4 * t + r];
+      v = v > 0.f ? v : 0.f;
+      if (keep) xres[4 * t + r] = v;
+      // swizzle key (ps % 10) & 7 = column + 1
+      const int o = ps * 64 + (((cb ^ (4 * ((lane >> 4) & 1) + r + 1)) & 7) << 3) + ce;
+      uint16_t h, m, l;
+      bx_split_d(v, h, m, l);
+      out[o] = h;
+      out[kBxComp + o] = m;
+      out[2 * kBxComp + o] = l;
+    }
+}
+
+// 1x1 layer (<= 32 out channels, waves 0 and 1): relu(conv + b) -> global [c][p]
+template <int DIAG>
+__device__ __forceinline__ void bx_conv1_layer(const uint16_t *in, const float *__restrict__ wl,
+                                               const float *__restrict__ bias, int nch, float *dst, int lane,
+                                               int wv) {
+  BxRing<2> r1;
+  const uint4 *wf = reinterpret_cast<const uint4 *>(wl) + wv * 2 * 3 * 64;
+  bx_prefetch<2, 2, DIAG>(r1, wf, lane);
+  const int c = 16 * wv + (lane & 15);
+  const float bc = c < nch ? bias[c] : 0.f;
+  bxf4 acc[4];
+  bx_conv<2, 2, DIAG>(in, wf, r1, lane, acc);
+  if (c >= nch) return;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    float4 v;
+    v.x = fmaxf(acc[t][0] + bc, 0.f);
+    v.y = fmaxf(acc[t][1] + bc, 0.f);
+    v.z = fmaxf(acc[t][2] + bc, 0.f);
+    v.w = fmaxf(acc[t][3] + bc, 0.f);
+    *reinterpret_cast<float4 *>(dst + c * kCvPix + 16 * t + 4 * (lane >> 4)) = v;
+  }
+}
+
+// The 3x3 layers in order: 0 = dynamics conv, then two per residual block (dynamics blocks, then
+// prediction blocks); the reward 1x1 follows layer 2 n_dres, the head 1x1 the last one. Activations
+// ping-pong between two LDS buffers (layer i reads buffer i & 1): residuals travel in registers.
+__device__ __forceinline__ int bx_layer_off(const ConvTrunkLayout &L, int n_dres, int i) {
+  if (i == 0) return L.dyn;
+  const int j = i - 1, base = j < 2 * n_dres ? L.dres : L.pres, k = j < 2 * n_dres ? j : j - 2 * n_dres;
+  return base + (k >> 1) * kBxBlock + (k & 1) * (kBx3Frag + kCvCh);
+}
+
+template <int AHEAD, int DIAG>
+__global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_trunk_bx_kernel(
+    ConvTrunkArgs a) {
+  extern __shared__ uint4 bx_lds4[];
+  uint16_t *lds = reinterpret_cast<uint16_t *>(bx_lds4);
+  auto buf = [&](int i) { return lds + i * kBxBuf; };
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int c = 16 * wv + (lane & 15);
+  const ConvTrunkLayout L = conv_trunk_layout_p(a.n_dres, a.n_pres, 1);
+  const int n3 = 1 + 2 * a.n_dres + 2 * a.n_pres;
+  auto layer_w = [&](int i) { return a.w + bx_layer_off(L, a.n_dres, i); };
+  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * 3 * 64; };
+  BxRing<AHEAD> ring;
+  bx_prefetch<18, AHEAD, DIAG>(ring, wave_stream(a.w + L.dyn), lane);
+  // the input latent: this lane's 16 values in registers (the dynamics residual, exact f32) ...
+  const float *src = a.pool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
+  float xres[16];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * t + 4 * (lane >> 4));
+    xres[4 * t] = v.x; xres[4 * t + 1] = v.y; xres[4 * t + 2] = v.z; xres[4 * t + 3] = v.w;
+  }
+  // ... and all of it split into buffer 0 (borders zero)
+  for (int i = tid; i < 2 * kBxBuf / 8; i += kCvThreads) bx_lds4[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  for (int i = tid; i < kCvCh * kCvPix; i += kCvThreads) bx_store(buf(0), cv_plane(i & 63), i >> 6, src[i]);
+  __syncthreads();
+  for (int i = 0; i < n3; ++i) {
+    const float *w = layer_w(i);
+    const bool second = i > 0 && ((i - 1) & 1);  // a block's second conv: + residual, new block input
+    // epilogue operands first (vmcnt counts in order: they must not queue behind the next prefetch)
+    const float bc = i ? w[kBx3Frag + c] : 0.f;
+    float4 am[4] = {};
+    if (i == 0) {
+      const float4 *amap = reinterpret_cast<const float4 *>(a.actmap + ((int64_t)a.action[b] * kCvCh + c) * kCvPix);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) am[t] = amap[4 * t + (lane >> 4)];
+    }
+    bxf4 acc[4];
+    bx_conv<18, AHEAD, DIAG>(buf(i & 1), wave_stream(w), ring, lane, acc);
+    if (i + 1 < n3) bx_prefetch<18, AHEAD, DIAG>(ring, wave_stream(layer_w(i + 1)), lane);
+    bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
+    __syncthreads();
+    if (i == 2 * a.n_dres) {  // the next latent (registers, exact) and the reward planes
+      float *dst = a.out_latent + (int64_t)b * kCvCh * kCvPix + c * kCvPix + 4 * (lane >> 4);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        *reinterpret_cast<float4 *>(dst + 16 * t) = float4{xres[4 * t], xres[4 * t + 1], xres[4 * t + 2], xres[4 * t + 3]};
+      if (wv < 2)
+        bx_conv1_layer<DIAG>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_ch * kCvPix,
+                             lane, wv);
+    }
+  }
+  if (wv < 2)
+    bx_conv1_layer<DIAG>(buf(n3 & 1), a.w + L.hw, a.w + L.hb, a.h_ch, a.out_h + (int64_t)b * a.h_ch * kCvPix, lane, wv);
+}
+
+// host packing for the split trunk. 3x3: W[64 out][64 in][9] -> [wave][chunk s][term][lane][8]:
+// chunk s = 2 * tap + j, lane -> (out 16 * wave + (lane & 15), in 32 j + 8 (lane >> 4) + e)
+inline void bx_pack3(const float *W, float *outf) {
+  uint16_t *out = reinterpret_cast<uint16_t *>(outf);
+  for (int w = 0; w < 4; ++w)
+    for (int s = 0; s < 18; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < 8; ++e) {
+          const int tap = s >> 1, j = s & 1, cin = 32 * j + 8 * (lane >> 4) + e, cout = 16 * w + (lane & 15);
+          uint16_t t[3];
+          bx_split(W[(cout * 64 + cin) * 9 + tap], t[0], t[1], t[2]);
+          for (int q = 0; q < 3; ++q) out[(((w * 18 + s) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+        }
+}
+
+// 1x1: W[n <= 32 out][64 in] -> [wave 0..1][chunk j][term][lane][8], zero columns past n
+inline void bx_pack1(const float *W, int n, float *outf) {
+  uint16_t *out = reinterpret_cast<uint16_t *>(outf);
+  for (int w = 0; w < 2; ++w)
+    for (int j = 0; j < 2; ++j)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < 8; ++e) {
+          const int cin = 32 * j + 8 * (lane >> 4) + e, cout = 16 * w + (lane & 15);
+          uint16_t t[3] = {0, 0, 0};
+          if (cout < n) bx_split(W[cout * 64 + cin], t[0], t[1], t[2]);
+          for (int q = 0; q < 3; ++q) out[(((w * 2 + j) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+        }
+}
+
 // host packing: natural layouts -> fragment layouts
 // 3x3: W[64 out][64 in][9]  ->  [half][s4][lane][q], step s = 4*s4 + q = tap*32 + c2,
 //      lane -> (in = 2*c2 + lane/32, out = 32*half + lane%32)

@@ -2273,44 +2273,57 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
 }
 
 
-int64_t lzm_conv_trunk_floats(int n_dres, int n_pres) {
-  if (n_dres < 0 || n_pres < 0 || n_dres > 8 || n_pres > 8) return -1;
-  return conv_trunk_layout(n_dres, n_pres).total;
+int64_t lzm_conv_trunk_floats_p(int n_dres, int n_pres, int precision) {
+  if (n_dres < 0 || n_pres < 0 || n_dres > 8 || n_pres > 8 || (precision != LZM_CONV_F32 && precision != LZM_CONV_BF16X3))
+    return -1;
+  return conv_trunk_layout_p(n_dres, n_pres, precision).total;
 }
 
-int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const float *raw, float *out) {
-  if (lzm_conv_trunk_floats(n_dres, n_pres) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 || h_ch > 32 || !raw || !out) {
-    set_err("lzm_conv_trunk_prepare: need 0..8 residual blocks, 1..32 reward / head channels and buffers");
+int64_t lzm_conv_trunk_floats(int n_dres, int n_pres) { return lzm_conv_trunk_floats_p(n_dres, n_pres, LZM_CONV_F32); }
+
+int lzm_conv_trunk_prepare_p(int precision, int n_dres, int n_pres, int r_ch, int h_ch, const float *raw, float *out) {
+  if (lzm_conv_trunk_floats_p(n_dres, n_pres, precision) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 || h_ch > 32 ||
+      !raw || !out) {
+    set_err("lzm_conv_trunk_prepare: need 0..8 residual blocks, 1..32 reward / head channels, a known precision and "
+            "buffers");
     return LZM_ERR_ARG;
   }
-  const ConvTrunkLayout L = conv_trunk_layout(n_dres, n_pres);
+  const bool bx = precision == LZM_CONV_BF16X3;
+  const ConvTrunkLayout L = conv_trunk_layout_p(n_dres, n_pres, precision);
+  const int frag3 = bx ? kBx3Frag : kCv3Frag, block = bx ? kBxBlock : kCvBlock;
+  auto pack3 = [&](const float *W, float *o) { bx ? bx_pack3(W, o) : conv_pack3(W, o); };
+  auto pack1 = [&](const float *W, int n, float *o) { bx ? bx_pack1(W, n, o) : conv_pack1(W, n, o); };
   memset(out, 0, sizeof(float) * (size_t)L.total);
   const float *r = raw;
   const int W3 = 64 * 64 * 9;
-  conv_pack3(r, out + L.dyn); r += W3;
+  pack3(r, out + L.dyn); r += W3;
   auto blocks = [&](int n, int base) {
     for (int k = 0; k < n; ++k) {
-      float *o = out + base + k * kCvBlock;
-      conv_pack3(r, o); r += W3;
-      memcpy(o + kCv3Frag, r, 64 * sizeof(float)); r += 64;
-      conv_pack3(r, o + kCv3Frag + 64); r += W3;
-      memcpy(o + 2 * kCv3Frag + 64, r, 64 * sizeof(float)); r += 64;
+      float *o = out + base + k * block;
+      pack3(r, o); r += W3;
+      memcpy(o + frag3, r, 64 * sizeof(float)); r += 64;
+      pack3(r, o + frag3 + 64); r += W3;
+      memcpy(o + 2 * frag3 + 64, r, 64 * sizeof(float)); r += 64;
     }
   };
   blocks(n_dres, L.dres);
-  conv_pack1(r, r_ch, out + L.rw); r += r_ch * 64;
+  pack1(r, r_ch, out + L.rw); r += r_ch * 64;
   memcpy(out + L.rb, r, r_ch * sizeof(float)); r += r_ch;
   blocks(n_pres, L.pres);
-  conv_pack1(r, h_ch, out + L.hw); r += h_ch * 64;
+  pack1(r, h_ch, out + L.hw); r += h_ch * 64;
   memcpy(out + L.hb, r, h_ch * sizeof(float));
   return LZM_OK;
 }
 
-int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,
-                   const float *pool, const int32_t *x, const int32_t *action, float *out_latent, float *out_r,
-                   float *out_h, void *stream) {
-  if (B <= 0 || lzm_conv_trunk_floats(n_dres, n_pres) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 || h_ch > 32 ||
-      !weights || !actmap || !pool || !action || !out_latent || !out_r || !out_h) {
+int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const float *raw, float *out) {
+  return lzm_conv_trunk_prepare_p(LZM_CONV_F32, n_dres, n_pres, r_ch, h_ch, raw, out);
+}
+
+int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
+                     const float *actmap, const float *pool, const int32_t *x, const int32_t *action, float *out_latent,
+                     float *out_r, float *out_h, void *stream) {
+  if (B <= 0 || lzm_conv_trunk_floats_p(n_dres, n_pres, precision) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 ||
+      h_ch > 32 || !weights || !actmap || !pool || !action || !out_latent || !out_r || !out_h) {
     set_err("lzm_conv_trunk: bad arguments");
     return LZM_ERR_ARG;
   }
@@ -2318,19 +2331,45 @@ int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const floa
     set_err("lzm_conv_trunk: weights and pool must be 16-byte aligned");
     return LZM_ERR_ARG;
   }
+  const bool bx = precision == LZM_CONV_BF16X3;
+  // split-bf16 variants: weight read-ahead depth (LZM_CONV_AHEAD) and timing-only ablations
+  // (LZM_CONV_DIAG=1: no weight loads; results invalid)
+  typedef void (*bx_fn)(ConvTrunkArgs);
+  static const int ahead = getenv("LZM_CONV_AHEAD") ? atoi(getenv("LZM_CONV_AHEAD")) : kBxAhead;
+  static const int diag = getenv("LZM_CONV_DIAG") ? atoi(getenv("LZM_CONV_DIAG")) : 0;
+  const bx_fn bx_kernel = diag == 1   ? conv_trunk_bx_kernel<kBxAhead, 1>
+                          : ahead == 8 ? conv_trunk_bx_kernel<8, 0>
+                          : ahead == 5 ? conv_trunk_bx_kernel<5, 0>
+                                       : conv_trunk_bx_kernel<kBxAhead, 0>;
   static std::once_flag once;
   static hipError_t attr_err = hipSuccess;
-  const size_t lds = 3 * kCvBuf * sizeof(float);
+  const size_t lds_f32 = 3 * kCvBuf * sizeof(float), lds_bx = 2 * kBxBuf * sizeof(uint16_t);
   std::call_once(once, [&] {
-    attr_err = hipFuncSetAttribute((const void *)conv_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_err = hipFuncSetAttribute((const void *)conv_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)lds_f32);
+    const bx_fn all[] = {conv_trunk_bx_kernel<kBxAhead, 0>, conv_trunk_bx_kernel<kBxAhead, 1>,
+                         conv_trunk_bx_kernel<8, 0>, conv_trunk_bx_kernel<5, 0>};
+    for (bx_fn f : all)
+      if (attr_err == hipSuccess)
+        attr_err = hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bx);
   });
   LZM_HIP(attr_err);
   ConvTrunkArgs a;
   a.B = B; a.n_dres = n_dres; a.n_pres = n_pres; a.r_ch = r_ch; a.h_ch = h_ch; a.w = weights; a.actmap = actmap;
   a.pool = pool; a.x = x; a.action = action; a.out_latent = out_latent; a.out_r = out_r; a.out_h = out_h;
-  hipLaunchKernelGGL(conv_trunk_kernel, dim3(B), dim3(kCvThreads), lds, (hipStream_t)stream, a);
+  if (bx)
+    hipLaunchKernelGGL(bx_kernel, dim3(B), dim3(kCvThreads), lds_bx, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(conv_trunk_kernel, dim3(B), dim3(kCvThreads), lds_f32, (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
+}
+
+int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,
+                   const float *pool, const int32_t *x, const int32_t *action, float *out_latent, float *out_r,
+                   float *out_h, void *stream) {
+  return lzm_conv_trunk_p(LZM_CONV_F32, B, n_dres, n_pres, r_ch, h_ch, weights, actmap, pool, x, action, out_latent,
+                          out_r, out_h, stream);
 }
 
 }  // extern "C"

@@ -62,3 +62,34 @@ def test_easydict_semantics():
     assert d.model.support_scale == 300
     d.update(dict(b=2))
     assert d.b == 2
+
+
+def test_split_bf16_trunk_packing_recovers_f32_weights():
+    """lzm_conv_trunk_prepare_p(LZM_CONV_BF16X3) (host code, no GPU): every packed weight's three bf16
+    terms h + m + l give back the f32 weight (within 2^-24 relative), h is the round-to-nearest bf16 of
+    the weight, and the [wave][chunk][term][lane][8] fragment map puts W[out][in][tap] where the
+    16x16x32 B operand expects it (out 16 wave + lane % 16, in 32 j + 8 (lane / 16) + e, chunk 2 tap + j)"""
+    import ctypes
+    import numpy as np
+    L = _lib.load()
+    n_dres, n_pres, r_ch, h_ch = 1, 1, 16, 32
+    W3 = 64 * 64 * 9
+    nraw = W3 + n_dres * 2 * (W3 + 64) + r_ch * 64 + r_ch + n_pres * 2 * (W3 + 64) + h_ch * 64 + h_ch
+    rng = np.random.default_rng(0)
+    raw = (rng.standard_normal(nraw) * 0.05).astype(np.float32)
+    n = L.lzm_conv_trunk_floats_p(n_dres, n_pres, 1)
+    assert n > 0 and L.lzm_conv_trunk_floats_p(n_dres, n_pres, 7) < 0
+    out = np.zeros(n, np.float32)
+    assert L.lzm_conv_trunk_prepare_p(1, n_dres, n_pres, r_ch, h_ch, ctypes.c_void_p(raw.ctypes.data),
+                                      ctypes.c_void_p(out.ctypes.data)) == 0
+    u = out.view(np.uint16)[: 4 * 18 * 3 * 64 * 8 * 2 // 2].reshape(4, 18, 3, 64, 8)  # dynamics conv blob
+    terms = (u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+    rec = terms.sum(axis=2)  # [w][s][lane][e]
+    W = raw[:W3].reshape(64, 64, 9).astype(np.float64)
+    w_, s_, l_, e_ = np.meshgrid(np.arange(4), np.arange(18), np.arange(64), np.arange(8), indexing="ij")
+    cout = 16 * w_ + (l_ & 15)
+    cin = 32 * (s_ & 1) + 8 * (l_ >> 4) + e_
+    want = W[cout, cin, s_ >> 1]
+    np.testing.assert_allclose(rec, want, rtol=2.0 ** -23, atol=0)
+    hi = terms[:, :, 0]
+    assert np.all(np.abs(hi - want) <= np.abs(want) * 2.0 ** -8)

@@ -163,12 +163,14 @@ def test_conv_search_graph_replay_equals_eager(kind):
         np.testing.assert_allclose(graph["values"], eager["values"], rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("precision", ["bf16x3", "f32"])
 @pytest.mark.parametrize("kind", ["ez", "mz"])
-def test_native_trunk_matches_module(kind):
-    """lzm_conv_trunk (+ batched heads) == the module's recurrent_inference (fp32, rtol 1e-4 / atol 1e-5)"""
+def test_native_trunk_matches_module(kind, precision):
+    """lzm_conv_trunk_p (+ batched heads) == the module's recurrent_inference (fp32, rtol 1e-4 / atol 1e-5),
+    for the split-bf16 trunk (the default) and the exact-f32 one"""
     from lightzero_amd.conv_infer import FoldedConvNet
     model = conv_model(kind, 5)
-    net = FoldedConvNet(model)
+    net = FoldedConvNet(model, precision=precision)
     assert net.native is not None, "native trunk not packed on the GPU"
     B = 37
     g = torch.Generator(device=DEV).manual_seed(0)
@@ -291,3 +293,25 @@ def test_heads_kernel_verdict_words(B):
                 exp[q] = int(ok[2 * q:2 * q + 2].all())
             assert np.array_equal(w[:, h], exp), (normalised, h)
         assert w.all() == normalised
+
+
+@pytest.mark.parametrize("kind", ["ez", "mz"])
+def test_split_bf16_trunk_close_to_exact_f32(kind):
+    """the split-bf16 trunk (six bf16 products per K) against the exact-f32 MFMA trunk on the same
+    folded weights: next latents and head planes agree to f32 round-off (rtol 2e-5 / atol 2e-6), and
+    the reported worst relative gap is far below the module tolerance"""
+    from lightzero_amd.conv_infer import FoldedConvNet
+    model = conv_model(kind, 9)
+    nets = {p: FoldedConvNet(model, precision=p) for p in ("f32", "bf16x3")}
+    B = 64
+    g = torch.Generator(device=DEV).manual_seed(4)
+    pool = torch.relu(torch.randn(3, B, 64, 8, 8, generator=g, device=DEV))
+    x = torch.randint(0, 3, (B,), generator=g, device=DEV).to(torch.int32)
+    act = torch.randint(0, model.action_space_size, (B,), generator=g, device=DEV).to(torch.int32)
+    outs = {}
+    for p, net in nets.items():
+        lat = torch.empty(B, 64, 8, 8, device=DEV)
+        r, h = net._trunk(pool, x, act, lat)
+        outs[p] = (lat, r, h)
+    for a, b in zip(outs["bf16x3"], outs["f32"]):
+        torch.testing.assert_close(a, b, rtol=2e-5, atol=2e-6)

@@ -8,6 +8,7 @@ and prints one JSON line with sims/s, the network FLOPs per simulation (torch Fl
 one recurrent_inference at batch B) and the achieved network TFLOP/s against the fp32 MFMA peak.
 
     python tools/conv_bench.py --kind ez|mz [--envs 256] [--sims 50] [--searches 5] [--graph 1]
+                               [--precision bf16x3|f32]
 """
 import argparse
 import json
@@ -49,7 +50,12 @@ def main():
     ap.add_argument("--searches", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--graph", type=int, default=1)
+    ap.add_argument("--precision", choices=["bf16x3", "f32"], default=None,
+                    help="native conv trunk precision (default: LZM_CONV_PRECISION or bf16x3)")
     a = ap.parse_args()
+    if a.precision:
+        os.environ["LZM_CONV_PRECISION"] = a.precision
+    precision = os.environ.get("LZM_CONV_PRECISION", "bf16x3")
     dev = torch.device("cuda", 0)
     B, S = a.envs, a.sims
     torch.manual_seed(0)
@@ -95,7 +101,8 @@ def main():
         "metric": "MCTS simulations/sec", "value": B * S / dt, "unit": "sims/s", "ms_per_search": dt * 1e3,
         "config": {"workload": "C3 Pong EfficientZero" if a.kind == "ez" else "C5 Breakout MuZero (per GPU)",
                    "envs": B, "num_simulations": S, "actions": A, "support": 2 * scale + 1, "latent": [64, 8, 8],
-                   "path": "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph)},
+                   "path": "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph),
+                   "conv_precision": precision},
         "net_flops_per_sim": flops, "net_tflops_whole_search": net_tflops,
         "fp32_mfma_peak_tflops": FP32_MFMA_PEAK_TFLOPS, "net_frac_of_peak": net_tflops / FP32_MFMA_PEAK_TFLOPS}))
 
