@@ -393,25 +393,42 @@ __device__ __forceinline__ int bx_ep_pos(int lane, int t, int r) {
 __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out, float bc, bool use_am,
                                              const float4 (&am)[4], float (&xres)[16], bool add_res, bool keep,
                                              int lane, int c) {
-  const int cb = c >> 3, ce = c & 7;
+  typedef float bxf2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bxb2 __attribute__((ext_vector_type(2)));
+  const int cb = c >> 3, odd = lane & 1;
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+  for (int t = 0; t < 4; ++t) {
+    float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int ps = bx_ep_pos(lane, t, r);
-      float v = acc[t][r] + bc;
-      if (use_am) v += r == 0 ? am[t].x : r == 1 ? am[t].y : r == 2 ? am[t].z : am[t].w;
-      if (add_res) v += xres[4 * t + r];
-      v = v > 0.f ? v : 0.f;
-      if (keep) xres[4 * t + r] = v;
-      // swizzle key (ps % 10) & 7 = column + 1
-      const int o = ps * 64 + (((cb ^ (4 * ((lane >> 4) & 1) + r + 1)) & 7) << 3) + ce;
-      uint16_t h, m, l;
-      bx_split_d(v, h, m, l);
-      out[o] = h;
-      out[kBxComp + o] = m;
-      out[2 * kBxComp + o] = l;
+      float x = acc[t][r] + bc;
+      if (use_am) x += r == 0 ? am[t].x : r == 1 ? am[t].y : r == 2 ? am[t].z : am[t].w;
+      if (add_res) x += xres[4 * t + r];
+      x = x > 0.f ? x : 0.f;
+      if (keep) xres[4 * t + r] = x;
+      v[r] = x;
     }
+    // lanes 2j, 2j + 1 hold channels c, c + 1 (one dword of a plane row): per pixel pair (2k, 2k + 1)
+    // the even lane writes pixel 2k's dword and the odd lane pixel 2k + 1's, after one DPP swap
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const float send = odd ? v[2 * k] : v[2 * k + 1];
+      const float recv = __builtin_bit_cast(
+          float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+      const bxf2 pr = odd ? bxf2{recv, v[2 * k + 1]} : bxf2{v[2 * k], recv};  // (channel c & ~1, channel c | 1)
+      const bxb2 h = __builtin_convertvector(pr, bxb2);
+      const bxf2 r1 = pr - __builtin_convertvector(h, bxf2);
+      const bxb2 m = __builtin_convertvector(r1, bxb2);
+      const bxb2 l = __builtin_convertvector(r1 - __builtin_convertvector(m, bxf2), bxb2);
+      const int r = 2 * k + odd;
+      const int ps = bx_ep_pos(lane, t, r);
+      // swizzle key (ps % 10) & 7 = column + 1; the pair's dword at channel c & ~1
+      const int o = ps * 64 + (((cb ^ (4 * ((lane >> 4) & 1) + r + 1)) & 7) << 3) + (c & 6);
+      *reinterpret_cast<bxb2 *>(out + o) = h;
+      *reinterpret_cast<bxb2 *>(out + kBxComp + o) = m;
+      *reinterpret_cast<bxb2 *>(out + 2 * kBxComp + o) = l;
+    }
+  }
 }
 
 // 1x1 layer (<= 32 out channels, waves 0 and 1): relu(conv + b) -> global [c][p]
