@@ -300,6 +300,15 @@ int lzm_conv_trunk_prepare_p(int precision, int n_dres, int n_pres, int r_ch, in
 int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
                      const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
                      float *out_latent, float *out_r, float *out_h, void *stream);
+/* lzm_conv_trunk_p writing the EfficientZero LSTM input row directly (mcts_ctree.py:776-790 +
+ * efficientzero_model.py:551-556: nn.LSTM over [reward planes | leaf hidden state]): row b of xin
+ * (xin_stride floats, >= r_ch*64 + H) gets the reward planes at [0, r_ch*64) and, when hpool
+ * (float[.][B][H], H % 4 == 0) is given, the leaf's hidden state hpool[x[b]][b] at [r_ch*64, +H)
+ * — the gather + concat that lzm_ez_lstm_input would do as a separate launch. */
+int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
+                         const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
+                         float *out_latent, float *xin, int xin_stride, const float *hpool, int H, float *out_h,
+                         void *stream);
 
 /* The MLP heads of the conv recurrent step in one launch (lzm_heads.h): reward hidden from
  * r [B][Kr] (optionally relu(r * r_scale + r_shift), the EfficientZero value-prefix BatchNorm),

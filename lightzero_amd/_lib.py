@@ -95,6 +95,7 @@ SIGNATURES = {
     "lzm_conv_trunk_floats_p": [_i, _i, _i],
     "lzm_conv_trunk_prepare_p": [_i, _i, _i, _i, _i, _vp, _vp],
     "lzm_conv_trunk_p": [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_conv_trunk_xin_p": [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp, _vp],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
             "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64,

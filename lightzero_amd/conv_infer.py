@@ -243,12 +243,19 @@ class FoldedConvNet:
         """EfficientZero step on the pools: leaf latent pool[x[b]][b] and LSTM state (hpool, cpool)[x[b]][b]
         ([S+1, B, H] each). The next latent goes to out_latent, the next LSTM state — zeroed where
         search_len % horizon == 0 (mcts_ctree.py:810-813) — to hpool[k + 1] / cpool[k + 1]
-        (csrc/lzm_lstm.h around the rocBLAS gate GEMM). Native trunk only."""
-        r, hd = self._trunk(pool, x, action, out_latent)
+        (csrc/lzm_lstm.h around the rocBLAS gate GEMM; the trunk kernel writes the LSTM input rows,
+        lzm_conv_trunk_xin_p). Native trunk only."""
         t, P = self.t, _lib.ptr
-        B, H = r.shape[0], hpool.shape[2]
-        xin = torch.empty((B, r.shape[1] + H), dtype=torch.float32, device=r.device)
-        _lib.call("lzm_ez_lstm_input", B, r.shape[1], H, P(r), P(hpool), P(x), P(xin), _lib.stream_ptr())
+        B, H = out_latent.shape[0], hpool.shape[2]
+        Kr = self.r_ch * 64
+        # the trunk writes the [reward planes | leaf hidden state] LSTM input rows itself
+        xin = torch.empty((B, Kr + H), dtype=torch.float32, device=out_latent.device)
+        hd = torch.empty((B, self.h_ch * 64), dtype=torch.float32, device=out_latent.device)
+        act = action if action.dtype == torch.int32 else action.to(torch.int32)
+        _lib.call("lzm_conv_trunk_xin_p", self.PRECISIONS[self.precision], B, self.n_dres, self.n_pres, self.r_ch,
+                  self.h_ch, P(self.native), P(self.actmap), P(pool), P(x), P(act.contiguous()), P(out_latent),
+                  P(xin), Kr + H, P(hpool), H, P(hd), _lib.stream_ptr())
+        r = xin[:, :Kr]
         gates = torch.addmm(t["lstm_b"], xin, t["lstm_w"].t())
         h1 = torch.empty((B, H), dtype=torch.float32, device=r.device)
         c1 = torch.empty_like(h1)

@@ -64,9 +64,21 @@ struct ConvTrunkArgs {
   const int32_t *x;      // nullable
   const int32_t *action; // [B]
   float *out_latent;     // [B][4096]
-  float *out_r;          // [B][r_ch * 64]
+  float *out_r;          // [B][r_stride]: reward planes at [0, r_ch * 64)
   float *out_h;          // [B][h_ch * 64]
+  int r_stride;          // floats per out_r row (r_ch * 64, or the EfficientZero LSTM input row)
+  const float *hpool;    // nullable: EfficientZero LSTM hidden-state pool [.][B][H]; row x[b] of env b
+  int H;                 // is copied to out_r[b][r_ch * 64 ..] (the [r | h] LSTM input row, no gather launch)
 };
+
+// [r | h] LSTM input row: the leaf's hidden state after the reward planes (every thread calls it)
+__device__ __forceinline__ void trunk_copy_hidden(const ConvTrunkArgs &a, int b) {
+  if (!a.hpool) return;
+  const float4 *src = reinterpret_cast<const float4 *>(
+      a.hpool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)a.H);
+  float4 *dst = reinterpret_cast<float4 *>(a.out_r + (int64_t)b * a.r_stride + a.r_ch * kCvPix);
+  for (int k = threadIdx.x; k < (a.H >> 2); k += blockDim.x) dst[k] = src[k];
+}
 
 // one 3x3 (TAPS = 9) or 1x1 (TAPS = 1) convolution of the LDS planes `in` for this wave's tile
 template <int TAPS>
@@ -154,6 +166,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const int pA = ph * 32 + (lane & 31);
   const int abase = (lane >> 5) * kCvCS + (pA >> 3) * 10 + (pA & 7);
   const ConvTrunkLayout L = conv_trunk_layout(a.n_dres, a.n_pres);
+  trunk_copy_hidden(a, b);
   for (int i = tid; i < 3 * kCvBuf; i += kCvThreads) cv_lds[i] = 0.f;  // zero borders
   __syncthreads();
   // x = -1 (a search-with-reuse root that needs no inference): any row will do, its output is unused
@@ -185,7 +198,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     const float *s = buf(xi);
     for (int i = tid; i < kCvCh * kCvPix; i += kCvThreads) dst[i] = s[(i >> 6) * kCvCS + cv_plane(i & 63)];
   }
-  if (ch == 0) conv1_layer(buf(xi), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_ch * kCvPix, lane, ph,
+  if (ch == 0) conv1_layer(buf(xi), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_stride, lane, ph,
                            abase);
   for (int k = 0; k < a.n_pres; ++k) {
     const float *wb = a.w + L.pres + k * kCvBlock;
@@ -486,6 +499,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * t + 4 * (lane >> 4));
     xres[4 * t] = v.x; xres[4 * t + 1] = v.y; xres[4 * t + 2] = v.z; xres[4 * t + 3] = v.w;
   }
+  trunk_copy_hidden(a, b);
   // ... and all of it split into buffer 0 (borders zero)
   for (int i = tid; i < 2 * kBxBuf / 8; i += kCvThreads) bx_lds4[i] = uint4{0u, 0u, 0u, 0u};
   __syncthreads();
@@ -513,7 +527,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       for (int t = 0; t < 4; ++t)
         *reinterpret_cast<float4 *>(dst + 16 * t) = float4{xres[4 * t], xres[4 * t + 1], xres[4 * t + 2], xres[4 * t + 3]};
       if (wv < 2)
-        bx_conv1_layer<DIAG>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_ch * kCvPix,
+        bx_conv1_layer<DIAG>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_stride,
                              lane, wv);
     }
   }

@@ -1068,10 +1068,31 @@ int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, 
     q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
     q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag; q.err = h->err;
     q.reuse_action = h->reuse_action; q.reuse_value = h->reuse_value;
-    const int per = kTlbThreads / 64;
-    dim3 g((h->B + per - 1) / per), b(kTlbThreads);
-    if (ez) hipLaunchKernelGGL(traverse_lookback_kernel<true>, g, b, 0, s, q);
-    else hipLaunchKernelGGL(traverse_lookback_kernel<false>, g, b, 0, s, q);
+    q.stamps = nullptr;
+    // LZM_TLB_WAVES (experiments): roots (waves) per workgroup, 1 (default), 2 or 4
+    static const int waves = getenv("LZM_TLB_WAVES") ? atoi(getenv("LZM_TLB_WAVES")) : 1;
+    const int per = (waves == 2 || waves == 4) ? waves : 1;
+    dim3 g((h->B + per - 1) / per), b(64 * per);
+    static const bool stamps = getenv("LZM_PHASE_TIMING") && atoi(getenv("LZM_PHASE_TIMING")) > 0;
+    if (stamps) {  // diagnostic instantiation: per-phase cycles into phase[32..38] (lzm_debug_phase_cycles)
+      if (!h->phase) {
+        LZM_HIP(hipMalloc(&h->phase, (64 + 1024) * sizeof(unsigned long long)));
+        LZM_HIP(hipMemset(h->phase, 0, (64 + 1024) * sizeof(unsigned long long)));
+      }
+      q.stamps = h->phase;
+      dim3 g1(h->B), b1(64);
+      if (ez) hipLaunchKernelGGL((traverse_lookback_kernel<true, 1, true>), g1, b1, 0, s, q);
+      else hipLaunchKernelGGL((traverse_lookback_kernel<false, 1, true>), g1, b1, 0, s, q);
+    } else if (per == 1) {
+      if (ez) hipLaunchKernelGGL((traverse_lookback_kernel<true, 1>), g, b, 0, s, q);
+      else hipLaunchKernelGGL((traverse_lookback_kernel<false, 1>), g, b, 0, s, q);
+    } else if (per == 2) {
+      if (ez) hipLaunchKernelGGL((traverse_lookback_kernel<true, 2>), g, b, 0, s, q);
+      else hipLaunchKernelGGL((traverse_lookback_kernel<false, 2>), g, b, 0, s, q);
+    } else {
+      if (ez) hipLaunchKernelGGL(traverse_lookback_kernel<true>, g, b, 0, s, q);
+      else hipLaunchKernelGGL(traverse_lookback_kernel<false>, g, b, 0, s, q);
+    }
   } else {
     // LZM_TRAVERSE=serial: one workgroup, speculative fixed-point passes over the stream
     int W = ((h->B + 63) / 64) * 64;
@@ -1228,6 +1249,7 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int cur, float discount, float *
   q.coef = h->coef; q.coef_positions = h->coef_positions; q.pow16807 = h->pow16807;
   q.flags = h->lb_flags; q.epoch = h->epoch; q.diag = h->diag; q.err = h->err;
   q.reuse_action = h->reuse_action; q.reuse_value = h->reuse_value;
+  q.stamps = nullptr;
   const int per = kTlbThreads / 64;
   dim3 g((h->B + per - 1) / per), b(kTlbThreads);
   const int32_t *nf = categorical ? (h->ext_norm ? h->ext_norm : h->norm_flag) : nullptr;
@@ -2319,18 +2341,21 @@ int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const flo
   return lzm_conv_trunk_prepare_p(LZM_CONV_F32, n_dres, n_pres, r_ch, h_ch, raw, out);
 }
 
-int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
-                     const float *actmap, const float *pool, const int32_t *x, const int32_t *action, float *out_latent,
-                     float *out_r, float *out_h, void *stream) {
+int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
+                         const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
+                         float *out_latent, float *xin, int xin_stride, const float *hpool, int H, float *out_h,
+                         void *stream) {
   if (B <= 0 || lzm_conv_trunk_floats_p(n_dres, n_pres, precision) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 ||
-      h_ch > 32 || !weights || !actmap || !pool || !action || !out_latent || !out_r || !out_h) {
+      h_ch > 32 || !weights || !actmap || !pool || !action || !out_latent || !xin || !out_h ||
+      xin_stride < r_ch * 64 + (hpool ? H : 0) || (hpool && (H <= 0 || H % 4)) || xin_stride % 4) {
     set_err("lzm_conv_trunk: bad arguments");
     return LZM_ERR_ARG;
   }
-  if (((uintptr_t)weights | (uintptr_t)pool) & 15) {
-    set_err("lzm_conv_trunk: weights and pool must be 16-byte aligned");
+  if (((uintptr_t)weights | (uintptr_t)pool | (uintptr_t)xin | (uintptr_t)hpool) & 15) {
+    set_err("lzm_conv_trunk: weights, pool, xin and hpool must be 16-byte aligned");
     return LZM_ERR_ARG;
   }
+  float *out_r = xin;
   const bool bx = precision == LZM_CONV_BF16X3;
   // split-bf16 variants: weight read-ahead depth (LZM_CONV_AHEAD) and timing-only ablations
   // (LZM_CONV_DIAG=1: no weight loads; results invalid)
@@ -2357,12 +2382,20 @@ int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int
   ConvTrunkArgs a;
   a.B = B; a.n_dres = n_dres; a.n_pres = n_pres; a.r_ch = r_ch; a.h_ch = h_ch; a.w = weights; a.actmap = actmap;
   a.pool = pool; a.x = x; a.action = action; a.out_latent = out_latent; a.out_r = out_r; a.out_h = out_h;
+  a.r_stride = xin_stride; a.hpool = hpool; a.H = hpool ? H : 0;
   if (bx)
     hipLaunchKernelGGL(bx_kernel, dim3(B), dim3(kCvThreads), lds_bx, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(conv_trunk_kernel, dim3(B), dim3(kCvThreads), lds_f32, (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
+}
+
+int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
+                     const float *actmap, const float *pool, const int32_t *x, const int32_t *action, float *out_latent,
+                     float *out_r, float *out_h, void *stream) {
+  return lzm_conv_trunk_xin_p(precision, B, n_dres, n_pres, r_ch, h_ch, weights, actmap, pool, x, action, out_latent,
+                              out_r, r_ch * 64, nullptr, 0, out_h, stream);
 }
 
 int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,

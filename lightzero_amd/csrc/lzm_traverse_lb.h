@@ -40,18 +40,35 @@ struct TraverseLbArgs {
                               // [1] draw positions beyond the coefficient table
   const int32_t *reuse_action;  // optional [B] ReZero true actions (search-with-reuse), with
   const float *reuse_value;     // [B] their reuse values; null: plain search
+  unsigned long long *stamps;   // LZM_PHASE_TIMING (diagnostic instantiation): per-phase shader cycles
+                                // summed over roots and launches: [32] setup, [33] draw-free walk,
+                                // [34] look-back + draw, [35] outputs, [36] roots, [37] roots needing
+                                // a draw, [38] max kernel-start -> root-done
 };
 
 // Workgroup-level part of a look-back traverse (every thread calls it): the seeded glibc state and
 // the launch epoch in LDS. Returns the epoch; *players = the batch's player count.
 __device__ inline unsigned long long traverse_lb_setup(const TraverseLbArgs &p, uint32_t *s_z0, uint32_t *s_pow,
                                                        int *s_epoch, int *players) {
-  const int tid = threadIdx.x;
-  *players = block_players(p.vtp_in, p.t.B);
+  // every global read of the setup in one round (seed, 16807 powers, epoch, the batch's to_play
+  // values for the player count), then one barrier: players = (max(virtual_to_play) == -1) ? 1 : 2
+  // (cnode.cpp:776-781) from per-wave maxima
+  __shared__ int s_wmax[16];
+  const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
   const uint32_t seed = *p.seed;
-  if (tid < 31) s_pow[tid] = p.pow16807[tid];
-  if (tid == 0) *s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t pw = tid < 31 ? p.pow16807[tid] : 0u;
+  const int ep = tid == 0 ? (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  int m = INT_MIN;
+  for (int q = tid; q < p.t.B; q += blockDim.x) m = max(m, p.vtp_in[q]);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+  if (lane == 0) s_wmax[tid >> 6] = m;
+  if (tid < 31) s_pow[tid] = pw;
+  if (tid == 0) *s_epoch = ep;
   __syncthreads();
+  int mx = s_wmax[0];
+  for (int w = 1; w < nw; ++w) mx = max(mx, s_wmax[w]);
+  *players = mx == -1 ? 1 : 2;
   seed_state_parallel(seed, s_pow, s_z0);
   __syncthreads();
   return (unsigned long long)(uint32_t)*s_epoch;
@@ -59,9 +76,9 @@ __device__ inline unsigned long long traverse_lb_setup(const TraverseLbArgs &p, 
 
 // One root's walk by one wave (all 64 lanes): draw-free classification, depth published at once,
 // look-back only when a draw value is needed (see the header comment).
-template <bool EZ>
+template <bool EZ, bool STAMPS = false>
 __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const uint32_t *s_z0, unsigned long long epoch,
-                                        int players) {
+                                        int players, unsigned long long t0 = 0, unsigned long long t1 = 0) {
   const TreeView &t = p.t;
   const int lane = threadIdx.x & 63, B = t.B;
   const float4 mm = p.minmax[i];
@@ -70,7 +87,8 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
   auto nodraw = [](int) -> uint32_t { return 0u; };
   const int ta = p.reuse_action ? p.reuse_action[i] : -1;
   const float rv = p.reuse_action ? p.reuse_value[i] : 0.0f;
-  Descent d = descend_wave<EZ, true>(t, i, i, B, mm, players, vtp0, p.disc, nodraw, &ti, ta, rv);
+  Descent d = descend_wave<EZ, true, true>(t, i, i, B, mm, players, vtp0, p.disc, nodraw, &ti, ta, rv);
+  const unsigned long long t2 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
   if (lane == 0 && ti.status != 2)
     __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (ti.status != 0) {
@@ -116,11 +134,12 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
       auto draw = [coef, npos, diag, base, s_z0](int level) -> uint32_t {
         return glibc_draw(coef, npos, s_z0, base + level, diag);
       };
-      d = descend_wave<EZ, false>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr, ta, rv);
+      d = descend_wave<EZ, false, true>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr, ta, rv);
       if (lane == 0)
         __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  const unsigned long long t3 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
   if (lane == 0) {
     p.out_x[i] = d.x;
     p.out_y[i] = i;
@@ -134,6 +153,16 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
   for (int l = lane; l < d.len; l += 64) {
     const int node = t.path[(size_t)l * B + i];
     t.meta[nidx(t, node, i)].best = t.path_act[(size_t)l * B + i];
+  }
+  if (STAMPS && lane == 0 && p.stamps) {
+    const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+    atomicAdd(p.stamps + 32, t1 - t0);
+    atomicAdd(p.stamps + 33, t2 - t1);
+    atomicAdd(p.stamps + 34, t3 - t2);
+    atomicAdd(p.stamps + 35, t4 - t3);
+    atomicAdd(p.stamps + 36, 1ull);
+    if (ti.status != 0) atomicAdd(p.stamps + 37, 1ull);
+    atomicMax(p.stamps + 38, t4 - t0);
   }
 }
 
@@ -153,14 +182,17 @@ __device__ inline void traverse_lb_finish(const TraverseLbArgs &p, unsigned long
   }
 }
 
-template <bool EZ>
-__global__ __launch_bounds__(kTlbThreads) void traverse_lookback_kernel(TraverseLbArgs p) {
+// W waves (roots) per workgroup
+template <bool EZ, int W = kTlbThreads / 64, bool STAMPS = false>
+__global__ __launch_bounds__(64 * W) void traverse_lookback_kernel(TraverseLbArgs p) {
   __shared__ uint32_t s_z0[31], s_pow[31];
   __shared__ int s_epoch;
   int players;
+  const unsigned long long t0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
   const unsigned long long epoch = traverse_lb_setup(p, s_z0, s_pow, &s_epoch, &players);
-  const int i = blockIdx.x * (kTlbThreads / 64) + (threadIdx.x >> 6);
-  if (i < p.t.B) traverse_lb_root<EZ>(p, i, s_z0, epoch, players);
+  const unsigned long long t1 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+  const int i = blockIdx.x * W + (threadIdx.x >> 6);
+  if (i < p.t.B) traverse_lb_root<EZ, STAMPS>(p, i, s_z0, epoch, players, t0, t1);
   traverse_lb_finish(p, epoch);
 }
 

@@ -243,7 +243,9 @@ __device__ __forceinline__ float wave_max_dpp(float v) {
 // ctree_muzero/lib/cnode.cpp:827-927): the true action's child is scored by carm_score (:702-749:
 // its value term uses reuse_value instead of the child's value, and a visited child scores the
 // value term alone), and choosing it ends the walk there even if the child is expanded (x = -1).
-template <bool EZ, bool CLASSIFY, typename Draw>
+// RL: take the chosen child's records from the lane that read them (readlane) instead of re-reading
+// them — for trees in global memory, where every dependent round of reads pays an L2-miss latency.
+template <bool EZ, bool CLASSIFY, bool RL = false, typename Draw>
 __device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps, float4 mm, int players, int vtp,
                                        float disc, Draw draw, TieInfo *tie, int true_action = -1,
                                        float reuse_value = 0.0f) {
@@ -262,13 +264,17 @@ __device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps,
     const int preset = m.is_reset;
     const bool valid = lane < n;
     const int a = valid ? legal_at(t, i, node, lane) : 0;
+    // RL: every child's stat AND meta in one round of reads
     NodeStat c;
+    NodeMeta cm;
     float cv = 0.0f;
     if (valid) {
       c = t.stat[nidx(t, base + a, i)];
+      if (RL) cm = t.meta[nidx(t, base + a, i)];
       cv = t.val ? t.val[nidx(t, base + a, i)] : node_value(c);
     } else {
       c.visit = 0; c.value_sum = 0.0f; c.prior = 0.0f; c.reward = 0.0f;
+      cm.latent = -1; cm.to_play = 0; cm.best = 0; cm.is_reset = 0;
     }
     float tr = c.reward;
     if (EZ) tr = preset == 1 ? c.reward : c.reward - pvp;
@@ -308,7 +314,7 @@ __device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps,
     const uint64_t mask = __ballot(valid && lane > r && score >= M - 0.000001f) | (1ull << r);
     const int nl = __popcll(mask);
     if (CLASSIFY && nl > 1) {
-      const bool leaf_child = !((mask >> lane) & 1ull) || t.meta[nidx(t, base + a, i)].latent < 0;
+      const bool leaf_child = !((mask >> lane) & 1ull) || (RL ? cm.latent : t.meta[nidx(t, base + a, i)].latent) < 0;
       const bool all_leaves = __ballot(!leaf_child) == 0ull;
       if (players > 1) vtp = (vtp == 1) ? 2 : 1;
       tie->status = all_leaves ? 1 : 2;
@@ -337,8 +343,19 @@ __device__ inline Descent descend_wave(const TreeView &t, int i, int li, int ps,
       t.path[(size_t)(len + 1) * ps + li] = node;
     }
     ++len;
-    s = t.stat[nidx(t, node, i)];
-    m = t.meta[nidx(t, node, i)];
+    if (RL) {
+      s.visit = __builtin_amdgcn_readlane(c.visit, jsel);
+      s.value_sum = readlane_f(c.value_sum, jsel);
+      s.prior = readlane_f(c.prior, jsel);
+      s.reward = readlane_f(c.reward, jsel);
+      m.latent = __builtin_amdgcn_readlane(cm.latent, jsel);
+      m.to_play = __builtin_amdgcn_readlane(cm.to_play, jsel);
+      m.best = __builtin_amdgcn_readlane(cm.best, jsel);
+      m.is_reset = __builtin_amdgcn_readlane(cm.is_reset, jsel);
+    } else {
+      s = t.stat[nidx(t, node, i)];
+      m = t.meta[nidx(t, node, i)];
+    }
     if (len == 1 && true_action >= 0 && action == true_action) {
       reuse_stop = true;  // cnode.cpp:888-891
       break;

@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--precision", choices=["bf16x3", "f32"], default=None,
                     help="native conv trunk precision (default: LZM_CONV_PRECISION or bf16x3)")
+    ap.add_argument("--rng", choices=["glibc", "philox"], default="glibc",
+                    help="tie-break stream: the reference's glibc rand() (parity) or per-root Philox")
     a = ap.parse_args()
     if a.precision:
         os.environ["LZM_CONV_PRECISION"] = a.precision
@@ -64,6 +66,7 @@ def main():
     A = model.action_space_size
     scale = 50 if a.kind == "ez" else 300
     cls = EfficientZeroMCTSCtree if a.kind == "ez" else MuZeroMCTSCtree
+    cls.rng_mode = a.rng
     cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=dev, lstm_horizon_len=5,
                         use_hip_graph=bool(a.graph), model=dict(support_scale=scale, categorical_distribution=True)))
     mcts = cls(cfg)
@@ -102,7 +105,7 @@ def main():
         "config": {"workload": "C3 Pong EfficientZero" if a.kind == "ez" else "C5 Breakout MuZero (per GPU)",
                    "envs": B, "num_simulations": S, "actions": A, "support": 2 * scale + 1, "latent": [64, 8, 8],
                    "path": "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph),
-                   "conv_precision": precision},
+                   "conv_precision": precision, "rng": a.rng},
         "net_flops_per_sim": flops, "net_tflops_whole_search": net_tflops,
         "fp32_mfma_peak_tflops": FP32_MFMA_PEAK_TFLOPS, "net_frac_of_peak": net_tflops / FP32_MFMA_PEAK_TFLOPS}))
 
