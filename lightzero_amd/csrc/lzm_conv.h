@@ -332,7 +332,9 @@ __device__ __forceinline__ void bx_prefetch(BxRing<AHEAD> &r, const uint4 *__res
 // experiments only, results invalid). Software pipeline, in issue order (the scheduling barriers keep
 // the compiler from sinking loads next to their first use): weights of chunk s + AHEAD, activations
 // of chunk s + 1, then chunk s's 24 MFMAs.
-template <int NCH, int AHEAD, int DIAG>
+// S0: index of the first chunk within the 18 of a 3x3 layer (the two-waves-per-SIMD kernel splits K;
+// wf then points at chunk S0's weights)
+template <int NCH, int AHEAD, int DIAG, int S0 = 0>
 __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restrict__ wf, BxRing<AHEAD> &r, int lane,
                                         bxf4 (&acc)[4]) {
   uint4 a[2][4][3];
@@ -341,7 +343,7 @@ __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restr
   // (dy, dx) reads bordered position (py + dy) * 10 + px + dx
   const int lbase = ((lane >> 3) & 1) * 10 + px;
   auto load_a = [&](int s) {
-    const int tap = NCH == 2 ? 4 : s >> 1, j = NCH == 2 ? s : s & 1;
+    const int tap = NCH == 2 ? 4 : (S0 + s) >> 1, j = NCH == 2 ? s : (S0 + s) & 1;
     const int dy = tap / 3, dx = tap % 3;
     const int chunk = ((4 * j + g) ^ (px + dx)) & 7;
 #pragma unroll
@@ -403,22 +405,24 @@ __device__ __forceinline__ int bx_ep_pos(int lane, int t, int r) {
 }
 
 // 3x3 epilogue: v = relu(acc + bias [+ amap] [+ xres]) -> split LDS planes of `out`; KEEP: xres = v
+// tiles T0 .. T0 + NT - 1 (xres / am hold those tiles only)
+template <int T0 = 0, int NT = 4>
 __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out, float bc, bool use_am,
-                                             const float4 (&am)[4], float (&xres)[16], bool add_res, bool keep,
+                                             const float4 (&am)[NT], float (&xres)[4 * NT], bool add_res, bool keep,
                                              int lane, int c) {
   typedef float bxf2 __attribute__((ext_vector_type(2)));
   typedef __bf16 bxb2 __attribute__((ext_vector_type(2)));
   const int cb = c >> 3, odd = lane & 1;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = T0; t < T0 + NT; ++t) {
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float x = acc[t][r] + bc;
-      if (use_am) x += r == 0 ? am[t].x : r == 1 ? am[t].y : r == 2 ? am[t].z : am[t].w;
-      if (add_res) x += xres[4 * t + r];
+      if (use_am) x += r == 0 ? am[t - T0].x : r == 1 ? am[t - T0].y : r == 2 ? am[t - T0].z : am[t - T0].w;
+      if (add_res) x += xres[4 * (t - T0) + r];
       x = x > 0.f ? x : 0.f;
-      if (keep) xres[4 * t + r] = x;
+      if (keep) xres[4 * (t - T0) + r] = x;
       v[r] = x;
     }
     // lanes 2j, 2j + 1 hold channels c, c + 1 (one dword of a plane row): per pixel pair (2k, 2k + 1)
@@ -533,6 +537,93 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   }
   if (wv < 2)
     bx_conv1_layer<DIAG>(buf(n3 & 1), a.w + L.hw, a.w + L.hb, a.h_ch, a.out_h + (int64_t)b * a.h_ch * kCvPix, lane, wv);
+}
+
+// Two waves per SIMD (512 threads): wave w owns out-channel group w & 3 and HALF of K — chunks
+// 9 (w >> 2) .. +8 of every 3x3 layer — so one wave's waits (barriers, vmcnt / lgkmcnt) and
+// epilogue overlap the other's MFMAs (the 4-wave form keeps the matrix pipe busy ≈ 51%). At a layer
+// end the two halves swap partial sums of two tiles each through LDS; the K-half-0 wave finishes
+// tiles 0-1 (epilogue, residual in registers), the K-half-1 wave tiles 2-3. The 1x1 convolutions
+// stay whole on waves 0-1.
+constexpr int kBx2Threads = 512;
+constexpr int kBx2Scratch = 4 * 2 * 64 * 8;  // floats: [group][tile pair][lane][8]
+
+template <int AHEAD>
+__global__ __launch_bounds__(kBx2Threads) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_trunk_bx2_kernel(
+    ConvTrunkArgs a) {
+  extern __shared__ uint4 bx_lds4[];
+  uint16_t *lds = reinterpret_cast<uint16_t *>(bx_lds4);
+  float *scr = reinterpret_cast<float *>(lds + 2 * kBxBuf);
+  auto buf = [&](int i) { return lds + i * kBxBuf; };
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int grp = wv & 3, kh = wv >> 2, t0 = 2 * kh;  // epilogue tiles t0, t0 + 1
+  const int c = 16 * grp + (lane & 15);
+  const ConvTrunkLayout L = conv_trunk_layout_p(a.n_dres, a.n_pres, 1);
+  const int n3 = 1 + 2 * a.n_dres + 2 * a.n_pres;
+  auto layer_w = [&](int i) { return a.w + bx_layer_off(L, a.n_dres, i); };
+  // this wave's chunk stream: group grp, chunks 9 kh ..
+  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + (grp * 18 + 9 * kh) * 3 * 64; };
+  BxRing<AHEAD> ring;
+  bx_prefetch<9, AHEAD, 0>(ring, wave_stream(a.w + L.dyn), lane);
+  const float *src = a.pool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
+  float xres[8];  // tiles t0, t0 + 1 of the block input (exact f32)
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * (t0 + u) + 4 * (lane >> 4));
+    xres[4 * u] = v.x; xres[4 * u + 1] = v.y; xres[4 * u + 2] = v.z; xres[4 * u + 3] = v.w;
+  }
+  trunk_copy_hidden(a, b);
+  for (int i = tid; i < 2 * kBxBuf / 8; i += kBx2Threads) bx_lds4[i] = uint4{0u, 0u, 0u, 0u};
+  __syncthreads();
+  for (int i = tid; i < kCvCh * kCvPix; i += kBx2Threads) bx_store(buf(0), cv_plane(i & 63), i >> 6, src[i]);
+  __syncthreads();
+  for (int i = 0; i < n3; ++i) {
+    const float *w = layer_w(i);
+    const bool second = i > 0 && ((i - 1) & 1);
+    const float bc = i ? w[kBx3Frag + c] : 0.f;
+    float4 am[2] = {};
+    if (i == 0) {
+      const float4 *amap = reinterpret_cast<const float4 *>(a.actmap + ((int64_t)a.action[b] * kCvCh + c) * kCvPix);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) am[u] = amap[4 * (t0 + u) + (lane >> 4)];
+    }
+    bxf4 acc[4];
+    if (kh == 0)
+      bx_conv<9, AHEAD, 0, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
+    else
+      bx_conv<9, AHEAD, 0, 9>(buf(i & 1), wave_stream(w), ring, lane, acc);
+    if (i + 1 < n3) bx_prefetch<9, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
+    // swap partial sums: K-half 0 hands tiles 2-3 over, K-half 1 tiles 0-1
+    {
+      float4 *mine = reinterpret_cast<float4 *>(scr + ((grp * 2 + (1 - kh)) * 64 + lane) * 8);
+      const int o = 2 * (1 - kh);
+      mine[0] = float4{acc[o][0], acc[o][1], acc[o][2], acc[o][3]};
+      mine[1] = float4{acc[o + 1][0], acc[o + 1][1], acc[o + 1][2], acc[o + 1][3]};
+    }
+    __syncthreads();
+    {
+      const float4 *theirs = reinterpret_cast<const float4 *>(scr + ((grp * 2 + kh) * 64 + lane) * 8);
+      const float4 p0 = theirs[0], p1 = theirs[1];
+      acc[t0][0] += p0.x; acc[t0][1] += p0.y; acc[t0][2] += p0.z; acc[t0][3] += p0.w;
+      acc[t0 + 1][0] += p1.x; acc[t0 + 1][1] += p1.y; acc[t0 + 1][2] += p1.z; acc[t0 + 1][3] += p1.w;
+    }
+    if (kh == 0)
+      bx_epilogue3<0, 2>(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
+    else
+      bx_epilogue3<2, 2>(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
+    __syncthreads();
+    if (i == 2 * a.n_dres) {
+      float *dst = a.out_latent + (int64_t)b * kCvCh * kCvPix + c * kCvPix + 4 * (lane >> 4);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        *reinterpret_cast<float4 *>(dst + 16 * (t0 + u)) =
+            float4{xres[4 * u], xres[4 * u + 1], xres[4 * u + 2], xres[4 * u + 3]};
+      if (wv < 2)
+        bx_conv1_layer<0>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_stride, lane, wv);
+    }
+  }
+  if (wv < 2)
+    bx_conv1_layer<0>(buf(n3 & 1), a.w + L.hw, a.w + L.hb, a.h_ch, a.out_h + (int64_t)b * a.h_ch * kCvPix, lane, wv);
 }
 
 // host packing for the split trunk. 3x3: W[64 out][64 in][9] -> [wave][chunk s][term][lane][8]:

@@ -2366,9 +2366,13 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
                           : ahead == 8 ? conv_trunk_bx_kernel<8, 0>
                           : ahead == 5 ? conv_trunk_bx_kernel<5, 0>
                                        : conv_trunk_bx_kernel<kBxAhead, 0>;
+  // LZM_CONV_WAVES (experiments): 8 = two waves per SIMD splitting K (conv_trunk_bx2_kernel; measured
+  // 43 vs 34 us per launch at Breakout), 4 (default) = one
+  static const int cwaves = getenv("LZM_CONV_WAVES") ? atoi(getenv("LZM_CONV_WAVES")) : 4;
   static std::once_flag once;
   static hipError_t attr_err = hipSuccess;
   const size_t lds_f32 = 3 * kCvBuf * sizeof(float), lds_bx = 2 * kBxBuf * sizeof(uint16_t);
+  const size_t lds_bx2 = lds_bx + kBx2Scratch * sizeof(float);
   std::call_once(once, [&] {
     attr_err = hipFuncSetAttribute((const void *)conv_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_f32);
@@ -2377,13 +2381,18 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
     for (bx_fn f : all)
       if (attr_err == hipSuccess)
         attr_err = hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bx);
+    if (attr_err == hipSuccess)
+      attr_err = hipFuncSetAttribute((const void *)conv_trunk_bx2_kernel<kBxAhead>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bx2);
   });
   LZM_HIP(attr_err);
   ConvTrunkArgs a;
   a.B = B; a.n_dres = n_dres; a.n_pres = n_pres; a.r_ch = r_ch; a.h_ch = h_ch; a.w = weights; a.actmap = actmap;
   a.pool = pool; a.x = x; a.action = action; a.out_latent = out_latent; a.out_r = out_r; a.out_h = out_h;
   a.r_stride = xin_stride; a.hpool = hpool; a.H = hpool ? H : 0;
-  if (bx)
+  if (bx && cwaves == 8 && diag == 0 && ahead == kBxAhead)
+    hipLaunchKernelGGL(conv_trunk_bx2_kernel<kBxAhead>, dim3(B), dim3(kBx2Threads), lds_bx2, (hipStream_t)stream, a);
+  else if (bx)
     hipLaunchKernelGGL(bx_kernel, dim3(B), dim3(kCvThreads), lds_bx, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(conv_trunk_kernel, dim3(B), dim3(kCvThreads), lds_f32, (hipStream_t)stream, a);
