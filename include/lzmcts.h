@@ -373,6 +373,14 @@ int lzm_set_reuse(lzm_handle *h, const int32_t *true_action, const float *reuse_
 int lzm_mlp_initial_inference(int B, int O, int H, int F, int V, int A, int group, const float *obs,
                               const float *weights, const int64_t *offsets, float *latent, float *value, float *policy,
                               void *stream);
+/* lzm_mlp_initial_inference followed, in the same launch, by lzm_roots_prepare on `h` (B roots, A
+ * actions) with the policy logits just computed — MuZeroPolicy._forward_collect's initial_inference +
+ * roots.prepare (muzero.py:643-660) without a second launch; the same root records bit for bit. */
+int lzm_mlp_initial_inference_prepare(lzm_handle *h, int B, int O, int H, int F, int V, int A, int group,
+                                      const float *obs, const float *weights, const int64_t *offsets, float *latent,
+                                      float *value, float *policy, const int32_t *legal, const int32_t *count,
+                                      const float *noises, float noise_weight, const float *rewards,
+                                      const int32_t *to_play, void *stream);
 
 /* EfficientZero reward LSTM, input side (lzm_lstm.h): xin[b] = [r[b] | hpool[x[b]][b]] — the leaf's
  * hidden-state gather and the concat ahead of the gate GEMM. Replaces the per-simulation gathers of

@@ -58,6 +58,8 @@ SIGNATURES = {
     "lzm_decode_backprop_traverse": [_vp, _i, _f, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _i64, _vp, _i, _f,
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_mlp_initial_inference": [_i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_mlp_initial_inference_prepare": [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                          _f, _vp, _vp, _vp],
     "lzm_set_reuse": [_vp, _vp, _vp],
     "lzm_ez_lstm_input": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "lzm_ez_lstm_cell": [_i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],

@@ -70,11 +70,16 @@ class DeviceSearchStep:
                     self.roots = self.mcts_cls.roots(self.B, self.legal)
                 pool0 = self._root_slot()
                 if self.initial is not None and pool0 is not None:
-                    out = self.initial.initial_inference(self.obs, latent_out=pool0)  # search skips its copy
+                    # one launch: initial_inference into the search's root slot (the search skips its
+                    # copy) and the root preparation from the policy logits
+                    out = self.initial.initial_inference(
+                        self.obs, latent_out=pool0,
+                        prepare=dict(roots=self.roots, noise_weight=self.noise_weight, noises=self.noises,
+                                     rewards=self.rewards, to_play=self.to_play))
                 else:
                     out = (self.initial or self.model).initial_inference(self.obs)
-                self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
-                                          self.to_play)
+                    self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
+                                              self.to_play)
                 # the seeds (from the step counter), fresh min-max bounds, the root outputs and the
                 # counter increment run inside the search (the one-launch search: in its kernel)
                 t = self.roots.tree

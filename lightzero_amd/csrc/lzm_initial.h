@@ -91,13 +91,33 @@ __device__ inline void ii_dense(const float *__restrict__ W, const float *__rest
   __syncthreads();
 }
 
-__global__ __launch_bounds__(kIiThreads) void initial_inference_kernel(IiArgs p) {
+// PREP: also CRoots::prepare for the workgroup's envs (prepare_root, lzm_tree.h) from the policy
+// logits just written — the collect step's root preparation without a launch of its own.
+template <bool PREP = false>
+__global__ __launch_bounds__(kIiThreads) void initial_inference_kernel(IiArgs p, PrepareArgs q = PrepareArgs{}) {
   __shared__ float s_a[kIiEnvs * kIiMaxW], s_b[kIiEnvs * kIiMaxW], s_c[kIiEnvs * 256];
   __shared__ float s_part[kIiEnvs * kIiThreads];
   const int t = threadIdx.x;
   const int e0 = blockIdx.x * kIiEnvs;
   const int ne = min(kIiEnvs, p.B - e0);
   const int H = p.H;
+  // PREP: the root's preparation inputs read at the start, into LDS / registers, so the tail below
+  // is arithmetic and stores only (kIiEnvs == 1: the workgroup's root is e0)
+  static_assert(!PREP || kIiEnvs == 1, "the fused preparation assumes one env per workgroup");
+  __shared__ int s_leg[PREP ? kIiMaxW : 1];
+  __shared__ float s_nz[PREP ? kIiMaxW : 1];
+  int pr_n = 0, pr_tp = 0;
+  float pr_rw = 0.0f;
+  if (PREP) {
+    const int A = q.A, cnt = q.count_in[e0];
+    for (int j = t; j < A; j += kIiThreads) {
+      s_leg[j] = cnt <= 0 ? j : (j < cnt ? q.legal_in[(size_t)e0 * A + j] : -1);
+      s_nz[j] = q.noises ? q.noises[(size_t)e0 * A + j] : 0.0f;
+    }
+    pr_n = cnt <= 0 ? A : cnt;
+    pr_tp = q.to_play[e0];
+    pr_rw = q.rewards[e0];
+  }
   for (int q = t; q < kIiEnvs * p.O; q += kIiThreads) {
     const int e = q / p.O, k = q - e * p.O;
     s_a[e * kIiMaxW + k] = e < ne ? p.obs[(size_t)(e0 + e) * p.O + k] : 0.0f;
@@ -135,6 +155,41 @@ __global__ __launch_bounds__(kIiThreads) void initial_inference_kernel(IiArgs p)
   for (int q = t; q < ne * p.A; q += kIiThreads) {
     const int e = q / p.A, k = q - e * p.A;
     p.policy[(size_t)(e0 + e) * p.A + k] = s_b[e * kIiMaxW + k];
+  }
+  if (PREP) {
+    // CRoots::prepare for root i = e0, the same operations in the same order as prepare_root
+    // (lzm_tree.h), with the legal list, noises and policy logits read from LDS
+    const int i = e0, A = q.A, n = pr_n;
+    for (int j = t; j < A; j += kIiThreads) q.legal[(size_t)i * A + j] = s_leg[j];
+    if (t == 0) {
+      q.nlegal[i] = n;
+      const float *lg = s_b;  // this env's policy logits (e = 0)
+      float pmax = kFloatMin;
+      for (int j = 0; j < n; ++j) {
+        const float l = lg[s_leg[j]];
+        if (pmax < l) pmax = l;
+      }
+      float sum = 0.0f;
+      for (int j = 0; j < n; ++j) sum += glibc_expf(lg[s_leg[j]] - pmax);
+      const float f = q.noise_weight;
+      for (int j = 0; j < n; ++j) {
+        const int a = s_leg[j];
+        float prior = glibc_expf(lg[a] - pmax) / sum;
+        if (q.noises) prior = prior * (1 - f) + s_nz[j] * f;
+        NodeStat c;
+        c.visit = 0; c.value_sum = 0.0f; c.prior = prior; c.reward = 0.0f;
+        q.stat[(size_t)(1 + a) * q.B + i] = c;
+        NodeMeta cm;
+        cm.latent = -1; cm.to_play = 0; cm.best = -1; cm.is_reset = 0;
+        q.meta[(size_t)(1 + a) * q.B + i] = cm;
+      }
+      NodeStat r;
+      r.visit = 1; r.value_sum = 0.0f; r.prior = 0.0f; r.reward = pr_rw;
+      q.stat[i] = r;
+      NodeMeta rm;
+      rm.latent = 0; rm.to_play = pr_tp; rm.best = -1; rm.is_reset = 0;
+      q.meta[i] = rm;
+    }
   }
 }
 

@@ -510,72 +510,9 @@ __global__ __launch_bounds__(256) void inverse_transform_kernel(const float *log
 }
 
 
-// CRoots::prepare / prepare_no_noise (cnode.cpp:321-358): expand each root over its legal list
-// (an empty list means every action, cnode.cpp:101-107), optional Dirichlet mix
-// (add_exploration_noise :149-167), visit_count = 1.
-struct PrepareArgs {
-  NodeStat *stat;
-  NodeMeta *meta;
-  int32_t *legal, *nlegal;
-  const int32_t *legal_in, *count_in, *to_play;
-  const float *noises, *rewards, *logits;
-  float noise_weight;
-  int B, A;
-};
-
 __global__ __launch_bounds__(256) void prepare_kernel(PrepareArgs p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.B) return;
-  const int A = p.A;
-  int n = p.count_in[i];
-  if (n <= 0) {
-    n = A;
-    for (int a = 0; a < A; ++a) p.legal[(size_t)i * A + a] = a;
-  } else {
-    for (int j = 0; j < A; ++j) p.legal[(size_t)i * A + j] = j < n ? p.legal_in[(size_t)i * A + j] : -1;
-  }
-  p.nlegal[i] = n;
-  const float *lg = p.logits + (size_t)i * A;
-  float pmax = kFloatMin;
-  for (int j = 0; j < n; ++j) {
-    const float l = lg[p.legal[(size_t)i * A + j]];
-    if (pmax < l) pmax = l;
-  }
-  float sum = 0.0f;
-  for (int j = 0; j < n; ++j) sum += glibc_expf(lg[p.legal[(size_t)i * A + j]] - pmax);
-  const float f = p.noise_weight;
-  for (int j = 0; j < n; ++j) {
-    const int a = p.legal[(size_t)i * A + j];
-    float prior = glibc_expf(lg[a] - pmax) / sum;
-    if (p.noises) {
-      const float noise = p.noises[(size_t)i * A + j];
-      prior = prior * (1 - f) + noise * f;
-    }
-    NodeStat c;
-    c.visit = 0;
-    c.value_sum = 0.0f;
-    c.prior = prior;
-    c.reward = 0.0f;
-    p.stat[(size_t)(1 + a) * p.B + i] = c;
-    NodeMeta cm;
-    cm.latent = -1;
-    cm.to_play = 0;
-    cm.best = -1;
-    cm.is_reset = 0;
-    p.meta[(size_t)(1 + a) * p.B + i] = cm;
-  }
-  NodeStat r;
-  r.visit = 1;
-  r.value_sum = 0.0f;
-  r.prior = 0.0f;
-  r.reward = p.rewards[i];
-  p.stat[i] = r;
-  NodeMeta rm;
-  rm.latent = 0;
-  rm.to_play = p.to_play[i];
-  rm.best = -1;
-  rm.is_reset = 0;
-  p.meta[i] = rm;
+  if (i < p.B) prepare_root(p, i);
 }
 
 __global__ void minmax_init_kernel(float4 *mm, int n, float delta) {
@@ -2490,8 +2427,42 @@ extern "C" int lzm_mlp_initial_inference(int B, int O, int H, int F, int V, int 
     p.b[l] = l < 8 ? weights + offsets[2 * l + 1] : nullptr;
   }
   p.latent = latent; p.value = value; p.policy = policy;
-  hipLaunchKernelGGL(initial_inference_kernel, dim3((B + kIiEnvs - 1) / kIiEnvs), dim3(kIiThreads), 0,
-                     (hipStream_t)stream, p);
+  hipLaunchKernelGGL(initial_inference_kernel<false>, dim3((B + kIiEnvs - 1) / kIiEnvs), dim3(kIiThreads), 0,
+                     (hipStream_t)stream, p, PrepareArgs{});
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" int lzm_mlp_initial_inference_prepare(lzm_handle *h, int B, int O, int H, int F, int V, int A, int group,
+                                                 const float *obs, const float *weights, const int64_t *offsets,
+                                                 float *latent, float *value, float *policy, const int32_t *legal,
+                                                 const int32_t *count, const float *noises, float noise_weight,
+                                                 const float *rewards, const int32_t *to_play, void *stream) {
+  if (!h || h->B != B || h->A != A || !legal || !count || !rewards || !to_play) {
+    set_err("lzm_mlp_initial_inference_prepare: the handle must have B roots and A actions; legal, count, rewards, "
+            "to_play required");
+    return LZM_ERR_ARG;
+  }
+  if (B <= 0 || O <= 0 || O > kIiMaxW || H <= 0 || H > kIiMaxW || F <= 0 || F > 256 || V <= 0 || V > kIiMaxW ||
+      A <= 0 || A > kIiMaxW || group <= 0 || H % group || !obs || !weights || !offsets || !latent || !value ||
+      !policy) {
+    set_err("lzm_mlp_initial_inference_prepare: bad arguments (widths <= 1024, head hidden <= 256, H % group == 0)");
+    return LZM_ERR_ARG;
+  }
+  IiArgs p;
+  p.B = B; p.O = O; p.H = H; p.F = F; p.V = V; p.A = A; p.group = group;
+  p.obs = obs;
+  for (int l = 0; l < kIiLayers; ++l) {
+    p.w[l] = l < 8 ? weights + offsets[2 * l] : nullptr;
+    p.b[l] = l < 8 ? weights + offsets[2 * l + 1] : nullptr;
+  }
+  p.latent = latent; p.value = value; p.policy = policy;
+  PrepareArgs q;
+  q.stat = h->stat; q.meta = h->meta; q.legal = h->legal; q.nlegal = h->nlegal;
+  q.legal_in = legal; q.count_in = count; q.to_play = to_play; q.noises = noises; q.rewards = rewards;
+  q.logits = policy; q.noise_weight = noise_weight; q.B = h->B; q.A = h->A;
+  hipLaunchKernelGGL(initial_inference_kernel<true>, dim3((B + kIiEnvs - 1) / kIiEnvs), dim3(kIiThreads), 0,
+                     (hipStream_t)stream, p, q);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }

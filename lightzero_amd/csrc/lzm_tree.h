@@ -639,4 +639,70 @@ __device__ inline float h_inverse(float value) {
   return sgn * (tmp * tmp - 1.0f);
 }
 
+// CRoots::prepare / prepare_no_noise (cnode.cpp:321-358): expand each root over its legal list
+// (an empty list means every action, cnode.cpp:101-107), optional Dirichlet mix
+// (add_exploration_noise :149-167), visit_count = 1.
+struct PrepareArgs {
+  NodeStat *stat;
+  NodeMeta *meta;
+  int32_t *legal, *nlegal;
+  const int32_t *legal_in, *count_in, *to_play;
+  const float *noises, *rewards, *logits;
+  float noise_weight;
+  int B, A;
+};
+
+__device__ inline void prepare_root(const PrepareArgs &p, int i) {
+  const int A = p.A;
+  int n = p.count_in[i];
+  if (n <= 0) {
+    n = A;
+    for (int a = 0; a < A; ++a) p.legal[(size_t)i * A + a] = a;
+  } else {
+    for (int j = 0; j < A; ++j) p.legal[(size_t)i * A + j] = j < n ? p.legal_in[(size_t)i * A + j] : -1;
+  }
+  p.nlegal[i] = n;
+  const float *lg = p.logits + (size_t)i * A;
+  float pmax = kFloatMin;
+  for (int j = 0; j < n; ++j) {
+    const float l = lg[p.legal[(size_t)i * A + j]];
+    if (pmax < l) pmax = l;
+  }
+  float sum = 0.0f;
+  for (int j = 0; j < n; ++j) sum += glibc_expf(lg[p.legal[(size_t)i * A + j]] - pmax);
+  const float f = p.noise_weight;
+  for (int j = 0; j < n; ++j) {
+    const int a = p.legal[(size_t)i * A + j];
+    float prior = glibc_expf(lg[a] - pmax) / sum;
+    if (p.noises) {
+      const float noise = p.noises[(size_t)i * A + j];
+      prior = prior * (1 - f) + noise * f;
+    }
+    NodeStat c;
+    c.visit = 0;
+    c.value_sum = 0.0f;
+    c.prior = prior;
+    c.reward = 0.0f;
+    p.stat[(size_t)(1 + a) * p.B + i] = c;
+    NodeMeta cm;
+    cm.latent = -1;
+    cm.to_play = 0;
+    cm.best = -1;
+    cm.is_reset = 0;
+    p.meta[(size_t)(1 + a) * p.B + i] = cm;
+  }
+  NodeStat r;
+  r.visit = 1;
+  r.value_sum = 0.0f;
+  r.prior = 0.0f;
+  r.reward = p.rewards[i];
+  p.stat[i] = r;
+  NodeMeta rm;
+  rm.latent = 0;
+  rm.to_play = p.to_play[i];
+  rm.best = -1;
+  rm.is_reset = 0;
+  p.meta[i] = rm;
+}
+
 }  // namespace lzm

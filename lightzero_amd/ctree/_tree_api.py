@@ -119,10 +119,17 @@ class _RootsBase:
 
     def prepare_device(self, root_noise_weight, noises, rewards, logits, to_play):
         """Device-tensor variant (not in the reference): all arguments torch tensors on the GPU."""
+        t, legal, count = self.device_legal(logits.shape[-1], logits.device)
+        t.prepare(legal, count,
+                  None if noises is None else noises.to(logits.device, torch.float32).contiguous(),
+                  _f32(root_noise_weight), rewards.to(logits.device, torch.float32).contiguous(),
+                  logits.to(logits.device, torch.float32).contiguous(), to_play.to(logits.device, torch.int32).contiguous())
+
+    def device_legal(self, A, dev):
+        """(tree, legal int32 [B, A], count int32 [B]) on `dev`: the device tree for A actions and the
+        root legal lists uploaded once per Roots object (so preparation can be captured in a graph)."""
         B = self.root_num
-        A = logits.shape[-1]
-        t = self._acquire(A, logits.device)
-        dev = logits.device
+        t = self._acquire(A, dev)
         key = (A, str(dev))
         if getattr(self, "_legal_dev_key", None) != key:
             # the legal lists are fixed per Roots object: upload once (no host copy on later calls,
@@ -136,10 +143,7 @@ class _RootsBase:
             self._legal_dev = (torch.from_numpy(legal).to(dev), torch.from_numpy(count).to(dev))
             self._legal_dev_key = key
         legal, count = self._legal_dev
-        t.prepare(legal, count,
-                  None if noises is None else noises.to(dev, torch.float32).contiguous(), _f32(root_noise_weight),
-                  rewards.to(dev, torch.float32).contiguous(), logits.to(dev, torch.float32).contiguous(),
-                  to_play.to(dev, torch.int32).contiguous())
+        return t, legal, count
 
     def get_trajectories(self):
         if self.tree is None:

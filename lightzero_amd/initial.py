@@ -76,9 +76,10 @@ class FusedInitialInference:
         self.dims = dims
         self.key = ver
 
-    def initial_inference(self, obs, latent_out=None):
+    def initial_inference(self, obs, latent_out=None, prepare=None):
         """latent_out: optional float32 [B, H] (contiguous) to write the latent into (e.g. a search's
-        root slot, so the search does not copy it)."""
+        root slot, so the search does not copy it). prepare: optional dict(roots, noise_weight, noises,
+        rewards, to_play) — also Roots.prepare_device with the policy logits, in the same launch."""
         self._pack()
         d = self.dims
         x = obs.reshape(obs.shape[0], -1)
@@ -93,9 +94,21 @@ class FusedInitialInference:
             raise ValueError("latent_out must be a contiguous float32 [B, H] tensor")
         value = torch.empty((B, d["support"]), **kw)
         policy = torch.empty((B, d["actions"]), **kw)
-        _lib.call("lzm_mlp_initial_inference", B, d["obs"], d["hidden"], d["head_hidden"], d["support"], d["actions"],
-                  d["group"], _lib.ptr(x), _lib.ptr(self.flat), self.offsets.ctypes.data, _lib.ptr(latent),
-                  _lib.ptr(value), _lib.ptr(policy), _lib.stream_ptr())
+        if prepare is None:
+            _lib.call("lzm_mlp_initial_inference", B, d["obs"], d["hidden"], d["head_hidden"], d["support"],
+                      d["actions"], d["group"], _lib.ptr(x), _lib.ptr(self.flat), self.offsets.ctypes.data,
+                      _lib.ptr(latent), _lib.ptr(value), _lib.ptr(policy), _lib.stream_ptr())
+        else:
+            t, legal, count = prepare["roots"].device_legal(d["actions"], x.device)
+            noises = prepare.get("noises")
+            f32 = dict(device=x.device, dtype=torch.float32)
+            _lib.call("lzm_mlp_initial_inference_prepare", t.h, B, d["obs"], d["hidden"], d["head_hidden"],
+                      d["support"], d["actions"], d["group"], _lib.ptr(x), _lib.ptr(self.flat),
+                      self.offsets.ctypes.data, _lib.ptr(latent), _lib.ptr(value), _lib.ptr(policy), _lib.ptr(legal),
+                      _lib.ptr(count), None if noises is None else _lib.ptr(noises.to(**f32).contiguous()),
+                      float(prepare["noise_weight"]), _lib.ptr(prepare["rewards"].to(**f32).contiguous()),
+                      _lib.ptr(prepare["to_play"].to(device=x.device, dtype=torch.int32).contiguous()),
+                      _lib.stream_ptr())
         return MZNetworkOutput(value, [0. for _ in range(B)], policy, latent)
 
 
