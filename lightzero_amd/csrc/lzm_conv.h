@@ -406,7 +406,8 @@ __device__ __forceinline__ int bx_ep_pos(int lane, int t, int r) {
 
 // 3x3 epilogue: v = relu(acc + bias [+ amap] [+ xres]) -> split LDS planes of `out`; KEEP: xres = v
 // tiles T0 .. T0 + NT - 1 (xres / am hold those tiles only)
-template <int T0 = 0, int NT = 4>
+// RELU = false: store acc as is (the input latent's staging)
+template <int T0 = 0, int NT = 4, bool RELU = true>
 __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out, float bc, bool use_am,
                                              const float4 (&am)[NT], float (&xres)[4 * NT], bool add_res, bool keep,
                                              int lane, int c) {
@@ -421,7 +422,7 @@ __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out
       float x = acc[t][r] + bc;
       if (use_am) x += r == 0 ? am[t - T0].x : r == 1 ? am[t - T0].y : r == 2 ? am[t - T0].z : am[t - T0].w;
       if (add_res) x += xres[4 * (t - T0) + r];
-      x = x > 0.f ? x : 0.f;
+      if (RELU) x = x > 0.f ? x : 0.f;
       if (keep) xres[4 * (t - T0) + r] = x;
       v[r] = x;
     }
@@ -504,10 +505,20 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     xres[4 * t] = v.x; xres[4 * t + 1] = v.y; xres[4 * t + 2] = v.z; xres[4 * t + 3] = v.w;
   }
   trunk_copy_hidden(a, b);
-  // ... and all of it split into buffer 0 (borders zero)
-  for (int i = tid; i < 2 * kBxBuf / 8; i += kCvThreads) bx_lds4[i] = uint4{0u, 0u, 0u, 0u};
-  __syncthreads();
-  for (int i = tid; i < kCvCh * kCvPix; i += kCvThreads) bx_store(buf(0), cv_plane(i & 63), i >> 6, src[i]);
+  // ... split into buffer 0 from those registers by the epilogue's store path (interior), while the
+  // 36 border positions of both buffers are zeroed (disjoint addresses: one barrier)
+  {
+    bxf4 in4[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) in4[t] = bxf4{xres[4 * t], xres[4 * t + 1], xres[4 * t + 2], xres[4 * t + 3]};
+    const float4 no_am[4] = {};
+    bx_epilogue3<0, 4, false>(in4, buf(0), 0.f, false, no_am, xres, false, false, lane, c);
+  }
+  for (int k = tid; k < 2 * 3 * 36 * 8; k += kCvThreads) {  // [buffer][term][border position][16-B chunk]
+    const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
+    const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
+    bx_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
+  }
   __syncthreads();
   for (int i = 0; i < n3; ++i) {
     const float *w = layer_w(i);
