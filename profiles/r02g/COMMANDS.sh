@@ -8,3 +8,5 @@
 #   conv_mz.json, conv_ez.json <- tools/conv_bench.py --kind mz|ez (split-bf16 trunk, default)
 #   bench_philox.json, bench_zero_heads.json <- bench.py --rng philox / --zero-heads
 bash tools/gpu_final.sh
+# after the last trunk change (commit e74b1c8): bash tools/gpu_verify.sh
+#   gpu_tests_final.log, smoke_final.log, bench_final.json (21.95 M sims/s)
