@@ -7,17 +7,25 @@ MuZeroPolicy._forward_collect runs it (lzero/policy/muzero.py:617-690): initial_
 Roots.prepare (Dirichlet-mixed priors) -> MuZeroMCTSCtree.search (50 simulations) -> root
 visit distributions and values. Inputs are resident in HBM before the timed region.
 
-Multi-GPU: one process per GPU (torchrun); every rank searches its own 256 envs (envs are
-independent trees: weak scaling, no collective in the data path). value = all ranks' sims / the
-slowest rank's time.
+Multi-GPU: one process per GPU. Under torchrun the ranks come from the environment;
+`python bench.py --gpus N` started directly launches the N rank processes itself (launch_ranks:
+fresh interpreters, the parent never touches the GPU). Every rank searches its own 256 envs (envs
+are independent trees: weak scaling, no collective in the data path). value = all ranks' sims /
+the slowest rank's time. `--step collect` runs the device collector per rank and ends the timed
+region with the trajectory return (device pack + RCCL all-gather + statistics sum, trajectory.py).
+`--dry-run` checks the launch on gloo without a GPU.
 
 Extra objects on the JSON line:
   roofline     - dominant HIP kernel of the step: algorithmic work per launch / its live HIP-event
-                 duration vs the peak (fused: fp32 FLOPs vs the dense fp32 peak, plus the L2 weight
-                 stream; generic: bytes vs HBM); traffic = PMC HBM bytes per launch from the committed
-                 profile (profiles/pmc_latest.json); profiles/ holds the matching rocprof stats
-  cpu_baseline - the oracle's CPU restatement of the reference ctree driving the same network on
-                 the host cores (the reference's architecture with device='cpu'), bounded sample.
+                 duration vs the peak (fused: fp32 FLOPs vs the fp32 VALU peak — the network runs on
+                 v_pk_fma_f32, MFMA utilisation 0 —, plus the L2 weight stream; generic: bytes vs
+                 HBM); traffic = PMC HBM bytes per launch from the committed profile
+                 (profiles/pmc_latest.json); profiles/ holds the matching rocprof stats
+  cpu_baseline - the oracle's bit-exact CPU restatement of the reference ctree ("port"; the
+                 reference never ships to the GPU box) in BASELINE.md's four variants (tree only on
+                 1 thread / the CPU share; the reference search architecture with the network on the
+                 GPU / on the CPU share), the host's nproc and CPU model, and the reference-vs-port
+                 calibration ratios measured in the build container (profiles/cpu_calibration.json).
 """
 import argparse
 import json
@@ -33,7 +41,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP32_PEAK_TFLOPS = 157.3  # MI355X dense fp32 (matrix = vector rate on gfx950, MI355X_MICROARCH.md)
+FP32_PEAK_TFLOPS = 157.3  # MI355X fp32 VALU peak (= the f32 MFMA rate on gfx950, MI355X_MICROARCH.md)
 L2_PEAK_TBS = 34.5  # aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md)
 
 
@@ -54,10 +62,74 @@ def parse():
                         "DeviceSearchStep); python: the same sequence driven call by call from Python; "
                         "collect: one full env step of the device collector (search + action selection + "
                         "CartPole step + recording, lightzero_amd.collector.DeviceCollector)")
-    p.add_argument("--cpu-baseline-secs", type=float, default=12.0)
+    p.add_argument("--cpu-baseline-secs", type=float, default=30.0,
+                   help="total CPU-baseline sample over the four variants")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--zero-heads", action="store_true", help="reference zero-init last layers (all-tie search)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher check without a GPU: the ranks join a gloo group and rank 0 prints who joined")
     return p.parse_args()
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` run directly (not under torchrun): start N fresh rank processes with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (one per GPU, rendezvous on 127.0.0.1) and wait
+    for them; rank 0 prints the line. This parent never initialises the GPU (nothing before this
+    point calls into HIP) and starts children instead of re-exec'ing. A failing rank stops the
+    others; returns the first failing exit code (0 when every rank succeeded)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        pending = set(range(n))
+        while pending:
+            for r in sorted(pending):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                pending.discard(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    for q in pending:
+                        procs[q].terminate()
+            time.sleep(0.05)
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+                pr.wait()
+    return rc
+
+
+def rank_info(rank, local, device):
+    d = {"rank": rank, "local_rank": local}
+    if device is not None:
+        props = torch.cuda.get_device_properties(device)
+        d.update(device=str(device), name=props.name, pci_bus_id=getattr(props, "pci_bus_id", None))
+    return d
+
+
+def dry_run(world, rank, local):
+    """The launch logic without a GPU: every rank joins a gloo group (as the real ranks join
+    RCCL), the ranks are gathered and rank 0 prints them on one JSON line."""
+    if world > 1:
+        dist.init_process_group("gloo")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank_info(rank, local, None))
+    else:
+        ranks = [rank_info(rank, local, None)]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def build_model(device, zero_heads, seed):
@@ -117,6 +189,13 @@ class CollectStep:
         self.col.step()
         out = self.col.search.out
         self.last = (out["distributions"], out["values"], None)
+
+    def finish(self, world):
+        """the episodes finished since the last call: packed on the device and, with more than one
+        rank, all-gathered (RCCL) with the step / episode / duration sums (trajectory.py)"""
+        eps, st = self.col.gather_finished()
+        return {"episodes_all_ranks": len(eps), "rows": int(sum(len(e["action_segment"]) + 1 for e in eps)),
+                "total_envstep": st["total_envstep"], "world": world}
 
     def tree(self):
         return self.col.search.roots.tree
@@ -290,75 +369,54 @@ def algorithmic_bytes(B, A, H, V, dbar):
     return {"traverse": trav, "decode_backprop": dec}
 
 
-def load_reference_ctree():
-    """The reference's own compiled ctree (LightZero ctree_muzero, built from its sources by
-    oracle/build_ref.sh into oracle/_ref; git-ignored, travels with the tree), or None. Only this
-    CPU-baseline leg loads it: it is the thing timed beside the GPU, never part of the product."""
-    import glob
-    import importlib.util
-    paths = sorted(glob.glob(os.path.join(REPO, "oracle", "_ref", "mz_tree*.so")))
-    if not paths:
-        return None
+def host_cpu_info():
+    """The box's host CPU as the CPU-baseline line records it: nproc (os.cpu_count, the whole
+    machine), the affinity mask, the job's thread share (OMP_NUM_THREADS, which the GPU pool sets
+    per GPU) and the model name."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
     try:
-        spec = importlib.util.spec_from_file_location("mz_tree", paths[0])
-        mod = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(mod)
-        return mod
-    except (ImportError, OSError):
-        return None
+        with open("/proc/cpuinfo") as f:
+            info["model"] = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        info["model"] = None
+    return info
 
 
-def cpu_reference_ctree_search(mod, B, S, model_cpu, secs, threads):
-    """The reference's search loop on the host (mcts_ctree.py:245-321 with device='cpu'): the
-    reference's compiled ctree (batch_traverse / batch_backpropagate on Python lists), the same
-    network on torch CPU, InverseScalarTransform. Returns (sims/s, searches run, seconds)."""
-    torch.set_num_threads(threads)
-    rng = np.random.default_rng(0)
-    obs = torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32))
-    support = torch.arange(-300, 301, dtype=torch.float64).unsqueeze(0)
-
-    def inv(logits):
-        p = torch.softmax(logits, dim=1)
-        v = p.mul_(support).sum(1, keepdim=True)
-        tmp = (torch.sqrt(1 + 4 * 0.001 * (torch.abs(v) + 1 + 0.001)) - 1) / (2 * 0.001)
-        return (torch.sign(v) * (tmp * tmp - 1)).float()
-
-    legal = [[0, 1] for _ in range(B)]
-    to_play = [-1] * B
-    n, t0 = 0, time.perf_counter()
-    with torch.no_grad():
-        while True:
-            out = model_cpu.initial_inference(obs)
-            roots = mod.Roots(B, legal)
-            noises = rng.dirichlet([0.3, 0.3], size=B).astype(np.float32).tolist()
-            roots.prepare(0.25, noises, [0.0] * B, out.policy_logits.numpy().tolist(), to_play)
-            pool = [out.latent_state.numpy()]
-            mms = mod.MinMaxStatsList(B)
-            mms.set_delta(0.01)
-            for k in range(S):
-                results = mod.ResultsWrapper(num=B)
-                x, y, a, vtp = mod.batch_traverse(roots, 19652, 1.25, 0.997, mms, results, to_play)
-                lat = torch.from_numpy(np.asarray([pool[ix][iy] for ix, iy in zip(x, y)]))
-                o = model_cpu.recurrent_inference(lat, torch.from_numpy(np.asarray(a)).long())
-                pool.append(o.latent_state.numpy())
-                mod.batch_backpropagate(k + 1, 0.997, inv(o.reward).numpy().reshape(-1).tolist(),
-                                        inv(o.value).numpy().reshape(-1).tolist(), o.policy_logits.numpy().tolist(),
-                                        mms, results, vtp)
-            n += 1
-            el = time.perf_counter() - t0
-            if el >= secs:
-                return n * B * S / el, n, el
+def share_threads():
+    """Threads for the all-cores variants: the job's CPU share (OMP_NUM_THREADS when set — the
+    pool gives each GPU job 16 — else the affinity mask)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    n = int(env) if env and env.isdigit() and int(env) > 0 else len(os.sched_getaffinity(0))
+    return max(1, min(n, len(os.sched_getaffinity(0))))
 
 
-def cpu_reference_search(B, S, model_cpu, secs, threads):
-    """The reference's architecture on the host: oracle ctree (restated cnode.cpp) + the same
-    network on torch CPU + InverseScalarTransform + list glue, as mcts_ctree.py:228-321 runs
-    with device='cpu'. Returns (sims/s, searches run)."""
+def cpu_tree_only(B, A, S, threads, secs):
+    """BASELINE.md CPU plan (a)/(b): the oracle's bit-exact restatement of the reference ctree
+    (oracle/lz_oracle.c, cnode.cpp restated), tree only — prepare + S x (cbatch_traverse,
+    cbatch_backpropagate) with scripted network outputs — envs partitioned over `threads`
+    pthreads (shard-local tie-break streams). Returns (sims/s, searches, seconds)."""
+    from oracle.oracle import lib
+    L = lib()
+    t1 = L.lzo_bench_tree_only(B, A, S, threads, 1, 12345)
+    n = max(1, int(secs / max(t1, 1e-6)))
+    el = L.lzo_bench_tree_only(B, A, S, threads, n, 12345)
+    return B * S * n / el, n, el
+
+
+def cpu_reference_search(B, S, model, secs, threads, device=None):
+    """BASELINE.md CPU plan (c)/(d): the reference's search architecture (mcts_ctree.py:228-321):
+    the host tree (the oracle's restatement of cnode.cpp, single-threaded as the reference's
+    ctree) + the network through PyTorch + InverseScalarTransform + the host gather of
+    latent[x][y] and the list glue. device=None: the network on torch-CPU with `threads` threads
+    (plan (d)); a GPU device: the network on the GPU with per-simulation H2D / D2H copies, as
+    LightZero runs it with cuda=True (plan (c)). Returns (sims/s, searches, seconds)."""
     from oracle.oracle import OracleTree
     torch.set_num_threads(threads)
+    dev = torch.device("cpu") if device is None else device
     rng = np.random.default_rng(0)
-    obs = torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32))
-    support = torch.arange(-300, 301, dtype=torch.float64).unsqueeze(0)
+    obs = torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32)).to(dev)
+    support = torch.arange(-300, 301, dtype=torch.float64, device=dev).unsqueeze(0)
 
     def inv(logits):
         p = torch.softmax(logits, dim=1)
@@ -369,37 +427,89 @@ def cpu_reference_search(B, S, model_cpu, secs, threads):
     n, t0 = 0, time.perf_counter()
     with torch.no_grad():
         while True:
-            out = model_cpu.initial_inference(obs)
+            out = model.initial_inference(obs)
             tree = OracleTree(B, 2, S)
             tree.set_delta(np.float32(0.01))
             noises = rng.dirichlet([0.3, 0.3], size=B).astype(np.float32)
-            tree.prepare(np.float32(0.25), noises, np.zeros(B, np.float32), out.policy_logits.numpy(),
+            tree.prepare(np.float32(0.25), noises, np.zeros(B, np.float32), out.policy_logits.cpu().numpy(),
                          np.full(B, -1, np.int32))
-            pool = [out.latent_state.numpy()]
+            pool = [out.latent_state.cpu().numpy()]
             tp = np.full(B, -1, np.int32)
             for k in range(S):
                 x, y, a, vtp, _ = tree.traverse(19652, np.float32(1.25), np.float32(0.997), k, tp)
-                lat = torch.from_numpy(np.asarray([pool[ix][iy] for ix, iy in zip(x, y)]))
-                o = model_cpu.recurrent_inference(lat, torch.from_numpy(a.astype(np.int64)))
-                pool.append(o.latent_state.numpy())
-                tree.backprop(k + 1, np.float32(0.997), inv(o.reward).numpy().reshape(-1),
-                              inv(o.value).numpy().reshape(-1), o.policy_logits.numpy(), vtp)
+                lat = torch.from_numpy(np.asarray([pool[ix][iy] for ix, iy in zip(x, y)])).to(dev)
+                o = model.recurrent_inference(lat, torch.from_numpy(a.astype(np.int64)).to(dev))
+                pool.append(o.latent_state.cpu().numpy())
+                tree.backprop(k + 1, np.float32(0.997), inv(o.reward).cpu().numpy().reshape(-1),
+                              inv(o.value).cpu().numpy().reshape(-1), o.policy_logits.cpu().numpy(), vtp)
             n += 1
             el = time.perf_counter() - t0
             if el >= secs:
                 return n * B * S / el, n, el
+
+
+def load_calibration():
+    """The reference-vs-restatement timing ratios measured in the build container, where the
+    reference's own ctree may run (tools/cpu_calibration.py -> profiles/cpu_calibration.json);
+    the reference itself never travels to the GPU box."""
+    try:
+        with open(os.path.join(REPO, "profiles", "cpu_calibration.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return {k: d[k] for k in ("ref_over_port_time_tree_only", "ref_over_port_time_ref_arch", "host") if k in d}
+
+
+def cpu_baseline(B, S, zero_heads, secs, device):
+    """The CPU baseline of the line (rank 0, N = 1): BASELINE.md's four variants of the bit-exact
+    restatement ("port"; the reference never ships to the box), each a bounded sample:
+    (a) tree only, 1 thread; (b) tree only, the job's CPU share, envs partitioned;
+    (c) the reference architecture with the network on this GPU (1 host thread, per-simulation
+    H2D/D2H: LightZero's own deployment); (d) the reference architecture all on the CPU share.
+    `value` is (d), the whole reference search loop on host cores."""
+    T = share_threads()
+    var = {}
+    v, n, el = cpu_tree_only(B, 2, S, 1, 0.2 * secs)
+    var["a_tree_only_1t"] = {"value": round(v, 1), "cores": 1, "searches": n, "seconds": round(el, 2)}
+    v, n, el = cpu_tree_only(B, 2, S, T, 0.15 * secs)
+    var["b_tree_only_share"] = {"value": round(v, 1), "cores": T, "searches": n, "seconds": round(el, 2)}
+    model_gpu = build_model(device, zero_heads, seed=0)
+    v, n, el = cpu_reference_search(B, S, model_gpu, 0.3 * secs, 1, device=device)
+    var["c_ref_arch_gpu_net_1t"] = {"value": round(v, 1), "cores": 1, "searches": n, "seconds": round(el, 2),
+                                    "network": "this GPU (PyTorch-ROCm), per-simulation H2D/D2H"}
+    model_cpu = build_model(torch.device("cpu"), zero_heads, seed=0)
+    v, n, el = cpu_reference_search(B, S, model_cpu, 0.35 * secs, T)
+    var["d_ref_arch_cpu_share"] = {"value": round(v, 1), "cores": T, "searches": n, "seconds": round(el, 2),
+                                   "network": f"torch-CPU, {T} threads"}
+    d = var["d_ref_arch_cpu_share"]
+    return {"value": d["value"], "unit": "sims/s", "cores": T, "kind": "port",
+            "sample": f"{d['searches']} full searches (B={B}, S={S}) of the reference search loop "
+                      f"(mcts_ctree.py:228-321) over the oracle's bit-exact ctree restatement, same MLP on "
+                      f"torch-CPU with {T} threads, {d['seconds']}s; variants a-d per BASELINE.md",
+            "variants": var, "host": host_cpu_info(), "calibration": load_calibration()}
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}", file=sys.stderr)
+    if args.dry_run:
+        return dry_run(world, rank, local)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, rank_info(rank, local, device))
+    else:
+        ranks = [rank_info(rank, local, device)]
     B, S = args.envs, args.sims
     model = build_model(device, args.zero_heads, seed=0)
     if args.path == "fused" and args.step == "graph":
@@ -411,6 +521,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if hasattr(step, "finish"):
+        step.finish(world)  # (episodes of the warmup steps, untimed)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -418,6 +530,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    # collect mode: the trajectory return ends the timed region (pack the episodes finished in
+    # it on the device, all-gather them over RCCL, sum-reduce the collector statistics)
+    traj = step.finish(world) if hasattr(step, "finish") else None
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -456,7 +571,11 @@ def main():
                 kname = "search_mlp_kernel"
                 wbytes = 4 * _lib_kernel_floats()
                 l2 = -(-B // R) * S * wbytes  # every workgroup streams the kernel-layout weights once per simulation
-            roofline = {"bound": "mfma", "kernel": kname, "achieved": round(achieved, 3),
+            # the network runs on the VALU (v_pk_fma_f32 chains on 1 row per workgroup: no M
+            # dimension for a matrix tile), so the bound is the fp32 VALU peak and the MFMA
+            # utilisation of this network step is 0 by design
+            roofline = {"bound": "valu", "compute": "fp32 VALU (v_pk_fma_f32)", "mfma_utilisation": 0.0,
+                        "kernel": kname, "achieved": round(achieved, 3),
                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
                         "traffic": pmc_traffic(kname), "alg_flops_per_launch": int(flops),
                         "alg_hbm_bytes_per_launch": int(hbm), "hbm_achieved_GBs": round(hbm / sec / 1e9, 2),
@@ -474,20 +593,7 @@ def main():
                         "kernels_us": {k: round(v * 1e3, 2) for k, v in ms.items()},
                         "mean_search_len": round(dbar, 3)}
         if world == 1 and not args.no_cpu_baseline:
-            cores = min(16, os.cpu_count() or 1)
-            model_cpu = build_model(torch.device("cpu"), args.zero_heads, seed=0)
-            ref = load_reference_ctree()
-            if ref is not None:
-                # the reference's compiled ctree (single-threaded, as in LightZero) driving the same
-                # network on `cores` torch threads
-                v, n, secs = cpu_reference_ctree_search(ref, B, S, model_cpu, args.cpu_baseline_secs, cores)
-                kind, what = "reference", "LightZero ctree_muzero compiled from the reference sources"
-            else:
-                v, n, secs = cpu_reference_search(B, S, model_cpu, args.cpu_baseline_secs, cores)
-                kind, what = "port", "oracle ctree restatement"
-            cpu = {"value": round(v, 1), "unit": "sims/s", "cores": cores, "kind": kind,
-                   "sample": f"{n} full searches (B={B}, S={S}, mcts_ctree.py search loop, {what}, same MLP on "
-                             f"torch-CPU with {cores} threads, {secs:.1f}s)"}
+            cpu = cpu_baseline(B, S, args.zero_heads, args.cpu_baseline_secs, device)
     if rank == 0:
         line = {"metric": "MCTS simulations/sec (whole node), 256 parallel envs x 50 sims/step",
                 "value": round(value, 1), "unit": "sims/s", "n_gpus": world, "steps": args.steps,
@@ -500,7 +606,8 @@ def main():
                            "hip_graph": (args.step != "python") if args.path == "fused" else bool(args.graph),
                            "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
-                "tie_stream_errors": int(sum(tie_errors)), "search_diag": sdiag, "roofline": roofline, "cpu_baseline": cpu}
+                "tie_stream_errors": int(sum(tie_errors)), "search_diag": sdiag, "ranks": ranks,
+                "trajectory": traj, "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -17,7 +17,7 @@ values, root latents and policy logits). `step_counter` counts the steps (device
 import torch
 
 from .initial import fused_initial_or_none
-from .mcts_ctree import MuZeroMCTSCtree
+from .mcts_ctree import MuZeroMCTSCtree, _step_net
 from .utils import EasyDict
 
 
@@ -128,7 +128,9 @@ class DeviceSearchStep:
         if self.initial is not None:
             self.initial._pack()
         if self.roots is not None and self.roots.tree is not None:
-            self.mcts._fused(self.model, self.roots.tree)
+            if self.mcts._fused(self.model, self.roots.tree) is None:
+                # generic path (e.g. a conv model): the folded step network re-folds in place
+                _step_net(self.mcts, self.model)
 
     def step(self):
         """One collect-time search pass over the current inputs; returns the static output dict."""

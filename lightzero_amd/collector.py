@@ -85,6 +85,7 @@ class DeviceCollector:
         self.search.reset_seed_counter()
         self._consumed = np.zeros(self.n, dtype=np.int64)
         self.envstep = 0
+        self._gathered_at = 0
 
     def step(self):
         """One env step for every env (one graph replay)."""
@@ -114,8 +115,22 @@ class DeviceCollector:
             if new.sum() >= n_episode:
                 break
         el = time.perf_counter() - t0
+        return self._return(counts, self.envstep - steps0, el, group)
+
+    def gather_finished(self, group=None):
+        """The episodes finished since the last collect / gather, without stepping: packed on the
+        device and, under a process group of more than one rank, all-gathered with the statistics
+        sum-reduced (as collect does). Returns (episodes, stats)."""
+        counts = self.ep_count.cpu().numpy().astype(np.int64)
+        self.search.roots.tree.check_errors()
+        if ((counts - self._consumed) >= self.E).any():  # the running episode reuses slot ep_count % E
+            raise RuntimeError("episode slots overwritten before collection: raise episode_slots")
+        steps = self.envstep - getattr(self, "_gathered_at", 0)
+        return self._return(counts, steps, 0.0, group)
+
+    def _return(self, counts, steps, el, group):
         packed, index = self._pack(counts)
-        steps = self.envstep - steps0
+        self._gathered_at = self.envstep
         world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         if world > 1:
             rank = dist.get_rank(group)
@@ -126,7 +141,8 @@ class DeviceCollector:
             rank = 0
             episodes = unpack_episodes(packed.cpu().numpy(), index.numpy(), self.OBS_DIM, self.A)
             tot_steps, tot_eps, tot_secs = steps, len(episodes), el
-        stats = dict(envstep=steps, seconds=el, env_steps_per_s=steps / el, sims_per_s=steps * self.S / el,
+        stats = dict(envstep=steps, seconds=el, env_steps_per_s=steps / el if el else None,
+                     sims_per_s=steps * self.S / el if el else None,
                      episode_returns=[float(e["reward_segment"].sum()) for e in episodes], rank=rank, world=world,
                      total_envstep=tot_steps, total_episodes=tot_eps, total_duration=tot_secs)
         return episodes, stats

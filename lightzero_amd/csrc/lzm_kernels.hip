@@ -55,7 +55,7 @@ struct TraverseArgs {
   const uint32_t *jfirst;  // [kMaxWG][31]
   const uint32_t *jnext;   // [kMaxWG][31]
   int32_t *off;            // [B]
-  int32_t *diag;           // [0] passes
+  int32_t *diag;           // [0] fixed-point passes of the last call ([1] unused: failures go to err)
   int32_t *err;            // sticky error counters (lzm_check_errors): [2] fixed point not reached
   int32_t *hint;           // [0] stream length used by the previous call
   float disc;
@@ -777,7 +777,10 @@ static void dfree(void *p) {
 
 static void free_tree(lzm_handle *h) {
   dfree(h->stat); dfree(h->meta); dfree(h->path); dfree(h->path_act); dfree(h->stream); dfree(h->lut);
+  dfree(h->step_seeds);
   h->stat = nullptr; h->meta = nullptr; h->path = nullptr; h->path_act = nullptr; h->stream = nullptr; h->lut = nullptr;
+  h->step_seeds = nullptr;
+  h->step_seeds_n = 0;
 }
 
 // pb_c table over the integer parent count N = visit-1 (cucb_score, cnode.cpp:673-674):
@@ -821,6 +824,11 @@ static int alloc_tree(lzm_handle *h, int sims) {
   h->lut_n = sims + 8;
   LZM_HIP(hipMalloc(&h->lut, sizeof(float2) * h->lut_n));
   h->lut_base = -1;
+  // the collect-step seeds of the weight-streaming search (lzm_search_set_step): sized with the
+  // tree, so a captured step never allocates and a reserve (generation bump) retires graphs that
+  // point at the old buffer together with the tree's
+  LZM_HIP(hipMalloc(&h->step_seeds, sizeof(int32_t) * (size_t)(sims + 1)));
+  h->step_seeds_n = sims + 1;
   if (!(h->flags & LZM_RNG_FAST)) {
     // parity-mode draw tables and look-back words, allocated here rather than at first use so
     // that a search captured into a HIP graph never allocates
@@ -877,7 +885,7 @@ int lzm_destroy(lzm_handle *h) {
   free_tree(h);
   dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag); dfree(h->err);
   dfree(h->hint); dfree(h->norm_flag); dfree(h->jmat);
-  dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag); dfree(h->phase); dfree(h->step_seeds);
+  dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag); dfree(h->phase);
   delete h;
   return LZM_OK;
 }
@@ -1778,11 +1786,9 @@ int lzm_search_mlp(lzm_handle *h, int hidden, int head_hidden, int support, int 
   // collect-step mode: the prologue (seeds, fresh min-max) and epilogue (root outputs, counter)
   // as one launch each around the search
   if (h->step_count || h->step_fresh) {
-    if (h->step_count && h->step_seeds_n < S) {
-      dfree(h->step_seeds);
-      h->step_seeds = nullptr;
-      LZM_HIP(hipMalloc(&h->step_seeds, (size_t)h->sims_cap * sizeof(int32_t)));
-      h->step_seeds_n = h->sims_cap;
+    if (h->step_count && h->step_seeds_n < S) {  // (allocated with the tree: S <= sims_cap)
+      set_err("lzm_search_mlp: step seeds buffer smaller than num_simulations (reserve first)");
+      return LZM_ERR_STATE;
     }
     const int n = std::max(S, h->B);
     hipLaunchKernelGGL(step_prologue_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->step_count,

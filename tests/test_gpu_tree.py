@@ -142,5 +142,5 @@ def test_traverse_passes_small():
         o = gt.traverse(19652, np.float32(1.25), np.float32(0.997), int(tr["seeds"][k]), tr["to_play"])
         passes.append(gt.t.traverse_passes())
         gt.backprop(k + 1, np.float32(0.997), tr["resp_reward"][k], tr["resp_value"][k], tr["resp_logits"][k], o[3])
-    assert all(p[1] == 0 for p in passes)
+    gt.t.check_errors()  # raises on a look-back timeout / draw-table overflow (sticky err words)
     assert max(p[0] for p in passes) <= 4, passes
