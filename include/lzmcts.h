@@ -208,18 +208,21 @@ int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*
  * lzm_cartpole_reset: every env to U(-0.05, 0.05)^4 (Philox stream `seed`).
  * lzm_cartpole_collect_step, one thread per env, after a search over `obs`: select the action from
  * `visits` int32[n][A] (select_action, lzero/policy/utils.py:515-539: visits^(1/temperature)
- * sampling, or argmax when `deterministic`), record obs / action / reward / child visits / root
- * value into episode slot ep_count[i] % E of rec_* ([n][E][T(+1)][...], GameSegment fields,
- * game_segment.py:129-218), step the env (gymnasium CartPole equations in float64, truncation at
+ * sampling, or argmax when `deterministic`), record obs / action / reward / root visit counts /
+ * root value (and, when `pred_value` is given, the root's predicted value for priorities,
+ * muzero_collector.py:200-227) into episode slot ep_count[i] % E of rec_* ([n][E][T(+1)][...],
+ * GameSegment fields, game_segment.py:129-218; the host normalises the counts as
+ * store_search_stats does), step the env (gymnasium CartPole equations in float64, truncation at
  * max_steps), auto-reset finished episodes (ep_len[n][E], ep_count[n]) and write the next root's
  * obs and Dirichlet(noise_alpha) noises float[n][A]. `counter` (int64, device) keys this step's
- * Philox streams; the caller advances it. */
+ * Philox streams; the caller advances it. pred_value / rec_pred: both or neither. */
 int lzm_cartpole_reset(int n, double *state, int32_t *steps, float *obs, uint32_t seed, void *stream);
 int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
-                              double *state, int32_t *steps, float *obs, float *noises, float noise_alpha,
-                              float temperature, int deterministic, float *rec_obs, int32_t *rec_action,
-                              float *rec_reward, float *rec_child, float *rec_value, int32_t *ep_len,
-                              int32_t *ep_count, int max_steps, uint32_t seed, const int64_t *counter, void *stream);
+                              const float *pred_value, double *state, int32_t *steps, float *obs, float *noises,
+                              float noise_alpha, float temperature, int deterministic, float *rec_obs,
+                              int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
+                              float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
+                              const int64_t *counter, void *stream);
 
 /* ---- batched AlphaZero for TicTacToe (replaces MCTS.get_next_action,
  * lzero/mcts/ctree/ctree_alphazero/mcts_alphazero.cpp:131-207, called per env from

@@ -78,8 +78,8 @@ SIGNATURES = {
     "lzm_debug_philox": [_vp, _vp, _i, _vp],
     "lzm_debug_phase_cycles": [_vp, _vp, _i],
     "lzm_cartpole_reset": [_i, _vp, _vp, _vp, _u32, _vp],
-    "lzm_cartpole_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp, _vp,
-                                  _vp, _vp, _i, _u32, _vp, _vp],
+    "lzm_cartpole_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
     "lzm_az_workspace_bytes": [_i, _i, ctypes.POINTER(_i64)],
     "lzm_az_noise_table": [_d, _i, _vp],
     "lzm_az_set_constants": [_i, _i, _vp, _d, _d, _d, _vp],

@@ -90,7 +90,7 @@ class DeviceSearchStep:
                                  step=dict(count=self._count, base=self._base, dist=dist, values=values,
                                            increment=self.epilogue is None))
                 res = dict(distributions=dist, values=values, latent_state=out.latent_state,
-                           policy_logits=out.policy_logits)
+                           policy_logits=out.policy_logits, value_logits=out.value)
                 if self.epilogue is not None:
                     self.epilogue(res)
                     self._count.add_(1)

@@ -36,8 +36,10 @@ struct CollectArgs {
   float *rec_obs;              // [n][E][T+1][4]
   int32_t *rec_action;         // [n][E][T]
   float *rec_reward;           // [n][E][T]
-  float *rec_child;            // [n][E][T][A]
+  int32_t *rec_visits;         // [n][E][T][A] root visit counts (store_search_stats normalises on the host)
   float *rec_value;            // [n][E][T]
+  const float *pred_value;     // [n] the root's predicted value (nullable: priorities off)
+  float *rec_pred;             // [n][E][T] (nullable)
   int32_t *ep_len;             // [n][E] length of the finished episode in each slot
   int32_t *ep_count;           // [n] finished episodes (slot of the running one = ep_count % E)
 };
@@ -128,8 +130,6 @@ __global__ void cartpole_collect_kernel(CollectArgs p) {
   PhiloxStream rs{p.seed, (uint32_t)i, (uint32_t)step, (uint32_t)(step >> 32), 2u, 0u};
   // ---- select_action: p_a = v_a^(1/T) / sum (float64), sample, or argmax (first max)
   const int32_t *v = p.visits + (size_t)i * A;
-  int vs = 0;
-  for (int a = 0; a < A; ++a) vs += v[a] > 0 ? v[a] : 0;
   int action = 0;
   if (p.deterministic) {
     for (int a = 1; a < A; ++a)
@@ -157,9 +157,9 @@ __global__ void cartpole_collect_kernel(CollectArgs p) {
   if (t < p.T) {
     for (int j = 0; j < 4; ++j) p.rec_obs[(slot * (p.T + 1) + t) * 4 + j] = ob[j];
     p.rec_action[slot * p.T + t] = action;
-    for (int a = 0; a < A; ++a)
-      p.rec_child[(slot * p.T + t) * A + a] = vs > 0 ? (float)v[a] / (float)vs : 0.0f;
+    for (int a = 0; a < A; ++a) p.rec_visits[(slot * p.T + t) * A + a] = v[a];
     p.rec_value[slot * p.T + t] = p.root_value[i];
+    if (p.rec_pred) p.rec_pred[slot * p.T + t] = p.pred_value[i];
   }
   // ---- env step
   double *s = p.state + (size_t)i * 4;

@@ -1904,13 +1904,14 @@ int lzm_cartpole_reset(int n, double *state, int32_t *steps, float *obs, uint32_
 }
 
 int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
-                              double *state, int32_t *steps, float *obs, float *noises, float noise_alpha,
-                              float temperature, int deterministic, float *rec_obs, int32_t *rec_action,
-                              float *rec_reward, float *rec_child, float *rec_value, int32_t *ep_len,
-                              int32_t *ep_count, int max_steps, uint32_t seed, const int64_t *counter, void *stream) {
+                              const float *pred_value, double *state, int32_t *steps, float *obs, float *noises,
+                              float noise_alpha, float temperature, int deterministic, float *rec_obs,
+                              int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
+                              float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
+                              const int64_t *counter, void *stream) {
   if (n <= 0 || A <= 0 || A > 64 || T <= 0 || E <= 0 || !visits || !root_value || !state || !steps || !obs ||
-      !noises || !rec_obs || !rec_action || !rec_reward || !rec_child || !rec_value || !ep_len || !ep_count ||
-      !counter || !(temperature > 0.0f) || !(noise_alpha > 0.0f)) {
+      !noises || !rec_obs || !rec_action || !rec_reward || !rec_visits || !rec_value || !ep_len || !ep_count ||
+      !counter || !(temperature > 0.0f) || !(noise_alpha > 0.0f) || (!pred_value) != (!rec_pred)) {
     set_err("lzm_cartpole_collect_step: bad arguments");
     return LZM_ERR_ARG;
   }
@@ -1918,8 +1919,9 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
   a.n = n; a.A = A; a.T = T; a.E = E; a.max_steps = max_steps; a.deterministic = deterministic;
   a.temperature = temperature; a.noise_alpha = noise_alpha; a.seed = seed; a.counter = counter;
   a.visits = visits; a.root_value = root_value; a.state = state; a.steps = steps; a.obs = obs; a.noises = noises;
-  a.rec_obs = rec_obs; a.rec_action = rec_action; a.rec_reward = rec_reward; a.rec_child = rec_child;
-  a.rec_value = rec_value; a.ep_len = ep_len; a.ep_count = ep_count;
+  a.rec_obs = rec_obs; a.rec_action = rec_action; a.rec_reward = rec_reward; a.rec_visits = rec_visits;
+  a.rec_value = rec_value; a.pred_value = pred_value; a.rec_pred = rec_pred; a.ep_len = ep_len;
+  a.ep_count = ep_count;
   hipLaunchKernelGGL(cartpole_collect_kernel, dim3((n + 127) / 128), dim3(128), 0, (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;

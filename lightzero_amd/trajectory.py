@@ -2,7 +2,7 @@
 collector.
 
 Each rank's DeviceCollector records its envs' episodes in device-resident slots (rec_obs
-[n, E, T+1, obs], rec_action / rec_reward / rec_value [n, E, T], rec_child [n, E, T, A]). After
+[n, E, T+1, obs], rec_action / rec_reward / rec_value [n, E, T], rec_visits [n, E, T, A]). After
 `collect()`, the finished episodes are packed on the device into one float32 block (no host copy
 of the payload), the blocks of all ranks are exchanged with one all-gather over the process group
 (RCCL over xGMI on the GPU node, gloo in the CPU tests), and unpacked into GameSegment-shaped
@@ -10,9 +10,10 @@ dicts (the fields of lzero/mcts/buffer/game_segment.py:229-294). The collector s
 sum-reduced as MuZeroCollector does under DDP (lzero/worker/muzero_collector.py:709-712).
 
 Packed layout: episode j of length L occupies L + 1 consecutive rows of width
-W = obs_dim + 1 + 1 + A + 1: [obs_t | action_t | reward_t | child_visits_t (A) | root_value_t];
-row L carries the final observation (the obs segment has L + 1 entries) and zeros elsewhere.
-Actions are small integers, exact in float32. The index is int64 [n_ep, 3] = (env_id, L, first row).
+W = obs_dim + 1 + 1 + A + 1 (+ 1 with predicted values): [obs_t | action_t | reward_t |
+root visit counts_t (A) | root_value_t (| pred_value_t)]; row L carries the final observation (the
+obs segment has L + 1 entries) and zeros elsewhere. Actions and visit counts are small integers,
+exact in float32. The index is int64 [n_ep, 3] = (env_id, L, first row).
 """
 from typing import List, Tuple
 
@@ -21,15 +22,16 @@ import torch
 import torch.distributed as dist
 
 
-def row_width(obs_dim: int, A: int) -> int:
-    return obs_dim + 3 + A
+def row_width(obs_dim: int, A: int, pred: bool = False) -> int:
+    return obs_dim + 3 + A + int(bool(pred))
 
 
-def pack_episodes(rec_obs, rec_action, rec_reward, rec_child, rec_value, episodes: List[Tuple[int, int, int]]):
+def pack_episodes(rec_obs, rec_action, rec_reward, rec_visits, rec_value, episodes: List[Tuple[int, int, int]],
+                  rec_pred=None):
     """episodes: [(env_id, slot, L)] -> (packed f32 [rows, W] on the buffers' device, index i64 [n_ep, 3])."""
     dev = rec_obs.device
-    obs_dim, A = rec_obs.shape[-1], rec_child.shape[-1]
-    W = row_width(obs_dim, A)
+    obs_dim, A = rec_obs.shape[-1], rec_visits.shape[-1]
+    W = row_width(obs_dim, A, rec_pred is not None)
     lens = np.array([L for _, _, L in episodes], np.int64)
     rows = int((lens + 1).sum())
     index = np.zeros((len(episodes), 3), np.int64)
@@ -47,25 +49,35 @@ def pack_episodes(rec_obs, rec_action, rec_reward, rec_child, rec_value, episode
     tc = torch.from_numpy(np.where(last, 0, tt)).to(dev)  # clamp to a valid step for the other fields
     keep = torch.from_numpy(~last).to(dev).to(torch.float32).unsqueeze(1)
     out = torch.empty((rows, W), dtype=torch.float32, device=dev)
-    out[:, :obs_dim] = rec_obs[i_t, e_t, t_t]
-    out[:, obs_dim:obs_dim + 1] = rec_action[i_t, e_t, tc].to(torch.float32).unsqueeze(1) * keep
-    out[:, obs_dim + 1:obs_dim + 2] = rec_reward[i_t, e_t, tc].unsqueeze(1) * keep
-    out[:, obs_dim + 2:obs_dim + 2 + A] = rec_child[i_t, e_t, tc] * keep
-    out[:, obs_dim + 2 + A:] = rec_value[i_t, e_t, tc].unsqueeze(1) * keep
+    c = obs_dim
+    out[:, :c] = rec_obs[i_t, e_t, t_t]
+    out[:, c:c + 1] = rec_action[i_t, e_t, tc].to(torch.float32).unsqueeze(1) * keep
+    out[:, c + 1:c + 2] = rec_reward[i_t, e_t, tc].unsqueeze(1) * keep
+    out[:, c + 2:c + 2 + A] = rec_visits[i_t, e_t, tc].to(torch.float32) * keep
+    out[:, c + 2 + A:c + 3 + A] = rec_value[i_t, e_t, tc].unsqueeze(1) * keep
+    if rec_pred is not None:
+        out[:, c + 3 + A:] = rec_pred[i_t, e_t, tc].unsqueeze(1) * keep
     return out, torch.from_numpy(index)
 
 
 def unpack_episodes(packed: np.ndarray, index: np.ndarray, obs_dim: int, A: int, rank: int = 0) -> List[dict]:
-    """GameSegment-shaped dicts from one rank's block (host arrays)."""
+    """GameSegment-shaped dicts from one rank's block (host arrays). child_visit_segment is
+    store_search_stats' visit / sum in float64; `visits` keeps the raw counts."""
     eps = []
+    has_pred = packed.shape[1] == row_width(obs_dim, A, True)
+    c = obs_dim
     for env_id, L, r0 in np.asarray(index, np.int64):
         blk = packed[r0:r0 + L + 1]
-        eps.append(dict(rank=rank, env_id=int(env_id), obs_segment=blk[:, :obs_dim].copy(),
-                        action_segment=blk[:L, obs_dim].astype(np.int64),
-                        reward_segment=blk[:L, obs_dim + 1].copy(),
-                        child_visit_segment=blk[:L, obs_dim + 2:obs_dim + 2 + A].copy(),
-                        root_value_segment=blk[:L, obs_dim + 2 + A].copy(),
-                        to_play_segment=np.full(L, -1, np.int32), action_mask_segment=np.ones((L, A), np.int8)))
+        visits = np.rint(blk[:L, c + 2:c + 2 + A]).astype(np.int64)
+        tot = visits.sum(axis=1, keepdims=True).astype(np.float64)
+        tot[tot == 0] = 1e-6
+        e = dict(rank=rank, env_id=int(env_id), obs_segment=blk[:, :c].copy(),
+                 action_segment=np.rint(blk[:L, c]).astype(np.int64), reward_segment=blk[:L, c + 1].copy(),
+                 visits=visits, child_visit_segment=visits / tot, root_value_segment=blk[:L, c + 2 + A].copy(),
+                 to_play_segment=np.full(L, -1, np.int32), action_mask_segment=np.ones((L, A), np.int8))
+        if has_pred:
+            e["pred_value_segment"] = blk[:L, c + 3 + A].copy()
+        eps.append(e)
     return eps
 
 

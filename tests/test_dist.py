@@ -73,7 +73,7 @@ def _fake_records(rank):
     rec = dict(obs=torch.randn(N_ENV, E_SLOTS, T_MAX + 1, OBS, generator=g),
                action=torch.randint(0, ACT, (N_ENV, E_SLOTS, T_MAX), generator=g, dtype=torch.int32),
                reward=torch.randn(N_ENV, E_SLOTS, T_MAX, generator=g),
-               child=torch.rand(N_ENV, E_SLOTS, T_MAX, ACT, generator=g),
+               child=torch.randint(0, 30, (N_ENV, E_SLOTS, T_MAX, ACT), generator=g, dtype=torch.int32),
                value=torch.randn(N_ENV, E_SLOTS, T_MAX, generator=g))
     rng = np.random.default_rng(rank)
     eps = [(int(i), int(e), int(rng.integers(1, T_MAX + 1))) for i in range(N_ENV) for e in range(E_SLOTS)
@@ -98,7 +98,10 @@ def _check_episodes(got, want, rank):
         assert np.array_equal(g["obs_segment"], w["obs"])
         assert np.array_equal(g["action_segment"], w["action"].astype(np.int64))
         assert np.array_equal(g["reward_segment"], w["reward"])
-        assert np.array_equal(g["child_visit_segment"], w["child"])
+        assert np.array_equal(g["visits"], w["child"].astype(np.int64))
+        tot = w["child"].sum(axis=1, keepdims=True).astype(np.float64)
+        tot[tot == 0] = 1e-6
+        assert np.array_equal(g["child_visit_segment"], w["child"] / tot)  # store_search_stats, float64
         assert np.array_equal(g["root_value_segment"], w["value"])
         assert g["to_play_segment"].shape == (len(w["action"]),)
 

@@ -20,15 +20,15 @@ def _raw_step(n, visits, state, steps, obs, counter, temperature=1.0, determinis
     A = visits.shape[1]
     rec = dict(obs=torch.zeros((n, E, T + 1, 4), device=DEV), action=torch.zeros((n, E, T), dtype=torch.int32,
                                                                                   device=DEV),
-               reward=torch.zeros((n, E, T), device=DEV), child=torch.zeros((n, E, T, A), device=DEV),
+               reward=torch.zeros((n, E, T), device=DEV), child=torch.zeros((n, E, T, A), dtype=torch.int32, device=DEV),
                value=torch.zeros((n, E, T), device=DEV), ep_len=torch.zeros((n, E), dtype=torch.int32, device=DEV),
                ep_count=torch.zeros(n, dtype=torch.int32, device=DEV))
     noises = torch.zeros((n, A), device=DEV)
     value = torch.zeros(n, device=DEV)
-    call("lzm_cartpole_collect_step", n, A, T, E, ptr(visits), ptr(value), ptr(state), ptr(steps), ptr(obs), ptr(noises),
-         0.3, float(temperature), int(deterministic), ptr(rec["obs"]), ptr(rec["action"]), ptr(rec["reward"]),
-         ptr(rec["child"]), ptr(rec["value"]), ptr(rec["ep_len"]), ptr(rec["ep_count"]), T, seed, ptr(counter),
-         stream_ptr())
+    call("lzm_cartpole_collect_step", n, A, T, E, ptr(visits), ptr(value), None, ptr(state), ptr(steps), ptr(obs),
+         ptr(noises), 0.3, float(temperature), int(deterministic), ptr(rec["obs"]), ptr(rec["action"]),
+         ptr(rec["reward"]), ptr(rec["child"]), ptr(rec["value"]), None, ptr(rec["ep_len"]), ptr(rec["ep_count"]), T,
+         seed, ptr(counter), stream_ptr())
     return rec, noises
 
 
@@ -119,6 +119,6 @@ def test_device_collector_graph_equals_eager():
         for _ in range(20):
             col.step()
         torch.cuda.synchronize()
-        out.append((col.rec_action.cpu().numpy(), col.rec_child.cpu().numpy(), col.state.cpu().numpy()))
+        out.append((col.rec_action.cpu().numpy(), col.rec_visits.cpu().numpy(), col.state.cpu().numpy()))
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)

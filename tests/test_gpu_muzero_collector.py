@@ -1,0 +1,114 @@
+"""GPU: the MuZeroCollector drop-in (lightzero_amd.worker) against the host restatement of the
+reference's collect loop (oracle/collector_ref.py).
+
+Host-parity mode — MuZeroCollector's host loop over MuZeroCollectPolicy (GPU search, numpy noise
+and action draws): on the same numpy seed and traverse seeds, the restatement — the reference's
+loop and _forward_collect with the ORACLE tree replaying the network outputs the GPU search
+recorded — issues the same tree requests, draws the same noises, picks the same actions and
+returns identical segments (observations, actions, rewards, visit distributions, root values,
+masks, players), priorities and done flags. At the config-1 shape (8 envs x 25 sims) and the
+headline shape (256 x 50), with segment rollover exercised (game_segment_length 7 and 50).
+
+Device path — DeviceCartPoleEnvManager (the graph-captured device collector, Philox streams): the
+episodes the device played, replayed through the restatement, give the segments, priorities,
+flags and pool order the collector returned (n_episode == env_num and > env_num).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle.collector_ref import EpisodeEnv, EpisodeForward, ReplayForward, ref_collect
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+
+
+def _model(seed=0):
+    from lightzero_amd.model_mlp import cartpole_muzero_model
+    torch.manual_seed(seed)
+    m = cartpole_muzero_model(random_heads=True)
+    g = torch.Generator().manual_seed(seed + 1)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm1d):
+            with torch.no_grad():
+                mod.running_mean.copy_(torch.randn(mod.running_mean.shape, generator=g) * 0.1)
+                mod.running_var.copy_(torch.rand(mod.running_var.shape, generator=g) * 0.5 + 0.75)
+    return m.to(DEV).eval()
+
+
+def _eq(a, b, what):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.dtype == b.dtype, (what, a.dtype, b.dtype)
+    assert a.shape == b.shape and np.array_equal(a, b), what
+
+
+def _compare(segs, meta, ref_segs, ref_meta):
+    assert len(segs) == len(ref_segs) and len(meta) == len(ref_meta)
+    for g, r in zip(segs, ref_segs):
+        for f in ("obs_segment", "action_segment", "reward_segment", "child_visit_segment", "root_value_segment",
+                  "action_mask_segment", "to_play_segment"):
+            _eq(getattr(g, f), r[f], f)
+    for m, rm in zip(meta, ref_meta):
+        assert m['done'] == rm['done'] and m['unroll_plus_td_steps'] == rm['unroll_plus_td_steps']
+        if rm['priorities'] is None:
+            assert m['priorities'] is None
+        else:
+            _eq(m['priorities'], rm['priorities'], 'priorities')
+
+
+@pytest.mark.parametrize("n,S,gsl", [(8, 25, 50), (8, 25, 7), (256, 50, 50)])
+def test_parity_mode_matches_host_restatement(n, S, gsl):
+    from lightzero_amd.envs import SyncEnvManager
+    from lightzero_amd.policy import MuZeroCollectPolicy, policy_config
+    from lightzero_amd.tree import SequentialSeeds, set_seed_source
+    from lightzero_amd.worker import MuZeroCollector
+    cfg = policy_config(num_simulations=S, game_segment_length=gsl, device=DEV, use_priority=True, n_episode=n)
+    policy = MuZeroCollectPolicy(cfg, _model(1))
+    policy.record = True
+    set_seed_source(SequentialSeeds(11))
+    np.random.seed(123)
+    try:
+        col = MuZeroCollector(env=SyncEnvManager.cartpole(n, seed=5), policy=policy, policy_config=cfg)
+        segs, meta = col.collect(n_episode=n, policy_kwargs=dict(temperature=1.0, epsilon=0.0))
+    finally:
+        set_seed_source(None)
+    np.random.seed(123)
+    fwd = ReplayForward(cfg, policy.records)
+    ref_segs, ref_meta, st = ref_collect(cfg, SyncEnvManager.cartpole(n, seed=5), fwd, n)
+    assert fwd.mismatch == [], fwd.mismatch[:5]
+    assert fwd.k == len(policy.records)
+    _compare(segs, meta, ref_segs, ref_meta)
+    assert col.envstep == st["steps"] and len(segs) >= n
+    # the visit counts behind the segments sum to the simulations
+    for r in policy.records:
+        assert all(sum(d) == S for d in r["dist"])
+
+
+def _played(sched):
+    return [[dict(obs=e["obs_segment"], action=e["action_segment"], reward=e["reward_segment"], visits=e["visits"],
+                  value=e["root_value_segment"], pred=e.get("pred_value_segment")) for e in eps] for eps in sched.played]
+
+
+@pytest.mark.parametrize("n,n_ep,gsl,prio", [(16, 16, 10, True), (32, 48, 50, False), (64, 64, 50, True)])
+def test_device_path_segments_match_restatement(n, n_ep, gsl, prio):
+    from lightzero_amd.envs import DeviceCartPoleEnvManager
+    from lightzero_amd.policy import MuZeroCollectPolicy, policy_config
+    from lightzero_amd.worker import MuZeroCollector
+    cfg = policy_config(num_simulations=12, game_segment_length=gsl, device=DEV, use_priority=prio, n_episode=n)
+    col = MuZeroCollector(env=DeviceCartPoleEnvManager(n, seed=3), policy=MuZeroCollectPolicy(cfg, _model(2)),
+                          policy_config=cfg)
+    seen = []
+    for temperature in (1.0, 0.5):
+        segs, meta = col.collect(n_episode=n_ep, policy_kwargs=dict(temperature=temperature, epsilon=0.0))
+        sched = col.last_schedule
+        eps = _played(sched)
+        assert sum(len(e) for e in eps) == n_ep and all(len(e) >= 1 for e in eps)
+        env = EpisodeEnv(eps)
+        ref_segs, ref_meta, st = ref_collect(cfg, env, EpisodeForward(env), n_ep)
+        _compare(segs, meta, ref_segs, ref_meta)
+        for e in sum(eps, []):
+            assert (e["visits"].sum(axis=1) == 12).all() and (e["reward"] == 1.0).all()
+            assert np.all(np.abs(e["obs"][0]) <= 0.05 + 1e-7)
+        seen.append(segs[0].obs_segment.copy())
+    assert not np.array_equal(seen[0], seen[1])  # the second collect plays fresh episodes
