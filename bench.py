@@ -398,10 +398,12 @@ def cpu_tree_only(B, A, S, threads, secs):
     pthreads (shard-local tie-break streams). Returns (sims/s, searches, seconds)."""
     from oracle.oracle import lib
     L = lib()
-    t1 = L.lzo_bench_tree_only(B, A, S, threads, 1, 12345)
-    n = max(1, int(secs / max(t1, 1e-6)))
-    el = L.lzo_bench_tree_only(B, A, S, threads, n, 12345)
-    return B * S * n / el, n, el
+    n = 1
+    while True:  # grow the sample until it fills at least half the budget (thread start-up aside)
+        el = L.lzo_bench_tree_only(B, A, S, threads, n, 12345)
+        if el >= 0.5 * secs or n >= 1 << 24:
+            return B * S * n / el, n, el
+        n = max(n + 1, int(n * min(64.0, 0.8 * secs / max(el, 1e-6))))
 
 
 def cpu_reference_search(B, S, model, secs, threads, device=None):

@@ -643,6 +643,7 @@ __global__ void debug_glibc_kernel(uint32_t seed, int n, int32_t *out, const uin
 }  // namespace lzm
 
 #include "lzm_traverse_lb.h"  // uses block_players above
+#include "lzm_search_conv.h"  // uses wave_support_expectation / wave_row_sum above
 
 namespace lzm {
 
@@ -2385,6 +2386,104 @@ extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const floa
   p.norm_words = norm_words; p.norm_nparts = norm_parts(B);
   hipLaunchKernelGGL(conv_heads_kernel, dim3((B + kHdEnvs - 1) / kHdEnvs, 3), dim3(kHdThreads), 0, (hipStream_t)stream, p);
   LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+// Whole-search launch for the conv MuZero networks (lzm_search_conv.h): one workgroup per root,
+// every simulation inside the kernel. The grid must be co-resident (one workgroup per CU, B <= CUs):
+// parity-mode roots wait on their predecessors' depth flags.
+extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount,
+                               float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool,
+                               const float *trunk_w, const float *actmap, int n_dres, int n_pres, int r_ch, int h_ch,
+                               const float *w1t, const float *b1, const float *w2c, const float *b2, int Kr, int Khd,
+                               int off_policy, int Vr, int Vv, int categorical, int32_t *rec_x, int32_t *rec_a,
+                               int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream) {
+  const int S = num_simulations;
+  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !trunk_w || !actmap || !w1t || !b1 || !w2c || !b2 ||
+      S <= 0) {
+    set_err("lzm_search_conv: null argument or no simulations");
+    return LZM_ERR_ARG;
+  }
+  if (h->flags & LZM_TREE_EZ) {
+    set_err("lzm_search_conv: MuZero trees only");
+    return LZM_ERR_ARG;
+  }
+  if (n_dres < 0 || n_pres < 0 || r_ch <= 0 || r_ch > 32 || h_ch <= 0 || h_ch > 32 || Kr != r_ch * 64 ||
+      Khd != h_ch * 64 || off_policy <= 0 || off_policy >= Khd || off_policy > kHdKMax || Khd - off_policy > kHdKMax ||
+      (off_policy % 128) || (Kr % 128) || (Khd % 128) || Vr <= 0 || Vv <= 0 || Vr > 1024 || Vv > 1024 ||
+      (!categorical && (Vr != 1 || Vv != 1)) ||
+      (((uintptr_t)trunk_w | (uintptr_t)actmap | (uintptr_t)w1t | (uintptr_t)w2c | (uintptr_t)latent_pool) & 15)) {
+    set_err("lzm_search_conv: unsupported network shape (64x8x8 latent, <= 32 reward / head planes, K per head a "
+            "multiple of 128 and <= 1024, supports <= 1024, 16-B aligned weights and pool)");
+    return LZM_ERR_ARG;
+  }
+  if (S > h->sims_cap) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d simulations > reserved %d (lzm_reserve)", S, h->sims_cap);
+    return LZM_ERR_CAPACITY;
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  if (h->B > cus) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d roots > %d CUs (one co-resident workgroup per root)", h->B,
+             cus);
+    return LZM_ERR_ARG;
+  }
+  int rc = fill_lut(h, pb_c_base, pb_c_init);
+  if (rc != LZM_OK) return rc;
+  const bool fast = (h->flags & LZM_RNG_FAST) != 0;
+  if (!fast) {
+    rc = ensure_coef(h, h->B * (S + 1) + 64);
+    if (rc != LZM_OK) return rc;
+  }
+  rc = ensure_flags(h, S, h->B);
+  if (rc != LZM_OK) return rc;
+  ConvSearchArgs p;
+  memset(&p, 0, sizeof(p));
+  p.stat = h->stat; p.meta = h->meta; p.legal = h->legal; p.nlegal = h->nlegal;
+  p.path = h->path; p.path_act = h->path_act; p.pathlen = h->pathlen; p.lut = h->lut;
+  p.B = h->B; p.A = h->A; p.cap = h->cap; p.lut_n = h->lut_n; p.depth_cap = h->depth_cap;
+  p.S = S; p.disc = discount; p.seeds = seeds; p.vtp_in = vtp_in; p.minmax = (float4 *)minmax; p.pool = latent_pool;
+  p.w = trunk_w; p.actmap = actmap; p.n_dres = n_dres; p.n_pres = n_pres; p.r_ch = r_ch; p.h_ch = h_ch;
+  p.w1t = w1t; p.b1 = b1; p.w2c = w2c; p.b2 = b2; p.Kr = Kr; p.Khd = Khd; p.off_policy = off_policy;
+  p.Vr = Vr; p.Vv = Vv; p.categorical = categorical ? 1 : 0;
+  p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
+  p.flags = h->lb_flags; p.epoch = h->epoch; p.err = h->err; p.sdiag = h->search_diag; p.fast = fast ? 1 : 0;
+  p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
+  // dynamic LDS plan (float offsets, 16-B aligned): the two split-bf16 activation buffers first
+  size_t o = (size_t)2 * kBxBuf / 2;
+  p.off_stat = (int)o; o += (size_t)h->cap * 4;
+  p.off_meta = (int)o; o += (size_t)h->cap * 4;
+  p.off_val = (int)o; o += round4((size_t)h->cap);
+  p.off_lut = (int)o; o += round4((size_t)2 * h->lut_n);
+  p.off_legal = (int)o; o += round4((size_t)h->A + 1);
+  p.off_path = (int)o; o += round4((size_t)h->depth_cap);
+  p.off_pact = (int)o; o += round4((size_t)h->depth_cap);
+  p.pbt_rows = ((size_t)h->lut_n * (h->lut_n + 1) / 2 <= 4096) ? h->lut_n : 0;
+  p.off_pbt = (int)o; o += round4((size_t)p.pbt_rows * (p.pbt_rows + 1) / 2);
+  p.off_r = (int)o; o += round4((size_t)Kr);
+  p.off_hd = (int)o; o += round4((size_t)Khd);
+  p.off_hid = (int)o; o += 96;
+  p.off_part = (int)o; o += kHdParts * 32;
+  p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
+  p.off_seed = (int)o; o += round4((size_t)S + 32);
+  const size_t lds = o * sizeof(float);
+  if (lds > kMaxLds) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv: %zu B of LDS needed (tree too large: lower num_simulations)",
+             lds);
+    return LZM_ERR_ARG;
+  }
+  auto fn = fast ? search_conv_kernel<kBxAhead, true> : search_conv_kernel<kBxAhead, false>;
+  hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(fn, dim3(h->B), dim3(kScThreads), lds, (hipStream_t)stream, p);
+    e = hipGetLastError();
+  }
+  LZM_HIP(e);
   return LZM_OK;
 }
 

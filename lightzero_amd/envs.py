@@ -100,18 +100,23 @@ class SyncEnvManager:
         self._ready = {}
         self._env_states = {}
         self._closed = False
-        self.launch()
+        self._launched = False
 
     @classmethod
     def cartpole(cls, env_num, seed=0):
         return cls([CartPoleEnv(seed + i) for i in range(env_num)])
 
     def launch(self):
+        """reset every env once (idempotent, like DI-engine's launch of a running manager)"""
+        if self._launched:
+            return
+        self._launched = True
         self._ready = {i: e.reset() for i, e in enumerate(self._envs)}
         self._env_states = {i: "run" for i in range(self.env_num)}
 
     @property
     def ready_obs(self):
+        self.launch()
         return dict(self._ready)
 
     def step(self, actions):

@@ -104,6 +104,17 @@ class _SearchBuffers:
         return self
 
 
+_CUS = {}
+
+
+def _device_cus(device):
+    """compute units of `device` (the one-launch conv search needs one co-resident workgroup per root)"""
+    key = str(device)
+    if key not in _CUS:
+        _CUS[key] = torch.cuda.get_device_properties(device).multi_processor_count
+    return _CUS[key]
+
+
 def _step_net(mcts, model):
     """the BN-folded recurrent step for the conv MuZeroModel / EfficientZeroModel family
     (conv_infer.FoldedConvNet, cfg.fold_network, default on), else the model itself"""
@@ -259,6 +270,24 @@ class MuZeroMCTSCtree(object):
             return None
         return packed, dims
 
+    def _fused_conv(self, model, t, shape):
+        """The native split-bf16 FoldedConvNet when the whole search can run as one lzm_search_conv
+        launch (conv MuZeroModel, 64 x 8 x 8 latent, packed heads with K multiples of 128, one root
+        per CU); None otherwise (the generic per-simulation path). cfg.fused_search (default on) and
+        LZM_FUSED_CONV=0 turn it off."""
+        if not self._cfg.get('fused_search', True) or t.ez or os.environ.get("LZM_FUSED_CONV", "1") == "0":
+            return None
+        if tuple(shape) != (64, 8, 8) or t.B > _device_cus(t.device):
+            return None
+        net = _step_net(self, model)
+        hp = getattr(net, "heads", None)
+        if getattr(net, "native", None) is None or hp is None or getattr(net, "precision", None) != "bf16x3" \
+                or getattr(net, "ez", True):
+            return None
+        if hp["Kr"] % 128 or hp["Khd"] % 128 or hp["off_policy"] % 128 or hp["A"] != t.A:
+            return None
+        return net
+
     def _loop(self, t, model, buf, mm, vtp_in, seeds, S, row, rec=None, infer=None, net=None):
         """The S simulations (mcts_ctree.py:255-321), all enqueued on the current stream.
         infer: optional device int64 [S], per simulation the number of roots that ran inference
@@ -326,15 +355,16 @@ class MuZeroMCTSCtree(object):
             row = int(np.prod(shape)) if len(shape) else 1
             rec = _Recorder(S, B, t.A, dev) if getattr(self, "record", False) else None
             fz = self._fused(model, t)
-            graph = fz is None and rec is None and self._cfg.get('use_hip_graph', False)
+            cz = self._fused_conv(model, t, shape) if fz is None else None
+            graph = fz is None and cz is None and rec is None and self._cfg.get('use_hip_graph', False)
             gkey = _graph_key(t, model, B, S, shape) if graph else None
             entry = self._graphs.get(gkey, model, t) if graph else None
             # a captured search owns its buffers (they are what its kernels point at)
             buf = entry.buf if entry is not None else (_SearchBuffers() if graph else self._buf).get(B, S, shape, dev)
             if lat0.data_ptr() != buf.pool[0].data_ptr():  # (the collect step writes it in place)
                 buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
-            # the one-launch search reads device seeds / to_play in place (no staging copies)
-            in_place = fz is not None and rec is None
+            # the one-launch searches read device seeds / to_play in place (no staging copies)
+            in_place = (fz is not None or cz is not None) and rec is None
             step_in_kernel = step is not None and in_place
             vt = to_play_batch if in_place and _usable_i32(to_play_batch, B, dev) else None
             if vt is None:
@@ -352,7 +382,15 @@ class MuZeroMCTSCtree(object):
                     sd = buf.seeds
             if rec is not None:
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
-            if fz is not None:
+            if cz is not None:
+                # the conv network's whole search in one launch (lzm_search_conv)
+                if step is not None:
+                    raise ValueError("search: step mode is for the MLP one-launch search")
+                cfg = self._cfg
+                new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
+                t.search_conv(cz, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base), float(cfg.pb_c_init),
+                              float(np.float32(cfg.discount_factor)), self._categorical(), rec=rec)
+            elif fz is not None:
                 packed, dims = fz
                 cfg = self._cfg
                 if step_in_kernel:

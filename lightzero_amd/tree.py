@@ -177,6 +177,18 @@ class DeviceTree:
              ptr(vtp_in), ptr(pool), r("x"), r("action"), r("search_len"), r("decoded"), r("policy_logits"),
              stream_ptr(stream))
 
+    def search_conv(self, net, S, minmax, seeds, vtp_in, pool, pb_c_base=19652, pb_c_init=1.25, discount=0.997,
+                    categorical=True, rec=None, stream=None):
+        """One launch for the whole search of a conv MuZeroModel (lzm_search_conv; net: a native
+        split-bf16 conv_infer.FoldedConvNet); rec: optional _Recorder-like object."""
+        r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n)))
+        hp = net.heads
+        call("lzm_search_conv", self.h, int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax),
+             ptr(seeds), ptr(vtp_in), ptr(pool), ptr(net.native), ptr(net.actmap), int(net.n_dres), int(net.n_pres),
+             int(net.r_ch), int(net.h_ch), ptr(hp["w1t"]), ptr(hp["b1"]), ptr(hp["w2c"]), ptr(hp["b2"]), int(hp["Kr"]),
+             int(hp["Khd"]), int(hp["off_policy"]), int(hp["Vr"]), int(hp["Vv"]), int(bool(categorical)), r("x"),
+             r("action"), r("search_len"), r("decoded"), r("policy_logits"), stream_ptr(stream))
+
     def set_step(self, count=None, base=0, increment=True, dist=None, values=None, fresh_minmax=False,
                  value_delta_max=0.0):
         """Collect-step mode of the next search_mlp calls (lzm_search_set_step; host state only):

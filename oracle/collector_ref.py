@@ -172,6 +172,8 @@ class ReplayForward:
         rec = self.records[self.k]
         self.k += 1
         B = len(ready_env_id)
+        assert B == len(rec['root_logits']), (f"forward {self.k - 1}: {B} ready envs, the GPU run had "
+                                              f"{len(rec['root_logits'])} (mismatches so far: {self.mismatch[:5]})")
         if not np.array_equal(np.asarray(data, np.float32), rec['data']):
             self.mismatch.append((self.k - 1, 'observations'))
         legal = [[a for a, m in enumerate(action_mask[j]) if m == 1] for j in range(B)]

@@ -39,7 +39,7 @@ def conv_model(kind, seed=0, zero_heads=False):
     return m.to(DEV).eval()
 
 
-def run_search(kind, B, S, seed, graph=False, record=True, model=None, mcts=None):
+def run_search(kind, B, S, seed, graph=False, record=True, model=None, mcts=None, fused=True, rng="glibc"):
     from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree, MuZeroMCTSCtree
     from lightzero_amd.tree import SequentialSeeds, set_seed_source
     from lightzero_amd.utils import EasyDict
@@ -53,11 +53,17 @@ def run_search(kind, B, S, seed, graph=False, record=True, model=None, mcts=None
     noises = rng.dirichlet([0.3] * A, size=B).astype(np.float32)
     logits0 = out.policy_logits.float().cpu().numpy()
     cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5,
-                        use_hip_graph=graph, model=dict(support_scale=scale, categorical_distribution=True)))
+                        use_hip_graph=graph, fused_search=fused,
+                        model=dict(support_scale=scale, categorical_distribution=True)))
     cls = EfficientZeroMCTSCtree if kind == "ez" else MuZeroMCTSCtree
     mcts = cls(cfg) if mcts is None else mcts
     mcts.record = record
-    roots = cls.roots(B, [list(range(A))] * B)
+    old_mode = cls.rng_mode
+    cls.rng_mode = rng
+    try:
+        roots = cls.roots(B, [list(range(A))] * B)
+    finally:
+        cls.rng_mode = old_mode
     roots.prepare(0.25, [n.tolist() for n in noises], [0.0] * B, logits0.tolist(), [-1] * B)
     set_seed_source(SequentialSeeds(seed))
     try:
@@ -137,13 +143,31 @@ def test_conv_search_tree_and_decode_parity(kind, B, S):
     torch_replay(kind, res, B, S)
 
 
-@pytest.mark.parametrize("kind", ["ez", "mz"])
-def test_conv_search_full_config_tree_parity(kind):
-    """configs 3 / 5 at their per-GPU size: 256 envs x 50 simulations"""
+@pytest.mark.parametrize("kind,fused", [("ez", False), ("mz", True), ("mz", False)])
+def test_conv_search_full_config_tree_parity(kind, fused):
+    """configs 3 / 5 at their per-GPU size: 256 envs x 50 simulations (MuZero: the one-launch search,
+    lzm_search_conv, and the generic per-simulation path)"""
     B, S = 256, 50
-    res = run_search(kind, B, S, seed=2)
+    res = run_search(kind, B, S, seed=2, fused=fused)
     oracle_replay(kind, res, B, S)
     assert (res["dist"].sum(axis=1) == S).all()
+
+
+@pytest.mark.parametrize("B,S,rng,zero", [(256, 50, "glibc", False), (64, 30, "glibc", True), (37, 20, "philox", False)])
+def test_fused_conv_search_equals_generic(B, S, rng, zero):
+    """lzm_search_conv (one launch for all simulations) runs the generic path's arithmetic in the same
+    order: identical requests at every simulation, decoded values, policy logits, visit counts, root
+    values and trajectories, in both RNG modes; with zero-init heads (all-tie search: ties reaching
+    expanded children take the serial draw path) too"""
+    model = conv_model("mz", 13, zero_heads=zero)
+    out = [run_search("mz", B, S, seed=14, model=model, fused=f, rng=rng) for f in (True, False)]
+    a, b = out
+    for key in ("dist", "values", "traj"):
+        assert np.array_equal(a[key], b[key]), key
+    for key in ("x", "action", "search_len", "decoded", "policy_logits"):
+        assert np.array_equal(a["rec"][key], b["rec"][key]), key
+    if rng == "glibc":
+        oracle_replay("mz", a, B, S)
 
 
 @pytest.mark.parametrize("kind", ["ez", "mz"])
@@ -152,13 +176,14 @@ def test_conv_search_graph_replay_equals_eager(kind):
     model = conv_model(kind, 3)
     from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree, MuZeroMCTSCtree
     from lightzero_amd.utils import EasyDict
-    eager = run_search(kind, B, S, seed=3, model=model, record=False)
+    eager = run_search(kind, B, S, seed=3, model=model, record=False, fused=False)
     cls = EfficientZeroMCTSCtree if kind == "ez" else MuZeroMCTSCtree
     cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5, use_hip_graph=True,
+                        fused_search=False,
                         model=dict(support_scale=50 if kind == "ez" else 300, categorical_distribution=True)))
     mcts = cls(cfg)
     for _ in range(2):  # capture, then a plain replay of the cached graph
-        graph = run_search(kind, B, S, seed=3, model=model, record=False, mcts=mcts)
+        graph = run_search(kind, B, S, seed=3, model=model, record=False, mcts=mcts, fused=False)
         assert np.array_equal(graph["dist"], eager["dist"])
         np.testing.assert_allclose(graph["values"], eager["values"], rtol=0, atol=1e-6)
 
@@ -246,8 +271,8 @@ def test_fused_decode_traverse_equals_separate(kind):
     out = []
     for fuse in (False, True):
         cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5,
-                            fuse_traverse=fuse, model=dict(support_scale=50 if kind == "ez" else 300,
-                                                          categorical_distribution=True)))
+                            fuse_traverse=fuse, fused_search=False,
+                            model=dict(support_scale=50 if kind == "ez" else 300, categorical_distribution=True)))
         out.append(run_search(kind, B, S, seed=5, model=model, mcts=cls(cfg)))
     a, b = out
     for key in ("dist", "values", "traj"):

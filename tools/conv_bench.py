@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--graph", type=int, default=1)
     ap.add_argument("--precision", choices=["bf16x3", "f32"], default=None,
                     help="native conv trunk precision (default: LZM_CONV_PRECISION or bf16x3)")
+    ap.add_argument("--fused", type=int, default=1,
+                    help="MuZero: the one-launch search (lzm_search_conv) when it applies; 0: the generic path")
     ap.add_argument("--rng", choices=["glibc", "philox"], default="glibc",
                     help="tie-break stream: the reference's glibc rand() (parity) or per-root Philox")
     a = ap.parse_args()
@@ -68,7 +70,8 @@ def main():
     cls = EfficientZeroMCTSCtree if a.kind == "ez" else MuZeroMCTSCtree
     cls.rng_mode = a.rng
     cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=dev, lstm_horizon_len=5,
-                        use_hip_graph=bool(a.graph), model=dict(support_scale=scale, categorical_distribution=True)))
+                        use_hip_graph=bool(a.graph), fused_search=bool(a.fused),
+                        model=dict(support_scale=scale, categorical_distribution=True)))
     mcts = cls(cfg)
     rng = np.random.default_rng(0)
     obs = torch.from_numpy(rng.integers(0, 256, size=(B, 4, 64, 64)).astype(np.float32) / 255.0).to(dev)
@@ -98,13 +101,16 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.searches
     assert int(d.sum()) == B * S
+    roots.tree.check_errors()
+    fused = a.kind == "mz" and mcts._fused_conv(model, roots.tree, (64, 8, 8)) is not None
     flops = recurrent_flops(model, a.kind, B, dev)
     net_tflops = flops * B * S / dt / 1e12
     print(json.dumps({
         "metric": "MCTS simulations/sec", "value": B * S / dt, "unit": "sims/s", "ms_per_search": dt * 1e3,
         "config": {"workload": "C3 Pong EfficientZero" if a.kind == "ez" else "C5 Breakout MuZero (per GPU)",
                    "envs": B, "num_simulations": S, "actions": A, "support": 2 * scale + 1, "latent": [64, 8, 8],
-                   "path": "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph),
+                   "path": "one-launch search (lzm_search_conv)" if fused else
+                   "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph) and not fused,
                    "conv_precision": precision, "rng": a.rng},
         "net_flops_per_sim": flops, "net_tflops_whole_search": net_tflops,
         "fp32_mfma_peak_tflops": FP32_MFMA_PEAK_TFLOPS, "net_frac_of_peak": net_tflops / FP32_MFMA_PEAK_TFLOPS}))
