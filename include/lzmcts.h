@@ -335,7 +335,7 @@ int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const
  * trunk from latent_pool[x][b] (next latent filed into latent_pool[k + 1][b]), the head MLPs, the
  * support decode, expand and backup — the generic path's arithmetic, so the same results bit for
  * bit. Weights: trunk_w / actmap from lzm_conv_trunk_prepare_p(precision 1) and the fold's action
- * map; w1t / b1 / b2 in lzm_conv_heads' layouts, w2c its output layer column-major [Vr + Vv + A][32]. latent_pool [S + 1][B][64 * 64] (slot 0 =
+ * map; w1t / b1 / b2 in lzm_conv_heads' layouts, w2q its output layer as float4s [8][Vr + Vv + A][4] (k = 4 k4 .. 4 k4 + 3). latent_pool [S + 1][B][64 * 64] (slot 0 =
  * root latents), minmax float4 [B] (fresh bounds), seeds uint32 [S] (the srand(tv_usec) values),
  * rec_* (nullable): per-simulation x / action / search_len int32 [S][B], decoded {reward, value}
  * float [S][B][2], policy logits float [S][B][A]. Requires B <= the device's CU count (the grid is
@@ -344,7 +344,7 @@ int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const
 int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount, float *minmax,
                     const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, const float *trunk_w,
                     const float *actmap, int n_dres, int n_pres, int r_ch, int h_ch, const float *w1t,
-                    const float *b1, const float *w2c, const float *b2, int Kr, int Khd, int off_policy, int Vr,
+                    const float *b1, const float *w2q, const float *b2, int Kr, int Khd, int off_policy, int Vr,
                     int Vv, int categorical, int32_t *rec_x, int32_t *rec_a, int32_t *rec_len, float *rec_decoded,
                     float *rec_logits, void *stream);
 

@@ -200,8 +200,8 @@ class FoldedConvNet:
     def _pack_heads(self):
         """lzm_conv_heads layouts (csrc/lzm_heads.h) of the folded head MLPs, or None if they do
         not fit the kernel: w1t [3][8][32][32][4] over the three hidden layers (reward from r,
-        value / policy from the value / policy planes), w2t [32][Vr + Vv + A] (and w2c, the same
-        column-major, for the one-launch search lzm_search_conv)."""
+        value / policy from the value / policy planes), w2t [32][Vr + Vv + A] (and w2q [8][N2][4],
+        k4-major float4s, for the one-launch search lzm_search_conv)."""
         t = self.t
         rw1, vw1 = t["rh_w1"], t["ph_w1"]
         Kr, fv = rw1.shape[1], self.hv * 64
@@ -217,10 +217,11 @@ class FoldedConvNet:
         W[64:96, :fp] = vw1[32:, fv:]
         w1t = W.reshape(3, 32, 8, 32, 4).permute(0, 2, 3, 1, 4).contiguous()  # [head][part][k4][col][4]
         b1 = torch.cat([t["rh_b1"], t["ph_b1"]]).contiguous()
-        w2c = torch.cat([t["rh_w2"], t["v_w2"], t["p_w2"]], dim=0).contiguous()  # [N2][32] (fused search)
+        w2c = torch.cat([t["rh_w2"], t["v_w2"], t["p_w2"]], dim=0)  # [N2][32]
         w2t = w2c.t().contiguous()
+        w2q = w2c.reshape(-1, 8, 4).permute(1, 0, 2).contiguous()  # [8][N2][4] (the one-launch search)
         b2 = torch.cat([t["rh_b2"], t["v_b2"], t["p_b2"]]).contiguous()
-        return dict(w1t=w1t, b1=b1, w2t=w2t, w2c=w2c, b2=b2, Kr=Kr, Khd=Khd, off_policy=fv, Vr=t["rh_w2"].shape[0],
+        return dict(w1t=w1t, b1=b1, w2t=w2t, w2q=w2q, b2=b2, Kr=Kr, Khd=Khd, off_policy=fv, Vr=t["rh_w2"].shape[0],
                     Vv=t["v_w2"].shape[0], A=t["p_w2"].shape[0])
 
     def _trunk(self, pool, x, action, out_latent):

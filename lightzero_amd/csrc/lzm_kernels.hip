@@ -2395,11 +2395,11 @@ extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const floa
 extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount,
                                float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool,
                                const float *trunk_w, const float *actmap, int n_dres, int n_pres, int r_ch, int h_ch,
-                               const float *w1t, const float *b1, const float *w2c, const float *b2, int Kr, int Khd,
+                               const float *w1t, const float *b1, const float *w2q, const float *b2, int Kr, int Khd,
                                int off_policy, int Vr, int Vv, int categorical, int32_t *rec_x, int32_t *rec_a,
                                int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream) {
   const int S = num_simulations;
-  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !trunk_w || !actmap || !w1t || !b1 || !w2c || !b2 ||
+  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !trunk_w || !actmap || !w1t || !b1 || !w2q || !b2 ||
       S <= 0) {
     set_err("lzm_search_conv: null argument or no simulations");
     return LZM_ERR_ARG;
@@ -2412,7 +2412,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
       Khd != h_ch * 64 || off_policy <= 0 || off_policy >= Khd || off_policy > kHdKMax || Khd - off_policy > kHdKMax ||
       (off_policy % 128) || (Kr % 128) || (Khd % 128) || Vr <= 0 || Vv <= 0 || Vr > 1024 || Vv > 1024 ||
       (!categorical && (Vr != 1 || Vv != 1)) ||
-      (((uintptr_t)trunk_w | (uintptr_t)actmap | (uintptr_t)w1t | (uintptr_t)w2c | (uintptr_t)latent_pool) & 15)) {
+      (((uintptr_t)trunk_w | (uintptr_t)actmap | (uintptr_t)w1t | (uintptr_t)w2q | (uintptr_t)latent_pool) & 15)) {
     set_err("lzm_search_conv: unsupported network shape (64x8x8 latent, <= 32 reward / head planes, K per head a "
             "multiple of 128 and <= 1024, supports <= 1024, 16-B aligned weights and pool)");
     return LZM_ERR_ARG;
@@ -2428,9 +2428,9 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
   }
-  if (h->B > cus) {
-    snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d roots > %d CUs (one co-resident workgroup per root)", h->B,
-             cus);
+  if (h->B > cus || h->B > 256) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d roots > min(%d CUs, 256) (one co-resident workgroup per root)",
+             h->B, cus);
     return LZM_ERR_ARG;
   }
   int rc = fill_lut(h, pb_c_base, pb_c_init);
@@ -2449,7 +2449,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.B = h->B; p.A = h->A; p.cap = h->cap; p.lut_n = h->lut_n; p.depth_cap = h->depth_cap;
   p.S = S; p.disc = discount; p.seeds = seeds; p.vtp_in = vtp_in; p.minmax = (float4 *)minmax; p.pool = latent_pool;
   p.w = trunk_w; p.actmap = actmap; p.n_dres = n_dres; p.n_pres = n_pres; p.r_ch = r_ch; p.h_ch = h_ch;
-  p.w1t = w1t; p.b1 = b1; p.w2c = w2c; p.b2 = b2; p.Kr = Kr; p.Khd = Khd; p.off_policy = off_policy;
+  p.w1t = w1t; p.b1 = b1; p.w2q = w2q; p.b2 = b2; p.Kr = Kr; p.Khd = Khd; p.off_policy = off_policy;
   p.Vr = Vr; p.Vv = Vv; p.categorical = categorical ? 1 : 0;
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
   p.flags = h->lb_flags; p.epoch = h->epoch; p.err = h->err; p.sdiag = h->search_diag; p.fast = fast ? 1 : 0;
@@ -2468,7 +2468,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_r = (int)o; o += round4((size_t)Kr);
   p.off_hd = (int)o; o += round4((size_t)Khd);
   p.off_hid = (int)o; o += 96;
-  p.off_part = (int)o; o += kHdParts * 32;
+  p.off_part = (int)o; o += 2 * kHdParts * 32;
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
   const size_t lds = o * sizeof(float);
@@ -2477,7 +2477,14 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
              lds);
     return LZM_ERR_ARG;
   }
-  auto fn = fast ? search_conv_kernel<kBxAhead, true> : search_conv_kernel<kBxAhead, false>;
+  const bool stamps = getenv("LZM_PHASE_TIMING") && atoi(getenv("LZM_PHASE_TIMING")) > 0;
+  if (stamps && !h->phase) {
+    LZM_HIP(hipMalloc(&h->phase, (64 + 1024) * sizeof(unsigned long long)));
+    LZM_HIP(hipMemset(h->phase, 0, (64 + 1024) * sizeof(unsigned long long)));
+  }
+  p.stamps = stamps ? h->phase : nullptr;
+  auto fn = stamps ? (fast ? search_conv_kernel<kBxAhead, true, true> : search_conv_kernel<kBxAhead, false, true>)
+                   : (fast ? search_conv_kernel<kBxAhead, true> : search_conv_kernel<kBxAhead, false>);
   hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(fn, dim3(h->B), dim3(kScThreads), lds, (hipStream_t)stream, p);

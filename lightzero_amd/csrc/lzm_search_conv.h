@@ -57,7 +57,7 @@ struct ConvSearchArgs {
   // trunk (split-bf16 layout, lzm_conv_trunk_prepare_p) and heads (lzm_heads.h layouts)
   const float *w, *actmap;
   int n_dres, n_pres, r_ch, h_ch;
-  const float *w1t, *b1, *w2c, *b2;  // w2c: the output layer column-major [N2][32] (16-B aligned)
+  const float *w1t, *b1, *w2q, *b2;  // w2q: the output layer as [8][N2][4] (k4-major float4s, 16-B aligned)
   int Kr, Khd, off_policy, Vr, Vv, categorical;
   // parity-mode draws
   const uint32_t *coef;
@@ -71,38 +71,33 @@ struct ConvSearchArgs {
   // optional per-simulation record
   int32_t *rec_x, *rec_a, *rec_len;
   float *rec_dec, *rec_logits;
+  unsigned long long *stamps;  // STAMPS instantiation only
   // dynamic LDS plan: float offsets (the two activation buffers come first)
   int off_stat, off_meta, off_val, off_lut, off_legal, off_path, off_pact, off_pbt, off_r, off_hd, off_hid, off_part,
       off_lg, off_seed;
 };
 
 // Hidden layer of one head for this workgroup's env (conv_heads_kernel's arithmetic, same order):
-// lane (part, c) sums its 128-wide K range (32 float4 of weights, fetched in two halves of 16 to
-// bound the registers), the partial sums meet in K-part order, + bias, ReLU -> hid[c].
+// lane (part, c) sums its 128-wide K range with its 32 weight float4s (all loads in flight at once:
+// one L2 round trip per head), the partial sums meet in K-part order, + bias, ReLU -> hid[c].
+// K is a multiple of 128 (lzm_search_conv checks).
 __device__ __forceinline__ void sc_head_hidden(const float *in, int K, const float *w1t, int head, float bias,
                                                float *part, float *hid, int tid) {
   const int pt = tid >> 5, c = tid & 31;
   float acc = 0.0f;
-  if (pt * 128 < K) {  // (K is a multiple of 128: lzm_search_conv checks)
+  if (pt * 128 < K) {
     const float4 *x4 = reinterpret_cast<const float4 *>(in + pt * 128);
     const float4 *w = reinterpret_cast<const float4 *>(w1t) + ((size_t)(head * kHdParts + pt) * 32) * 32 + c;
+    float4 w1[32];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      // (a compiler barrier: keep the half's loads here rather than hoisted to the top of the kernel,
-      // where every head's weights would be live at once)
-      asm volatile("" ::: "memory");
-      float4 w1[16];
+    for (int q = 0; q < 32; ++q) w1[q] = w[(size_t)q * 32];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) w1[q] = w[(size_t)(16 * h + q) * 32];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int k4 = 16 * h + q;
-        const float4 x = x4[k4];
-        acc = __fmaf_rn(x.x, w1[q].x, acc);
-        acc = __fmaf_rn(x.y, w1[q].y, acc);
-        acc = __fmaf_rn(x.z, w1[q].z, acc);
-        acc = __fmaf_rn(x.w, w1[q].w, acc);
-      }
+    for (int q = 0; q < 32; ++q) {
+      const float4 x = x4[q];
+      acc = __fmaf_rn(x.x, w1[q].x, acc);
+      acc = __fmaf_rn(x.y, w1[q].y, acc);
+      acc = __fmaf_rn(x.z, w1[q].z, acc);
+      acc = __fmaf_rn(x.w, w1[q].w, acc);
     }
   }
   part[pt * 32 + c] = acc;
@@ -116,7 +111,102 @@ __device__ __forceinline__ void sc_head_hidden(const float *in, int K, const flo
   __syncthreads();
 }
 
-template <int AHEAD, bool FAST>
+// Parity-mode draw offset of root b in simulation k: the sum of the depth flags of roots < b (the
+// reference's single rand() stream, cnode.cpp:783-796). Wave-wide, b <= 256 (lzm_search_conv checks
+// B <= 256): sc_lookback_issue puts every flag of a lane in flight (four loads), sc_lookback_finish
+// spins (bounded, counted in err[0]) on the ones not yet published and returns the wave-uniform
+// sum. The late draw issues before the dynamics conv and finishes after it, so the cross-XCD
+// round trip of the flag loads overlaps the MFMAs.
+__device__ __forceinline__ void sc_lookback_issue(const ConvSearchArgs &p, int k, int b, unsigned long long epoch,
+                                                  int lane, unsigned long long (&v)[4]) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = 64 * u + lane;
+    v[u] = q < b ? __hip_atomic_load(&p.flags[(size_t)k * p.B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : (epoch << 32);
+  }
+}
+
+__device__ __forceinline__ int sc_lookback_finish(const ConvSearchArgs &p, int k, int b, unsigned long long epoch,
+                                                  int lane, unsigned long long (&v)[4]) {
+  int base = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = 64 * u + lane;
+    long long spins = 0;
+    while ((v[u] >> 32) != epoch) {
+      if (++spins > (1ll << 22)) {
+        atomicAdd(p.err, 1);
+        v[u] = epoch << 32;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v[u] = __hip_atomic_load(&p.flags[(size_t)k * p.B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    base += (int)(v[u] & 0xffffffffu);
+  }
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
+  return base;
+}
+
+__device__ __forceinline__ int sc_lookback(const ConvSearchArgs &p, int k, int b, unsigned long long epoch, int lane) {
+  unsigned long long v[4];
+  sc_lookback_issue(p, k, b, epoch, lane, v);
+  return sc_lookback_finish(p, k, b, epoch, lane, v);
+}
+
+// this lane's 16 values of the dynamics conv's action map (the epilogue's order)
+__device__ __forceinline__ void sc_load_amap(float4 (&am)[4], const float *actmap, int action, int c, int lane) {
+  const float4 *amap = reinterpret_cast<const float4 *>(actmap + ((size_t)action * kCvCh + c) * kCvPix);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) am[q] = amap[4 * q + (lane >> 4)];
+}
+
+// InverseScalarTransform's expectation of one support row by one wave (wave_support_expectation_reg
+// arithmetic, the row read once) together with the row's raw sum for ensure_softmax's check
+// (wave_row_sum's order).
+template <int NPL>
+__device__ __forceinline__ float sc_decode_row(const float *row, int V, float *raw_sum) {
+  const int lane = threadIdx.x & 63;
+  const float half = (float)((V - 1) / 2);
+  float x[NPL];
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    const int j = lane + 64 * q;
+    x[q] = j < V ? row[j] : 0.0f;
+  }
+  float rs = 0.0f, mx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q)
+    if (lane + 64 * q < V) {
+      rs += x[q];
+      mx = fmaxf(mx, x[q]);
+    }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    rs += __shfl_xor(rs, d, 64);
+    mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+  }
+  *raw_sum = rs;
+  float e[NPL], sum = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q) {
+    e[q] = lane + 64 * q < V ? expf(x[q] - mx) : 0.0f;
+    if (lane + 64 * q < V) sum += e[q];
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  float acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < NPL; ++q)
+    if (lane + 64 * q < V) acc += (e[q] / sum) * ((float)(lane + 64 * q) - half);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  return acc;
+}
+
+template <int AHEAD, bool FAST, bool STAMPS = false>
 __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void search_conv_kernel(
     ConvSearchArgs p) {
   extern __shared__ uint4 sc_lds4[];
@@ -127,10 +217,20 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const int c = 16 * wv + (lane & 15);
   const int B = p.B, A = p.A, S = p.S;
   __shared__ uint32_t s_z0[31];
-  __shared__ int s_players, s_epoch, s_x, s_act, s_vtp0, s_leafvtp;
+  __shared__ int s_players, s_epoch, s_x, s_act, s_vtp0, s_leafvtp, s_late, s_tlevel;
+  __shared__ unsigned long long s_tmask;
   __shared__ int s_len[1];
   __shared__ float4 s_mm[1];
   __shared__ float s_dec[2];
+  unsigned long long st_prev = 0, st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long st_begin = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto stamp = [&](int n) {
+    if (STAMPS && tid == 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      st_acc[n] += now - st_prev;
+      st_prev = now;
+    }
+  };
 
   // ---- stage root b's tree slice, the pUCT tables, seeds; zero the activation borders
   TreeView t;
@@ -193,8 +293,12 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 
   for (int k = 0; k < S; ++k) {
     // ---- selection (wave 0; parity mode: draw-free walk, depth flag, look-back only for a value)
+    // the dynamics conv's first weight chunks, in flight during the walk
+    bx_prefetch<18, AHEAD, 0>(ring, wave_stream(p.w + L.dyn), lane);
     if (!FAST && tid < 31) seed_state_parallel(s_seed[k], s_pow, s_z0);
     __syncthreads();
+    if (STAMPS && tid == 0) st_prev = __builtin_amdgcn_s_memtime();
+    if (tid == 0) s_late = 0;
     if (wv == 0) {
       const float4 mm = s_mm[0];
       Descent d;
@@ -212,53 +316,23 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         if (lane == 0 && ti.status != 2)
           __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
-        if (ti.status != 0) {
-          int base = 0;
-          for (int q = lane; q < b; q += 64) {
-            unsigned long long v;
-            long long spins = 0;
-            while (true) {
-              v = __hip_atomic_load(&p.flags[(size_t)k * B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              if ((v >> 32) == epoch) break;
-              if (++spins > (1ll << 22)) {
-                atomicAdd(p.err, 1);
-                v = 0;
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-            }
-            base += (int)(v & 0xffffffffu);
-          }
-#pragma unroll
-          for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
-          const uint32_t *coef = p.coef;
-          const int npos = p.coef_positions;
-          int32_t *ovf = p.err + 1;
-          if (ti.status == 1) {
-            // a tie among unexpanded children: the draw picks the leaf, the depth stays
-            const uint32_t rr = glibc_draw(coef, npos, s_z0, base + ti.level, ovf);
-            unsigned long long m = ti.mask;
-            int kk = (int)(rr % (uint32_t)__popcll(m));
-            for (; kk > 0; --kk) m &= m - 1;
-            const int jsel = __ffsll((long long)m) - 1;
-            const int parent = t.path[ti.level];
-            const int action = legal_at(t, 0, parent, jsel);
-            const int leaf = 1 + A * t.meta[parent].latent + action;
-            if (lane == 0) {
-              t.path_act[ti.level] = action;
-              t.path[ti.level + 1] = leaf;
-            }
-            d.action = action;
-            d.leaf = leaf;
-          } else {
-            // the depth depends on the draws: walk with them, then publish
-            auto draw = [coef, npos, ovf, base](int level) -> uint32_t {
-              return glibc_draw(coef, npos, s_z0, base + level, ovf);
-            };
-            d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
-            if (lane == 0)
-              __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+        if (ti.status == 2) {
+          // the depth depends on the draws: look back, walk with them, then publish
+          const int base = sc_lookback(p, k, b, epoch, lane);
+          const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, 0, t.depth_cap, p.err + 1);
+          d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+          if (lane == 0)
+            __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        } else if (ti.status == 1) {
+          // a tie among unexpanded children: the leaf's parent (the latent to read) and the depth are
+          // known, only the action waits for the draw — resolved after the dynamics conv's MFMAs
+          // (late draw; issuing the flag loads here instead measured even: the wait is for the
+          // predecessors to reach this simulation, not the loads' latency)
+          if (lane == 0) {
+            s_late = 1;
+            s_tlevel = ti.level;
+            s_tmask = ti.mask;
           }
         }
       }
@@ -275,20 +349,20 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       }
     }
     __syncthreads();
-    // ---- trunk: the dynamics conv's first weight chunks, the leaf's parent latent pool[x][b] and the
-    // action's map (registers; all loads in flight together), then the layers
+    stamp(0);
+    // ---- trunk: the leaf's parent latent pool[x][b] and the action's map (registers; loads in flight
+    // together), then the layers
     {
-      bx_prefetch<18, AHEAD, 0>(ring, wave_stream(p.w + L.dyn), lane);
+      const bool late = s_late != 0;
       const float *src = p.pool + ((size_t)max(s_x, 0) * B + b) * (kCvCh * kCvPix);
       float xres[16];
       float4 am[4];
-      const float4 *amap = reinterpret_cast<const float4 *>(p.actmap + ((size_t)s_act * kCvCh + c) * kCvPix);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * q + 4 * (lane >> 4));
         xres[4 * q] = v.x; xres[4 * q + 1] = v.y; xres[4 * q + 2] = v.z; xres[4 * q + 3] = v.w;
-        am[q] = amap[4 * q + (lane >> 4)];
       }
+      if (!late) sc_load_amap(am, p.actmap, s_act, c, lane);
       {
         bxf4 in4[4];
 #pragma unroll
@@ -297,6 +371,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         bx_epilogue3<0, 4, false>(in4, buf(0), 0.f, false, no_am, xres, false, false, lane, c);
       }
       __syncthreads();
+      stamp(1);
       for (int i = 0; i < n3; ++i) {
         const float *w = layer_w(i);
         const bool second = i > 0 && ((i - 1) & 1);  // a block's second conv: + residual, new block input
@@ -304,6 +379,30 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         bxf4 acc[4];
         bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
         if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
+        if (i == 0 && late) {
+          // late draw: the look-back and the tie's draw, then the action's map for the epilogue
+          if (wv == 0) {
+            const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+            const int base = sc_lookback(p, k, b, epoch, lane);
+            if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;
+            const uint32_t rr = glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
+            unsigned long long m = s_tmask;
+            int kk = (int)(rr % (uint32_t)__popcll(m));
+            for (; kk > 0; --kk) m &= m - 1;
+            const int jsel = __ffsll((long long)m) - 1;
+            const int lvl = s_tlevel;
+            const int parent = t.path[lvl];
+            const int action = legal_at(t, 0, parent, jsel);
+            if (lane == 0) {
+              t.path_act[lvl] = action;
+              t.path[lvl + 1] = 1 + A * t.meta[parent].latent + action;
+              s_act = action;
+              if (p.rec_a) p.rec_a[(size_t)k * B + b] = action;
+            }
+          }
+          __syncthreads();
+          sc_load_amap(am, p.actmap, s_act, c, lane);
+        }
         bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
         __syncthreads();
         if (i == 2 * p.n_dres) {  // the next latent (registers, exact) and the reward planes
@@ -314,50 +413,65 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           if (wv < 2) bx_conv1_layer<0>(buf((i + 1) & 1), p.w + L.rw, p.w + L.rb, p.r_ch, lr, lane, wv);
         }
       }
-      if (wv < 2) bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, p.h_ch, lhd, lane, wv);
-      __syncthreads();
     }
-    // ---- head MLPs (conv_heads_kernel's arithmetic): hidden layers, then the output columns
+    if (wv < 2) bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, p.h_ch, lhd, lane, wv);
+    __syncthreads();
+    stamp(2);
+    // ---- head MLPs: the three hidden layers
     sc_head_hidden(lr, p.Kr, p.w1t, 0, tid < 32 ? p.b1[tid] : 0.0f, lpart, lhid, tid);
     sc_head_hidden(lhd, p.off_policy, p.w1t, 1, tid < 32 ? p.b1[32 + tid] : 0.0f, lpart, lhid + 32, tid);
     sc_head_hidden(lhd + p.off_policy, p.Khd - p.off_policy, p.w1t, 2, tid < 32 ? p.b1[64 + tid] : 0.0f, lpart,
                    lhid + 64, tid);
-    // output columns: column-major weights (w2c [N2][32], 8 contiguous float4 per column), one column
-    // per thread per round; the FMA order of conv_heads_kernel (k = 0 .. 31 from zero, then + bias)
-    for (int j = tid; j < N2; j += kScThreads) {
-      const float4 *wc = reinterpret_cast<const float4 *>(p.w2c) + (size_t)j * 8;
-      float4 w2[8];
+    stamp(3);
+    // output columns (w2q [8][N2][4]: float4 k4 of column j at (k4 * N2 + j), so a wave-instruction
+    // reads 64 consecutive columns' float4s, 1 KiB contiguous), up to three columns per thread per
+    // round with every load of the round in flight; the FMA order of conv_heads_kernel (k = 0 .. 31
+    // from zero, then + bias)
+    for (int j0 = 0; j0 < N2; j0 += 3 * kScThreads) {
+      float4 w2[3][8];
+      float b2[3];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) w2[q] = wc[q];
-      const float b2 = p.b2[j];
-      const float *hid = lhid + 32 * (j < p.Vr ? 0 : (j < p.Vr + p.Vv ? 1 : 2));
-      float acc = 0.0f;
+      for (int u = 0; u < 3; ++u) {
+        const int j = min(j0 + u * kScThreads + tid, N2 - 1);
+        const float4 *wc = reinterpret_cast<const float4 *>(p.w2q) + j;
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float4 h4 = *reinterpret_cast<const float4 *>(hid + 4 * q);
-        acc = __fmaf_rn(h4.x, w2[q].x, acc);
-        acc = __fmaf_rn(h4.y, w2[q].y, acc);
-        acc = __fmaf_rn(h4.z, w2[q].z, acc);
-        acc = __fmaf_rn(h4.w, w2[q].w, acc);
+        for (int q = 0; q < 8; ++q) w2[u][q] = wc[(size_t)q * N2];
+        b2[u] = p.b2[j];
       }
-      llg[j] = acc + b2;
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int j = j0 + u * kScThreads + tid;
+        const float *hid = lhid + 32 * (j < p.Vr ? 0 : (j < p.Vr + p.Vv ? 1 : 2));
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float4 h4 = *reinterpret_cast<const float4 *>(hid + 4 * q);
+          acc = __fmaf_rn(h4.x, w2[u][q].x, acc);
+          acc = __fmaf_rn(h4.y, w2[u][q].y, acc);
+          acc = __fmaf_rn(h4.z, w2[u][q].z, acc);
+          acc = __fmaf_rn(h4.w, w2[u][q].w, acc);
+        }
+        if (j < N2) llg[j] = acc + b2[u];
+      }
     }
     __syncthreads();
+    stamp(4);
     // ---- decode (wave 0 reward, wave 1 value), then expand + backup (wave 0)
     if (wv < 2) {
       const float *row = llg + (wv == 0 ? 0 : p.Vr);
       const int V = wv == 0 ? p.Vr : p.Vv;
       float e;
       if (p.categorical) {
-        const float sm = wave_row_sum(row, V);
+        float sm;
+        e = V <= 640 ? sc_decode_row<10>(row, V, &sm) : sc_decode_row<16>(row, V, &sm);
         if (lane == 0 && fabsf(sm - 1.0f) <= 1e-5f + 1e-5f) atomicAdd(p.sdiag, 1);  // batch verdict undecidable
-        e = wave_support_expectation(row, V, true);
       } else {
         e = row[0];
       }
       if (lane == 0) s_dec[wv] = h_inverse(e);
     }
     __syncthreads();
+    stamp(5);
     if (wv == 0) {
       const float r = s_dec[0], v = s_dec[1];
       const int leaf = t.path[s_len[0]];
@@ -369,6 +483,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         if (lane < A) p.rec_logits[((size_t)k * B + b) * A + lane] = plg[lane];
       }
     }
+    stamp(6);
   }
   __syncthreads();
   // ---- write back the slice (tree, last path, min-max)
@@ -379,6 +494,10 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   for (int l = tid; l < p.depth_cap; l += kScThreads) {
     p.path[(size_t)l * B + b] = t.path[l];
     p.path_act[(size_t)l * B + b] = t.path_act[l];
+  }
+  if (STAMPS && tid == 0 && p.stamps) {
+    st_acc[7] = __builtin_amdgcn_s_memtime() - st_begin;
+    for (int n = 0; n < 9; ++n) atomicAdd(p.stamps + 40 + n, st_acc[n]);
   }
   if (tid == 0) {
     p.minmax[b] = s_mm[0];

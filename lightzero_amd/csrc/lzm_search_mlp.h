@@ -537,6 +537,38 @@ __device__ inline uint32_t glibc_draw(const uint32_t *coef, int positions, const
   return v >> 1;
 }
 
+// The draws of one walk's levels lo .. lo + 63, one per lane (lane l: stream position
+// base + lo + l), all coefficient rows in flight at once. cselect_child consumes a rand() at every
+// level (cnode.cpp:587-590), so a walk resolved with draws paid one coefficient-row round trip per
+// level through glibc_draw; through this it pays one. Built by a whole wave; operator() must be
+// called wave-uniformly (readlane). Levels outside the window, or positions past the table, take
+// glibc_draw (which flags the overflow) — the same values either way.
+struct LaneDraws {
+  const uint32_t *coef;
+  const uint32_t *z0;
+  int32_t *diag;
+  int npos, base, lo;
+  uint32_t v;
+  __device__ uint32_t operator()(int level) const {
+    const int l = level - lo;
+    if (l >= 0 && l < 64 && base + level < npos) return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+    return glibc_draw(coef, npos, z0, base + level, diag);
+  }
+};
+__device__ inline LaneDraws lane_draws(const uint32_t *coef, int npos, const uint32_t *z0, int base, int lo, int hi,
+                                       int32_t *diag) {
+  const int lane = threadIdx.x & 63;
+  const int p = base + lo + lane;
+  uint32_t v = 0;
+  if (lo + lane < hi && p < npos) {
+    const uint32_t *c = coef + (size_t)p * 31;
+#pragma unroll
+    for (int j = 0; j < 31; ++j) v += c[j] * z0[j];
+    v >>= 1;
+  }
+  return LaneDraws{coef, z0, diag, npos, base, lo, v};
+}
+
 // z0[i] = seed * 16807^i mod (2^31 - 1) for seed in [1, 2^31-2] (srandom_r's Schrage loop
 // computes exactly this); other seeds take the serial loop.
 __device__ inline void seed_state_parallel(uint32_t seed, const uint32_t *pw, uint32_t *z0) {

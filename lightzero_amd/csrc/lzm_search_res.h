@@ -1316,6 +1316,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // (A == 2), when every draw outcome gives the same depth (speculate_depth_a2), publish it at
       // once so that the roots after this one need not wait for this root's look-back (st = 3).
       int st = 2, d0 = -1;
+      unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
       if (smode == 4 && n.spec_depth && wid == 0) {
         const int de = speculate_depth_a2(t, NQ, DEC, CS, s_mm, rleg, nleg, s_walk, lane);
         d0 = __builtin_amdgcn_readfirstlane(de);
@@ -1326,16 +1327,13 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+      LZM_SUBSTAMP(20);
       const int base = lookback_sum(p, k, g, G, epoch, s_part);
+      LZM_SUBSTAMP(21);
       if (wid == 0) {
         if (lane == 0) atomicAdd(p.diag + (st == 2 ? 1 : 2), 1);
-        const uint32_t *coef = p.coef;
-        const int npos = p.coef_positions;
-        int32_t *diag = p.diag;
-        auto draw = [coef, npos, diag, base](int level) -> uint32_t {
-          return glibc_draw(coef, npos, s_z0, base + level, diag);
-        };
         WalkState ws = s_walk;
+        const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, ws.len, t.depth_cap, p.diag);
         Descent d;
         if (smode == 4)
           d = descend_a2<false>(t, NQ, DEC, CS, s_mm, s_vtp, players, rleg, nleg, draw, nullptr, &ws);
@@ -1353,7 +1351,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+      LZM_SUBSTAMP(22);
       __syncthreads();
+      LZM_SUBSTAMP(23);
     } else if (status == 2) {
       // the depth depends on a draw: look back now, then walk with the draws (exact semantics)
       const int base = lookback_sum(p, k, g, G, epoch, s_part);

@@ -131,9 +131,7 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
       d.leaf = 1 + t.A * t.meta[nidx(t, parent, i)].latent + action;
     } else {
       // the depth depends on the draws: walk with them, then publish
-      auto draw = [coef, npos, diag, base, s_z0](int level) -> uint32_t {
-        return glibc_draw(coef, npos, s_z0, base + level, diag);
-      };
+      const LaneDraws draw = lane_draws(coef, npos, s_z0, base, 0, t.depth_cap, diag);
       d = descend_wave<EZ, false, true>(t, i, i, B, mm, players, vtp0, p.disc, draw, nullptr, ta, rv);
       if (lane == 0)
         __hip_atomic_store(&p.flags[i], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

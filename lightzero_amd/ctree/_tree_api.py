@@ -62,11 +62,36 @@ class _RootsBase:
     def __init__(self, root_num, legal_actions_list, fast_rng=False):
         self.fast_rng = bool(fast_rng)
         self.root_num = int(root_num)
-        self.legal_actions_list = [list(map(int, l)) for l in legal_actions_list]
-        if len(self.legal_actions_list) < self.root_num:
+        self._legal_list = [list(map(int, l)) for l in legal_actions_list]
+        self._mask = None
+        if len(self._legal_list) < self.root_num:
             raise IndexError("legal_actions_list shorter than root_num")
         self.tree = None
         self._sims = _DEFAULT_SIMS
+
+    @classmethod
+    def from_action_mask(cls, action_mask, fast_rng=False):
+        """Roots whose legal lists come from an [N, A] {0, 1} action mask ON THE DEVICE (not in the
+        reference; its callers build `[[i for i, x in enumerate(mask[j]) if x == 1] ...]` on the host,
+        game_buffer_muzero.py:587-594): legal action j of root i = the j-th set bit of row i, computed
+        by a stable sort on the device, no host copy. The host list view is built only if asked for."""
+        m = action_mask.detach().to(torch.int32)
+        N, A = m.shape
+        r = cls.__new__(cls)
+        r.fast_rng, r.root_num, r._legal_list, r._mask = bool(fast_rng), int(N), None, m
+        r.tree, r._sims = None, _DEFAULT_SIMS
+        count = m.sum(dim=1, dtype=torch.int32)
+        order = torch.argsort(1 - m, dim=1, stable=True).to(torch.int32)  # set bits first, ascending
+        cols = torch.arange(A, device=m.device, dtype=torch.int32).unsqueeze(0)
+        legal = torch.where(cols < count.unsqueeze(1), order, torch.full_like(order, -1)).contiguous()
+        r._legal_dev, r._legal_dev_key = (legal, count.contiguous()), (A, str(m.device))
+        return r
+
+    @property
+    def legal_actions_list(self):
+        if self._legal_list is None:  # (from_action_mask roots: the host view on demand)
+            self._legal_list = [torch.nonzero(row).flatten().tolist() for row in self._mask.cpu()]
+        return self._legal_list
 
     @property
     def num(self):

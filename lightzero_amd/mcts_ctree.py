@@ -254,6 +254,11 @@ class MuZeroMCTSCtree(object):
     def roots(cls: int, active_collect_env_num: int, legal_actions: List[Any]) -> "mz_tree.Roots":
         return mz_tree.Roots(active_collect_env_num, legal_actions, fast_rng=(cls.rng_mode == 'philox'))
 
+    @classmethod
+    def roots_from_mask(cls, action_mask: torch.Tensor) -> "mz_tree.Roots":
+        """roots() with the legal lists taken from a device action mask (no host round trip)"""
+        return mz_tree.Roots.from_action_mask(action_mask, fast_rng=(cls.rng_mode == 'philox'))
+
     def _categorical(self):
         return bool(self._cfg.model.get('categorical_distribution', True))
 
@@ -277,7 +282,7 @@ class MuZeroMCTSCtree(object):
         LZM_FUSED_CONV=0 turn it off."""
         if not self._cfg.get('fused_search', True) or t.ez or os.environ.get("LZM_FUSED_CONV", "1") == "0":
             return None
-        if tuple(shape) != (64, 8, 8) or t.B > _device_cus(t.device):
+        if tuple(shape) != (64, 8, 8) or t.B > min(256, _device_cus(t.device)):
             return None
         net = _step_net(self, model)
         hp = getattr(net, "heads", None)

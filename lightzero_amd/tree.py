@@ -185,7 +185,7 @@ class DeviceTree:
         hp = net.heads
         call("lzm_search_conv", self.h, int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax),
              ptr(seeds), ptr(vtp_in), ptr(pool), ptr(net.native), ptr(net.actmap), int(net.n_dres), int(net.n_pres),
-             int(net.r_ch), int(net.h_ch), ptr(hp["w1t"]), ptr(hp["b1"]), ptr(hp["w2c"]), ptr(hp["b2"]), int(hp["Kr"]),
+             int(net.r_ch), int(net.h_ch), ptr(hp["w1t"]), ptr(hp["b1"]), ptr(hp["w2q"]), ptr(hp["b2"]), int(hp["Kr"]),
              int(hp["Khd"]), int(hp["off_policy"]), int(hp["Vr"]), int(hp["Vv"]), int(bool(categorical)), r("x"),
              r("action"), r("search_len"), r("decoded"), r("policy_logits"), stream_ptr(stream))
 

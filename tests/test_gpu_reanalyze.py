@@ -60,3 +60,28 @@ def test_reanalyze_policy_targets():
                 want[a] = d[j] / d.sum()
         np.testing.assert_allclose(tgt[i], want, rtol=1e-6, atol=1e-7)
     np.testing.assert_array_equal(values.cpu().numpy(), np.asarray(vals, np.float32))
+
+
+def test_roots_from_action_mask_equal_list_roots():
+    """Roots.from_action_mask (legal lists built on the device) == Roots(n, host lists): the same
+    device legal table and count, the same host list view, and the same prepared root priors"""
+    from lightzero_amd.mcts_ctree import MuZeroMCTSCtree
+    rng = np.random.default_rng(3)
+    N, A = 257, 6
+    mask = (rng.uniform(size=(N, A)) > 0.4).astype(np.int8)
+    mask[5] = 0  # an empty row: every action legal (cnode.cpp:100-107), count 0 on both sides
+    lists = [[i for i, x in enumerate(row) if x == 1] for row in mask]
+    r1 = MuZeroMCTSCtree.roots(N, lists)
+    r2 = MuZeroMCTSCtree.roots_from_mask(torch.from_numpy(mask).to(DEV))
+    _, l1, c1 = r1.device_legal(A, DEV)
+    _, l2, c2 = r2.device_legal(A, DEV)
+    assert torch.equal(l1, l2) and torch.equal(c1, c2)
+    assert r2.legal_actions_list == lists
+    logits = torch.randn(N, A, device=DEV)
+    z = torch.zeros(N, device=DEV)
+    tp = torch.full((N,), -1, dtype=torch.int32, device=DEV)
+    for r in (r1, r2):
+        r.prepare_device(0.0, None, z, logits, tp)
+    assert r1.get_distributions() == r2.get_distributions()
+    s1 = r1.tree.dump_stats() if hasattr(r1.tree, "dump_stats") else None
+    assert s1 is None or torch.equal(s1, r2.tree.dump_stats())
