@@ -419,6 +419,26 @@ int lzm_ez_lstm_input(int B, int Kr, int H, const float *r, const float *hpool, 
 int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *cpool, const int32_t *x, const int32_t *search_len,
                      int horizon, float *h1, float *c1, float *hslot, float *cslot, void *stream);
 
+/* EfficientZero reward LSTM in one launch: the gate GEMM gates = xin W^T + bias on split-bf16 MFMA
+ * with the cell (lzm_ez_lstm_cell's operations) in its epilogue — replaces the nn.LSTM step
+ * (efficientzero_model.py:526-574) and the state bookkeeping of mcts_ctree.py:756-816 that the
+ * rocBLAS GEMM + lzm_ez_lstm_cell pair did in two launches. xin [B][K] (K = Kr + H, % 64 == 0),
+ * wfrag = lzm_ez_lstm_prepare(W [4H][K], nn.LSTM gate order i, f, g, o), bias [4H], c0 =
+ * cpool[x[b]][b]; writes h1 / c1 [B][H] and the next state slot hslot / cslot (zeroed where
+ * search_len[b] % horizon == 0). H % 16 == 0. Within f32 tolerance of the f32 GEMM (rtol 1e-4). */
+int64_t lzm_ez_lstm_frag_floats(int K, int H);
+int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out);
+/* workspace (optional, zero-filled once): lzm_ez_lstm_workspace_bytes(B, H) bytes; with it the K range
+ * is split over two workgroups per tile when every workgroup fits on the GPU at once (err: a sticky
+ * int32 counting hand-off timeouts, required with the workspace). */
+int64_t lzm_ez_lstm_workspace_bytes(int B, int H);
+/* Device address of the handle's sticky error word i (0..3) for kernels launched outside the handle
+ * (word 3: lzm_ez_lstm_step's hand-off timeouts); lzm_check_errors reports it. */
+int32_t *lzm_error_word(lzm_handle *h, int i);
+int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const float *wfrag, const float *bias, const float *cpool,
+                     const int32_t *x, const int32_t *search_len, int horizon, float *h1, float *c1, float *hslot,
+                     float *cslot, void *workspace, int32_t *err, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

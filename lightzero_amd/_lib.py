@@ -63,6 +63,11 @@ SIGNATURES = {
     "lzm_set_reuse": [_vp, _vp, _vp],
     "lzm_ez_lstm_input": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "lzm_ez_lstm_cell": [_i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
+    "lzm_ez_lstm_frag_floats": [_i, _i],
+    "lzm_ez_lstm_prepare": [_i, _i, _vp, _vp],
+    "lzm_ez_lstm_workspace_bytes": [_i, _i],
+    "lzm_error_word": [_vp, _i],
+    "lzm_ez_lstm_step": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_conv": [_vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i,
                         _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_conv_heads": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
@@ -103,7 +108,9 @@ SIGNATURES = {
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
             "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64,
-            "lzm_conv_trunk_floats": ctypes.c_int64, "lzm_conv_trunk_floats_p": ctypes.c_int64}
+            "lzm_conv_trunk_floats": ctypes.c_int64, "lzm_conv_trunk_floats_p": ctypes.c_int64,
+            "lzm_ez_lstm_frag_floats": ctypes.c_int64, "lzm_ez_lstm_workspace_bytes": ctypes.c_int64,
+            "lzm_error_word": ctypes.c_void_p}
 
 _lib = None
 

@@ -143,6 +143,11 @@ class FoldedConvNet:
         self.t = None
         self._ver = None
         self.native = None  # device weight blob of lzm_conv_trunk (GPU models with a 64x8x8 latent)
+        self.lstm_frag = None  # EZ: lzm_ez_lstm_step's gate-weight fragments
+        self._lstm_ws = {}
+        # EZ: the gate GEMM + cell as one split-bf16 launch (the f32 precision keeps rocBLAS + the cell
+        # pass; LZM_LSTM_FUSED=0 too)
+        self.lstm_fused = precision == "bf16x3" and os.environ.get("LZM_LSTM_FUSED", "1") != "0"
         self.refresh()
 
     def _version(self):
@@ -186,16 +191,35 @@ class FoldedConvNet:
                                               raw.ctypes.data, host.ctypes.data), "lzm_conv_trunk_prepare_p")
         blob = torch.from_numpy(host).to(dev)
         heads = self._pack_heads()
+        lstm = self._pack_lstm(L)
         if self.native is None:
             self.native = blob
             self.actmap = t["dyn_actmap"]  # [A, 64, 8, 8], re-folded in place
             self.heads = heads
+            self.lstm_frag = lstm
         else:
             self.native.copy_(blob)
+            if lstm is not None:
+                self.lstm_frag.copy_(lstm)
             if heads is not None:
                 for k, v in heads.items():
                     if torch.is_tensor(v):
                         self.heads[k].copy_(v)
+
+    def _pack_lstm(self, L):
+        """lzm_ez_lstm_step's split-bf16 fragments of the LSTM gate weights [4H, K] (EZ), or None
+        (MuZero, or a shape the fused gate GEMM + cell kernel does not take)."""
+        if not self.ez or "lstm_w" not in self.t:
+            return None
+        W = self.t["lstm_w"]
+        H4, K = W.shape
+        n = L.lzm_ez_lstm_frag_floats(K, H4 // 4)
+        if H4 % 4 or n < 0:
+            return None
+        host = np.zeros(n, np.float32)
+        w = np.ascontiguousarray(W.detach().float().cpu().numpy())
+        _lib.check(L.lzm_ez_lstm_prepare(K, H4 // 4, w.ctypes.data, host.ctypes.data), "lzm_ez_lstm_prepare")
+        return torch.from_numpy(host).to(W.device)
 
     def _pack_heads(self):
         """lzm_conv_heads layouts (csrc/lzm_heads.h) of the folded head MLPs, or None if they do
@@ -242,12 +266,28 @@ class FoldedConvNet:
         r, h = self._trunk(pool, x, action, out_latent)
         return self._heads(r, h, out_latent, hidden)
 
-    def step_from_pool_lstm(self, pool, x, action, out_latent, hpool, cpool, k, search_len, horizon):
+    def _lstm_workspace(self, B, H, dev):
+        """split-K workspace of lzm_ez_lstm_step for batch B (zero-filled once, kept per B: captured
+        graphs hold its address) and a fallback error word"""
+        ws = self._lstm_ws.get(B)
+        if ws is None:
+            n = int(_lib.load().lzm_ez_lstm_workspace_bytes(B, H))
+            ws = (torch.zeros((n + 15) // 16 * 4, dtype=torch.float32, device=dev),
+                  torch.zeros(1, dtype=torch.int32, device=dev))
+            self._lstm_ws[B] = ws
+        return ws
+
+    def lstm_errors(self):
+        """hand-off timeouts counted by lzm_ez_lstm_step calls made without a tree's error word"""
+        return sum(int(e.item()) for _, e in self._lstm_ws.values())
+
+    def step_from_pool_lstm(self, pool, x, action, out_latent, hpool, cpool, k, search_len, horizon, err=None):
         """EfficientZero step on the pools: leaf latent pool[x[b]][b] and LSTM state (hpool, cpool)[x[b]][b]
         ([S+1, B, H] each). The next latent goes to out_latent, the next LSTM state — zeroed where
         search_len % horizon == 0 (mcts_ctree.py:810-813) — to hpool[k + 1] / cpool[k + 1]
         (csrc/lzm_lstm.h around the rocBLAS gate GEMM; the trunk kernel writes the LSTM input rows,
-        lzm_conv_trunk_xin_p). Native trunk only."""
+        lzm_conv_trunk_xin_p). Native trunk only. err: device int32 word counting the fused LSTM
+        step's hand-off timeouts (a tree's lzm_error_word, reported by its check_errors)."""
         t, P = self.t, _lib.ptr
         B, H = out_latent.shape[0], hpool.shape[2]
         Kr = self.r_ch * 64
@@ -259,11 +299,18 @@ class FoldedConvNet:
                   self.h_ch, P(self.native), P(self.actmap), P(pool), P(x), P(act.contiguous()), P(out_latent),
                   P(xin), Kr + H, P(hpool), H, P(hd), _lib.stream_ptr())
         r = xin[:, :Kr]
-        gates = torch.addmm(t["lstm_b"], xin, t["lstm_w"].t())
         h1 = torch.empty((B, H), dtype=torch.float32, device=r.device)
         c1 = torch.empty_like(h1)
-        _lib.call("lzm_ez_lstm_cell", B, H, P(gates), P(cpool), P(x), P(search_len), int(horizon), P(h1), P(c1),
-                  P(hpool[k + 1]), P(cpool[k + 1]), _lib.stream_ptr())
+        if self.lstm_frag is not None and self.lstm_fused:
+            # the gate GEMM and the cell in one launch (split-bf16 MFMA, csrc/lzm_lstm.h)
+            ws, werr = self._lstm_workspace(B, H, xin.device)
+            _lib.call("lzm_ez_lstm_step", B, Kr + H, H, P(xin), P(self.lstm_frag), P(t["lstm_b"]), P(cpool), P(x),
+                      P(search_len), int(horizon), P(h1), P(c1), P(hpool[k + 1]), P(cpool[k + 1]), P(ws),
+                      err if err is not None else P(werr), _lib.stream_ptr())
+        else:
+            gates = torch.addmm(t["lstm_b"], xin, t["lstm_w"].t())
+            _lib.call("lzm_ez_lstm_cell", B, H, P(gates), P(cpool), P(x), P(search_len), int(horizon), P(h1), P(c1),
+                      P(hpool[k + 1]), P(cpool[k + 1]), _lib.stream_ptr())
         return self._head_mlps(r, hd, out_latent, h1, c1)
 
     def initial_inference(self, obs):

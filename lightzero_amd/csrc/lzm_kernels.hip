@@ -1869,13 +1869,17 @@ int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream) {
 // times out, or a draw position beyond the coefficient table, would otherwise leave a silently
 // wrong tie-break stream). Synchronises `stream`; out_host (nullable) gets {look-back timeouts,
 // draw-table overflows, traverse fixed-point failures, fused-search errors}.
+int32_t *lzm_error_word(lzm_handle *h, int i) { return (h && i >= 0 && i < 4) ? h->err + i : nullptr; }
+
 int lzm_check_errors(lzm_handle *h, int32_t *out_host, int clear, void *stream) {
   if (!h) return LZM_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   int32_t w[4] = {0, 0, 0, 0};
-  LZM_HIP(hipMemcpyAsync(w, h->err, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-  if (h->search_diag) LZM_HIP(hipMemcpyAsync(w + 3, h->search_diag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  int32_t sd = 0;
+  LZM_HIP(hipMemcpyAsync(w, h->err, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (h->search_diag) LZM_HIP(hipMemcpyAsync(&sd, h->search_diag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   LZM_HIP(hipStreamSynchronize(s));
+  w[3] += sd;  // err[3]: the EZ LSTM step's split-K hand-off timeouts (lzm_error_word(h, 3))
   if (out_host) memcpy(out_host, w, sizeof(w));
   const bool bad = w[0] || w[1] || w[2] || w[3];
   if (bad && clear) {
@@ -2520,6 +2524,62 @@ extern "C" int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *c
   const int grid = (int)std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(ez_lstm_cell_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, B, H, gates, cpool, x,
                      search_len, horizon, h1, c1, hslot, cslot);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" int64_t lzm_ez_lstm_frag_floats(int K, int H) {
+  if (K <= 0 || H <= 0 || K % kLsKc || H % kLsUnits) return -1;
+  return (int64_t)K * 4 * H * 3 / 2;
+}
+
+extern "C" int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out) {
+  if (lzm_ez_lstm_frag_floats(K, H) < 0 || !W || !out) {
+    set_err("lzm_ez_lstm_prepare: need K % 64 == 0, H % 16 == 0 and buffers");
+    return LZM_ERR_ARG;
+  }
+  ls_pack(W, K, H, out);
+  return LZM_OK;
+}
+
+extern "C" int64_t lzm_ez_lstm_workspace_bytes(int B, int H) {
+  if (B <= 0 || H <= 0 || H % kLsUnits) return -1;
+  const int64_t tiles = (int64_t)((B + kLsRows - 1) / kLsRows) * (H / kLsUnits);
+  return tiles * kLsPartFloats * 4 + tiles * 4;
+}
+
+extern "C" int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const float *wfrag, const float *bias,
+                                const float *cpool, const int32_t *x, const int32_t *search_len, int horizon, float *h1,
+                                float *c1, float *hslot, float *cslot, void *workspace, int32_t *err, void *stream) {
+  if (B <= 0 || lzm_ez_lstm_frag_floats(K, H) < 0 || !xin || !wfrag || !bias || !cpool || !x || !search_len || !h1 ||
+      !c1 || !hslot || !cslot || (((uintptr_t)xin | (uintptr_t)wfrag | (uintptr_t)workspace) & 15) ||
+      (workspace && !err)) {
+    set_err("lzm_ez_lstm_step: bad arguments (K % 64 == 0, H % 16 == 0, 16-B aligned xin / fragments / workspace, "
+            "an error word with the workspace)");
+    return LZM_ERR_ARG;
+  }
+  LstmArgs a;
+  a.B = B; a.K = K; a.H = H; a.nmb = (B + kLsRows - 1) / kLsRows;
+  a.xin = xin; a.wf = reinterpret_cast<const uint4 *>(wfrag); a.bias = bias; a.cpool = cpool; a.x = x;
+  a.search_len = search_len; a.horizon = horizon; a.h1 = h1; a.c1 = c1; a.hslot = hslot; a.cslot = cslot;
+  const int tiles = a.nmb * (H / kLsUnits);
+  // split K in two when a workspace is given and every workgroup is resident at once (the lower K
+  // half waits for the upper; one 512-thread workgroup per CU by its LDS)
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 0;
+  a.splitk = (workspace && K % (2 * kLsKc) == 0 && 2 * tiles <= cus) ? 2 : 1;
+  a.part = reinterpret_cast<float *>(workspace);
+  a.flags = workspace ? reinterpret_cast<uint32_t *>(a.part + (size_t)tiles * kLsPartFloats) : nullptr;
+  a.err = err;
+  static bool attr = false;
+  if (!attr) {
+    LZM_HIP(hipFuncSetAttribute((const void *)ez_lstm_gemm_cell_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kLsLdsBytes));
+    attr = true;
+  }
+  hipLaunchKernelGGL(ez_lstm_gemm_cell_kernel, dim3(tiles * a.splitk), dim3(kLsThreads), kLsLdsBytes,
+                     (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }

@@ -13,9 +13,14 @@
 //                         value-prefix head reads h1), and masked into the next state slot
 //                         (zero where search_len % horizon == 0, mcts_ctree.py:810-813).
 // Both are float4-vectorised grid-stride passes: HBM/L2 bound, ~3 MB per simulation at B = 256.
+// ez_lstm_gemm_cell_kernel (below) replaces the GEMM and the cell pass with one launch.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
+
+#include "lzm_conv.h"
 
 namespace lzm {
 
@@ -61,6 +66,278 @@ __global__ __launch_bounds__(256) void ez_lstm_cell_kernel(int B, int H, const f
     const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     reinterpret_cast<float4 *>(hslot)[q] = reset ? z : h;
     reinterpret_cast<float4 *>(cslot)[q] = reset ? z : c;
+  }
+}
+
+// ---- the gate GEMM and the cell in one launch, on split-bf16 MFMA (lzm_conv.h's bf16x3 scheme)
+//
+// gates = xin W^T + b is M = B rows x N = 4H columns x K; rocBLAS ran it in f32 (16 us at Pong's
+// 256 x 2048 x 1536) and the cell was a second pass over the gates in HBM. Here a tile is 64 rows
+// (envs) x 16 hidden units, i.e. the 64 gate columns {i, f, g, o} x 16 units, so the cell runs in the
+// GEMM's epilogue from registers. Operands: each f32 value is held as h + m + l (three bf16 terms,
+// exact splits) and every product is summed from the six terms >= 2^-16 of h.h
+// (v_mfma_f32_16x16x32_bf16), as in the conv trunk.
+//   * 512 threads, two waves per SIMD: wave w owns column tile w & 3 (units 4 (w & 3) .. + 3, column
+//     4 u + gate) and row half w >> 2 (two 16-row tiles). The four gates of a (row, unit) then sit in
+//     the four lanes of a quad, and one DPP broadcast per gate hands them to the lane that writes it.
+//   * Split K in two: the tile's two K halves run in two workgroups; the upper half (lower block ids,
+//     dispatched first, so its partner is always resident) leaves its partial sums in a workspace and
+//     raises a flag, the lower half adds them (lower + upper) and runs the cell. 256 workgroups at
+//     B = 256 (every CU), 126 MB of L2 reads instead of 201 MB for 64 x 32 tiles without the split.
+//   * Per 64-K stage both operands go through LDS, double-buffered, one barrier per stage: xin rows
+//     are loaded as f32 and split on the fly ([term][row][64 K] bf16, 16-B chunk c of row r at
+//     c ^ (r & 7)); W comes pre-split from the host in MFMA fragment order
+//     ([n-block][column tile][32-K chunk][term][lane][8 bf16], copied as is). Global loads run two
+//     stages ahead.
+//   * Tiles are mapped XCD by XCD (block id % 8 = XCD), whole n-blocks per XCD, so an XCD's L2 holds
+//     its slice of W and every row of xin.
+constexpr int kLsRows = 64;                      // rows (envs) per tile
+constexpr int kLsUnits = 16;                     // hidden units per tile (64 gate columns)
+constexpr int kLsKc = 64;                        // K per LDS stage
+constexpr int kLsThreads = 512;
+constexpr int kLsPlane = kLsRows * kLsKc;        // bf16 per A term plane
+constexpr int kLsABuf = 3 * kLsPlane;            // bf16: A stage (three planes)
+constexpr int kLsBBuf = 2 * 4 * 3 * 64 * 8;      // bf16: B stage [chunk 2][col tile 4][term 3][lane][8]
+constexpr int kLsStage = kLsABuf + kLsBBuf;      // bf16 per stage buffer
+constexpr int kLsLdsBytes = 2 * kLsStage * 2;    // two stage buffers
+constexpr int kLsPartFloats = kLsThreads * 8;    // one tile's partial sums (8 per thread)
+
+struct LstmArgs {
+  int B, K, H, nmb, splitk;  // nmb = ceil(B / 64); splitk 1 or 2
+  const float *xin;          // [B][K]
+  const uint4 *wf;           // fragments (lzm_ez_lstm_prepare)
+  const float *bias;         // [4H] (b_ih + b_hh), nn.LSTM gate order
+  const float *cpool;        // [slots][B][H]
+  const int32_t *x, *search_len;
+  int horizon;
+  float *h1, *c1, *hslot, *cslot;  // [B][H]
+  float *part;                     // split K: [tiles][kLsPartFloats]
+  uint32_t *flags;                 // split K: [tiles], 0 between launches
+  int32_t *err;                    // split K: bounded-spin timeouts (sticky)
+};
+
+// fragment element (nb, column tile, chunk, term, lane, e) <- W[(gate H + unit) K + k]
+inline void ls_pack(const float *W, int K, int H, float *outf) {
+  uint16_t *out = reinterpret_cast<uint16_t *>(outf);
+  const int nch = K / 32, NB = H / kLsUnits;
+  for (int nb = 0; nb < NB; ++nb)
+    for (int w = 0; w < 4; ++w)
+      for (int j = 0; j < nch; ++j)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 8; ++e) {
+            const int n = lane & 15, unit = kLsUnits * nb + 4 * w + (n >> 2), gate = n & 3;
+            const int k = 32 * j + 8 * (lane >> 4) + e;
+            uint16_t t[3];
+            bx_split(W[((size_t)gate * H + unit) * K + k], t[0], t[1], t[2]);
+            for (int q = 0; q < 3; ++q) out[((((size_t)(nb * 4 + w) * nch + j) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+          }
+}
+
+__device__ __forceinline__ float ls_quad_bcast(float v, int g) {
+  const int x = __builtin_bit_cast(int, v);
+  const int r = g == 0 ? __builtin_amdgcn_update_dpp(0, x, 0x00, 0xF, 0xF, false)
+              : g == 1 ? __builtin_amdgcn_update_dpp(0, x, 0x55, 0xF, 0xF, false)
+              : g == 2 ? __builtin_amdgcn_update_dpp(0, x, 0xAA, 0xF, 0xF, false)
+                       : __builtin_amdgcn_update_dpp(0, x, 0xFF, 0xF, 0xF, false);
+  return __builtin_bit_cast(float, r);
+}
+
+__global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs p) {
+  extern __shared__ uint4 ls_lds4[];
+  uint16_t *lds = reinterpret_cast<uint16_t *>(ls_lds4);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ct = wv & 3, mh = wv >> 2;
+  const int NB = p.H / kLsUnits, T = NB * p.nmb, G = T * p.splitk;
+  // block -> (K half, tile): the upper K half takes the lower block ids; tiles XCD-major
+  const int kh = p.splitk == 2 && (int)blockIdx.x < T ? 1 : 0;
+  int q = (int)blockIdx.x - (p.splitk == 2 && kh == 0 ? T : 0);
+  if ((T & 7) == 0) q = (q & 7) * (T >> 3) + (q >> 3);
+  (void)G;
+  const int nb = q / p.nmb, mb = q - nb * p.nmb;
+  const int row0 = kLsRows * mb, B = p.B, K = p.K, H = p.H;
+  const int nch = K / 32, kspan = K / p.splitk, nst = kspan / kLsKc, k0 = kh * kspan;
+  // the cell's inputs for this lane's rows (lower K half only), in flight during the GEMM
+  const int gate = lane & 3, unit = kLsUnits * nb + 4 * ct + ((lane & 15) >> 2);
+  float c0[2] = {0.f, 0.f}, bias_l = 0.f;
+  int rst[2] = {0, 0};
+  if (kh == 0) {
+    bias_l = p.bias[(size_t)gate * H + unit];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int b = row0 + 32 * mh + 16 * t + 4 * (lane >> 4) + gate;
+      if (b < B) {
+        c0[t] = p.cpool[((size_t)max(p.x[b], 0) * B + b) * H + unit];
+        rst[t] = p.horizon > 0 && (p.search_len[b] % p.horizon) == 0;
+      }
+    }
+  }
+  // ---- staging: thread -> A (row tid / 8, 8 K values at 8 (tid % 8)) and 3 B uint4s per stage
+  const int sr = tid >> 3, sseg = tid & 7;
+  const bool srow = row0 + sr < B;
+  const float4 *asrc = reinterpret_cast<const float4 *>(p.xin + (size_t)(srow ? row0 + sr : 0) * K + k0) + 2 * sseg;
+  const uint4 *bsrc = p.wf + (size_t)nb * 4 * nch * 3 * 64;  // [col tile][chunk][term][lane]
+  // staging registers of two stages (native vector types: HIP's uint4 / float4 structs kept these
+  // arrays in scratch)
+  typedef unsigned ls_u4 __attribute__((ext_vector_type(4)));
+  typedef float ls_f4 __attribute__((ext_vector_type(4)));
+  ls_f4 va0[2], va1[2];
+  ls_u4 vb0[3], vb1[3];
+  const ls_u4 *bsrc4 = reinterpret_cast<const ls_u4 *>(bsrc);
+  const ls_f4 *asrc4 = reinterpret_cast<const ls_f4 *>(asrc);
+  auto load_stage = [&](int s, ls_f4(&VA)[2], ls_u4(&VB)[3]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) VA[u] = srow ? asrc4[s * (kLsKc / 4) + u] : ls_f4{0.f, 0.f, 0.f, 0.f};
+    // B stage = [chunk c][col tile][term][lane]: element e = tid + 512 u of 1536 uint4s
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + kLsThreads * u, c = e / 768, r = e - c * 768, tl = r / 192, rest = r - tl * 192;
+      const int j = (k0 / 32) + 2 * s + c;
+      VB[u] = bsrc4[((size_t)tl * nch + j) * 192 + rest];
+    }
+  };
+  auto store_stage = [&](int bsel, const ls_f4(&VA)[2], const ls_u4(&VB)[3]) __attribute__((always_inline)) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    uint32_t h[4], m[4], l[4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const f2 pr[2] = {f2{VA[u][0], VA[u][1]}, f2{VA[u][2], VA[u][3]}};
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const b2 hh = __builtin_convertvector(pr[v], b2);
+        const f2 r1 = pr[v] - __builtin_convertvector(hh, f2);
+        const b2 mm = __builtin_convertvector(r1, b2);
+        const b2 ll = __builtin_convertvector(r1 - __builtin_convertvector(mm, f2), b2);
+        h[2 * u + v] = __builtin_bit_cast(uint32_t, hh);
+        m[2 * u + v] = __builtin_bit_cast(uint32_t, mm);
+        l[2 * u + v] = __builtin_bit_cast(uint32_t, ll);
+      }
+    }
+    uint16_t *abuf = lds + bsel * kLsStage;
+    uint16_t *base = abuf + sr * kLsKc + ((sseg ^ (sr & 7)) & 7) * 8;
+    *reinterpret_cast<uint4 *>(base) = uint4{h[0], h[1], h[2], h[3]};
+    *reinterpret_cast<uint4 *>(base + kLsPlane) = uint4{m[0], m[1], m[2], m[3]};
+    *reinterpret_cast<uint4 *>(base + 2 * kLsPlane) = uint4{l[0], l[1], l[2], l[3]};
+    ls_u4 *bbuf = reinterpret_cast<ls_u4 *>(abuf + kLsABuf);
+#pragma unroll
+    for (int u = 0; u < 3; ++u) bbuf[tid + kLsThreads * u] = VB[u];
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  load_stage(0, va0, vb0);
+  if (nst > 1) load_stage(1, va1, vb1);
+  store_stage(0, va0, vb0);
+  bxf4 acc[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) acc[t] = bxf4{0.f, 0.f, 0.f, 0.f};
+  const int ar = lane & 15, ag = lane >> 4;
+  auto stage = [&](int s, auto par) __attribute__((always_inline)) {
+    constexpr int PAR = decltype(par)::value;
+    __syncthreads();
+    if (s + 2 < nst) {
+      if constexpr (PAR == 0)
+        load_stage(s + 2, va0, vb0);
+      else
+        load_stage(s + 2, va1, vb1);
+    }  // (slot PAR went to LDS at the end of stage s - 1)
+    const uint16_t *abuf = lds + PAR * kLsStage;
+    const uint4 *bbuf = reinterpret_cast<const uint4 *>(abuf + kLsABuf);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint4 a[2][3], w[3];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = 32 * mh + 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm) a[t][tm] = *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 3; ++tm) w[tm] = bbuf[((c * 4 + ct) * 3 + tm) * 64 + lane];
+      // small terms first: l.h, h.l, m.m, m.h, h.m, h.h (the conv trunk's order)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[2]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[1]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[0]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[1]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
+    }
+    if (s + 1 < nst) {
+      if constexpr (PAR == 0)
+        store_stage(1, va1, vb1);
+      else
+        store_stage(0, va0, vb0);
+    }
+  };
+  for (int s = 0; s < nst; s += 2) {
+    stage(s, I0());
+    if (s + 1 < nst) stage(s + 1, I1());
+  }
+  // ---- split K: the upper half hands its partial sums over; the lower half adds them. Hand-off
+  // (MI355X_MICROARCH.md, cross-CU hand-off table, first row): payload and flag stored sc1 (agent-scope
+  // relaxed atomics, 8-B payload words), every storing wave's vmcnt(0) and a workgroup barrier before
+  // the one flag store; the consumer's one lane polls the flag sc1, a barrier, then sc1 payload loads.
+  if (p.splitk == 2) {
+    unsigned long long *part = reinterpret_cast<unsigned long long *>(p.part + (size_t)q * kLsPartFloats) + tid * 4;
+    auto pk = [](float a, float b) {
+      return (unsigned long long)__builtin_bit_cast(uint32_t, a) | ((unsigned long long)__builtin_bit_cast(uint32_t, b) << 32);
+    };
+    if (kh == 1) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        __hip_atomic_store(part + 2 * t, pk(acc[t][0], acc[t][1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(part + 2 * t + 1, pk(acc[t][2], acc[t][3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(p.flags + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    if (tid == 0) {
+      long long spins = 0;
+      while (__hip_atomic_load(p.flags + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        if (++spins > (1ll << 24)) {
+          atomicAdd(p.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __hip_atomic_store(p.flags + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const unsigned long long u0 = __hip_atomic_load(part + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long u1 = __hip_atomic_load(part + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      acc[t] += bxf4{__builtin_bit_cast(float, (uint32_t)u0), __builtin_bit_cast(float, (uint32_t)(u0 >> 32)),
+                     __builtin_bit_cast(float, (uint32_t)u1), __builtin_bit_cast(float, (uint32_t)(u1 >> 32))};
+    }
+  }
+  // ---- epilogue: + bias, the four gates of (row, unit) from the quad, the cell by lane gate = r
+  // (ez_lstm_cell_kernel's operations in its order)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    float gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = acc[t][r] + bias_l;
+      const float vi = ls_quad_bcast(v, 0), vf = ls_quad_bcast(v, 1), vg = ls_quad_bcast(v, 2), vo = ls_quad_bcast(v, 3);
+      if (gate == r) { gi = vi; gf = vf; gg = vg; go = vo; }
+    }
+    const int b = row0 + 32 * mh + 16 * t + 4 * (lane >> 4) + gate;
+    if (b < B) {
+      const float c = lstm_sigmoid(gf) * c0[t] + lstm_sigmoid(gi) * tanhf(gg);
+      const float h = lstm_sigmoid(go) * tanhf(c);
+      const size_t o = (size_t)b * H + unit;
+      p.h1[o] = h;
+      p.c1[o] = c;
+      p.hslot[o] = rst[t] ? 0.0f : h;
+      p.cslot[o] = rst[t] ? 0.0f : c;
+    }
   }
 }
 

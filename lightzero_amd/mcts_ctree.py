@@ -548,7 +548,7 @@ class EfficientZeroMCTSCtree(object):
             if native:
                 # the LSTM state is gathered from / filed (reset-masked) into the state pools on the device
                 out = model.step_from_pool_lstm(buf.pool, t.x, t.action, buf.pool[k + 1], buf.extra[0], buf.extra[1],
-                                                k, t.search_len, horizon)
+                                                k, t.search_len, horizon, err=t.error_word(3))
             else:
                 t.gather(buf.extra[0], Hl, buf.extra_in[0])
                 t.gather(buf.extra[1], Hl, buf.extra_in[1])

@@ -198,6 +198,10 @@ class DeviceTree:
         call("lzm_search_set_step", self.h, ptr(count), int(base), int(bool(increment)), ptr(dist), ptr(values),
              int(bool(fresh_minmax)), float(np.float32(value_delta_max)))
 
+    def error_word(self, i):
+        """device address (ctypes) of sticky error word i, for kernels launched outside the handle"""
+        return ctypes.c_void_p(_lib.load().lzm_error_word(self.h, int(i)))
+
     def check_errors(self, clear=True, stream=None):
         """Post-search integrity check (synchronises the stream): raises LzmError when a look-back
         spin timed out or a draw fell outside the coefficient table on any search path of this

@@ -259,6 +259,41 @@ def test_native_lstm_step_matches_module():
     assert torch.all(hpool[slots][slen % 5 == 0] == 0) and torch.all(cpool[slots][slen % 5 == 0] == 0)
 
 
+@pytest.mark.parametrize("B", [37, 256])
+def test_fused_lstm_gate_gemm_cell_close_to_f32_gemm(B):
+    """lzm_ez_lstm_step (gate GEMM on split-bf16 MFMA + cell in the epilogue, one launch) vs the f32
+    rocBLAS GEMM + lzm_ez_lstm_cell on the same inputs: new state slots and head outputs within
+    rtol 2e-5 / atol 2e-6 (f32-level error), reset masks identical"""
+    from lightzero_amd.conv_infer import FoldedConvNet
+    model = conv_model("ez", 6)
+    net = FoldedConvNet(model)
+    assert net.lstm_frag is not None and net.lstm_fused, "fused LSTM step not packed"
+    slots, H = 4, 512
+    g = torch.Generator(device=DEV).manual_seed(5)
+    pool = torch.relu(torch.randn(slots, B, 64, 8, 8, generator=g, device=DEV))
+    hpool0 = torch.randn(slots + 1, B, H, generator=g, device=DEV) * 0.5
+    cpool0 = torch.randn(slots + 1, B, H, generator=g, device=DEV) * 0.5
+    x = torch.randint(0, slots, (B,), generator=g, device=DEV).to(torch.int32)
+    act = torch.randint(0, model.action_space_size, (B,), generator=g, device=DEV).to(torch.int32)
+    slen = torch.randint(1, 13, (B,), generator=g, device=DEV).to(torch.int32)
+    res = []
+    for fused in (True, False):
+        net.lstm_fused = fused
+        hpool, cpool = hpool0.clone(), cpool0.clone()
+        slot = torch.empty(B, 64, 8, 8, device=DEV)
+        with torch.no_grad():
+            out = net.step_from_pool_lstm(pool, x, act, slot, hpool, cpool, slots - 1, slen, 5)
+        torch.cuda.synchronize()
+        res.append((out, hpool[slots].clone(), cpool[slots].clone()))
+    net.lstm_fused = True
+    (o1, h1, c1), (o0, h0, c0) = res
+    torch.testing.assert_close(h1, h0, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(c1, c0, rtol=2e-5, atol=2e-6)
+    assert torch.equal(h1 == 0, h0 == 0) and torch.all(h1[slen % 5 == 0] == 0)
+    for name in ("value_prefix", "value", "policy_logits"):
+        torch.testing.assert_close(getattr(o1, name), getattr(o0, name), rtol=2e-5, atol=2e-6)
+
+
 @pytest.mark.parametrize("kind", ["ez", "mz"])
 def test_fused_decode_traverse_equals_separate(kind):
     """cfg.fuse_traverse (lzm_decode_backprop_traverse: backup of simulation k and traverse of k + 1 in
