@@ -432,6 +432,8 @@ int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out);
  * is split over two workgroups per tile when every workgroup fits on the GPU at once (err: a sticky
  * int32 counting hand-off timeouts, required with the workspace). */
 int64_t lzm_ez_lstm_workspace_bytes(int B, int H);
+/* diagnostics: lzm_ez_lstm_step launches record shader-clock stamps into buf [blocks][8] (nullptr: off) */
+int lzm_debug_lstm_stamps(void *buf);
 /* Device address of the handle's sticky error word i (0..3) for kernels launched outside the handle
  * (word 3: lzm_ez_lstm_step's hand-off timeouts); lzm_check_errors reports it. */
 int32_t *lzm_error_word(lzm_handle *h, int i);

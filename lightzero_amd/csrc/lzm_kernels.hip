@@ -2542,6 +2542,12 @@ extern "C" int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out) {
   return LZM_OK;
 }
 
+static unsigned long long *g_ls_stamps = nullptr;  // diagnostics: lzm_debug_lstm_stamps
+extern "C" int lzm_debug_lstm_stamps(void *buf) {
+  g_ls_stamps = reinterpret_cast<unsigned long long *>(buf);
+  return LZM_OK;
+}
+
 extern "C" int64_t lzm_ez_lstm_workspace_bytes(int B, int H) {
   if (B <= 0 || H <= 0 || H % kLsUnits) return -1;
   const int64_t tiles = (int64_t)((B + kLsRows - 1) / kLsRows) * (H / kLsUnits);
@@ -2572,6 +2578,7 @@ extern "C" int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const flo
   a.part = reinterpret_cast<float *>(workspace);
   a.flags = workspace ? reinterpret_cast<uint32_t *>(a.part + (size_t)tiles * kLsPartFloats) : nullptr;
   a.err = err;
+  a.stamps = g_ls_stamps;
   static bool attr = false;
   if (!attr) {
     LZM_HIP(hipFuncSetAttribute((const void *)ez_lstm_gemm_cell_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -91,6 +91,10 @@ __global__ __launch_bounds__(256) void ez_lstm_cell_kernel(int B, int H, const f
 //     stages ahead.
 //   * Tiles are mapped XCD by XCD (block id % 8 = XCD), whole n-blocks per XCD, so an XCD's L2 holds
 //     its slice of W and every row of xin.
+#ifndef LZM_LS_DIAG
+#define LZM_LS_DIAG 0  // timing experiments only (results invalid): 1 = no global loads after the first
+                       // stages, 2 = no MFMAs, 3 = no LDS fragment reads
+#endif
 constexpr int kLsRows = 64;                      // rows (envs) per tile
 constexpr int kLsUnits = 16;                     // hidden units per tile (64 gate columns)
 constexpr int kLsKc = 64;                        // K per LDS stage
@@ -114,6 +118,7 @@ struct LstmArgs {
   float *part;                     // split K: [tiles][kLsPartFloats]
   uint32_t *flags;                 // split K: [tiles], 0 between launches
   int32_t *err;                    // split K: bounded-spin timeouts (sticky)
+  unsigned long long *stamps;      // diagnostics (nullptr in production): [block][8] 100 MHz real-time stamps
 };
 
 // fragment element (nb, column tile, chunk, term, lane, e) <- W[(gate H + unit) K + k]
@@ -155,21 +160,11 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
   const int nb = q / p.nmb, mb = q - nb * p.nmb;
   const int row0 = kLsRows * mb, B = p.B, K = p.K, H = p.H;
   const int nch = K / 32, kspan = K / p.splitk, nst = kspan / kLsKc, k0 = kh * kspan;
-  // the cell's inputs for this lane's rows (lower K half only), in flight during the GEMM
   const int gate = lane & 3, unit = kLsUnits * nb + 4 * ct + ((lane & 15) >> 2);
-  float c0[2] = {0.f, 0.f}, bias_l = 0.f;
-  int rst[2] = {0, 0};
-  if (kh == 0) {
-    bias_l = p.bias[(size_t)gate * H + unit];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int b = row0 + 32 * mh + 16 * t + 4 * (lane >> 4) + gate;
-      if (b < B) {
-        c0[t] = p.cpool[((size_t)max(p.x[b], 0) * B + b) * H + unit];
-        rst[t] = p.horizon > 0 && (p.search_len[b] % p.horizon) == 0;
-      }
-    }
-  }
+  auto stamp = [&](int i) {
+    if (p.stamps && tid == 0) p.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   // ---- staging: thread -> A (row tid / 8, 8 K values at 8 (tid % 8)) and 3 B uint4s per stage
   const int sr = tid >> 3, sseg = tid & 7;
   const bool srow = row0 + sr < B;
@@ -226,6 +221,7 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
   load_stage(0, va0, vb0);
   if (nst > 1) load_stage(1, va1, vb1);
   store_stage(0, va0, vb0);
+  stamp(1);
   bxf4 acc[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) acc[t] = bxf4{0.f, 0.f, 0.f, 0.f};
@@ -233,7 +229,7 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
   auto stage = [&](int s, auto par) __attribute__((always_inline)) {
     constexpr int PAR = decltype(par)::value;
     __syncthreads();
-    if (s + 2 < nst) {
+    if (s + 2 < nst && LZM_LS_DIAG != 1) {
       if constexpr (PAR == 0)
         load_stage(s + 2, va0, vb0);
       else
@@ -248,10 +244,21 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
       for (int t = 0; t < 2; ++t) {
         const int r = 32 * mh + 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
 #pragma unroll
-        for (int tm = 0; tm < 3; ++tm) a[t][tm] = *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
+        for (int tm = 0; tm < 3; ++tm)
+          a[t][tm] = LZM_LS_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)s, (uint32_t)t, (uint32_t)tm}
+                                      : *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
       }
 #pragma unroll
-      for (int tm = 0; tm < 3; ++tm) w[tm] = bbuf[((c * 4 + ct) * 3 + tm) * 64 + lane];
+      for (int tm = 0; tm < 3; ++tm)
+        w[tm] = LZM_LS_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)c, 1u, (uint32_t)tm}
+                                 : bbuf[((c * 4 + ct) * 3 + tm) * 64 + lane];
+      if (LZM_LS_DIAG == 2) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y),
+                         __builtin_bit_cast(float, a[t][2].z ^ w[2].z), 0.f};
+        continue;
+      }
       // small terms first: l.h, h.l, m.m, m.h, h.m, h.h (the conv trunk's order)
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
@@ -266,35 +273,54 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
     }
-    if (s + 1 < nst) {
+    if (s + 1 < nst && LZM_LS_DIAG != 5) {
       if constexpr (PAR == 0)
         store_stage(1, va1, vb1);
       else
         store_stage(0, va0, vb0);
+  stamp(1);
     }
   };
   for (int s = 0; s < nst; s += 2) {
     stage(s, I0());
     if (s + 1 < nst) stage(s + 1, I1());
   }
+  stamp(2);
+  // the cell's inputs for this lane's rows (lower K half only): issued after the GEMM's loads (vmcnt
+  // counts in order: issued first, the dependent x -> cpool gather would hold up the first stage),
+  // in flight during the hand-off
+  float c0[2] = {0.f, 0.f}, bias_l = 0.f;
+  int rst[2] = {0, 0};
+  if (kh == 0) {
+    bias_l = p.bias[(size_t)gate * H + unit];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int b = row0 + 32 * mh + 16 * t + 4 * (lane >> 4) + gate;
+      if (b < B) {
+        c0[t] = p.cpool[((size_t)max(p.x[b], 0) * B + b) * H + unit];
+        rst[t] = p.horizon > 0 && (p.search_len[b] % p.horizon) == 0;
+      }
+    }
+  }
   // ---- split K: the upper half hands its partial sums over; the lower half adds them. Hand-off
-  // (MI355X_MICROARCH.md, cross-CU hand-off table, first row): payload and flag stored sc1 (agent-scope
-  // relaxed atomics, 8-B payload words), every storing wave's vmcnt(0) and a workgroup barrier before
-  // the one flag store; the consumer's one lane polls the flag sc1, a barrier, then sc1 payload loads.
-  if (p.splitk == 2) {
-    unsigned long long *part = reinterpret_cast<unsigned long long *>(p.part + (size_t)q * kLsPartFloats) + tid * 4;
-    auto pk = [](float a, float b) {
-      return (unsigned long long)__builtin_bit_cast(uint32_t, a) | ((unsigned long long)__builtin_bit_cast(uint32_t, b) << 32);
-    };
+  // (MI355X_MICROARCH.md, cross-CU hand-off table, first row): payload and flag stored sc1 (16-B buffer
+  // stores with the sc1 policy; the flag by an agent-scope relaxed atomic), every storing wave's
+  // vmcnt(0) and a workgroup barrier before the one flag store; the consumer's one lane polls the flag
+  // sc1, a barrier, then sc1 payload loads.
+  if (p.splitk == 2 && LZM_LS_DIAG == 4 && kh == 1) return;
+  if (p.splitk == 2 && LZM_LS_DIAG != 4) {
+    // payload: 16-B buffer stores / loads with the sc1 cache policy (aux = 16)
+    typedef unsigned ls_u4v __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(p.part + (size_t)q * kLsPartFloats, 0, kLsPartFloats * 4, 0x00020000);
     if (kh == 1) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        __hip_atomic_store(part + 2 * t, pk(acc[t][0], acc[t][1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(part + 2 * t + 1, pk(acc[t][2], acc[t][3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      for (int t = 0; t < 2; ++t)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(ls_u4v, acc[t]), rs, (tid * 8 + 4 * t) * 4, 0, 16);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) __hip_atomic_store(p.flags + q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      stamp(3);
       return;
     }
     if (tid == 0) {
@@ -304,18 +330,15 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
           atomicAdd(p.err, 1);
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(1);
       }
       __hip_atomic_store(p.flags + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    stamp(3);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const unsigned long long u0 = __hip_atomic_load(part + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned long long u1 = __hip_atomic_load(part + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      acc[t] += bxf4{__builtin_bit_cast(float, (uint32_t)u0), __builtin_bit_cast(float, (uint32_t)(u0 >> 32)),
-                     __builtin_bit_cast(float, (uint32_t)u1), __builtin_bit_cast(float, (uint32_t)(u1 >> 32))};
-    }
+    for (int t = 0; t < 2; ++t)
+      acc[t] += __builtin_bit_cast(bxf4, __builtin_amdgcn_raw_buffer_load_b128(rs, (tid * 8 + 4 * t) * 4, 0, 16));
   }
   // ---- epilogue: + bias, the four gates of (row, unit) from the quad, the cell by lane gate = r
   // (ez_lstm_cell_kernel's operations in its order)
@@ -339,6 +362,7 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
       p.cslot[o] = rst[t] ? 0.0f : c;
     }
   }
+  stamp(4);
 }
 
 }  // namespace lzm

@@ -263,7 +263,8 @@ def test_native_lstm_step_matches_module():
 def test_fused_lstm_gate_gemm_cell_close_to_f32_gemm(B):
     """lzm_ez_lstm_step (gate GEMM on split-bf16 MFMA + cell in the epilogue, one launch) vs the f32
     rocBLAS GEMM + lzm_ez_lstm_cell on the same inputs: new state slots and head outputs within
-    rtol 2e-5 / atol 2e-6 (f32-level error), reset masks identical"""
+    rtol 1e-4 / atol 1e-5 (both are f32-level: K = 1536 products summed in different orders differ by
+    a few 1e-6 absolute; a plain bf16 GEMM would miss by ~1e-2), reset masks identical"""
     from lightzero_amd.conv_infer import FoldedConvNet
     model = conv_model("ez", 6)
     net = FoldedConvNet(model)
@@ -287,11 +288,12 @@ def test_fused_lstm_gate_gemm_cell_close_to_f32_gemm(B):
         res.append((out, hpool[slots].clone(), cpool[slots].clone()))
     net.lstm_fused = True
     (o1, h1, c1), (o0, h0, c0) = res
-    torch.testing.assert_close(h1, h0, rtol=2e-5, atol=2e-6)
-    torch.testing.assert_close(c1, c0, rtol=2e-5, atol=2e-6)
+    torch.testing.assert_close(h1, h0, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(c1, c0, rtol=1e-4, atol=1e-5)
     assert torch.equal(h1 == 0, h0 == 0) and torch.all(h1[slen % 5 == 0] == 0)
     for name in ("value_prefix", "value", "policy_logits"):
-        torch.testing.assert_close(getattr(o1, name), getattr(o0, name), rtol=2e-5, atol=2e-6)
+        torch.testing.assert_close(getattr(o1, name), getattr(o0, name), rtol=1e-4, atol=1e-5)
+    assert net.lstm_errors() == 0
 
 
 @pytest.mark.parametrize("kind", ["ez", "mz"])

@@ -1,13 +1,21 @@
 # GPU: the round's closing set — GPU tests, smoke, the profile set of the headline bench (kernel stats,
-# PMC passes, bench line), the conv benches
+# PMC passes, bench line with the CPU baseline), the conv benches (Breakout one launch: kernel trace),
+# Philox / zero-heads lines, the collect-mode line. usage: bash tools/gpu_final.sh <tag>
 set -e
-mkdir -p gpurun_out/f
+tag=${1:-r03}
+out=gpurun_out/f_$tag
+mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/f/gpu_tests.log 2>&1
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/f/smoke.log 2>&1
-bash tools/profile_round.sh r02g
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/gpu_tests.log 2>&1
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+bash tools/profile_round.sh $tag
 for k in mz ez; do
-  timeout -k 10 150 python tools/conv_bench.py --kind $k > gpurun_out/f/conv_$k.json 2>gpurun_out/f/conv_$k.err
+  timeout -k 10 150 python tools/conv_bench.py --kind $k > $out/conv_$k.json 2>$out/conv_$k.err
 done
-timeout -k 10 120 python bench.py --no-cpu-baseline --rng philox > gpurun_out/f/bench_philox.json 2>&1
-timeout -k 10 120 python bench.py --no-cpu-baseline --zero-heads > gpurun_out/f/bench_zero_heads.json 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_conv_mz -o conv_mz --output-format csv -- \
+  python3 tools/conv_bench.py --kind mz --searches 3 > $out/trace_conv_mz.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_conv_ez -o conv_ez --output-format csv -- \
+  python3 tools/conv_bench.py --kind ez --searches 3 > $out/trace_conv_ez.log 2>&1
+timeout -k 10 120 python bench.py --no-cpu-baseline --rng philox > $out/bench_philox.json 2>&1
+timeout -k 10 120 python bench.py --no-cpu-baseline --zero-heads > $out/bench_zero_heads.json 2>&1
+timeout -k 10 200 python bench.py --step collect --no-cpu-baseline > $out/bench_collect.json 2>$out/bench_collect.err

