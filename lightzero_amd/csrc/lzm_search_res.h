@@ -187,10 +187,18 @@ __device__ __forceinline__ float dot4(const float4 *x4, WF w) {
   return (a[0] + a[1]) + (a[2] + a[3]);
 }
 
+// 128-wide activation rows in LDS are padded: the upper 64 floats start 4 floats after the lower
+// ones (row stride kRRow), so the two lanes of a pair, which read float4 j of their half, hit
+// different banks (unpadded, the halves are 256 B apart: the same bank, a 2-way conflict on every
+// activation read of every dense layer). rpad(c): column c's float offset in a padded row.
+constexpr int kRRow = kRHid + 4;
+constexpr int kRHalf4 = kRHid / 8 + 1;  // float4 offset of the upper half
+__device__ __forceinline__ int rpad(int c) { return c + ((c >> 6) << 2); }
+
 // Full pre-activation of this lane's column of a 128 x 128 layer (both lanes of a pair get it).
 template <typename WF>
 __device__ __forceinline__ float dense128(const float *x, WF w) {
-  const float h = dot4<16>(reinterpret_cast<const float4 *>(x) + 16 * (threadIdx.x & 1), w);
+  const float h = dot4<16>(reinterpret_cast<const float4 *>(x) + kRHalf4 * (threadIdx.x & 1), w);
   return h + dpp_f<0xB1>(h);
 }
 
@@ -920,7 +928,7 @@ __device__ __forceinline__ void dense128n(const float *x, WF w, float *z, SF sid
     side(j);
     const float4 q = w(j);
 #pragma unroll
-    for (int r = 0; r < NR; ++r) fma4(reinterpret_cast<const float4 *>(x + r * kRHid)[16 * p + j], q, a[r]);
+    for (int r = 0; r < NR; ++r) fma4(reinterpret_cast<const float4 *>(x + r * kRRow)[kRHalf4 * p + j], q, a[r]);
   }
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
@@ -1047,7 +1055,7 @@ __device__ inline int lookback_sum_w0(const SearchArgs &p, int k, int g, int G, 
 // S: simulations the selection tables hold. (A compile-time plan for the production handle, which
 // frees ~45 scalar registers of offsets, measured even: the scalar spills are not on the path.)
 // static LDS of the kernel: activations (two rows), biases, scalars (below 2 KiB)
-constexpr int kResStaticBytes = (kRHid + 4 * kRHid + 2 * (4 * kRHid + kRF + 2 * kRF + kRMaxA) + kResBiasFloats) * 4 + 2048;
+constexpr int kResStaticBytes = (kRRow + 4 * kRRow + 2 * (4 * kRRow + kRF + 2 * kRF + kRMaxA) + kResBiasFloats) * 4 + 2048;
 constexpr int kResMaxBytes = 160 * 1024 - kResStaticBytes;
 __host__ __device__ constexpr int res_round4(int x) { return (x + 3) & ~3; }
 __host__ __device__ constexpr ResPlan res_plan(int cap, int lut_n, int depth_cap, int S, int A) {
@@ -1181,10 +1189,10 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // registers and fold the arrays' offsets into the instructions' immediates
   // T1 / NL hold two rows even at NR = 1: the two candidates of a leaf tie run the dynamics
   // layers side by side while the draw offset is still unknown (see the simulation loop)
-  __shared__ float4 s_acts[(kRHid + 4 * kRHid + NR * (4 * kRHid + kRF + 2 * kRF + kRMaxA)) / 4];
+  __shared__ float4 s_acts[(kRRow + 4 * kRRow + NR * (4 * kRRow + kRF + 2 * kRF + kRMaxA)) / 4];
   __shared__ float4 s_bias[kResBiasFloats / 4];
-  float *X0 = reinterpret_cast<float *>(s_acts), *T1 = X0 + kRHid, *NL = T1 + 2 * kRHid, *T2 = NL + 2 * kRHid,
-        *T3 = T2 + NR * kRHid, *U2 = T3 + NR * kRHid, *U3 = U2 + NR * kRHid, *RHo = U3 + NR * kRHid,
+  float *X0 = reinterpret_cast<float *>(s_acts), *T1 = X0 + kRRow, *NL = T1 + 2 * kRRow, *T2 = NL + 2 * kRRow,
+        *T3 = T2 + NR * kRRow, *U2 = T3 + NR * kRRow, *U3 = U2 + NR * kRRow, *RHo = U3 + NR * kRRow,
         *HV = RHo + NR * kRF, *LG = HV + NR * 2 * kRF;
   float *ACT = smem + L.act;
   const float4 *WD1 = reinterpret_cast<const float4 *>(smem + L.wd1);
@@ -1377,7 +1385,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     LZM_STAMP(1);
     // ---- gather the leaf's parent latent: X0 = pool[x][i]
     if (tid < kRHid / 4)
-      reinterpret_cast<float4 *>(X0)[tid] =
+      reinterpret_cast<float4 *>(X0)[tid + (tid >= kRHid / 8)] =
           reinterpret_cast<const float4 *>(p.pool + ((size_t)max(s_x, 0) * B + i) * kRHid)[tid];
     __syncthreads();
     LZM_STAMP(2);
@@ -1421,7 +1429,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (pD == 0) {
 #pragma unroll
       for (int r = 0; r < 2; ++r)
-        if (r < NR || late) T1[r * kRHid + cD] = fmaxf((z0 + ACT[act_r[r] * kRHid + cD]) + BD[cD], 0.0f);
+        if (r < NR || late) T1[r * kRRow + rpad(cD)] = fmaxf((z0 + ACT[act_r[r] * kRHid + cD]) + BD[cD], 0.0f);
     }
     __syncthreads();
     LZM_SUBSTAMP(18);
@@ -1435,7 +1443,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
       if (pD == 0) {
 #pragma unroll
-        for (int r = 0; r < 2; ++r) NL[r * kRHid + cD] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[cD];
+        for (int r = 0; r < 2; ++r) NL[r * kRRow + rpad(cD)] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[rpad(cD)];
       }
     } else {
       float z[NR];
@@ -1446,7 +1454,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #endif
       if (pD == 0) {
 #pragma unroll
-        for (int r = 0; r < NR; ++r) NL[r * kRHid + cD] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[cD];
+        for (int r = 0; r < NR; ++r) NL[r * kRRow + rpad(cD)] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[rpad(cD)];
       }
     }
     __syncthreads();
@@ -1466,7 +1474,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       __syncthreads();
     }
     // the next latent row the rest of the network reads (NR = 1: the late draw's pick)
-    const float *NLb = NL + ((NR == 1 && late && s_act == act_r[1]) ? kRHid : 0);
+    const float *NLb = NL + ((NR == 1 && late && s_act == act_r[1]) ? kRRow : 0);
     LZM_STAMP(3);
     // The reward chain (fc_dynamics_2 -> reward head) and the prediction chain (prediction
     // common -> value / policy heads) both start from the next latent: one step per layer pair.
@@ -1483,8 +1491,8 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-          T2[r * kRHid + cD] = fmaxf(z2[r] + BD[2 * kRHid + cD], 0.0f);
-          U2[r * kRHid + cD] = fmaxf(z6[r] + BD[4 * kRHid + cD], 0.0f);
+          T2[r * kRRow + rpad(cD)] = fmaxf(z2[r] + BD[2 * kRHid + cD], 0.0f);
+          U2[r * kRRow + rpad(cD)] = fmaxf(z6[r] + BD[4 * kRHid + cD], 0.0f);
         }
       }
     }
@@ -1512,8 +1520,8 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
-          T3[r * kRHid + cD] = fmaxf(z3[r] + BD[3 * kRHid + cD], 0.0f);
-          U3[r * kRHid + cD] = fmaxf(z7[r] + BD[5 * kRHid + cD], 0.0f);
+          T3[r * kRRow + rpad(cD)] = fmaxf(z3[r] + BD[3 * kRHid + cD], 0.0f);
+          U3[r * kRRow + rpad(cD)] = fmaxf(z7[r] + BD[5 * kRHid + cD], 0.0f);
         }
       }
     }
@@ -1522,8 +1530,10 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // ---- [reward head hidden | (value | policy) head hidden]
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-      float h = dot4<kRSlotsRH>(reinterpret_cast<const float4 *>(T3 + r * kRHid) + 4 * pRH, [&](int j) { return wRH[j]; });
-      float u = dot4<kRSlotsVPH>(reinterpret_cast<const float4 *>(U3 + r * kRHid) + 8 * pVP, [&](int j) { return wVPH[j]; });
+      float h = dot4<kRSlotsRH>(reinterpret_cast<const float4 *>(T3 + r * kRRow) + 4 * pRH + (pRH >= 4),
+                                [&](int j) { return wRH[j]; });
+      float u = dot4<kRSlotsVPH>(reinterpret_cast<const float4 *>(U3 + r * kRRow) + 8 * pVP + (pVP >= 2),
+                                 [&](int j) { return wVPH[j]; });
       h += dpp_f<0xB1>(h);
       u += dpp_f<0xB1>(u);
       h += dpp_f<0x4E>(h);
@@ -1577,7 +1587,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // file the next latent (mcts_ctree.py:305): pool[k + 1][i], by wave 1 (wave 0 expands)
     if (tid >= 64 && tid < 64 + kRHid / 4)
       reinterpret_cast<float4 *>(p.pool + ((size_t)(k + 1) * B + i) * kRHid)[tid - 64] =
-          reinterpret_cast<const float4 *>(NLb + row * kRHid)[tid - 64];
+          reinterpret_cast<const float4 *>(NLb + row * kRRow)[(tid - 64) + (tid - 64 >= kRHid / 8)];
     if (p.rec_x && tid == 0) {
       p.rec_x[(size_t)k * B + i] = s_x;
       p.rec_a[(size_t)k * B + i] = s_act;
