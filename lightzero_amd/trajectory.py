@@ -87,6 +87,8 @@ def all_gather_packed(packed: torch.Tensor, index: torch.Tensor, group=None):
     Returns host numpy [(packed_r, index_r)] for every rank r."""
     world = dist.get_world_size(group)
     dev = packed.device
+    if dev.type == "cuda" and dist.get_backend(group) == "gloo":
+        dev = torch.device("cpu")  # gloo all-gathers host tensors only (RCCL groups keep them on the GPU)
     W = packed.shape[1]
     sizes = torch.tensor([packed.shape[0], index.shape[0]], dtype=torch.int64, device=dev)
     all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
@@ -95,7 +97,7 @@ def all_gather_packed(packed: torch.Tensor, index: torch.Tensor, group=None):
     max_rows = max(1, max(s[0] for s in all_sizes))
     max_eps = max(1, max(s[1] for s in all_sizes))
     pay = torch.zeros((max_rows, W), dtype=torch.float32, device=dev)
-    pay[:packed.shape[0]] = packed
+    pay[:packed.shape[0]] = packed.to(dev)
     idx = torch.zeros((max_eps, 3), dtype=torch.int64, device=dev)
     idx[:index.shape[0]] = index.to(dev)
     pays = [torch.empty_like(pay) for _ in range(world)]
@@ -108,6 +110,8 @@ def all_gather_packed(packed: torch.Tensor, index: torch.Tensor, group=None):
 def allreduce_stats(collected_step: float, collected_episode: float, collected_duration: float, device,
                     group=None):
     """muzero_collector.py:709-712: sum the three collector statistics over ranks."""
+    if torch.device(device).type == "cuda" and dist.get_backend(group) == "gloo":
+        device = "cpu"
     t = torch.tensor([collected_step, collected_episode, collected_duration], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
     return tuple(float(v) for v in t.cpu().tolist())

@@ -1,0 +1,38 @@
+"""Worker of tests/test_gpu_dist.py: one rank of an env-sharded device collect on cuda:0 (the one
+GPU of the test box; every rank shares it), trajectories all-gathered over a gloo group. Reads
+RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT from the environment, writes out_<rank>.npz."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from lightzero_amd.collector import DeviceCollector  # noqa: E402
+
+
+def main():
+    out_dir = sys.argv[1]
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dev = torch.device("cuda", 0)
+        model = bench.build_model(dev, False, seed=0)
+        col = DeviceCollector(model, 16, 8, device=dev, seed=bench.shard_seed(rank), graph=True, poll_every=4,
+                              episode_slots=16)
+        col.collect(n_episode=4)  # warm-up collect (all-gathered too)
+        eps_all, st_all = col.collect(n_episode=4, group=None)
+        ranks = np.array([e["rank"] for e in eps_all], np.int64)
+        lens = np.array([len(e["action_segment"]) for e in eps_all], np.int64)
+        own = np.array([len(e["action_segment"]) for e in eps_all if e["rank"] == rank], np.int64)
+        np.savez(os.path.join(out_dir, f"out_{rank}.npz"), ranks=ranks, lens=lens, own=own,
+                 envstep=st_all["envstep"], total_envstep=st_all["total_envstep"],
+                 total_episodes=st_all["total_episodes"], world=st_all["world"])
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
