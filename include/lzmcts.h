@@ -348,6 +348,28 @@ int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_
                     int Vv, int categorical, int32_t *rec_x, int32_t *rec_a, int32_t *rec_len, float *rec_decoded,
                     float *rec_logits, void *stream);
 
+/* The whole EfficientZeroMCTSCtree.search (mcts_ctree.py:696-827) for the conv EfficientZeroModel in ONE
+ * launch (EZ trees): lzm_search_conv's per-root flow with the value-prefix tree (ctree_efficientzero
+ * cnode.cpp:173-212, :482-575, :756-814) plus the reward LSTM step (efficientzero_model.py:526-574) as
+ * lzm_ez_lstm_step's split-K tiles spread over the same grid: each root publishes its LSTM input row
+ * [reward planes | hpool[x][b]] with its search_len, the tiles run the gate GEMM + cell for 64 rows x 16
+ * units and hand the h1 rows back; c state filed into cpool[k + 1] and h state into hpool[k + 1],
+ * zeroed where search_len % horizon == 0 (mcts_ctree.py:810-813). hpool / cpool [S + 1][B][H] (slot 0
+ * = the roots' reward_hidden_state), lstm_frag = lzm_ez_lstm_prepare(W [4H][r_ch * 64 + H]),
+ * lstm_bias [4H] = b_ih + b_hh, vp_s / vp_t the value-prefix BatchNorm as an affine map; heads as
+ * lzm_search_conv with the reward head reading relu(h1 * vp_s + vp_t) (K = H). rec_reset (nullable)
+ * is_reset int32 [S][B]. Same results as the generic path (traverse, lzm_conv_trunk_xin_p,
+ * lzm_ez_lstm_step, lzm_conv_heads, lzm_decode_backprop) bit for bit. Requires max(B, 2 T) <= the
+ * device's CU count, T = ceil(B / 64) * H / 16 (the grid is co-resident). */
+int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount,
+                       float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, float *hpool,
+                       float *cpool, int H, int horizon, const float *trunk_w, const float *actmap, int n_dres,
+                       int n_pres, int r_ch, int h_ch, const float *lstm_frag, const float *lstm_bias,
+                       const float *vp_s, const float *vp_t, const float *w1t, const float *b1, const float *w2q,
+                       const float *b2, int Khd, int off_policy, int Vr, int Vv, int categorical, int32_t *rec_x,
+                       int32_t *rec_a, int32_t *rec_len, float *rec_decoded, float *rec_logits, int32_t *rec_reset,
+                       void *stream);
+
 /* lzm_decode_backprop of simulation `cur` fused with lzm_traverse of the next simulation (parity /
  * glibc mode only): one launch in which the wave that backs up root i then walks root i again
  * (same requests, draws and outputs as the two separate calls). Replaces the pair

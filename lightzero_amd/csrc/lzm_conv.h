@@ -450,7 +450,8 @@ __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out
 }
 
 // 1x1 layer (<= 32 out channels, waves 0 and 1): relu(conv + b) -> global [c][p]
-template <int DIAG>
+// (SC1: 16-B sc1 buffer stores, for planes another CU reads in the same launch)
+template <int DIAG, bool SC1 = false>
 __device__ __forceinline__ void bx_conv1_layer(const uint16_t *in, const float *__restrict__ wl,
                                                const float *__restrict__ bias, int nch, float *dst, int lane,
                                                int wv) {
@@ -469,7 +470,14 @@ __device__ __forceinline__ void bx_conv1_layer(const uint16_t *in, const float *
     v.y = fmaxf(acc[t][1] + bc, 0.f);
     v.z = fmaxf(acc[t][2] + bc, 0.f);
     v.w = fmaxf(acc[t][3] + bc, 0.f);
-    *reinterpret_cast<float4 *>(dst + c * kCvPix + 16 * t + 4 * (lane >> 4)) = v;
+    if constexpr (SC1) {
+      typedef unsigned u4v __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, nch * kCvPix * 4, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, (c * kCvPix + 16 * t + 4 * (lane >> 4)) * 4,
+                                             0, 16);
+    } else {
+      *reinterpret_cast<float4 *>(dst + c * kCvPix + 16 * t + 4 * (lane >> 4)) = v;
+    }
   }
 }
 

@@ -723,6 +723,9 @@ struct lzm_handle {
   const int32_t *ext_norm = nullptr;       // lzm_set_norm_words: verdict words written by lzm_conv_heads
   const int32_t *reuse_action = nullptr;   // lzm_set_reuse: search-with-reuse inputs (device, [B])
   const float *reuse_value = nullptr;
+  // lzm_search_conv_ez's hand-off workspace (LSTM input rows, outputs, split-K partials, flags)
+  void *ez_ws = nullptr;
+  size_t ez_ws_bytes = 0;
 };
 
 // Jump matrices of glibc random_r: row m of J_first expresses z[344+m] (the m-th rand()
@@ -887,6 +890,7 @@ int lzm_destroy(lzm_handle *h) {
   dfree(h->legal); dfree(h->nlegal); dfree(h->pathlen); dfree(h->off); dfree(h->diag); dfree(h->err);
   dfree(h->hint); dfree(h->norm_flag); dfree(h->jmat);
   dfree(h->coef); dfree(h->pow16807); dfree(h->lb_flags); dfree(h->epoch); dfree(h->search_diag); dfree(h->phase);
+  dfree(h->ez_ws);
   delete h;
   return LZM_OK;
 }
@@ -2492,6 +2496,141 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(fn, dim3(h->B), dim3(kScThreads), lds, (hipStream_t)stream, p);
+    e = hipGetLastError();
+  }
+  LZM_HIP(e);
+  return LZM_OK;
+}
+
+// Whole-search launch for the conv EfficientZero networks (lzm_search_conv.h, EZ instantiation): the
+// MuZero launch's flow plus the reward LSTM as split-K tiles spread over the grid (G = max(B, 2 T)
+// workgroups, one per CU, co-resident: the tiles wait on the roots' LSTM input rows and the roots on
+// their rows' tiles inside the launch).
+extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount,
+                                  float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool,
+                                  float *hpool, float *cpool, int H, int horizon, const float *trunk_w,
+                                  const float *actmap, int n_dres, int n_pres, int r_ch, int h_ch,
+                                  const float *lstm_frag, const float *lstm_bias, const float *vp_s, const float *vp_t,
+                                  const float *w1t, const float *b1, const float *w2q, const float *b2, int Khd,
+                                  int off_policy, int Vr, int Vv, int categorical, int32_t *rec_x, int32_t *rec_a,
+                                  int32_t *rec_len, float *rec_decoded, float *rec_logits, int32_t *rec_reset,
+                                  void *stream) {
+  const int S = num_simulations;
+  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !hpool || !cpool || !trunk_w || !actmap || !lstm_frag ||
+      !lstm_bias || !vp_s || !vp_t || !w1t || !b1 || !w2q || !b2 || S <= 0) {
+    set_err("lzm_search_conv_ez: null argument or no simulations");
+    return LZM_ERR_ARG;
+  }
+  if (!(h->flags & LZM_TREE_EZ)) {
+    set_err("lzm_search_conv_ez: EfficientZero trees only");
+    return LZM_ERR_ARG;
+  }
+  const int Kx = r_ch * 64 + H;
+  if (n_dres < 0 || n_pres < 0 || r_ch <= 0 || r_ch > 32 || h_ch <= 0 || h_ch > 32 || Khd != h_ch * 64 ||
+      off_policy <= 0 || off_policy >= Khd || off_policy > kHdKMax || Khd - off_policy > kHdKMax || (off_policy % 128) ||
+      (Khd % 128) || H <= 0 || H % kLsUnits || H % 128 || H > kHdKMax || H / kLsUnits > 64 || Kx % (2 * kLsKc) ||
+      horizon <= 0 || Vr <= 0 || Vv <= 0 || Vr > 1024 || Vv > 1024 || (!categorical && (Vr != 1 || Vv != 1)) ||
+      S + 1 > 0xffff ||
+      (((uintptr_t)trunk_w | (uintptr_t)actmap | (uintptr_t)w1t | (uintptr_t)w2q | (uintptr_t)latent_pool |
+        (uintptr_t)hpool | (uintptr_t)cpool | (uintptr_t)lstm_frag | (uintptr_t)vp_s | (uintptr_t)vp_t) & 15)) {
+    set_err("lzm_search_conv_ez: unsupported network shape (64x8x8 latent, <= 32 reward / head planes, K per head a "
+            "multiple of 128 and <= 1024, LSTM width a multiple of 128, (r_ch * 64 + H) % 128 == 0, horizon > 0, "
+            "16-B aligned weights and pools)");
+    return LZM_ERR_ARG;
+  }
+  if (S > h->sims_cap) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: %d simulations > reserved %d (lzm_reserve)", S, h->sims_cap);
+    return LZM_ERR_CAPACITY;
+  }
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int B = h->B, nmb = (B + kLsRows - 1) / kLsRows, T = nmb * (H / kLsUnits), G = std::max(B, 2 * T);
+  if (B > 256 || G > cus) {
+    snprintf(g_err, sizeof(g_err),
+             "lzm_search_conv_ez: %d workgroups (%d roots, %d LSTM tiles x 2) > min(%d CUs) or B > 256 (the grid is "
+             "co-resident)", G, B, T, cus);
+    return LZM_ERR_ARG;
+  }
+  int rc = fill_lut(h, pb_c_base, pb_c_init);
+  if (rc != LZM_OK) return rc;
+  const bool fast = (h->flags & LZM_RNG_FAST) != 0;
+  if (!fast) {
+    rc = ensure_coef(h, B * (S + 1) + 64);
+    if (rc != LZM_OK) return rc;
+  }
+  rc = ensure_flags(h, S, B);
+  if (rc != LZM_OK) return rc;
+  // hand-off workspace, grown on demand (flags zeroed: epoch 0 never matches)
+  const size_t f_xin = round4((size_t)B * Kx), f_h1 = round4((size_t)B * H), f_part = (size_t)T * kLpThreads * 16;
+  const size_t flag_words = (size_t)S * B + 2 * (size_t)S * T;
+  const size_t need = (f_xin + f_h1 + f_part) * sizeof(float) + flag_words * sizeof(unsigned long long);
+  if (h->ez_ws_bytes < need) {
+    dfree(h->ez_ws);
+    h->ez_ws = nullptr;
+    h->ez_ws_bytes = 0;
+    LZM_HIP(hipMalloc(&h->ez_ws, need));
+    LZM_HIP(hipMemset(h->ez_ws, 0, need));
+    h->ez_ws_bytes = need;
+  }
+  float *wsf = reinterpret_cast<float *>(h->ez_ws);
+  unsigned long long *wsl = reinterpret_cast<unsigned long long *>(wsf + f_xin + f_h1 + f_part);
+  ConvSearchArgs p;
+  memset(&p, 0, sizeof(p));
+  p.stat = h->stat; p.meta = h->meta; p.legal = h->legal; p.nlegal = h->nlegal;
+  p.path = h->path; p.path_act = h->path_act; p.pathlen = h->pathlen; p.lut = h->lut;
+  p.B = B; p.A = h->A; p.cap = h->cap; p.lut_n = h->lut_n; p.depth_cap = h->depth_cap;
+  p.S = S; p.disc = discount; p.seeds = seeds; p.vtp_in = vtp_in; p.minmax = (float4 *)minmax; p.pool = latent_pool;
+  p.w = trunk_w; p.actmap = actmap; p.n_dres = n_dres; p.n_pres = n_pres; p.r_ch = r_ch; p.h_ch = h_ch;
+  p.w1t = w1t; p.b1 = b1; p.w2q = w2q; p.b2 = b2; p.Kr = H; p.Khd = Khd; p.off_policy = off_policy;
+  p.Vr = Vr; p.Vv = Vv; p.categorical = categorical ? 1 : 0;
+  p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
+  p.flags = h->lb_flags; p.epoch = h->epoch; p.err = h->err; p.sdiag = h->search_diag; p.fast = fast ? 1 : 0;
+  p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
+  p.rec_reset = rec_reset;
+  p.xin = wsf; p.h1g = wsf + f_xin; p.kpart = wsf + f_xin + f_h1;
+  p.xflags = wsl; p.tflags = wsl + (size_t)S * B; p.pflags = wsl + (size_t)S * B + (size_t)S * T;
+  p.Kx = Kx; p.H = H; p.horizon = horizon; p.hpool = hpool; p.cpool = cpool;
+  p.lwf = reinterpret_cast<const uint4 *>(lstm_frag); p.lbias = lstm_bias; p.vp_s = vp_s; p.vp_t = vp_t;
+  p.nmb = nmb; p.T = T;
+  // dynamic LDS plan (float offsets, 16-B aligned): the activation buffers / LSTM stage buffers first
+  size_t o = std::max((size_t)2 * kBxBuf / 2, (size_t)kLsLdsBytes / 4);
+  p.off_stat = (int)o; o += (size_t)h->cap * 4;
+  p.off_meta = (int)o; o += (size_t)h->cap * 4;
+  p.off_val = (int)o; o += round4((size_t)h->cap);
+  p.off_lut = (int)o; o += round4((size_t)2 * h->lut_n);
+  p.off_legal = (int)o; o += round4((size_t)h->A + 1);
+  p.off_path = (int)o; o += round4((size_t)h->depth_cap);
+  p.off_pact = (int)o; o += round4((size_t)h->depth_cap);
+  p.pbt_rows = ((size_t)h->lut_n * (h->lut_n + 1) / 2 <= 4096) ? h->lut_n : 0;
+  p.off_pbt = (int)o; o += round4((size_t)p.pbt_rows * (p.pbt_rows + 1) / 2);
+  p.off_r = (int)o; o += round4((size_t)H);
+  p.off_hd = (int)o; o += round4((size_t)Khd);
+  p.off_hid = (int)o; o += 96;
+  p.off_part = (int)o; o += 2 * kHdParts * 32;
+  p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
+  p.off_seed = (int)o; o += round4((size_t)S + 32);
+  const size_t lds = o * sizeof(float);
+  if (lds > kMaxLds) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: %zu B of LDS needed (tree too large: lower num_simulations)",
+             lds);
+    return LZM_ERR_ARG;
+  }
+  const bool stamps = getenv("LZM_PHASE_TIMING") && atoi(getenv("LZM_PHASE_TIMING")) > 0;
+  if (stamps && !h->phase) {
+    LZM_HIP(hipMalloc(&h->phase, (64 + 1024) * sizeof(unsigned long long)));
+    LZM_HIP(hipMemset(h->phase, 0, (64 + 1024) * sizeof(unsigned long long)));
+  }
+  p.stamps = stamps ? h->phase : nullptr;
+  auto fn = stamps ? (fast ? search_conv_ez_kernel<kBxAhead, true, true> : search_conv_ez_kernel<kBxAhead, false, true>)
+                   : (fast ? search_conv_ez_kernel<kBxAhead, true> : search_conv_ez_kernel<kBxAhead, false>);
+  hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(fn, dim3(G), dim3(kScThreads), lds, (hipStream_t)stream, p);
     e = hipGetLastError();
   }
   LZM_HIP(e);

@@ -365,4 +365,133 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
   stamp(4);
 }
 
+// ---- one gate-GEMM + cell tile inside a persistent launch (the EfficientZero one-launch search,
+// lzm_search_conv.h): 256 threads, same tile (64 rows x 16 hidden units, K split in two halves over
+// two workgroups), same operand layouts, stage pipeline and MFMA order as ez_lstm_gemm_cell_kernel,
+// so every output bit is the same. Wave w owns column tile w and all four 16-row tiles (the 512-thread
+// kernel gives each wave two); the staging thread map changes with the thread count (thread -> row
+// tid / 4, two 16-B K chunks), the LDS layout does not. The xin rows are read with sc1 loads (they were
+// handed over by other workgroups, MI355X_MICROARCH.md's first hand-off row).
+typedef unsigned lp_u4 __attribute__((ext_vector_type(4)));
+typedef float lp_f4 __attribute__((ext_vector_type(4)));
+constexpr int kLpThreads = 256;
+
+struct LpTile {
+  int row0, nb, kh;  // tile rows [row0, row0 + 64), hidden units [16 nb, 16 nb + 16), K half
+};
+
+// the GEMM part: acc[t] = the tile's K-half partial sums (row tile t = rows 16 t .. + 15 of the tile,
+// this wave's 16 gate columns), accumulated from zero exactly as the 512-thread kernel does.
+// lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4).
+__device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, const __amdgpu_buffer_rsrc_t xr,
+                                             const uint4 *wf, uint16_t *lds, bxf4 (&acc)[4]) {
+  const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6;
+  const int nch = K / 32, kspan = K / 2, nst = kspan / kLsKc, k0 = tl.kh * kspan;
+  const int sr = tid >> 2, sq = tid & 3;
+  const bool srow = tl.row0 + sr < B;
+  const int abyte = ((tl.row0 + (srow ? sr : 0)) * K + k0 + 16 * sq) * 4;
+  const lp_u4 *bsrc4 = reinterpret_cast<const lp_u4 *>(wf + (size_t)tl.nb * 4 * nch * 3 * 64);
+  lp_f4 va0[4], va1[4];
+  lp_u4 vb0[6], vb1[6];
+  auto load_stage = [&](int s, lp_f4(&VA)[4], lp_u4(&VB)[6]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      VA[u] = srow ? __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(xr, abyte + (s * kLsKc + 4 * u) * 4, 0, 16))
+                   : lp_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int e = tid + kLpThreads * u, c = e / 768, r = e - c * 768, tc = r / 192, rest = r - tc * 192;
+      const int j = (k0 / 32) + 2 * s + c;
+      VB[u] = bsrc4[((size_t)tc * nch + j) * 192 + rest];
+    }
+  };
+  auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const lp_u4(&VB)[6]) __attribute__((always_inline)) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    uint16_t *abuf = lds + bsel * kLsStage;
+#pragma unroll
+    for (int hc = 0; hc < 2; ++hc) {  // the thread's two 16-B chunks: K 16 sq + 8 hc .. + 7
+      uint32_t h[4], m[4], l[4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const lp_f4 x = VA[2 * hc + u];
+        const f2 pr[2] = {f2{x[0], x[1]}, f2{x[2], x[3]}};
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const b2 hh = __builtin_convertvector(pr[v], b2);
+          const f2 r1 = pr[v] - __builtin_convertvector(hh, f2);
+          const b2 mm = __builtin_convertvector(r1, b2);
+          const b2 ll = __builtin_convertvector(r1 - __builtin_convertvector(mm, f2), b2);
+          h[2 * u + v] = __builtin_bit_cast(uint32_t, hh);
+          m[2 * u + v] = __builtin_bit_cast(uint32_t, mm);
+          l[2 * u + v] = __builtin_bit_cast(uint32_t, ll);
+        }
+      }
+      const int chunk = 2 * sq + hc;
+      uint16_t *base = abuf + sr * kLsKc + ((chunk ^ (sr & 7)) & 7) * 8;
+      *reinterpret_cast<uint4 *>(base) = uint4{h[0], h[1], h[2], h[3]};
+      *reinterpret_cast<uint4 *>(base + kLsPlane) = uint4{m[0], m[1], m[2], m[3]};
+      *reinterpret_cast<uint4 *>(base + 2 * kLsPlane) = uint4{l[0], l[1], l[2], l[3]};
+    }
+    lp_u4 *bbuf = reinterpret_cast<lp_u4 *>(abuf + kLsABuf);
+#pragma unroll
+    for (int u = 0; u < 6; ++u) bbuf[tid + kLpThreads * u] = VB[u];
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  load_stage(0, va0, vb0);
+  if (nst > 1) load_stage(1, va1, vb1);
+  store_stage(0, va0, vb0);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = bxf4{0.f, 0.f, 0.f, 0.f};
+  const int ar = lane & 15, ag = lane >> 4;
+  auto stage = [&](int s, auto par) __attribute__((always_inline)) {
+    constexpr int PAR = decltype(par)::value;
+    __syncthreads();
+    if (s + 2 < nst) {
+      if constexpr (PAR == 0)
+        load_stage(s + 2, va0, vb0);
+      else
+        load_stage(s + 2, va1, vb1);
+    }
+    const uint16_t *abuf = lds + PAR * kLsStage;
+    const uint4 *bbuf = reinterpret_cast<const uint4 *>(abuf + kLsABuf);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint4 a[4][3], w[3];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int r = 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
+#pragma unroll
+        for (int tm = 0; tm < 3; ++tm) a[t][tm] = *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 3; ++tm) w[tm] = bbuf[((c * 4 + ct) * 3 + tm) * 64 + lane];
+      // small terms first: l.h, h.l, m.m, m.h, h.m, h.h (ez_lstm_gemm_cell_kernel's order)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[2]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[1]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[0]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[1]), acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
+    }
+    if (s + 1 < nst) {
+      if constexpr (PAR == 0)
+        store_stage(1, va1, vb1);
+      else
+        store_stage(0, va0, vb0);
+    }
+  };
+  for (int s = 0; s < nst; s += 2) {
+    stage(s, I0());
+    if (s + 1 < nst) stage(s + 1, I1());
+  }
+}
+
 }  // namespace lzm

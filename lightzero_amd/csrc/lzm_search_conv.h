@@ -32,6 +32,7 @@
 
 #include "lzm_conv.h"
 #include "lzm_heads.h"
+#include "lzm_lstm.h"
 #include "lzm_search_mlp.h"
 #include "lzm_tree.h"
 
@@ -71,6 +72,18 @@ struct ConvSearchArgs {
   // optional per-simulation record
   int32_t *rec_x, *rec_a, *rec_len;
   float *rec_dec, *rec_logits;
+  int32_t *rec_reset;  // EfficientZero: is_reset [S][B]
+  // EfficientZero (search_conv_ez_kernel): the reward LSTM of the recurrent step (lzm_lstm.h)
+  float *xin;             // [B][Kx] LSTM input rows [reward planes | leaf hidden state] (sc1 hand-off)
+  int Kx, H, horizon;     // Kx = r_ch * 64 + H; lstm_horizon_len
+  float *hpool, *cpool;   // [S + 1][B][H] state pools (slot 0 = the roots' state)
+  const uint4 *lwf;       // gate weight fragments (lzm_ez_lstm_prepare)
+  const float *lbias;     // [4H] b_ih + b_hh
+  const float *vp_s, *vp_t;  // value-prefix BatchNorm as an affine map (relu(h1 * s + t) feeds the head)
+  float *h1g;             // [B][H] unmasked LSTM outputs (sc1 hand-off, tile -> root)
+  float *kpart;           // [T][kLpThreads * 16] split-K partial sums (sc1 hand-off, upper -> lower half)
+  unsigned long long *xflags, *tflags, *pflags;  // [S][B], [S][T], [S][T] {epoch, payload} words
+  int nmb, T;             // row blocks of 64, tiles (nmb * H / 16)
   unsigned long long *stamps;  // STAMPS instantiation only
   // dynamic LDS plan: float offsets (the two activation buffers come first)
   int off_stat, off_meta, off_val, off_lut, off_legal, off_path, off_pact, off_pbt, off_r, off_hd, off_hid, off_part,
@@ -204,6 +217,73 @@ __device__ __forceinline__ float sc_decode_row(const float *row, int V, float *r
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
   return acc;
+}
+
+// Output columns [jlo, jhi) of the three head layers (w2q [8][N2][4]: float4 k4 of column j at
+// (k4 * N2 + j), so a wave-instruction reads 64 consecutive columns' float4s, 1 KiB contiguous), up to
+// three columns per thread per round with every load of the round in flight; the FMA order of
+// conv_heads_kernel (k = 0 .. 31 from zero, then + bias). Columns are independent, so any split of
+// [0, N2) into ranges gives the same bits.
+__device__ __forceinline__ void sc_head_out(const ConvSearchArgs &p, const float *lhid, float *llg, int N2, int jlo,
+                                            int jhi, int tid) {
+  for (int j0 = jlo; j0 < jhi; j0 += 3 * kScThreads) {
+    float4 w2[3][8];
+    float b2[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int j = min(j0 + u * kScThreads + tid, jhi - 1);
+      const float4 *wc = reinterpret_cast<const float4 *>(p.w2q) + j;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) w2[u][q] = wc[(size_t)q * N2];
+      b2[u] = p.b2[j];
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int j = j0 + u * kScThreads + tid;
+      const float *hid = lhid + 32 * (j < p.Vr ? 0 : (j < p.Vr + p.Vv ? 1 : 2));
+      float acc = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float4 h4 = *reinterpret_cast<const float4 *>(hid + 4 * q);
+        acc = __fmaf_rn(h4.x, w2[u][q].x, acc);
+        acc = __fmaf_rn(h4.y, w2[u][q].y, acc);
+        acc = __fmaf_rn(h4.z, w2[u][q].z, acc);
+        acc = __fmaf_rn(h4.w, w2[u][q].w, acc);
+      }
+      if (j < jhi) llg[j] = acc + b2[u];
+    }
+  }
+}
+
+// ensure_softmax + InverseScalarTransform of one decoded head by one wave (wave_support_expectation's
+// arithmetic); returns h^-1 of the expectation (categorical) or of the raw value
+__device__ __forceinline__ float sc_decode(const ConvSearchArgs &p, const float *row, int V) {
+  float e;
+  if (p.categorical) {
+    float sm;
+    e = V <= 640 ? sc_decode_row<10>(row, V, &sm) : sc_decode_row<16>(row, V, &sm);
+    if ((threadIdx.x & 63) == 0 && fabsf(sm - 1.0f) <= 1e-5f + 1e-5f) atomicAdd(p.sdiag, 1);  // verdict undecidable
+  } else {
+    e = row[0];
+  }
+  return h_inverse(e);
+}
+
+// bounded spin of one lane on a 64-bit {epoch, payload} word (sc1 loads); returns the word (err[0]
+// counts timeouts, the payload then reads 0)
+__device__ __forceinline__ unsigned long long sc_wait_word(const unsigned long long *w, unsigned long long epoch,
+                                                           int32_t *err) {
+  unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  long long spins = 0;
+  while ((v >> 32) != epoch) {
+    if (++spins > (1ll << 22)) {
+      atomicAdd(err, 1);
+      return epoch << 32;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return v;
 }
 
 template <int AHEAD, bool FAST, bool STAMPS = false>
@@ -502,6 +582,471 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   if (tid == 0) {
     p.minmax[b] = s_mm[0];
     p.pathlen[b] = s_len[0];
+    // the last workgroup advances the epoch (no release fence: the kernel boundary orders the
+    // write-back for every later reader)
+    const uint32_t done = atomicAdd(p.epoch + 1, 1u);
+    if (done == (uint32_t)gridDim.x - 1) {
+      p.epoch[1] = 0;
+      __hip_atomic_store(p.epoch, (uint32_t)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+
+// The EfficientZero one-launch search (lzm_search_conv_ez). The grid is G = max(B, 2 T)
+// workgroups; workgroup g owns root g (g < B) and K half (g & 1 or the XCD map below) of LSTM tile
+// q(g) (g < 2 T). Per simulation, on top of the MuZero flow:
+//   - the trunk writes root b's LSTM input row xin[b] = [reward planes | hpool[x][b]] with sc1 stores
+//     and publishes {epoch, x, search_len} in xflags[k][b] (every storing wave's vmcnt(0), a barrier,
+//     one agent-scope flag store: MI355X_MICROARCH.md's first hand-off row);
+//   - the value / policy heads run while the other roots finish their trunks;
+//   - the tile waits for its 64 rows' flags, runs the split-bf16 gate GEMM over its K half
+//     (lp_tile_gemm, ez_lstm_gemm_cell_kernel's arithmetic), the upper half hands its partial sums to
+//     the lower (pflags), which adds them, runs the cell with c0 = cpool[x][b] and files the masked c
+//     state (its own slots: the tile map is fixed, so only this workgroup ever reads them), and hands
+//     the unmasked h1 rows over (h1g, tflags);
+//   - the root waits for its row's NB tiles, files the masked h state into hpool[k + 1][b] (read back
+//     only by itself), and runs the value-prefix head on relu(BN(h1)), the decode, expand (is_reset =
+//     search_len % horizon == 0) and the EfficientZero backup.
+// Waits are only on events of the same simulation that precede the wait in every workgroup's
+// program order, and every workgroup is resident (G <= CUs, one per CU), so the grid cannot deadlock;
+// each spin is bounded and counted (err[0]).
+template <int AHEAD, bool FAST, bool STAMPS = false>
+__global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void search_conv_ez_kernel(
+    ConvSearchArgs p) {
+  extern __shared__ uint4 sc_lds4[];
+  uint16_t *act = reinterpret_cast<uint16_t *>(sc_lds4);
+  float *smem = reinterpret_cast<float *>(sc_lds4);
+  auto buf = [&](int i) { return act + i * kBxBuf; };
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int c = 16 * wv + (lane & 15);
+  const int B = p.B, A = p.A, S = p.S;
+  const bool has_root = b < B;
+  __shared__ uint32_t s_z0[31];
+  __shared__ int s_players, s_epoch, s_x, s_act, s_vtp0, s_leafvtp, s_late, s_tlevel;
+  __shared__ unsigned long long s_tmask;
+  __shared__ int s_len[1];
+  __shared__ float4 s_mm[1];
+  __shared__ float s_dec[2];
+  // STAMPS: [0] walk, [1] trunk input, [2] trunk layers, [3] value / policy hidden, [4] their outputs +
+  // value decode, [5] LSTM tile, [6] value-prefix head, [7] expand + backup, [8] late look-back, [9] kernel,
+  // [10] wait for the tile's rows, [11] wait for the upper K half, [12] wait for the row's tiles, [13] gate GEMM
+  unsigned long long st_prev = 0, st_acc[14] = {};
+  auto st_now = [&]() { return STAMPS ? __builtin_amdgcn_s_memtime() : 0ull; };
+  const unsigned long long st_begin = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto stamp = [&](int n) {
+    if (STAMPS && tid == 0) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      st_acc[n] += now - st_prev;
+      st_prev = now;
+    }
+  };
+
+  // ---- stage root b's tree slice, the pUCT tables, seeds; zero the activation borders
+  TreeView t;
+  t.A = A; t.cap = p.cap; t.lut_n = p.lut_n; t.depth_cap = p.depth_cap; t.B = 1;
+  NodeStat *ls = reinterpret_cast<NodeStat *>(smem + p.off_stat);
+  NodeMeta *lm = reinterpret_cast<NodeMeta *>(smem + p.off_meta);
+  float *lval = smem + p.off_val;
+  float2 *llut = reinterpret_cast<float2 *>(smem + p.off_lut);
+  int32_t *llegal = reinterpret_cast<int32_t *>(smem + p.off_legal);
+  if (has_root) {
+    for (int e = tid; e < p.cap; e += kScThreads) {
+      const NodeStat s = p.stat[(size_t)e * B + b];
+      ls[e] = s;
+      lm[e] = p.meta[(size_t)e * B + b];
+      lval[e] = node_value(s);
+    }
+    for (int e = tid; e < p.lut_n; e += kScThreads) llut[e] = p.lut[e];
+    for (int e = tid; e < A; e += kScThreads) llegal[e] = p.legal[(size_t)b * A + e];
+    if (tid == 0) llegal[A] = p.nlegal[b];
+  }
+  float *lpbt = smem + p.off_pbt;
+  if (has_root) build_pbt(p.lut, p.pbt_rows, lpbt, tid, kScThreads);
+  t.stat = ls; t.meta = lm; t.val = lval; t.lut = llut; t.legal = llegal; t.nlegal = llegal + A;
+  t.pbt = p.pbt_rows ? lpbt : nullptr;
+  t.path = reinterpret_cast<int32_t *>(smem + p.off_path);
+  t.path_act = reinterpret_cast<int32_t *>(smem + p.off_pact);
+  t.pathlen = s_len;
+  uint32_t *s_seed = reinterpret_cast<uint32_t *>(smem + p.off_seed);
+  uint32_t *s_pow = s_seed + S;
+  for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
+  if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
+  auto zero_borders = [&]() {
+    for (int k = tid; k < 2 * 3 * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
+      const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
+      const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
+      sc_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
+    }
+  };
+  if (tid == 0) {
+    if (has_root) {
+      s_mm[0] = p.minmax[b];
+      s_vtp0 = p.vtp_in[b];
+    }
+    s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid < 64) {  // players (cnode.cpp:776-781), every load in flight at once
+    int m = INT_MIN;
+    for (int q = tid; q < B; q += 64) m = max(m, p.vtp_in[q]);
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+    if (tid == 0) s_players = (m == -1) ? 1 : 2;
+  }
+  __syncthreads();
+  const int players = s_players;
+  const unsigned long long epoch = (unsigned long long)(uint32_t)s_epoch;
+  float *lr = smem + p.off_r, *lhd = smem + p.off_hd, *lhid = smem + p.off_hid, *lpart = smem + p.off_part;
+  float *llg = smem + p.off_lg;
+  const int N2 = p.Vr + p.Vv + A;
+
+  // EfficientZero: this workgroup's LSTM tile (fixed for the launch)
+  __shared__ int s_rx[64], s_rlen[64];
+  const int T = p.T, NB = p.H / kLsUnits;
+  const bool has_tile = b < 2 * T;
+  int q = 0;
+  LpTile tile{0, 0, 0};
+  {
+    int kh = b & 1;
+    q = b >> 1;
+    if ((T & 7) == 0) {  // XCD-major: whole n-blocks per XCD (block % 8 = XCD), K halves on one XCD
+      const int j = b >> 3;
+      q = (b & 7) * (T >> 3) + (j >> 1);
+      kh = j & 1;
+    }
+    const int nb = q / p.nmb, mb = q - nb * p.nmb;
+    tile = LpTile{kLsRows * mb, nb, kh};
+  }
+  const int Kx = p.Kx, H = p.H;
+  typedef unsigned sc_u4 __attribute__((ext_vector_type(4)));
+
+  // trunk weights: this wave's stream of each 3x3 layer (lzm_conv.h bx layout)
+  const ConvTrunkLayout L = conv_trunk_layout_p(p.n_dres, p.n_pres, 1);
+  const int n3 = 1 + 2 * p.n_dres + 2 * p.n_pres;
+  auto layer_w = [&](int i) { return p.w + bx_layer_off(L, p.n_dres, i); };
+  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * 3 * 64; };
+  BxRing<AHEAD> ring;
+
+  for (int k = 0; k < S; ++k) {
+    if (has_root) {
+      // ---- selection (wave 0; parity mode: draw-free walk, depth flag, look-back only for a value)
+      // the dynamics conv's first weight chunks, in flight during the walk
+      bx_prefetch<18, AHEAD, 0>(ring, wave_stream(p.w + L.dyn), lane);
+      if (!FAST && tid < 31) seed_state_parallel(s_seed[k], s_pow, s_z0);
+      zero_borders();  // (every simulation: the LSTM stages reuse the activation buffers)
+      __syncthreads();
+      if (STAMPS && tid == 0) st_prev = __builtin_amdgcn_s_memtime();
+      if (tid == 0) s_late = 0;
+      if (wv == 0) {
+        const float4 mm = s_mm[0];
+        Descent d;
+        if (FAST) {
+          const uint32_t seed = s_seed[k];
+          auto draw = [seed, b](int level) -> uint32_t {
+            uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)b, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
+            return o.x >> 1;
+          };
+          d = descend_wave<true, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+        } else {
+          TieInfo ti;
+          auto nodraw = [](int) -> uint32_t { return 0u; };
+          d = descend_wave<true, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
+          if (lane == 0 && ti.status != 2)
+            __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+          if (ti.status == 2) {
+            // the depth depends on the draws: look back, walk with them, then publish
+            const int base = sc_lookback(p, k, b, epoch, lane);
+            const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, 0, t.depth_cap, p.err + 1);
+            d = descend_wave<true, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+            if (lane == 0)
+              __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+          } else if (ti.status == 1) {
+            // a tie among unexpanded children: the leaf's parent (the latent to read) and the depth are
+            // known, only the action waits for the draw — resolved after the dynamics conv's MFMAs
+            // (late draw; issuing the flag loads here instead measured even: the wait is for the
+            // predecessors to reach this simulation, not the loads' latency)
+            if (lane == 0) {
+              s_late = 1;
+              s_tlevel = ti.level;
+              s_tmask = ti.mask;
+            }
+          }
+        }
+        if (lane == 0) {
+          s_x = d.x;
+          s_act = d.action;
+          s_len[0] = d.len;
+          s_leafvtp = d.vtp;
+          if (p.rec_x) {
+            p.rec_x[(size_t)k * B + b] = d.x;
+            p.rec_a[(size_t)k * B + b] = d.action;
+            p.rec_len[(size_t)k * B + b] = d.len;
+          }
+        }
+      }
+      __syncthreads();
+      stamp(0);
+      // ---- trunk: the leaf's parent latent pool[x][b] and the action's map (registers; loads in flight
+      // together), then the layers
+      {
+        const bool late = s_late != 0;
+        const float *src = p.pool + ((size_t)max(s_x, 0) * B + b) * (kCvCh * kCvPix);
+        float xres[16];
+        float4 am[4];
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * q4 + 4 * (lane >> 4));
+          xres[4 * q4] = v.x; xres[4 * q4 + 1] = v.y; xres[4 * q4 + 2] = v.z; xres[4 * q4 + 3] = v.w;
+        }
+        if (!late) sc_load_amap(am, p.actmap, s_act, c, lane);
+        {
+          // the LSTM input row's hidden-state part: hpool[x][b] (this workgroup's own earlier writes, or
+          // the roots' state) -> xin[b][r_ch * 64 ..] by sc1 stores
+          if (tid < (H >> 2)) {
+            const float4 v = reinterpret_cast<const float4 *>(p.hpool + ((size_t)max(s_x, 0) * B + b) * H)[tid];
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.xin + (size_t)b * Kx, 0, Kx * 4, 0x00020000);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sc_u4, v), rs, (Kx - H + 4 * tid) * 4, 0, 16);
+          }
+        }
+        {
+          bxf4 in4[4];
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) in4[q4] = bxf4{xres[4 * q4], xres[4 * q4 + 1], xres[4 * q4 + 2], xres[4 * q4 + 3]};
+          const float4 no_am[4] = {};
+          bx_epilogue3<0, 4, false>(in4, buf(0), 0.f, false, no_am, xres, false, false, lane, c);
+        }
+        __syncthreads();
+        stamp(1);
+        for (int i = 0; i < n3; ++i) {
+          const float *w = layer_w(i);
+          const bool second = i > 0 && ((i - 1) & 1);  // a block's second conv: + residual, new block input
+          const float bc = i ? w[kBx3Frag + c] : 0.f;
+          bxf4 acc[4];
+          bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
+          if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
+          if (i == 0 && late) {
+            // late draw: the look-back and the tie's draw, then the action's map for the epilogue
+            if (wv == 0) {
+              const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+              const int base = sc_lookback(p, k, b, epoch, lane);
+              if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;
+              const uint32_t rr = glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
+              unsigned long long m = s_tmask;
+              int kk = (int)(rr % (uint32_t)__popcll(m));
+              for (; kk > 0; --kk) m &= m - 1;
+              const int jsel = __ffsll((long long)m) - 1;
+              const int lvl = s_tlevel;
+              const int parent = t.path[lvl];
+              const int action = legal_at(t, 0, parent, jsel);
+              if (lane == 0) {
+                t.path_act[lvl] = action;
+                t.path[lvl + 1] = 1 + A * t.meta[parent].latent + action;
+                s_act = action;
+                if (p.rec_a) p.rec_a[(size_t)k * B + b] = action;
+              }
+            }
+            __syncthreads();
+            sc_load_amap(am, p.actmap, s_act, c, lane);
+          }
+          bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
+          __syncthreads();
+          if (i == 2 * p.n_dres) {  // the next latent (registers, exact) and the reward planes
+            float *dst = p.pool + ((size_t)(k + 1) * B + b) * (kCvCh * kCvPix) + c * kCvPix + 4 * (lane >> 4);
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4)
+              *reinterpret_cast<float4 *>(dst + 16 * q4) = float4{xres[4 * q4], xres[4 * q4 + 1], xres[4 * q4 + 2], xres[4 * q4 + 3]};
+            if (wv < 2)  // the reward planes: the LSTM input row's first part, sc1
+              bx_conv1_layer<0, true>(buf((i + 1) & 1), p.w + L.rw, p.w + L.rb, p.r_ch, p.xin + (size_t)b * Kx, lane, wv);
+          }
+        }
+      }
+      if (wv < 2) bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, p.h_ch, lhd, lane, wv);
+      // publish the LSTM input row: every storing wave drained, one barrier, one flag store
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(&p.xflags[(size_t)k * B + b],
+                           (epoch << 32) | ((unsigned long long)(max(s_x, 0) & 0xffff) << 16) | (unsigned)(s_len[0] & 0xffff),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      stamp(2);
+      // ---- head MLPs: value and policy now (while the other roots finish their trunks), the value
+      // prefix after the LSTM
+      sc_head_hidden(lhd, p.off_policy, p.w1t, 1, tid < 32 ? p.b1[32 + tid] : 0.0f, lpart, lhid + 32, tid);
+      sc_head_hidden(lhd + p.off_policy, p.Khd - p.off_policy, p.w1t, 2, tid < 32 ? p.b1[64 + tid] : 0.0f, lpart,
+                     lhid + 64, tid);
+      stamp(3);
+      sc_head_out(p, lhid, llg, N2, p.Vr, N2, tid);
+      __syncthreads();
+      if (wv == 1) {
+        const float v = sc_decode(p, llg + p.Vr, p.Vv);
+        if (lane == 0) s_dec[1] = v;
+      }
+      stamp(4);
+    }
+    {
+      // ---- the LSTM tile (gate GEMM over the tile's K half; the lower half runs the cell)
+      if (has_tile) {
+        const unsigned long long w0 = st_now();
+        if (wv == 0) {  // the tile's rows: {x, search_len} from their flags
+          const int row = tile.row0 + lane;
+          unsigned long long v = 0;
+          if (row < B) v = sc_wait_word(&p.xflags[(size_t)k * B + row], epoch, p.err);
+          s_rx[lane] = (int)((v >> 16) & 0xffff);
+          s_rlen[lane] = (int)(v & 0xffff);
+        }
+        __syncthreads();
+        const unsigned long long w1 = st_now();
+        if (STAMPS && tid == 0) st_acc[10] += w1 - w0;
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(p.xin, 0, B * Kx * 4, 0x00020000);
+        bxf4 acc[4];
+        lp_tile_gemm(tile, B, Kx, xr, p.lwf, act, acc);
+        if (STAMPS && tid == 0) st_acc[13] += st_now() - w1;
+        const __amdgpu_buffer_rsrc_t pr =
+            __builtin_amdgcn_make_buffer_rsrc(p.kpart + (size_t)q * (kLpThreads * 16), 0, kLpThreads * 16 * 4, 0x00020000);
+        if (tile.kh == 1) {
+          // upper K half: partial sums to the lower half (sc1 payload, drained, barrier, flag)
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sc_u4, acc[tt]), pr, (tid * 16 + 4 * tt) * 4, 0, 16);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0)
+            __hip_atomic_store(&p.pflags[(size_t)k * T + q], (epoch << 32) | 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          const int gate = lane & 3, ct = wv;
+          const int unit = kLsUnits * tile.nb + 4 * ct + ((lane & 15) >> 2);
+          // the cell's inputs (c0 from this workgroup's own state slots, or the roots' state)
+          const float bias_l = p.lbias[(size_t)gate * H + unit];
+          float c0[4];
+          int rst[4];
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            const int rl = 16 * tt + 4 * (lane >> 4) + gate, row = tile.row0 + rl;
+            c0[tt] = 0.f;
+            rst[tt] = 0;
+            if (row < B) {
+              c0[tt] = p.cpool[((size_t)s_rx[rl] * B + row) * H + unit];
+              rst[tt] = p.horizon > 0 && (s_rlen[rl] % p.horizon) == 0;
+            }
+          }
+          const unsigned long long w2 = st_now();
+          if (tid == 0) (void)sc_wait_word(&p.pflags[(size_t)k * T + q], epoch, p.err);
+          __syncthreads();
+          if (STAMPS && tid == 0) st_acc[11] += st_now() - w2;
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt)
+            acc[tt] += __builtin_bit_cast(bxf4, __builtin_amdgcn_raw_buffer_load_b128(pr, (tid * 16 + 4 * tt) * 4, 0, 16));
+          // epilogue: + bias, the four gates of (row, unit) from the quad, the cell by lane gate = r
+          // (ez_lstm_gemm_cell_kernel's operations in its order); h1 through LDS to whole 64-B rows
+          float *s_h = smem;  // [64 rows][16 units] (the stage buffers are free after the barrier)
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            float gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[tt][r] + bias_l;
+              const float vi = ls_quad_bcast(v, 0), vf = ls_quad_bcast(v, 1), vg = ls_quad_bcast(v, 2), vo = ls_quad_bcast(v, 3);
+              if (gate == r) { gi = vi; gf = vf; gg = vg; go = vo; }
+            }
+            const int rl = 16 * tt + 4 * (lane >> 4) + gate, row = tile.row0 + rl;
+            const float cc = lstm_sigmoid(gf) * c0[tt] + lstm_sigmoid(gi) * tanhf(gg);
+            const float hh = lstm_sigmoid(go) * tanhf(cc);
+            s_h[rl * kLsUnits + (unit - kLsUnits * tile.nb)] = hh;
+            if (row < B) p.cpool[((size_t)(k + 1) * B + row) * H + unit] = rst[tt] ? 0.0f : cc;
+          }
+          __syncthreads();
+          {
+            const int rl = tid >> 2, row = tile.row0 + rl;
+            if (row < B) {
+              const float4 v = reinterpret_cast<const float4 *>(s_h)[tid];
+              const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(p.h1g, 0, B * H * 4, 0x00020000);
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sc_u4, v), hr,
+                                                     (row * H + kLsUnits * tile.nb + 4 * (tid & 3)) * 4, 0, 16);
+            }
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          if (tid == 0)
+            __hip_atomic_store(&p.tflags[(size_t)k * T + q], (epoch << 32) | 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      stamp(5);
+      if (has_root) {
+        // ---- the value-prefix head on this root's LSTM output: wait for the row's NB tiles (sc1 loads)
+        const int mb = b / kLsRows;
+        const unsigned long long w3 = st_now();
+        if (wv == 0 && lane < NB) (void)sc_wait_word(&p.tflags[(size_t)k * T + lane * p.nmb + mb], epoch, p.err);
+        __syncthreads();
+        if (STAMPS && tid == 0) st_acc[12] += st_now() - w3;
+        const bool reset = p.horizon > 0 && (s_len[0] % p.horizon) == 0;
+        if (tid < (H >> 2)) {
+          const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(p.h1g + (size_t)b * H, 0, H * 4, 0x00020000);
+          const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(hr, tid * 16, 0, 16));
+          const float4 s4 = reinterpret_cast<const float4 *>(p.vp_s)[tid], t4 = reinterpret_cast<const float4 *>(p.vp_t)[tid];
+          float4 x;
+          x.x = fmaxf(__fmaf_rn(v.x, s4.x, t4.x), 0.0f);
+          x.y = fmaxf(__fmaf_rn(v.y, s4.y, t4.y), 0.0f);
+          x.z = fmaxf(__fmaf_rn(v.z, s4.z, t4.z), 0.0f);
+          x.w = fmaxf(__fmaf_rn(v.w, s4.w, t4.w), 0.0f);
+          reinterpret_cast<float4 *>(lr)[tid] = x;
+          reinterpret_cast<float4 *>(p.hpool + ((size_t)(k + 1) * B + b) * H)[tid] =
+              reset ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
+        }
+        __syncthreads();
+        sc_head_hidden(lr, p.Kr, p.w1t, 0, tid < 32 ? p.b1[tid] : 0.0f, lpart, lhid, tid);
+        sc_head_out(p, lhid, llg, N2, 0, p.Vr, tid);
+        __syncthreads();
+        if (wv == 0) {
+          const float r = sc_decode(p, llg, p.Vr);
+          if (lane == 0) s_dec[0] = r;
+        }
+        __syncthreads();
+        stamp(6);
+      }
+    }
+    // ---- expand + backup (wave 0)
+    if (has_root && wv == 0) {
+      const float r = s_dec[0], v = s_dec[1];
+      const int len = s_len[0];
+      const int leaf = t.path[len];
+      const float *plg = llg + p.Vr + p.Vv;
+      const int is_reset = (p.horizon > 0 && len % p.horizon == 0) ? 1 : 0;
+      expand_wave(t, 0, leaf, s_leafvtp, k + 1, r, plg, is_reset);
+      for (int l = lane; l < len; l += 64) t.meta[t.path[l]].best = t.path_act[l];  // cnode.cpp:806
+      backup_wave_ez(t, 0, 0, 1, s_mm, s_leafvtp, v, p.disc);
+      if (p.rec_reset && lane == 0) p.rec_reset[(size_t)k * B + b] = is_reset;
+      if (p.rec_dec) {
+        if (lane < 2) p.rec_dec[((size_t)k * B + b) * 2 + lane] = lane ? v : r;
+        if (lane < A) p.rec_logits[((size_t)k * B + b) * A + lane] = plg[lane];
+      }
+    }
+    stamp(7);
+  }
+  __syncthreads();
+  // ---- write back the slice (tree, last path, min-max)
+  if (has_root) {
+    for (int e = tid; e < p.cap; e += kScThreads) {
+      p.stat[(size_t)e * B + b] = ls[e];
+      p.meta[(size_t)e * B + b] = lm[e];
+    }
+    for (int l = tid; l < p.depth_cap; l += kScThreads) {
+      p.path[(size_t)l * B + b] = t.path[l];
+      p.path_act[(size_t)l * B + b] = t.path_act[l];
+    }
+  }
+  if (STAMPS && tid == 0 && p.stamps) {
+    st_acc[9] = __builtin_amdgcn_s_memtime() - st_begin;
+    for (int n = 0; n < 14; ++n) atomicAdd(p.stamps + 40 + n, st_acc[n]);
+  }
+  if (tid == 0) {
+    if (has_root) {
+      p.minmax[b] = s_mm[0];
+      p.pathlen[b] = s_len[0];
+    }
     // the last workgroup advances the epoch (no release fence: the kernel boundary orders the
     // write-back for every later reader)
     const uint32_t done = atomicAdd(p.epoch + 1, 1u);

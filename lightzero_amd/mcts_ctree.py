@@ -525,6 +525,29 @@ class EfficientZeroMCTSCtree(object):
     def roots(cls: int, active_collect_env_num: int, legal_actions: List[Any]) -> "ez_tree.Roots":
         return ez_tree.Roots(active_collect_env_num, legal_actions, fast_rng=(cls.rng_mode == 'philox'))
 
+    def _fused_conv(self, model, t, shape, Hl):
+        """The native split-bf16 FoldedConvNet (with the fused LSTM step packed) when the whole search
+        can run as one lzm_search_conv_ez launch: conv EfficientZeroModel, 64 x 8 x 8 latent, head K
+        multiples of 128, LSTM width a multiple of 128, max(B, 2 T) workgroups co-resident (T = ceil(B / 64)
+        * H / 16 LSTM tiles); None otherwise (the generic per-simulation path). cfg.fused_search (default
+        on) and LZM_FUSED_CONV=0 turn it off."""
+        if not self._cfg.get('fused_search', True) or not t.ez or os.environ.get("LZM_FUSED_CONV", "1") == "0":
+            return None
+        if tuple(shape) != (64, 8, 8) or Hl % 128 or Hl > 1024 or Hl // 16 > 64:
+            return None
+        tiles = -(-t.B // 64) * (Hl // 16)
+        if t.B > 256 or max(t.B, 2 * tiles) > _device_cus(t.device):
+            return None
+        net = _step_net(self, model)
+        hp = getattr(net, "heads", None)
+        if getattr(net, "native", None) is None or hp is None or getattr(net, "precision", None) != "bf16x3" \
+                or not getattr(net, "ez", False) or getattr(net, "lstm_frag", None) is None:
+            return None
+        if hp["Khd"] % 128 or hp["off_policy"] % 128 or hp["A"] != t.A or hp["Kr"] != Hl \
+                or (net.r_ch * 64 + Hl) % 128:
+            return None
+        return net
+
     def _loop(self, t, model, buf, S, row, Hl, rec=None, net=None):
         """The S simulations (mcts_ctree.py:756-827), all enqueued on the current stream."""
         cfg = self._cfg
@@ -601,7 +624,8 @@ class EfficientZeroMCTSCtree(object):
             hh0 = _latent_tensor(reward_hidden_state_roots[1], dev).reshape(B, -1)
             Hl = hc0.shape[1]
             rec = None
-            graph = self._cfg.get('use_hip_graph', False) and not getattr(self, "record", False)
+            graph = self._cfg.get('use_hip_graph', False) and not getattr(self, "record", False) \
+                and self._fused_conv(model, t, shape, Hl) is None
             gkey = _graph_key(t, model, B, S, shape, (Hl, Hl)) if graph else None
             entry = self._graphs.get(gkey, model, t) if graph else None
             buf = entry.buf if entry is not None else (_SearchBuffers() if graph else self._buf).get(
@@ -615,7 +639,16 @@ class EfficientZeroMCTSCtree(object):
                 rec = _Recorder(S, B, t.A, dev)
                 rec.is_reset = torch.zeros((S, B), dtype=torch.int32, device=dev)
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
-            if graph:
+            cz = self._fused_conv(model, t, shape, Hl)
+            if cz is not None:
+                # the conv network's whole search, reward LSTM included, in one launch (lzm_search_conv_ez)
+                cfg = self._cfg
+                new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
+                t.search_conv_ez(cz, S, buf.mm, buf.seeds, buf.vtp_in, buf.pool, buf.extra[0], buf.extra[1],
+                                 int(cfg.lstm_horizon_len), int(cfg.pb_c_base), float(cfg.pb_c_init),
+                                 float(np.float32(cfg.discount_factor)),
+                                 bool(cfg.model.get('categorical_distribution', True)), rec=rec)
+            elif graph:
                 if entry is None:
                     entry = self._capture(t, model, buf, S, row, Hl)
                     self._graphs.put(gkey, entry)

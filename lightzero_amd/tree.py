@@ -189,6 +189,22 @@ class DeviceTree:
              int(hp["Khd"]), int(hp["off_policy"]), int(hp["Vr"]), int(hp["Vv"]), int(bool(categorical)), r("x"),
              r("action"), r("search_len"), r("decoded"), r("policy_logits"), stream_ptr(stream))
 
+    def search_conv_ez(self, net, S, minmax, seeds, vtp_in, pool, hpool, cpool, horizon, pb_c_base=19652,
+                       pb_c_init=1.25, discount=0.997, categorical=True, rec=None, stream=None):
+        """One launch for the whole search of a conv EfficientZeroModel (lzm_search_conv_ez; net: a native
+        split-bf16 conv_infer.FoldedConvNet with the fused LSTM step packed); hpool / cpool: the LSTM
+        state pools [S + 1, B, H] with slot 0 = the roots' state; rec: optional _Recorder-like object
+        (with is_reset)."""
+        r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n, None)))
+        hp, t = net.heads, net.t
+        call("lzm_search_conv_ez", self.h, int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax),
+             ptr(seeds), ptr(vtp_in), ptr(pool), ptr(hpool), ptr(cpool), int(hpool.shape[2]), int(horizon),
+             ptr(net.native), ptr(net.actmap), int(net.n_dres), int(net.n_pres), int(net.r_ch), int(net.h_ch),
+             ptr(net.lstm_frag), ptr(t["lstm_b"]), ptr(t["vp_s"]), ptr(t["vp_t"]), ptr(hp["w1t"]), ptr(hp["b1"]),
+             ptr(hp["w2q"]), ptr(hp["b2"]), int(hp["Khd"]), int(hp["off_policy"]), int(hp["Vr"]), int(hp["Vv"]),
+             int(bool(categorical)), r("x"), r("action"), r("search_len"), r("decoded"), r("policy_logits"),
+             r("is_reset"), stream_ptr(stream))
+
     def set_step(self, count=None, base=0, increment=True, dist=None, values=None, fresh_minmax=False,
                  value_delta_max=0.0):
         """Collect-step mode of the next search_mlp calls (lzm_search_set_step; host state only):

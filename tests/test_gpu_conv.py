@@ -143,31 +143,52 @@ def test_conv_search_tree_and_decode_parity(kind, B, S):
     torch_replay(kind, res, B, S)
 
 
-@pytest.mark.parametrize("kind,fused", [("ez", False), ("mz", True), ("mz", False)])
+@pytest.mark.parametrize("kind,fused", [("ez", True), ("ez", False), ("mz", True), ("mz", False)])
 def test_conv_search_full_config_tree_parity(kind, fused):
-    """configs 3 / 5 at their per-GPU size: 256 envs x 50 simulations (MuZero: the one-launch search,
-    lzm_search_conv, and the generic per-simulation path)"""
+    """configs 3 / 5 at their per-GPU size: 256 envs x 50 simulations (the one-launch searches,
+    lzm_search_conv / lzm_search_conv_ez, and the generic per-simulation path)"""
     B, S = 256, 50
     res = run_search(kind, B, S, seed=2, fused=fused)
     oracle_replay(kind, res, B, S)
     assert (res["dist"].sum(axis=1) == S).all()
 
 
+@pytest.mark.parametrize("kind", ["mz", "ez"])
 @pytest.mark.parametrize("B,S,rng,zero", [(256, 50, "glibc", False), (64, 30, "glibc", True), (37, 20, "philox", False)])
-def test_fused_conv_search_equals_generic(B, S, rng, zero):
-    """lzm_search_conv (one launch for all simulations) runs the generic path's arithmetic in the same
-    order: identical requests at every simulation, decoded values, policy logits, visit counts, root
-    values and trajectories, in both RNG modes; with zero-init heads (all-tie search: ties reaching
-    expanded children take the serial draw path) too"""
-    model = conv_model("mz", 13, zero_heads=zero)
-    out = [run_search("mz", B, S, seed=14, model=model, fused=f, rng=rng) for f in (True, False)]
+def test_fused_conv_search_equals_generic(kind, B, S, rng, zero):
+    """lzm_search_conv / lzm_search_conv_ez (one launch for all simulations) run the generic path's
+    arithmetic in the same order: identical requests at every simulation, decoded values, policy
+    logits, visit counts, root values and trajectories (EZ: is_reset too), in both RNG modes; with
+    zero-init heads (all-tie search: ties reaching expanded children take the serial draw path) too.
+    EZ at B = 37: 64 workgroups, 27 of them LSTM tiles without a root."""
+    model = conv_model(kind, 13, zero_heads=zero)
+    out = [run_search(kind, B, S, seed=14, model=model, fused=f, rng=rng) for f in (True, False)]
     a, b = out
     for key in ("dist", "values", "traj"):
         assert np.array_equal(a[key], b[key]), key
-    for key in ("x", "action", "search_len", "decoded", "policy_logits"):
+    for key in ("x", "action", "search_len", "decoded", "policy_logits") + (("is_reset",) if kind == "ez" else ()):
         assert np.array_equal(a["rec"][key], b["rec"][key]), key
     if rng == "glibc":
-        oracle_replay("mz", a, B, S)
+        oracle_replay(kind, a, B, S)
+
+
+def test_fused_ez_search_pools_equal_generic():
+    """the one-launch EZ search files the same latent and LSTM state pools as the generic path
+    (next latents, reset-masked h / c slots, mcts_ctree.py:805-816)"""
+    from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree
+    from lightzero_amd.utils import EasyDict
+    model = conv_model("ez", 21)
+    B, S = 64, 12
+    bufs = []
+    for f in (True, False):
+        cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5,
+                            use_hip_graph=False, fused_search=f,
+                            model=dict(support_scale=50, categorical_distribution=True)))
+        mcts = EfficientZeroMCTSCtree(cfg)
+        run_search("ez", B, S, seed=22, model=model, mcts=mcts)
+        bufs.append([x.clone() for x in (mcts._buf.pool, mcts._buf.extra[0], mcts._buf.extra[1])])
+    for name, x, y in zip(("latent", "h", "c"), *bufs):
+        assert torch.equal(x, y), name
 
 
 @pytest.mark.parametrize("kind", ["ez", "mz"])

@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--precision", choices=["bf16x3", "f32"], default=None,
                     help="native conv trunk precision (default: LZM_CONV_PRECISION or bf16x3)")
     ap.add_argument("--fused", type=int, default=1,
-                    help="MuZero: the one-launch search (lzm_search_conv) when it applies; 0: the generic path")
+                    help="the one-launch search (lzm_search_conv / lzm_search_conv_ez) when it applies; 0: the generic path")
     ap.add_argument("--rng", choices=["glibc", "philox"], default="glibc",
                     help="tie-break stream: the reference's glibc rand() (parity) or per-root Philox")
     a = ap.parse_args()
@@ -102,14 +102,15 @@ def main():
     dt = (time.perf_counter() - t0) / a.searches
     assert int(d.sum()) == B * S
     roots.tree.check_errors()
-    fused = a.kind == "mz" and mcts._fused_conv(model, roots.tree, (64, 8, 8)) is not None
+    fused = (mcts._fused_conv(model, roots.tree, (64, 8, 8)) if a.kind == "mz" else
+             mcts._fused_conv(model, roots.tree, (64, 8, 8), model.lstm_hidden_size)) is not None
     flops = recurrent_flops(model, a.kind, B, dev)
     net_tflops = flops * B * S / dt / 1e12
     print(json.dumps({
         "metric": "MCTS simulations/sec", "value": B * S / dt, "unit": "sims/s", "ms_per_search": dt * 1e3,
         "config": {"workload": "C3 Pong EfficientZero" if a.kind == "ez" else "C5 Breakout MuZero (per GPU)",
                    "envs": B, "num_simulations": S, "actions": A, "support": 2 * scale + 1, "latent": [64, 8, 8],
-                   "path": "one-launch search (lzm_search_conv)" if fused else
+                   "path": ("one-launch search (lzm_search_conv%s)" % ("_ez" if a.kind == "ez" else "")) if fused else
                    "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph) and not fused,
                    "conv_precision": precision, "rng": a.rng},
         "net_flops_per_sim": flops, "net_tflops_whole_search": net_tflops,
