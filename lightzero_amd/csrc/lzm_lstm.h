@@ -390,19 +390,29 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
   const int sr = tid >> 2, sq = tid & 3;
   const bool srow = tl.row0 + sr < B;
   const int abyte = ((tl.row0 + (srow ? sr : 0)) * K + k0 + 16 * sq) * 4;
-  const lp_u4 *bsrc4 = reinterpret_cast<const lp_u4 *>(wf + (size_t)tl.nb * 4 * nch * 3 * 64);
+  // B through a buffer resource over this n-block's fragments: B stage element e = tid + 256 u of
+  // [chunk c][col tile][term][lane] has c = u / 3 and (col tile, rest) from tid + 256 (u % 3), so three
+  // per-thread 32-bit offsets serve all six loads and the chunk index goes to the scalar offset (no
+  // 64-bit address per load for the compiler to hoist out of the simulation loop and spill)
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint4 *>(wf + (size_t)tl.nb * 4 * nch * 3 * 64), 0, 4 * nch * 3 * 64 * 16, 0x00020000);
+  int bvo[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int r = tid + kLpThreads * u, tc = r / 192, rest = r - tc * 192;
+    bvo[u] = (tc * nch * 192 + rest) * 16;
+  }
   lp_f4 va0[4], va1[4];
   lp_u4 vb0[6], vb1[6];
   auto load_stage = [&](int s, lp_f4(&VA)[4], lp_u4(&VB)[6]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      VA[u] = srow ? __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(xr, abyte + (s * kLsKc + 4 * u) * 4, 0, 16))
+      VA[u] = srow ? __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(xr, abyte, (s * kLsKc + 4 * u) * 4, 16))
                    : lp_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 6; ++u) {
-      const int e = tid + kLpThreads * u, c = e / 768, r = e - c * 768, tc = r / 192, rest = r - tc * 192;
-      const int j = (k0 / 32) + 2 * s + c;
-      VB[u] = bsrc4[((size_t)tc * nch + j) * 192 + rest];
+      const int j = (k0 / 32) + 2 * s + u / 3;
+      VB[u] = __builtin_bit_cast(lp_u4, __builtin_amdgcn_raw_buffer_load_b128(wr, bvo[u % 3], j * 192 * 16, 0));
     }
   };
   auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const lp_u4(&VB)[6]) __attribute__((always_inline)) {

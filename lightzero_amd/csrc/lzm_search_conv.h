@@ -255,6 +255,67 @@ __device__ __forceinline__ void sc_head_out(const ConvSearchArgs &p, const float
   }
 }
 
+// sc_head_hidden / sc_head_out with the weights read through buffer resources: one 32-bit per-thread
+// offset, the per-load constant in the scalar / immediate offset. With plain pointers the compiler
+// hoisted one 64-bit address per load out of the simulation loop (24 per head) and, in the
+// EfficientZero kernel, spilled them: every load then waited for a scratch reload (V/P hidden layers
+// 40 K cycles per simulation instead of ~10 K). Same values, same FMA order, same bits.
+__device__ __forceinline__ void sc_head_hidden_rs(const float *in, int K, const float *w1t, int head, float bias,
+                                                  float *part, float *hid, int tid) {
+  const int pt = tid >> 5, c = tid & 31;
+  float acc = 0.0f;
+  if (pt * 128 < K) {
+    const float4 *x4 = reinterpret_cast<const float4 *>(in + pt * 128);
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w1t), 0, 3 * kHdParts * 32 * 32 * 16, 0x00020000);
+    const int vo = (((head * kHdParts + pt) * 32) * 32 + c) * 16;
+    float4 w1[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) w1[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, q * 512, 0));
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const float4 x = x4[q];
+      acc = __fmaf_rn(x.x, w1[q].x, acc);
+      acc = __fmaf_rn(x.y, w1[q].y, acc);
+      acc = __fmaf_rn(x.z, w1[q].z, acc);
+      acc = __fmaf_rn(x.w, w1[q].w, acc);
+    }
+  }
+  part[pt * 32 + c] = acc;
+  __syncthreads();
+  if (tid < 32) {
+    float s = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kHdParts; ++q) s += part[q * 32 + tid];
+    hid[tid] = fmaxf(s + bias, 0.0f);
+  }
+  __syncthreads();
+}
+
+// output columns [jlo, jhi), jhi - jlo <= kScThreads: one column per thread (sc_head_out's arithmetic)
+__device__ __forceinline__ void sc_head_out1_rs(const ConvSearchArgs &p, const float *lhid, float *llg, int N2, int jlo,
+                                                int jhi, int tid) {
+  const int j = jlo + tid;
+  if (j >= jhi) return;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p.w2q), 0, N2 * 8 * 16, 0x00020000);
+  float4 w2[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) w2[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, j * 16, q * N2 * 16, 0));
+  const float b2 = p.b2[j];
+  const float *hid = lhid + 32 * (j < p.Vr ? 0 : (j < p.Vr + p.Vv ? 1 : 2));
+  float acc = 0.0f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float4 h4 = *reinterpret_cast<const float4 *>(hid + 4 * q);
+    acc = __fmaf_rn(h4.x, w2[q].x, acc);
+    acc = __fmaf_rn(h4.y, w2[q].y, acc);
+    acc = __fmaf_rn(h4.z, w2[q].z, acc);
+    acc = __fmaf_rn(h4.w, w2[q].w, acc);
+  }
+  llg[j] = acc + b2;
+}
+
 // ensure_softmax + InverseScalarTransform of one decoded head by one wave (wave_support_expectation's
 // arithmetic); returns h^-1 of the expectation (categorical) or of the raw value
 __device__ __forceinline__ float sc_decode(const ConvSearchArgs &p, const float *row, int V) {
@@ -873,11 +934,14 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       stamp(2);
       // ---- head MLPs: value and policy now (while the other roots finish their trunks), the value
       // prefix after the LSTM
-      sc_head_hidden(lhd, p.off_policy, p.w1t, 1, tid < 32 ? p.b1[32 + tid] : 0.0f, lpart, lhid + 32, tid);
-      sc_head_hidden(lhd + p.off_policy, p.Khd - p.off_policy, p.w1t, 2, tid < 32 ? p.b1[64 + tid] : 0.0f, lpart,
+      sc_head_hidden_rs(lhd, p.off_policy, p.w1t, 1, tid < 32 ? p.b1[32 + tid] : 0.0f, lpart, lhid + 32, tid);
+      sc_head_hidden_rs(lhd + p.off_policy, p.Khd - p.off_policy, p.w1t, 2, tid < 32 ? p.b1[64 + tid] : 0.0f, lpart,
                      lhid + 64, tid);
       stamp(3);
-      sc_head_out(p, lhid, llg, N2, p.Vr, N2, tid);
+      if (N2 - p.Vr <= kScThreads)
+        sc_head_out1_rs(p, lhid, llg, N2, p.Vr, N2, tid);
+      else
+        sc_head_out(p, lhid, llg, N2, p.Vr, N2, tid);
       __syncthreads();
       if (wv == 1) {
         const float v = sc_decode(p, llg + p.Vr, p.Vv);
@@ -997,8 +1061,11 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
               reset ? make_float4(0.f, 0.f, 0.f, 0.f) : v;
         }
         __syncthreads();
-        sc_head_hidden(lr, p.Kr, p.w1t, 0, tid < 32 ? p.b1[tid] : 0.0f, lpart, lhid, tid);
-        sc_head_out(p, lhid, llg, N2, 0, p.Vr, tid);
+        sc_head_hidden_rs(lr, p.Kr, p.w1t, 0, tid < 32 ? p.b1[tid] : 0.0f, lpart, lhid, tid);
+        if (p.Vr <= kScThreads)
+          sc_head_out1_rs(p, lhid, llg, N2, 0, p.Vr, tid);
+        else
+          sc_head_out(p, lhid, llg, N2, 0, p.Vr, tid);
         __syncthreads();
         if (wv == 0) {
           const float r = sc_decode(p, llg, p.Vr);
