@@ -375,97 +375,146 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
 typedef unsigned lp_u4 __attribute__((ext_vector_type(4)));
 typedef float lp_f4 __attribute__((ext_vector_type(4)));
 constexpr int kLpThreads = 256;
+#ifndef LZM_LP_DEPTH
+#define LZM_LP_DEPTH 3  // register sets of staged loads: global loads run LZM_LP_DEPTH - 1 stages ahead (2..4)
+#endif
+#ifndef LZM_LP_DIAG
+#define LZM_LP_DIAG 0  // timing experiments only (results invalid): 1 = no global loads after the first two
+                       // stages, 2 = no MFMAs, 3 = no LDS A reads, 4 = no split / LDS stores after the first
+#endif
 
 struct LpTile {
   int row0, nb, kh;  // tile rows [row0, row0 + 64), hidden units [16 nb, 16 nb + 16), K half
 };
 
+// f32 gate weights in MFMA fragment order for the one-launch search: element (nb, column tile, 32-K
+// chunk, half e / 4, lane, e % 4) = W[(gate H + unit) K + k] with unit = 16 nb + 4 ct + (lane & 15) / 4, gate = lane & 3,
+// k = 32 chunk + 8 (lane >> 4) + e — ls_pack's order before the split, so splitting a lane's 8 values
+// on the device (the same round-to-nearest-even terms as the host's bx_split) gives ls_pack's
+// fragments bit for bit, from two thirds of the bytes.
+inline void ls_pack_f32(const float *W, int K, int H, float *out) {
+  const int nch = K / 32, NB = H / kLsUnits;
+  for (int nb = 0; nb < NB; ++nb)
+    for (int w = 0; w < 4; ++w)
+      for (int j = 0; j < nch; ++j)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int e = 0; e < 8; ++e) {
+            const int n = lane & 15, unit = kLsUnits * nb + 4 * w + (n >> 2), gate = n & 3;
+            const int k = 32 * j + 8 * (lane >> 4) + e;
+            out[(((((size_t)(nb * 4 + w) * nch + j) * 2 + (e >> 2)) * 64 + lane) * 4) + (e & 3)] =
+                W[((size_t)gate * H + unit) * K + k];
+          }
+}
+
+// three bf16 terms of 8 f32 values (two float4s) as three 16-B words (bx_split's terms, hardware cvt)
+__device__ __forceinline__ void lp_split8(const lp_f4 &x0, const lp_f4 &x1, uint4 &h, uint4 &m, uint4 &l) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  uint32_t hh[4], mm[4], ll[4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const lp_f4 x = u ? x1 : x0;
+    const f2 pr[2] = {f2{x[0], x[1]}, f2{x[2], x[3]}};
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const b2 th = __builtin_convertvector(pr[v], b2);
+      const f2 r1 = pr[v] - __builtin_convertvector(th, f2);
+      const b2 tm = __builtin_convertvector(r1, b2);
+      const b2 tl = __builtin_convertvector(r1 - __builtin_convertvector(tm, f2), b2);
+      hh[2 * u + v] = __builtin_bit_cast(uint32_t, th);
+      mm[2 * u + v] = __builtin_bit_cast(uint32_t, tm);
+      ll[2 * u + v] = __builtin_bit_cast(uint32_t, tl);
+    }
+  }
+  h = uint4{hh[0], hh[1], hh[2], hh[3]};
+  m = uint4{mm[0], mm[1], mm[2], mm[3]};
+  l = uint4{ll[0], ll[1], ll[2], ll[3]};
+}
+
 // the GEMM part: acc[t] = the tile's K-half partial sums (row tile t = rows 16 t .. + 15 of the tile,
 // this wave's 16 gate columns), accumulated from zero exactly as the 512-thread kernel does.
-// lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4).
+// lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4); wf32:
+// ls_pack_f32's layout. Both operands are read as f32 and split on the fly; a thread stages 4 values
+// of 4 A rows through LDS and loads the B fragments (chunk 0 and 1, column tile = its wave, its lane)
+// of every stage, which its own MFMAs consume: B never touches LDS.
+// Loads go through buffer resources (one
+// 32-bit per-thread offset each, the stage in the scalar offset): no 64-bit address per load for the
+// compiler to hoist out of the simulation loop and spill.
 __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, const __amdgpu_buffer_rsrc_t xr,
-                                             const uint4 *wf, uint16_t *lds, bxf4 (&acc)[4]) {
+                                             const float *wf32, uint16_t *lds, bxf4 (&acc)[4]) {
   const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6;
   const int nch = K / 32, kspan = K / 2, nst = kspan / kLsKc, k0 = tl.kh * kspan;
-  const int sr = tid >> 2, sq = tid & 3;
-  const bool srow = tl.row0 + sr < B;
-  const int abyte = ((tl.row0 + (srow ? sr : 0)) * K + k0 + 16 * sq) * 4;
-  // B through a buffer resource over this n-block's fragments: B stage element e = tid + 256 u of
-  // [chunk c][col tile][term][lane] has c = u / 3 and (col tile, rest) from tid + 256 (u % 3), so three
-  // per-thread 32-bit offsets serve all six loads and the chunk index goes to the scalar offset (no
-  // 64-bit address per load for the compiler to hoist out of the simulation loop and spill)
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint4 *>(wf + (size_t)tl.nb * 4 * nch * 3 * 64), 0, 4 * nch * 3 * 64 * 16, 0x00020000);
-  int bvo[3];
+  // A: wave-instruction u of wave w reads 4 whole 256-B row segments of the stage (rows 16 w + 4 u +
+  // lane / 16, float4 lane % 16): 1 KiB contiguous per row quarter, no partially used lines
+  const int a4 = lane & 15;
+  int avo[4];
+  bool arow[4];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int r = tid + kLpThreads * u, tc = r / 192, rest = r - tc * 192;
-    bvo[u] = (tc * nch * 192 + rest) * 16;
+  for (int u = 0; u < 4; ++u) {
+    const int rr = 16 * ct + 4 * u + (lane >> 4);
+    arow[u] = tl.row0 + rr < B;
+    avo[u] = ((tl.row0 + (arow[u] ? rr : 0)) * K + k0 + 4 * a4) * 4;
   }
-  lp_f4 va0[4], va1[4];
-  lp_u4 vb0[6], vb1[6];
-  auto load_stage = [&](int s, lp_f4(&VA)[4], lp_u4(&VB)[6]) __attribute__((always_inline)) {
+  // B: ls_pack_f32's layout [nb][column tile][chunk][half][lane][4]: wave-instruction (chunk, half)
+  // reads 1 KiB contiguous
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(wf32 + (size_t)tl.nb * 4 * nch * 64 * 8), 0, 4 * nch * 64 * 8 * 4, 0x00020000);
+  const int bvo = ((ct * nch * 2) * 64 + lane) * 16;  // (column tile, chunk 0, half 0, lane), bytes
+  lp_f4 va[LZM_LP_DEPTH][4], vb[LZM_LP_DEPTH][4];  // global loads LZM_LP_DEPTH - 1 stages ahead
+  uint4 wreg[2][3];  // the next stage's B fragments (chunk, term) of this wave's column tile, split
+  auto load_stage = [&](int s, lp_f4(&VA)[4], lp_f4(&VB)[4]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      VA[u] = srow ? __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(xr, abyte, (s * kLsKc + 4 * u) * 4, 16))
-                   : lp_f4{0.f, 0.f, 0.f, 0.f};
+      VA[u] = arow[u] ? __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(xr, avo[u], s * kLsKc * 4, 16))
+                      : lp_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 6; ++u) {
-      const int j = (k0 / 32) + 2 * s + u / 3;
-      VB[u] = __builtin_bit_cast(lp_u4, __builtin_amdgcn_raw_buffer_load_b128(wr, bvo[u % 3], j * 192 * 16, 0));
+    for (int u = 0; u < 4; ++u) {  // chunk c = u / 2 of the stage, half u % 2 of the lane's 8 values
+      const int j = (k0 / 32) + 2 * s + u / 2;
+      VB[u] = __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(wr, bvo, (2 * j + (u & 1)) * 64 * 16, 0));
     }
   };
-  auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const lp_u4(&VB)[6]) __attribute__((always_inline)) {
+  auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const lp_f4(&VB)[4]) __attribute__((always_inline)) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     typedef __bf16 b2 __attribute__((ext_vector_type(2)));
     uint16_t *abuf = lds + bsel * kLsStage;
 #pragma unroll
-    for (int hc = 0; hc < 2; ++hc) {  // the thread's two 16-B chunks: K 16 sq + 8 hc .. + 7
-      uint32_t h[4], m[4], l[4];
+    for (int u = 0; u < 4; ++u) {  // row 16 ct + 4 u + lane / 16: 4 values, half (a4 & 1) of chunk a4 / 2
+      const int rr = 16 * ct + 4 * u + (lane >> 4);
+      uint32_t hh[2], mm[2], ll[2];
+      const f2 pr[2] = {f2{VA[u][0], VA[u][1]}, f2{VA[u][2], VA[u][3]}};
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const lp_f4 x = VA[2 * hc + u];
-        const f2 pr[2] = {f2{x[0], x[1]}, f2{x[2], x[3]}};
-#pragma unroll
-        for (int v = 0; v < 2; ++v) {
-          const b2 hh = __builtin_convertvector(pr[v], b2);
-          const f2 r1 = pr[v] - __builtin_convertvector(hh, f2);
-          const b2 mm = __builtin_convertvector(r1, b2);
-          const b2 ll = __builtin_convertvector(r1 - __builtin_convertvector(mm, f2), b2);
-          h[2 * u + v] = __builtin_bit_cast(uint32_t, hh);
-          m[2 * u + v] = __builtin_bit_cast(uint32_t, mm);
-          l[2 * u + v] = __builtin_bit_cast(uint32_t, ll);
-        }
+      for (int v = 0; v < 2; ++v) {
+        const b2 th = __builtin_convertvector(pr[v], b2);
+        const f2 r1 = pr[v] - __builtin_convertvector(th, f2);
+        const b2 tm = __builtin_convertvector(r1, b2);
+        const b2 tq = __builtin_convertvector(r1 - __builtin_convertvector(tm, f2), b2);
+        hh[v] = __builtin_bit_cast(uint32_t, th);
+        mm[v] = __builtin_bit_cast(uint32_t, tm);
+        ll[v] = __builtin_bit_cast(uint32_t, tq);
       }
-      const int chunk = 2 * sq + hc;
-      uint16_t *base = abuf + sr * kLsKc + ((chunk ^ (sr & 7)) & 7) * 8;
-      *reinterpret_cast<uint4 *>(base) = uint4{h[0], h[1], h[2], h[3]};
-      *reinterpret_cast<uint4 *>(base + kLsPlane) = uint4{m[0], m[1], m[2], m[3]};
-      *reinterpret_cast<uint4 *>(base + 2 * kLsPlane) = uint4{l[0], l[1], l[2], l[3]};
+      uint16_t *base = abuf + rr * kLsKc + (((a4 >> 1) ^ (rr & 7)) & 7) * 8 + 4 * (a4 & 1);
+      *reinterpret_cast<uint2 *>(base) = uint2{hh[0], hh[1]};
+      *reinterpret_cast<uint2 *>(base + kLsPlane) = uint2{mm[0], mm[1]};
+      *reinterpret_cast<uint2 *>(base + 2 * kLsPlane) = uint2{ll[0], ll[1]};
     }
-    lp_u4 *bbuf = reinterpret_cast<lp_u4 *>(abuf + kLsABuf);
+    // B: a wave loads exactly the fragments its own MFMAs consume, so they stay in registers
 #pragma unroll
-    for (int u = 0; u < 6; ++u) bbuf[tid + kLpThreads * u] = VB[u];
+    for (int c = 0; c < 2; ++c) lp_split8(VB[2 * c], VB[2 * c + 1], wreg[c][0], wreg[c][1], wreg[c][2]);
   };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  load_stage(0, va0, vb0);
-  if (nst > 1) load_stage(1, va1, vb1);
-  store_stage(0, va0, vb0);
+#pragma unroll
+  for (int s0 = 0; s0 < LZM_LP_DEPTH - 1; ++s0)
+    if (s0 < nst) load_stage(s0, va[s0], vb[s0]);
+  store_stage(0, va[0], vb[0]);
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = bxf4{0.f, 0.f, 0.f, 0.f};
   const int ar = lane & 15, ag = lane >> 4;
+  // stage s with register set P = s % LZM_LP_DEPTH (a compile-time index: the loop below is unrolled
+  // by the depth); the A planes ping-pong between two LDS buffers (s & 1)
   auto stage = [&](int s, auto par) __attribute__((always_inline)) {
-    constexpr int PAR = decltype(par)::value;
+    constexpr int P = decltype(par)::value, D = LZM_LP_DEPTH;
     __syncthreads();
-    if (s + 2 < nst) {
-      if constexpr (PAR == 0)
-        load_stage(s + 2, va0, vb0);
-      else
-        load_stage(s + 2, va1, vb1);
-    }
-    const uint16_t *abuf = lds + PAR * kLsStage;
-    const uint4 *bbuf = reinterpret_cast<const uint4 *>(abuf + kLsABuf);
+    if (s + D - 1 < nst && LZM_LP_DIAG != 1) load_stage(s + D - 1, va[(P + D - 1) % D], vb[(P + D - 1) % D]);
+    const uint16_t *abuf = lds + (s & 1) * kLsStage;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       uint4 a[4][3], w[3];
@@ -473,10 +522,19 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
       for (int t = 0; t < 4; ++t) {
         const int r = 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
 #pragma unroll
-        for (int tm = 0; tm < 3; ++tm) a[t][tm] = *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
+        for (int tm = 0; tm < 3; ++tm)
+          a[t][tm] = LZM_LP_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)s, (uint32_t)t, (uint32_t)tm}
+                                      : *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
       }
 #pragma unroll
-      for (int tm = 0; tm < 3; ++tm) w[tm] = bbuf[((c * 4 + ct) * 3 + tm) * 64 + lane];
+      for (int tm = 0; tm < 3; ++tm) w[tm] = wreg[c][tm];
+      if (LZM_LP_DIAG == 2) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y),
+                         __builtin_bit_cast(float, a[t][2].z ^ w[2].z), 0.f};
+        continue;
+      }
       // small terms first: l.h, h.l, m.m, m.h, h.m, h.h (ez_lstm_gemm_cell_kernel's order)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
@@ -491,16 +549,13 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
     }
-    if (s + 1 < nst) {
-      if constexpr (PAR == 0)
-        store_stage(1, va1, vb1);
-      else
-        store_stage(0, va0, vb0);
-    }
+    if (s + 1 < nst && LZM_LP_DIAG != 4) store_stage((s + 1) & 1, va[(P + 1) % D], vb[(P + 1) % D]);
   };
-  for (int s = 0; s < nst; s += 2) {
-    stage(s, I0());
-    if (s + 1 < nst) stage(s + 1, I1());
+  for (int s = 0; s < nst; s += LZM_LP_DEPTH) {
+    stage(s, std::integral_constant<int, 0>());
+    if (LZM_LP_DEPTH > 1 && s + 1 < nst) stage(s + 1, std::integral_constant<int, 1 % LZM_LP_DEPTH>());
+    if (LZM_LP_DEPTH > 2 && s + 2 < nst) stage(s + 2, std::integral_constant<int, 2 % LZM_LP_DEPTH>());
+    if (LZM_LP_DEPTH > 3 && s + 3 < nst) stage(s + 3, std::integral_constant<int, 3 % LZM_LP_DEPTH>());
   }
 }
 

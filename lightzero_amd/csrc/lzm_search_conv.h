@@ -77,7 +77,7 @@ struct ConvSearchArgs {
   float *xin;             // [B][Kx] LSTM input rows [reward planes | leaf hidden state] (sc1 hand-off)
   int Kx, H, horizon;     // Kx = r_ch * 64 + H; lstm_horizon_len
   float *hpool, *cpool;   // [S + 1][B][H] state pools (slot 0 = the roots' state)
-  const uint4 *lwf;       // gate weight fragments (lzm_ez_lstm_prepare)
+  const float *lwf32;     // gate weights, f32 in fragment order (lzm_ez_lstm_prepare_f32)
   const float *lbias;     // [4H] b_ih + b_hh
   const float *vp_s, *vp_t;  // value-prefix BatchNorm as an affine map (relu(h1 * s + t) feeds the head)
   float *h1g;             // [B][H] unmasked LSTM outputs (sc1 hand-off, tile -> root)
@@ -654,6 +654,9 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 }
 
 
+#ifndef LZM_EZ_POOL_AUX
+#define LZM_EZ_POOL_AUX 16  // cache policy of the latent pool stores (16: sc1)
+#endif
 // The EfficientZero one-launch search (lzm_search_conv_ez). The grid is G = max(B, 2 T)
 // workgroups; workgroup g owns root g (g < B) and K half (g & 1 or the XCD map below) of LSTM tile
 // q(g) (g < 2 T). Per simulation, on top of the MuZero flow:
@@ -770,10 +773,13 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   {
     int kh = b & 1;
     q = b >> 1;
-    if ((T & 7) == 0) {  // XCD-major: whole n-blocks per XCD (block % 8 = XCD), K halves on one XCD
-      const int j = b >> 3;
-      q = (b & 7) * (T >> 3) + (j >> 1);
-      kh = j & 1;
+    if ((T & 3) == 0) {
+      // XCD map (block % 8 = XCD): one K half per XCD (XCD & 1) and consecutive tiles — whole
+      // n-blocks, every row block — so an XCD's L2 holds its W slice (K / 2 x 64 columns per n-block)
+      // and only its K half of the LSTM input rows; the split-K partner sits on the next XCD
+      const int xcd = b & 7, j = b >> 3;
+      q = (xcd >> 1) * (T >> 2) + j;
+      kh = xcd & 1;
     }
     const int nb = q / p.nmb, mb = q - nb * p.nmb;
     tile = LpTile{kLsRows * mb, nb, kh};
@@ -914,10 +920,16 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
           __syncthreads();
           if (i == 2 * p.n_dres) {  // the next latent (registers, exact) and the reward planes
-            float *dst = p.pool + ((size_t)(k + 1) * B + b) * (kCvCh * kCvPix) + c * kCvPix + 4 * (lane >> 4);
+            // the latent by sc1 (write-through) stores, which do not keep the line in this XCD's L2: 16 KB
+            // per root and simulation that would otherwise push the LSTM weights and the trunk's out of
+            // it; read back (as a parent) at most once per later simulation
+            const __amdgpu_buffer_rsrc_t lr4 = __builtin_amdgcn_make_buffer_rsrc(
+                p.pool + ((size_t)(k + 1) * B + b) * (kCvCh * kCvPix), 0, kCvCh * kCvPix * 4, 0x00020000);
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4)
-              *reinterpret_cast<float4 *>(dst + 16 * q4) = float4{xres[4 * q4], xres[4 * q4 + 1], xres[4 * q4 + 2], xres[4 * q4 + 3]};
+              __builtin_amdgcn_raw_buffer_store_b128(
+                  __builtin_bit_cast(sc_u4, float4{xres[4 * q4], xres[4 * q4 + 1], xres[4 * q4 + 2], xres[4 * q4 + 3]}),
+                  lr4, (c * kCvPix + 4 * (lane >> 4) + 16 * q4) * 4, 0, LZM_EZ_POOL_AUX);
             if (wv < 2)  // the reward planes: the LSTM input row's first part, sc1
               bx_conv1_layer<0, true>(buf((i + 1) & 1), p.w + L.rw, p.w + L.rb, p.r_ch, p.xin + (size_t)b * Kx, lane, wv);
           }
@@ -965,7 +977,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         if (STAMPS && tid == 0) st_acc[10] += w1 - w0;
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(p.xin, 0, B * Kx * 4, 0x00020000);
         bxf4 acc[4];
-        lp_tile_gemm(tile, B, Kx, xr, p.lwf, act, acc);
+        lp_tile_gemm(tile, B, Kx, xr, p.lwf32, act, acc);
         if (STAMPS && tid == 0) st_acc[13] += st_now() - w1;
         const __amdgpu_buffer_rsrc_t pr =
             __builtin_amdgcn_make_buffer_rsrc(p.kpart + (size_t)q * (kLpThreads * 16), 0, kLpThreads * 16 * 4, 0x00020000);
