@@ -549,6 +549,8 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
     }
+    // (measured: splitting / storing stage s + 1 BEFORE this stage's MFMAs instead, into the other LDS
+    // buffer, made the GEMM slower, 33 K -> 40 K cycles per simulation)
     if (s + 1 < nst && LZM_LP_DIAG != 4) store_stage((s + 1) & 1, va[(P + 1) % D], vb[(P + 1) % D]);
   };
   for (int s = 0; s < nst; s += LZM_LP_DEPTH) {

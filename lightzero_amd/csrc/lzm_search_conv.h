@@ -322,7 +322,7 @@ __device__ __forceinline__ float sc_decode(const ConvSearchArgs &p, const float 
   float e;
   if (p.categorical) {
     float sm;
-    e = V <= 640 ? sc_decode_row<10>(row, V, &sm) : sc_decode_row<16>(row, V, &sm);
+    e = V <= 128 ? sc_decode_row<2>(row, V, &sm) : V <= 640 ? sc_decode_row<10>(row, V, &sm) : sc_decode_row<16>(row, V, &sm);
     if ((threadIdx.x & 63) == 0 && fabsf(sm - 1.0f) <= 1e-5f + 1e-5f) atomicAdd(p.sdiag, 1);  // verdict undecidable
   } else {
     e = row[0];
@@ -1056,6 +1056,14 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         const int mb = b / kLsRows;
         const unsigned long long w3 = st_now();
         if (wv == 0 && lane < NB) (void)sc_wait_word(&p.tflags[(size_t)k * T + lane * p.nmb + mb], epoch, p.err);
+        if (wv == 1) {
+          // meanwhile the leaf's expansion (everything but its value prefix, filed after the decode) and
+          // best_action along the path (cnode.cpp:806)
+          const int len = s_len[0];
+          const int is_reset = (p.horizon > 0 && len % p.horizon == 0) ? 1 : 0;
+          expand_wave(t, 0, t.path[len], s_leafvtp, k + 1, 0.0f, llg + p.Vr + p.Vv, is_reset);
+          for (int l = lane; l < len; l += 64) t.meta[t.path[l]].best = t.path_act[l];
+        }
         __syncthreads();
         if (STAMPS && tid == 0) st_acc[12] += st_now() - w3;
         const bool reset = p.horizon > 0 && (s_len[0] % p.horizon) == 0;
@@ -1094,8 +1102,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       const int leaf = t.path[len];
       const float *plg = llg + p.Vr + p.Vv;
       const int is_reset = (p.horizon > 0 && len % p.horizon == 0) ? 1 : 0;
-      expand_wave(t, 0, leaf, s_leafvtp, k + 1, r, plg, is_reset);
-      for (int l = lane; l < len; l += 64) t.meta[t.path[l]].best = t.path_act[l];  // cnode.cpp:806
+      if (lane == 0) t.stat[leaf].reward = r;  // the expansion's value prefix (expand_wave ran above)
       backup_wave_ez(t, 0, 0, 1, s_mm, s_leafvtp, v, p.disc);
       if (p.rec_reset && lane == 0) p.rec_reset[(size_t)k * B + b] = is_reset;
       if (p.rec_dec) {
