@@ -1603,7 +1603,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     LZM_SUBSTAMP(29);
     if (wid == 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
     LZM_SUBSTAMP(30);
-    // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500), wave 0
+    // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500): wave 0 files the leaf's own
+    // record and backs up; wave 1 meanwhile initialises the leaf's children (disjoint nodes; the
+    // next simulation's terms pass reads both after its barrier)
     if (wid == 0) {
       const int len = s_len[0];
       const int leaf = t.path[len];
@@ -1611,10 +1613,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (players > 1)
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
       LZM_SUBSTAMP(31);
-      expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA, -1, s_exptab);
+      expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA, -1, s_exptab, 1);
       LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
+    } else if (wid == 1) {
+      expand_wave(t, 0, 0, 0, k + 1, 0.0f, LG + row * kRMaxA, -1, s_exptab, 2);
     }
     LZM_STAMP(9);
   }

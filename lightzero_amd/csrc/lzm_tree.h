@@ -467,11 +467,14 @@ __device__ inline void backup(const TreeView &t, int i, float4 *mm_ptr, int to_p
 // expand_leaf with one lane per child (MuZero; all 64 lanes of the wave call it, A <= 64).
 // Bit-identical: pmax is a max (order-free), the prior denominator is summed in action order by a
 // readlane chain, every other quantity is per child.
+// part: 0 = the whole expansion, 1 = the leaf's own record only (meta, reward), 2 = its children only
+// (priors, fresh records): the two halves touch disjoint nodes, so two waves can run them at once.
 __device__ inline void expand_wave(const TreeView &t, int i, int leaf, int to_play, int latent, float reward,
-                                   const float *logits, int is_reset = -1, const uint64_t *exptab = kExp2fTab) {
+                                   const float *logits, int is_reset = -1, const uint64_t *exptab = kExp2fTab,
+                                   int part = 0) {
   const int lane = threadIdx.x & 63;
   const int A = t.A;
-  if (lane == 0) {
+  if (part != 2 && lane == 0) {
     NodeMeta m = t.meta[nidx(t, leaf, i)];
     m.latent = latent;
     m.to_play = to_play;
@@ -479,6 +482,7 @@ __device__ inline void expand_wave(const TreeView &t, int i, int leaf, int to_pl
     t.meta[nidx(t, leaf, i)] = m;
     t.stat[nidx(t, leaf, i)].reward = reward;
   }
+  if (part == 1) return;
   const bool act = lane < A;
   const float lg = act ? logits[lane] : -INFINITY;
   const float pmax = fmaxf(kFloatMin, wave_max_dpp(lg));
