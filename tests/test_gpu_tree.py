@@ -15,7 +15,7 @@ from oracle.oracle import OracleTree, load_transcript, replay_transcript  # noqa
 from tests.helpers import GpuTree, random_transcript, run_transcript  # noqa: E402
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-TRANSCRIPTS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("glibc_rand.npz") and not os.path.basename(p).startswith(("az_", "reuse_")))
+TRANSCRIPTS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("glibc_rand.npz") and not os.path.basename(p).startswith(("az_", "reuse_", "ptree_")))
 
 
 @pytest.mark.parametrize("path", TRANSCRIPTS, ids=lambda p: os.path.basename(p)[:-4])

@@ -11,7 +11,7 @@ from oracle.oracle import (OracleTree, glibc_rand_stream, lib, load_transcript, 
 from tests.helpers import random_transcript, run_scripted_search_oracle, run_transcript
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
-TRANSCRIPTS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("glibc_rand.npz") and not os.path.basename(p).startswith(("az_", "reuse_")))
+TRANSCRIPTS = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("glibc_rand.npz") and not os.path.basename(p).startswith(("az_", "reuse_", "ptree_")))
 
 
 def test_golden_files_present():
