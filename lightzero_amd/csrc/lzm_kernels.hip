@@ -257,11 +257,12 @@ struct BackpropArgs {
   const int32_t *to_play, *is_reset;
   int cur;
   float disc;
-  const int32_t *reuse_action;  // optional (MuZero): search-with-reuse, see reuse_leaf
+  const int32_t *reuse_action;  // optional: search-with-reuse, see reuse_leaf
   const float *reuse_value;
 };
 
-// cbatch_backpropagate_with_reuse (ctree_muzero/lib/cnode.cpp:502-546) for root i whose walk ended
+// cbatch_backpropagate_with_reuse (ctree_muzero/lib/cnode.cpp:502-546; EfficientZero
+// ctree_efficientzero/lib/cnode.cpp:603-641, there with is_reset set on every leaf) for root i whose walk ended
 // at `leaf` after `len` levels: no inference when the walk stopped on an expanded node (the root
 // child of the true action: no expand, back up the reuse value); a walk that stopped at the
 // unexpanded true-action child expands it but backs up the reuse value too.
@@ -285,9 +286,11 @@ __global__ __launch_bounds__(256) void backprop_kernel(BackpropArgs p) {
   const int tp = p.to_play[i];
   float v = p.values[i];
   bool no_inf;
-  reuse_leaf(t, i, leaf, len, EZ ? nullptr : p.reuse_action, p.reuse_value, &no_inf, &v);
+  reuse_leaf(t, i, leaf, len, p.reuse_action, p.reuse_value, &no_inf, &v);
   if (!no_inf)
     expand_leaf(t, i, leaf, tp, p.cur, p.rewards[i], p.logits + (size_t)i * t.A, p.is_reset ? p.is_reset[i] : 0, EZ);
+  else if (EZ)  // the reference sets every leaf's is_reset, expanded or not (ctree_efficientzero cnode.cpp:638)
+    t.meta[nidx(t, leaf, i)].is_reset = p.is_reset ? p.is_reset[i] : 0;
   backup<EZ>(t, i, p.minmax + i, tp, v, p.disc);
 }
 
@@ -404,7 +407,7 @@ struct DecodeArgs {
   int V, categorical, cur, horizon;
   float disc;
   float *out_decoded;  // [B][2] {reward, value} after h^-1, optional
-  const int32_t *reuse_action;  // optional (MuZero): search-with-reuse, see reuse_leaf
+  const int32_t *reuse_action;  // optional: search-with-reuse, see reuse_leaf
   const float *reuse_value;
 };
 
@@ -469,8 +472,9 @@ __device__ inline void decode_root(const DecodeArgs &p, const int32_t *norm_part
     const int is_reset = (EZ && p.horizon > 0 && len % p.horizon == 0) ? 1 : 0;
     if (p.out_is_reset && lane == 0) p.out_is_reset[i] = is_reset;
     bool no_inf;
-    reuse_leaf(t, i, leaf, len, EZ ? nullptr : p.reuse_action, p.reuse_value, &no_inf, &v);
+    reuse_leaf(t, i, leaf, len, p.reuse_action, p.reuse_value, &no_inf, &v);
     if (!no_inf) expand_wave(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, EZ ? is_reset : -1);
+    else if (EZ && lane == 0) t.meta[nidx(t, leaf, i)].is_reset = is_reset;  // (cnode.cpp:638, every leaf)
     if (EZ)
       backup_wave_ez(t, i, i, t.B, p.minmax + i, tp, v, p.disc);
     else
@@ -485,8 +489,9 @@ __device__ inline void decode_root(const DecodeArgs &p, const int32_t *norm_part
   if (p.out_is_reset) p.out_is_reset[i] = is_reset;
   const int tp = p.to_play[i];
   bool no_inf;
-  reuse_leaf(t, i, leaf, len, EZ ? nullptr : p.reuse_action, p.reuse_value, &no_inf, &v);
+  reuse_leaf(t, i, leaf, len, p.reuse_action, p.reuse_value, &no_inf, &v);
   if (!no_inf) expand_leaf(t, i, leaf, tp, p.cur, r, p.policy_logits + (size_t)i * t.A, is_reset, EZ);
+  else if (EZ) t.meta[nidx(t, leaf, i)].is_reset = is_reset;
   backup<EZ>(t, i, p.minmax + i, tp, v, p.disc);
 }
 
@@ -997,8 +1002,8 @@ int lzm_traverse(lzm_handle *h, int pb_c_base, float pb_c_init, float discount, 
   const bool ez = h->flags & LZM_TREE_EZ;
   hipStream_t s = (hipStream_t)stream;
   const bool serial = getenv("LZM_TRAVERSE") && strcmp(getenv("LZM_TRAVERSE"), "serial") == 0;
-  if (h->reuse_action && (ez || (h->flags & LZM_RNG_FAST) || serial)) {
-    set_err("lzm_traverse: search-with-reuse needs a MuZero tree in parity mode with the look-back traverse");
+  if (h->reuse_action && ((h->flags & LZM_RNG_FAST) || serial)) {
+    set_err("lzm_traverse: search-with-reuse needs parity mode with the look-back traverse");
     return LZM_ERR_ARG;
   }
   if (h->flags & LZM_RNG_FAST) {
@@ -2799,10 +2804,6 @@ extern "C" int lzm_mlp_initial_inference_prepare(lzm_handle *h, int B, int O, in
 extern "C" int lzm_set_reuse(lzm_handle *h, const int32_t *true_action, const float *reuse_value) {
   if (!h || (!true_action) != (!reuse_value)) {
     set_err("lzm_set_reuse: both arrays or neither");
-    return LZM_ERR_ARG;
-  }
-  if (true_action && (h->flags & LZM_TREE_EZ)) {
-    set_err("lzm_set_reuse: MuZero trees only (the EfficientZero reuse search is not built)");
     return LZM_ERR_ARG;
   }
   h->reuse_action = true_action;

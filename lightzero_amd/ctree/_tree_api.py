@@ -271,7 +271,8 @@ def _traverse_with_reuse(roots, pb_c_base, pb_c_init, discount_factor, min_max_s
 
 
 def _backprop_with_reuse(current_latent_state_index, discount_factor, value_prefixs, values, policies,
-                         min_max_stats_lst, results, to_play_batch, no_inference_lst, reuse_lst, reuse_value_lst):
+                         min_max_stats_lst, results, to_play_batch, no_inference_lst, reuse_lst, reuse_value_lst,
+                         is_reset_list=None):
     """batch_backpropagate_with_reuse (mz_tree.pyx:84-93): the outputs arrive compacted to the envs
     that ran inference (every env not in no_inference_lst, in env order); they are scattered back
     to env rows, the device backup derives the no-inference / reuse cases from the tree itself
@@ -302,6 +303,11 @@ def _backprop_with_reuse(current_latent_state_index, discount_factor, value_pref
         if not hasattr(roots, "_batch_index"):
             roots._batch_index = {}
         roots._batch_index[cur] = {i: n for n, i in enumerate(inf)}
+    if is_reset_list is not None and len(is_reset_list) != B:
+        raise ValueError("batch_backpropagate_with_reuse: is_reset_list must hold one flag per env (len == batch): "
+                         "the reference builds it over the inferred envs only and then reads it by env index "
+                         "(ctree_efficientzero/lib/cnode.cpp:638), which is undefined once an env skips inference; "
+                         "pass search_len % lstm_horizon_len == 0 for every env")
     _backprop(cur, discount_factor, full_r.tolist(), full_v.tolist(), full_p.tolist(), min_max_stats_lst, results,
-              to_play_batch)
+              to_play_batch, is_reset_list)
     t.set_reuse(None)

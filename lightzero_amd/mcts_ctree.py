@@ -548,8 +548,9 @@ class EfficientZeroMCTSCtree(object):
             return None
         return net
 
-    def _loop(self, t, model, buf, S, row, Hl, rec=None, net=None):
-        """The S simulations (mcts_ctree.py:756-827), all enqueued on the current stream."""
+    def _loop(self, t, model, buf, S, row, Hl, rec=None, net=None, infer=None):
+        """The S simulations (mcts_ctree.py:756-827), all enqueued on the current stream. infer: optional
+        device int64 [S], per simulation the number of roots that ran inference (search-with-reuse)."""
         cfg = self._cfg
         disc = float(np.float32(cfg.discount_factor))
         horizon = int(cfg.lstm_horizon_len)
@@ -559,15 +560,17 @@ class EfficientZeroMCTSCtree(object):
         model = _step_net(self, model) if net is None else net
         native = _native_trunk(model, buf)
         with _HeadVerdicts(t, model, buf, native and cat and getattr(model, "heads", None) is not None):
-            self._sims(t, model, buf, S, row, Hl, rec, native, cat, disc, horizon)
+            self._sims(t, model, buf, S, row, Hl, rec, native, cat, disc, horizon, infer)
 
-    def _sims(self, t, model, buf, S, row, Hl, rec, native, cat, disc, horizon):
+    def _sims(self, t, model, buf, S, row, Hl, rec, native, cat, disc, horizon, infer=None):
         cfg = self._cfg
         B = t.B
-        fuse = _fuse_traverse(cfg, t)
+        fuse = _fuse_traverse(cfg, t) and infer is None
         for k in range(S):
             if k == 0 or not fuse:
                 t.traverse(buf.mm, buf.seeds[k:k + 1], buf.vtp_in, int(cfg.pb_c_base), float(cfg.pb_c_init), disc)
+            if infer is not None:
+                infer[k] = (t.x >= 0).sum()
             if native:
                 # the LSTM state is gathered from / filed (reset-masked) into the state pools on the device
                 out = model.step_from_pool_lstm(buf.pool, t.x, t.action, buf.pool[k + 1], buf.extra[0], buf.extra[1],
@@ -657,6 +660,65 @@ class EfficientZeroMCTSCtree(object):
                 self._loop(t, model, buf, S, row, Hl, rec)
             roots._last_minmax = buf.mm
             self.last_record = rec
+
+    def search_with_reuse(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
+                          reward_hidden_state_roots: List[Any], to_play_batch: Union[int, List[Any]],
+                          true_action_list=None, reuse_value_list=None, seeds: torch.Tensor = None):
+        """ReZero search with value reuse for EfficientZero (mcts_ctree.py:829-955; arXiv 2404.16364), in
+        its DEFINED form: the reference builds is_reset_list over the envs that ran inference and
+        cbatch_backpropagate_with_reuse then reads it by env index (ctree_efficientzero/lib/cnode.cpp:638),
+        an out-of-range, misaligned read as soon as an env skips inference; here every env's leaf gets
+        is_reset = search_len % lstm_horizon_len == 0 (what the reference computes when no env skips).
+        Otherwise as MuZeroMCTSCtree.search_with_reuse: the true action's root child is scored with the
+        reuse value, a walk stopping on it ends there (no inference when it is expanded, its reuse
+        value backed up), the device loop runs every env's network row (skipped rows unused). Returns
+        (length, average_infer) as the reference."""
+        if true_action_list is None or reuse_value_list is None:
+            raise TypeError("search_with_reuse needs true_action_list and reuse_value_list")
+        with torch.no_grad():
+            model.eval()
+            t = roots.tree
+            if t is None:
+                raise RuntimeError("search_with_reuse: roots must be prepared (Roots.prepare / prepare_no_noise) first")
+            if t.fast_rng:
+                raise ValueError("search_with_reuse: parity (glibc) mode only")
+            if int(self._cfg.lstm_horizon_len) <= 0:
+                raise ValueError("lstm_horizon_len must be > 0 (mcts_ctree.py:899)")
+            B, S = roots.num, int(self._cfg.num_simulations)
+            t.reserve(S)
+            t.set_pb_c(int(self._cfg.pb_c_base), float(self._cfg.pb_c_init))
+            dev = t.device
+            lat0 = _latent_tensor(latent_state_roots, dev)
+            shape = lat0.shape[1:]
+            row = int(np.prod(shape)) if len(shape) else 1
+            hc0 = _latent_tensor(reward_hidden_state_roots[0], dev).reshape(B, -1)
+            hh0 = _latent_tensor(reward_hidden_state_roots[1], dev).reshape(B, -1)
+            Hl = hc0.shape[1]
+            buf = self._buf.get(B, S, shape, dev, extra=(Hl, Hl))
+            buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
+            buf.extra[0][0].copy_(hc0)
+            buf.extra[1][0].copy_(hh0)
+            buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
+            buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
+            ta = torch.as_tensor(np.asarray(true_action_list, np.int32).reshape(B) if not torch.is_tensor(
+                true_action_list) else true_action_list, device=dev)
+            rv = torch.as_tensor(np.asarray(reuse_value_list, np.float32).reshape(B) if not torch.is_tensor(
+                reuse_value_list) else reuse_value_list, device=dev)
+            rec = None
+            if getattr(self, "record", False):
+                rec = _Recorder(S, B, t.A, dev)
+                rec.is_reset = torch.zeros((S, B), dtype=torch.int32, device=dev)
+                rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
+            infer = torch.zeros(S, dtype=torch.int64, device=dev)
+            t.set_reuse(ta, rv)
+            try:
+                self._loop(t, model, buf, S, row, Hl, rec, infer=infer)
+            finally:
+                t.set_reuse(None)
+            roots._last_minmax = buf.mm
+            self.last_record = rec
+            counts = infer.cpu().numpy()
+        return int(counts[-1]) if S else 0, float(counts.sum()) / max(S, 1)
 
     def _capture(self, t, model, buf, S, row, Hl):
         """The S-simulation loop captured as one HIP graph (see MuZeroMCTSCtree._capture)."""
