@@ -614,15 +614,19 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     __syncthreads();
     stamp(5);
     if (wv == 0) {
+      // wave 0 files the leaf's record and backs up while wave 1 initialises the leaf's children
+      // (disjoint nodes, expand_wave's part argument)
       const float r = s_dec[0], v = s_dec[1];
       const int leaf = t.path[s_len[0]];
       const float *plg = llg + p.Vr + p.Vv;
-      expand_wave(t, 0, leaf, s_leafvtp, k + 1, r, plg);
+      expand_wave(t, 0, leaf, s_leafvtp, k + 1, r, plg, -1, kExp2fTab, 1);
       backup_wave(t, 0, 0, 1, s_mm, s_leafvtp, v, p.disc);
       if (p.rec_dec) {
         if (lane < 2) p.rec_dec[((size_t)k * B + b) * 2 + lane] = lane ? v : r;
         if (lane < A) p.rec_logits[((size_t)k * B + b) * A + lane] = plg[lane];
       }
+    } else if (wv == 1) {
+      expand_wave(t, 0, 0, 0, k + 1, 0.0f, llg + p.Vr + p.Vv, -1, kExp2fTab, 2);
     }
     stamp(6);
   }

@@ -19,3 +19,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_conv_ez -o conv
 timeout -k 10 120 python bench.py --no-cpu-baseline --rng philox > $out/bench_philox.json 2>&1
 timeout -k 10 120 python bench.py --no-cpu-baseline --zero-heads > $out/bench_zero_heads.json 2>&1
 timeout -k 10 200 python bench.py --step collect --no-cpu-baseline > $out/bench_collect.json 2>$out/bench_collect.err
+# config 1 (8 envs x 25 sims): the GPU search at that shape and the pure-Python ptree restatement on
+# this box's host (1 thread, MLP on torch-CPU)
+timeout -k 10 120 python bench.py --envs 8 --sims 25 --no-cpu-baseline > $out/bench_c1_gpu.json 2>$out/bench_c1_gpu.err
+timeout -k 10 120 python tools/ptree_bench.py --secs 15 > $out/ptree_c1_cpu.json 2>$out/ptree_c1_cpu.err
+# EfficientZero one-launch: phase timing; MuZero conv phase timing
+timeout -k 10 150 python tools/conv_phase_timing.py --kind ez > $out/conv_phase_ez.txt 2>&1
+timeout -k 10 150 python tools/conv_phase_timing.py --kind mz > $out/conv_phase_mz.txt 2>&1
