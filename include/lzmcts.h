@@ -355,7 +355,7 @@ int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_
  * [reward planes | hpool[x][b]] with its search_len, the tiles run the gate GEMM + cell for 64 rows x 16
  * units and hand the h1 rows back; c state filed into cpool[k + 1] and h state into hpool[k + 1],
  * zeroed where search_len % horizon == 0 (mcts_ctree.py:810-813). hpool / cpool [S + 1][B][H] (slot 0
- * = the roots' reward_hidden_state), lstm_w32 = lzm_ez_lstm_prepare_f32(W [4H][r_ch * 64 + H]),
+ * = the roots' reward_hidden_state), lstm_frag = lzm_ez_lstm_prepare(W [4H][r_ch * 64 + H]),
  * lstm_bias [4H] = b_ih + b_hh, vp_s / vp_t the value-prefix BatchNorm as an affine map; heads as
  * lzm_search_conv with the reward head reading relu(h1 * vp_s + vp_t) (K = H). rec_reset (nullable)
  * is_reset int32 [S][B]. Same results as the generic path (traverse, lzm_conv_trunk_xin_p,
@@ -364,7 +364,7 @@ int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_
 int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount,
                        float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, float *hpool,
                        float *cpool, int H, int horizon, const float *trunk_w, const float *actmap, int n_dres,
-                       int n_pres, int r_ch, int h_ch, const float *lstm_w32, const float *lstm_bias,
+                       int n_pres, int r_ch, int h_ch, const float *lstm_frag, const float *lstm_bias,
                        const float *vp_s, const float *vp_t, const float *w1t, const float *b1, const float *w2q,
                        const float *b2, int Khd, int off_policy, int Vr, int Vv, int categorical, int32_t *rec_x,
                        int32_t *rec_a, int32_t *rec_len, float *rec_decoded, float *rec_logits, int32_t *rec_reset,
@@ -450,9 +450,6 @@ int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *cpool, const
  * search_len[b] % horizon == 0). H % 16 == 0. Within f32 tolerance of the f32 GEMM (rtol 1e-4). */
 int64_t lzm_ez_lstm_frag_floats(int K, int H);
 int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out);
-/* the same weights in f32, in the fragment order before the split (K * 4H floats): the one-launch
- * EfficientZero search (lzm_search_conv_ez) splits them on the device into the identical terms */
-int lzm_ez_lstm_prepare_f32(int K, int H, const float *W, float *out);
 /* workspace (optional, zero-filled once): lzm_ez_lstm_workspace_bytes(B, H) bytes; with it the K range
  * is split over two workgroups per tile when every workgroup fits on the GPU at once (err: a sticky
  * int32 counting hand-off timeouts, required with the workspace). */

@@ -65,7 +65,6 @@ SIGNATURES = {
     "lzm_ez_lstm_cell": [_i, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp],
     "lzm_ez_lstm_frag_floats": [_i, _i],
     "lzm_ez_lstm_prepare": [_i, _i, _vp, _vp],
-    "lzm_ez_lstm_prepare_f32": [_i, _i, _vp, _vp],
     "lzm_ez_lstm_workspace_bytes": [_i, _i],
     "lzm_error_word": [_vp, _i],
     "lzm_debug_lstm_stamps": [_vp],

@@ -143,8 +143,7 @@ class FoldedConvNet:
         self.t = None
         self._ver = None
         self.native = None  # device weight blob of lzm_conv_trunk (GPU models with a 64x8x8 latent)
-        self.lstm_frag = None  # EZ: lzm_ez_lstm_step's gate-weight fragments
-        self.lstm_w32 = None  # EZ: the same in f32 (lzm_search_conv_ez splits them on the device)
+        self.lstm_frag = None  # EZ: the gate-weight fragments of lzm_ez_lstm_step and lzm_search_conv_ez
         self._lstm_ws = {}
         # EZ: the gate GEMM + cell as one split-bf16 launch (the f32 precision keeps rocBLAS + the cell
         # pass; LZM_LSTM_FUSED=0 too)
@@ -197,14 +196,11 @@ class FoldedConvNet:
             self.native = blob
             self.actmap = t["dyn_actmap"]  # [A, 64, 8, 8], re-folded in place
             self.heads = heads
-            self.lstm_pack = lstm
-            if lstm is not None:  # views into one blob: [pre-split fragments | f32 fragment order]
-                n32 = t["lstm_w"].numel()
-                self.lstm_frag, self.lstm_w32 = lstm[:lstm.numel() - n32], lstm[lstm.numel() - n32:]
+            self.lstm_frag = lstm
         else:
             self.native.copy_(blob)
             if lstm is not None:
-                self.lstm_pack.copy_(lstm)
+                self.lstm_frag.copy_(lstm)
             if heads is not None:
                 for k, v in heads.items():
                     if torch.is_tensor(v):
@@ -223,11 +219,7 @@ class FoldedConvNet:
         host = np.zeros(n, np.float32)
         w = np.ascontiguousarray(W.detach().float().cpu().numpy())
         _lib.check(L.lzm_ez_lstm_prepare(K, H4 // 4, w.ctypes.data, host.ctypes.data), "lzm_ez_lstm_prepare")
-        # the one-launch search's copy: f32 in the same fragment order, split on the device
-        host32 = np.zeros(H4 * K, np.float32)
-        _lib.check(L.lzm_ez_lstm_prepare_f32(K, H4 // 4, w.ctypes.data, host32.ctypes.data),
-                   "lzm_ez_lstm_prepare_f32")
-        return torch.cat([torch.from_numpy(host), torch.from_numpy(host32)]).to(W.device)
+        return torch.from_numpy(host).to(W.device)
 
     def _pack_heads(self):
         """lzm_conv_heads layouts (csrc/lzm_heads.h) of the folded head MLPs, or None if they do

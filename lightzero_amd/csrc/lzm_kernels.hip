@@ -2515,13 +2515,13 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
                                   float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool,
                                   float *hpool, float *cpool, int H, int horizon, const float *trunk_w,
                                   const float *actmap, int n_dres, int n_pres, int r_ch, int h_ch,
-                                  const float *lstm_w32, const float *lstm_bias, const float *vp_s, const float *vp_t,
+                                  const float *lstm_frag, const float *lstm_bias, const float *vp_s, const float *vp_t,
                                   const float *w1t, const float *b1, const float *w2q, const float *b2, int Khd,
                                   int off_policy, int Vr, int Vv, int categorical, int32_t *rec_x, int32_t *rec_a,
                                   int32_t *rec_len, float *rec_decoded, float *rec_logits, int32_t *rec_reset,
                                   void *stream) {
   const int S = num_simulations;
-  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !hpool || !cpool || !trunk_w || !actmap || !lstm_w32 ||
+  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !hpool || !cpool || !trunk_w || !actmap || !lstm_frag ||
       !lstm_bias || !vp_s || !vp_t || !w1t || !b1 || !w2q || !b2 || S <= 0) {
     set_err("lzm_search_conv_ez: null argument or no simulations");
     return LZM_ERR_ARG;
@@ -2537,7 +2537,7 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
       horizon <= 0 || Vr <= 0 || Vv <= 0 || Vr > 1024 || Vv > 1024 || (!categorical && (Vr != 1 || Vv != 1)) ||
       S + 1 > 0xffff ||
       (((uintptr_t)trunk_w | (uintptr_t)actmap | (uintptr_t)w1t | (uintptr_t)w2q | (uintptr_t)latent_pool |
-        (uintptr_t)hpool | (uintptr_t)cpool | (uintptr_t)lstm_w32 | (uintptr_t)vp_s | (uintptr_t)vp_t) & 15)) {
+        (uintptr_t)hpool | (uintptr_t)cpool | (uintptr_t)lstm_frag | (uintptr_t)vp_s | (uintptr_t)vp_t) & 15)) {
     set_err("lzm_search_conv_ez: unsupported network shape (64x8x8 latent, <= 32 reward / head planes, K per head a "
             "multiple of 128 and <= 1024, LSTM width a multiple of 128, (r_ch * 64 + H) % 128 == 0, horizon > 0, "
             "16-B aligned weights and pools)");
@@ -2600,7 +2600,7 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
   p.xin = wsf; p.h1g = wsf + f_xin; p.kpart = wsf + f_xin + f_h1;
   p.xflags = wsl; p.tflags = wsl + (size_t)S * B; p.pflags = wsl + (size_t)S * B + (size_t)S * T;
   p.Kx = Kx; p.H = H; p.horizon = horizon; p.hpool = hpool; p.cpool = cpool;
-  p.lwf32 = lstm_w32; p.lbias = lstm_bias; p.vp_s = vp_s; p.vp_t = vp_t;
+  p.lwfrag = reinterpret_cast<const uint16_t *>(lstm_frag); p.lbias = lstm_bias; p.vp_s = vp_s; p.vp_t = vp_t;
   p.nmb = nmb; p.T = T;
   // dynamic LDS plan (float offsets, 16-B aligned): the activation buffers / LSTM stage buffers first
   size_t o = std::max((size_t)2 * kBxBuf / 2, (size_t)kLsLdsBytes / 4);
@@ -2675,15 +2675,6 @@ extern "C" int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *c
 extern "C" int64_t lzm_ez_lstm_frag_floats(int K, int H) {
   if (K <= 0 || H <= 0 || K % kLsKc || H % kLsUnits) return -1;
   return (int64_t)K * 4 * H * 3 / 2;
-}
-
-extern "C" int lzm_ez_lstm_prepare_f32(int K, int H, const float *W, float *out) {
-  if (lzm_ez_lstm_frag_floats(K, H) < 0 || !W || !out) {
-    set_err("lzm_ez_lstm_prepare_f32: need K % 64 == 0, H % 16 == 0 and buffers");
-    return LZM_ERR_ARG;
-  }
-  ls_pack_f32(W, K, H, out);
-  return LZM_OK;
 }
 
 extern "C" int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out) {

@@ -376,7 +376,7 @@ typedef unsigned lp_u4 __attribute__((ext_vector_type(4)));
 typedef float lp_f4 __attribute__((ext_vector_type(4)));
 constexpr int kLpThreads = 256;
 #ifndef LZM_LP_DEPTH
-#define LZM_LP_DEPTH 3  // register sets of staged loads: global loads run LZM_LP_DEPTH - 1 stages ahead (2..4)
+#define LZM_LP_DEPTH 2  // register sets of staged loads: global loads run LZM_LP_DEPTH - 1 stages ahead (2..4)
 #endif
 #ifndef LZM_LP_DIAG
 #define LZM_LP_DIAG 0  // timing experiments only (results invalid): 1 = no global loads after the first two
@@ -387,61 +387,19 @@ struct LpTile {
   int row0, nb, kh;  // tile rows [row0, row0 + 64), hidden units [16 nb, 16 nb + 16), K half
 };
 
-// f32 gate weights in MFMA fragment order for the one-launch search: element (nb, column tile, 32-K
-// chunk, half e / 4, lane, e % 4) = W[(gate H + unit) K + k] with unit = 16 nb + 4 ct + (lane & 15) / 4, gate = lane & 3,
-// k = 32 chunk + 8 (lane >> 4) + e — ls_pack's order before the split, so splitting a lane's 8 values
-// on the device (the same round-to-nearest-even terms as the host's bx_split) gives ls_pack's
-// fragments bit for bit, from two thirds of the bytes.
-inline void ls_pack_f32(const float *W, int K, int H, float *out) {
-  const int nch = K / 32, NB = H / kLsUnits;
-  for (int nb = 0; nb < NB; ++nb)
-    for (int w = 0; w < 4; ++w)
-      for (int j = 0; j < nch; ++j)
-        for (int lane = 0; lane < 64; ++lane)
-          for (int e = 0; e < 8; ++e) {
-            const int n = lane & 15, unit = kLsUnits * nb + 4 * w + (n >> 2), gate = n & 3;
-            const int k = 32 * j + 8 * (lane >> 4) + e;
-            out[(((((size_t)(nb * 4 + w) * nch + j) * 2 + (e >> 2)) * 64 + lane) * 4) + (e & 3)] =
-                W[((size_t)gate * H + unit) * K + k];
-          }
-}
-
-// three bf16 terms of 8 f32 values (two float4s) as three 16-B words (bx_split's terms, hardware cvt)
-__device__ __forceinline__ void lp_split8(const lp_f4 &x0, const lp_f4 &x1, uint4 &h, uint4 &m, uint4 &l) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  uint32_t hh[4], mm[4], ll[4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const lp_f4 x = u ? x1 : x0;
-    const f2 pr[2] = {f2{x[0], x[1]}, f2{x[2], x[3]}};
-#pragma unroll
-    for (int v = 0; v < 2; ++v) {
-      const b2 th = __builtin_convertvector(pr[v], b2);
-      const f2 r1 = pr[v] - __builtin_convertvector(th, f2);
-      const b2 tm = __builtin_convertvector(r1, b2);
-      const b2 tl = __builtin_convertvector(r1 - __builtin_convertvector(tm, f2), b2);
-      hh[2 * u + v] = __builtin_bit_cast(uint32_t, th);
-      mm[2 * u + v] = __builtin_bit_cast(uint32_t, tm);
-      ll[2 * u + v] = __builtin_bit_cast(uint32_t, tl);
-    }
-  }
-  h = uint4{hh[0], hh[1], hh[2], hh[3]};
-  m = uint4{mm[0], mm[1], mm[2], mm[3]};
-  l = uint4{ll[0], ll[1], ll[2], ll[3]};
-}
-
 // the GEMM part: acc[t] = the tile's K-half partial sums (row tile t = rows 16 t .. + 15 of the tile,
 // this wave's 16 gate columns), accumulated from zero exactly as the 512-thread kernel does.
-// lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4); wf32:
-// ls_pack_f32's layout. Both operands are read as f32 and split on the fly; a thread stages 4 values
-// of 4 A rows through LDS and loads the B fragments (chunk 0 and 1, column tile = its wave, its lane)
-// of every stage, which its own MFMAs consume: B never touches LDS.
-// Loads go through buffer resources (one
-// 32-bit per-thread offset each, the stage in the scalar offset): no 64-bit address per load for the
-// compiler to hoist out of the simulation loop and spill.
+// lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4); wfrag:
+// ls_pack's split-bf16 fragments (lzm_ez_lstm_prepare, the ones ez_lstm_gemm_cell_kernel reads). A
+// is read as f32 and split on the fly (a thread stages 4 values of 4 rows through LDS); a wave loads
+// the B fragments its own MFMAs consume (chunk 0 and 1, column tile = the wave, its lane, 3 terms)
+// straight into registers: B never touches LDS. (Measured: B read as f32 in the same order and split
+// on the device — two thirds of the bytes — made the GEMM slower, 29 K -> 33 K cycles per
+// simulation: the split's VALU work sits on the stage's critical path, the bytes do not.)
+// Loads go through buffer resources (one 32-bit per-thread offset each, the stage in the scalar
+// offset): no 64-bit address per load for the compiler to hoist out of the simulation loop and spill.
 __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, const __amdgpu_buffer_rsrc_t xr,
-                                             const float *wf32, uint16_t *lds, bxf4 (&acc)[4]) {
+                                             const uint16_t *wfrag, uint16_t *lds, bxf4 (&acc)[4]) {
   const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6;
   const int nch = K / 32, kspan = K / 2, nst = kspan / kLsKc, k0 = tl.kh * kspan;
   // A: wave-instruction u of wave w reads 4 whole 256-B row segments of the stage (rows 16 w + 4 u +
@@ -455,25 +413,26 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
     arow[u] = tl.row0 + rr < B;
     avo[u] = ((tl.row0 + (arow[u] ? rr : 0)) * K + k0 + 4 * a4) * 4;
   }
-  // B: ls_pack_f32's layout [nb][column tile][chunk][half][lane][4]: wave-instruction (chunk, half)
+  // B: ls_pack's layout [nb][column tile][chunk][term][lane][8 bf16]: wave-instruction (chunk, term)
   // reads 1 KiB contiguous
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float *>(wf32 + (size_t)tl.nb * 4 * nch * 64 * 8), 0, 4 * nch * 64 * 8 * 4, 0x00020000);
-  const int bvo = ((ct * nch * 2) * 64 + lane) * 16;  // (column tile, chunk 0, half 0, lane), bytes
-  lp_f4 va[LZM_LP_DEPTH][4], vb[LZM_LP_DEPTH][4];  // global loads LZM_LP_DEPTH - 1 stages ahead
-  uint4 wreg[2][3];  // the next stage's B fragments (chunk, term) of this wave's column tile, split
-  auto load_stage = [&](int s, lp_f4(&VA)[4], lp_f4(&VB)[4]) __attribute__((always_inline)) {
+  const __amdgpu_buffer_rsrc_t wq = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t *>(wfrag + (size_t)tl.nb * 4 * nch * 3 * 64 * 8), 0, 4 * nch * 3 * 64 * 16, 0x00020000);
+  const int bqo = ((ct * nch * 3) * 64 + lane) * 16;  // (column tile, chunk 0, term 0, lane), bytes
+  lp_f4 va[LZM_LP_DEPTH][4];
+  uint4 vb[LZM_LP_DEPTH][6];  // global loads LZM_LP_DEPTH - 1 stages ahead
+  uint4 wreg[2][3];  // the next stage's B fragments (chunk, term) of this wave's column tile
+  auto load_stage = [&](int s, lp_f4(&VA)[4], uint4(&VB)[6]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       VA[u] = arow[u] ? __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(xr, avo[u], s * kLsKc * 4, 16))
                       : lp_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {  // chunk c = u / 2 of the stage, half u % 2 of the lane's 8 values
-      const int j = (k0 / 32) + 2 * s + u / 2;
-      VB[u] = __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(wr, bvo, (2 * j + (u & 1)) * 64 * 16, 0));
+    for (int u = 0; u < 6; ++u) {  // chunk u / 3 of the stage, term u % 3
+      const int j = (k0 / 32) + 2 * s + u / 3;
+      VB[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wq, bqo, (3 * j + u % 3) * 64 * 16, 0));
     }
   };
-  auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const lp_f4(&VB)[4]) __attribute__((always_inline)) {
+  auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const uint4(&VB)[6]) __attribute__((always_inline)) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     typedef __bf16 b2 __attribute__((ext_vector_type(2)));
     uint16_t *abuf = lds + bsel * kLsStage;
@@ -499,7 +458,9 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
     }
     // B: a wave loads exactly the fragments its own MFMAs consume, so they stay in registers
 #pragma unroll
-    for (int c = 0; c < 2; ++c) lp_split8(VB[2 * c], VB[2 * c + 1], wreg[c][0], wreg[c][1], wreg[c][2]);
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) wreg[c][q] = VB[3 * c + q];
   };
 #pragma unroll
   for (int s0 = 0; s0 < LZM_LP_DEPTH - 1; ++s0)

@@ -77,7 +77,7 @@ struct ConvSearchArgs {
   float *xin;             // [B][Kx] LSTM input rows [reward planes | leaf hidden state] (sc1 hand-off)
   int Kx, H, horizon;     // Kx = r_ch * 64 + H; lstm_horizon_len
   float *hpool, *cpool;   // [S + 1][B][H] state pools (slot 0 = the roots' state)
-  const float *lwf32;     // gate weights, f32 in fragment order (lzm_ez_lstm_prepare_f32)
+  const uint16_t *lwfrag; // gate weights, split-bf16 fragments (lzm_ez_lstm_prepare)
   const float *lbias;     // [4H] b_ih + b_hh
   const float *vp_s, *vp_t;  // value-prefix BatchNorm as an affine map (relu(h1 * s + t) feeds the head)
   float *h1g;             // [B][H] unmasked LSTM outputs (sc1 hand-off, tile -> root)
@@ -981,7 +981,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         if (STAMPS && tid == 0) st_acc[10] += w1 - w0;
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(p.xin, 0, B * Kx * 4, 0x00020000);
         bxf4 acc[4];
-        lp_tile_gemm(tile, B, Kx, xr, p.lwf32, act, acc);
+        lp_tile_gemm(tile, B, Kx, xr, p.lwfrag, act, acc);
         if (STAMPS && tid == 0) st_acc[13] += st_now() - w1;
         const __amdgpu_buffer_rsrc_t pr =
             __builtin_amdgcn_make_buffer_rsrc(p.kpart + (size_t)q * (kLpThreads * 16), 0, kLpThreads * 16 * 4, 0x00020000);

@@ -541,7 +541,7 @@ class EfficientZeroMCTSCtree(object):
         net = _step_net(self, model)
         hp = getattr(net, "heads", None)
         if getattr(net, "native", None) is None or hp is None or getattr(net, "precision", None) != "bf16x3" \
-                or not getattr(net, "ez", False) or getattr(net, "lstm_w32", None) is None:
+                or not getattr(net, "ez", False) or getattr(net, "lstm_frag", None) is None:
             return None
         if hp["Khd"] % 128 or hp["off_policy"] % 128 or hp["A"] != t.A or hp["Kr"] != Hl \
                 or (net.r_ch * 64 + Hl) % 128:

@@ -200,7 +200,7 @@ class DeviceTree:
         call("lzm_search_conv_ez", self.h, int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax),
              ptr(seeds), ptr(vtp_in), ptr(pool), ptr(hpool), ptr(cpool), int(hpool.shape[2]), int(horizon),
              ptr(net.native), ptr(net.actmap), int(net.n_dres), int(net.n_pres), int(net.r_ch), int(net.h_ch),
-             ptr(net.lstm_w32), ptr(t["lstm_b"]), ptr(t["vp_s"]), ptr(t["vp_t"]), ptr(hp["w1t"]), ptr(hp["b1"]),
+             ptr(net.lstm_frag), ptr(t["lstm_b"]), ptr(t["vp_s"]), ptr(t["vp_t"]), ptr(hp["w1t"]), ptr(hp["b1"]),
              ptr(hp["w2q"]), ptr(hp["b2"]), int(hp["Khd"]), int(hp["off_policy"]), int(hp["Vr"]), int(hp["Vv"]),
              int(bool(categorical)), r("x"), r("action"), r("search_len"), r("decoded"), r("policy_logits"),
              r("is_reset"), stream_ptr(stream))
