@@ -2481,7 +2481,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_r = (int)o; o += round4((size_t)Kr);
   p.off_hd = (int)o; o += round4((size_t)Khd);
   p.off_hid = (int)o; o += 96;
-  p.off_part = (int)o; o += 2 * kHdParts * 32;
+  p.off_part = (int)o; o += 3 * kHdParts * 32;
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
   const size_t lds = o * sizeof(float);
@@ -2616,7 +2616,7 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
   p.off_r = (int)o; o += round4((size_t)H);
   p.off_hd = (int)o; o += round4((size_t)Khd);
   p.off_hid = (int)o; o += 96;
-  p.off_part = (int)o; o += 2 * kHdParts * 32;
+  p.off_part = (int)o; o += 3 * kHdParts * 32;
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
   const size_t lds = o * sizeof(float);

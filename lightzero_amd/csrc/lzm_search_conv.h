@@ -90,40 +90,6 @@ struct ConvSearchArgs {
       off_lg, off_seed;
 };
 
-// Hidden layer of one head for this workgroup's env (conv_heads_kernel's arithmetic, same order):
-// lane (part, c) sums its 128-wide K range with its 32 weight float4s (all loads in flight at once:
-// one L2 round trip per head), the partial sums meet in K-part order, + bias, ReLU -> hid[c].
-// K is a multiple of 128 (lzm_search_conv checks).
-__device__ __forceinline__ void sc_head_hidden(const float *in, int K, const float *w1t, int head, float bias,
-                                               float *part, float *hid, int tid) {
-  const int pt = tid >> 5, c = tid & 31;
-  float acc = 0.0f;
-  if (pt * 128 < K) {
-    const float4 *x4 = reinterpret_cast<const float4 *>(in + pt * 128);
-    const float4 *w = reinterpret_cast<const float4 *>(w1t) + ((size_t)(head * kHdParts + pt) * 32) * 32 + c;
-    float4 w1[32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) w1[q] = w[(size_t)q * 32];
-#pragma unroll
-    for (int q = 0; q < 32; ++q) {
-      const float4 x = x4[q];
-      acc = __fmaf_rn(x.x, w1[q].x, acc);
-      acc = __fmaf_rn(x.y, w1[q].y, acc);
-      acc = __fmaf_rn(x.z, w1[q].z, acc);
-      acc = __fmaf_rn(x.w, w1[q].w, acc);
-    }
-  }
-  part[pt * 32 + c] = acc;
-  __syncthreads();
-  if (tid < 32) {
-    float s = 0.0f;
-#pragma unroll
-    for (int q = 0; q < kHdParts; ++q) s += part[q * 32 + tid];
-    hid[tid] = fmaxf(s + bias, 0.0f);
-  }
-  __syncthreads();
-}
-
 // Parity-mode draw offset of root b in simulation k: the sum of the depth flags of roots < b (the
 // reference's single rand() stream, cnode.cpp:783-796). Wave-wide, b <= 256 (lzm_search_conv checks
 // B <= 256): sc_lookback_issue puts every flag of a lane in flight (four loads), sc_lookback_finish
@@ -255,8 +221,12 @@ __device__ __forceinline__ void sc_head_out(const ConvSearchArgs &p, const float
   }
 }
 
-// sc_head_hidden / sc_head_out with the weights read through buffer resources: one 32-bit per-thread
-// offset, the per-load constant in the scalar / immediate offset. With plain pointers the compiler
+// Hidden layer of one head for this workgroup's env (conv_heads_kernel's arithmetic, same order):
+// lane (part, c) sums its 128-wide K range with its 32 weight float4s (all loads in flight at once:
+// one L2 round trip per head), the partial sums meet in K-part order, + bias, ReLU -> hid[c]. K is a
+// multiple of 128 (lzm_search_conv checks). The weights are read through buffer resources (here and
+// in sc_head_out1_rs): one 32-bit per-thread offset, the per-load constant in the scalar /
+// immediate offset. With plain pointers the compiler
 // hoisted one 64-bit address per load out of the simulation loop (24 per head) and, in the
 // EfficientZero kernel, spilled them: every load then waited for a scratch reload (V/P hidden layers
 // 40 K cycles per simulation instead of ~10 K). Same values, same FMA order, same bits.
@@ -288,6 +258,66 @@ __device__ __forceinline__ void sc_head_hidden_rs(const float *in, int K, const 
 #pragma unroll
     for (int q = 0; q < kHdParts; ++q) s += part[q * 32 + tid];
     hid[tid] = fmaxf(s + bias, 0.0f);
+  }
+  __syncthreads();
+}
+
+// NH hidden layers (heads H0 .. H0 + NH - 1 of w1t) in one pass, sc_head_hidden's arithmetic and
+// order for each head (same bits): the weights stream as 2 NH half-heads of 16 float4s per lane, the
+// next half's loads in flight while the FMAs consume the current one, so the heads' L2 streams run
+// back to back instead of one load-wait-reduce round each; one barrier pair for all of them.
+// in[h] / K[h]: head H0 + h's input (LDS) and width; part: NH kHdParts 32 floats; hid[32 h + c].
+// (Measured, Breakout one-launch search: the three hidden layers 14.9 K -> 12.7 K cycles per
+// simulation.)
+template <int NH, int H0>
+__device__ __forceinline__ void sc_heads_hidden_rs(const float *const (&in)[NH], const int (&K)[NH], const float *w1t,
+                                                   const float *b1, float *part, float *hid, int tid) {
+  const int pt = tid >> 5, c = tid & 31;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w1t), 0, 3 * kHdParts * 32 * 32 * 16, 0x00020000);
+  const int vo = ((pt * 32) * 32 + c) * 16;
+  bool on[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) on[h] = pt * 128 < K[h];
+  float4 wb[2][16];
+  float acc[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) acc[h] = 0.0f;
+  auto load = [&](int s, float4(&W)[16]) __attribute__((always_inline)) {
+    const int h = s >> 1, half = s & 1;
+    if (on[h]) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        W[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rs, vo, ((H0 + h) * kHdParts * 32 * 32 + (16 * half + q) * 32) * 16, 0));
+    }
+  };
+  load(0, wb[0]);
+#pragma unroll
+  for (int s = 0; s < 2 * NH; ++s) {
+    if (s + 1 < 2 * NH) load(s + 1, wb[(s + 1) & 1]);
+    const int h = s >> 1, half = s & 1;
+    if (on[h]) {
+      const float4 *x4 = reinterpret_cast<const float4 *>(in[h] + pt * 128) + 16 * half;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float4 x = x4[q], w = wb[s & 1][q];
+        acc[h] = __fmaf_rn(x.x, w.x, acc[h]);
+        acc[h] = __fmaf_rn(x.y, w.y, acc[h]);
+        acc[h] = __fmaf_rn(x.z, w.z, acc[h]);
+        acc[h] = __fmaf_rn(x.w, w.w, acc[h]);
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < NH; ++h) part[(h * kHdParts + pt) * 32 + c] = acc[h];
+  __syncthreads();
+  if (tid < 32 * NH) {
+    const int h = tid >> 5, cc = tid & 31;
+    float s = 0.0f;
+#pragma unroll
+    for (int q = 0; q < kHdParts; ++q) s += part[(h * kHdParts + q) * 32 + cc];
+    hid[tid] = fmaxf(s + b1[32 * H0 + tid], 0.0f);
   }
   __syncthreads();
 }
@@ -559,10 +589,11 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     __syncthreads();
     stamp(2);
     // ---- head MLPs: the three hidden layers
-    sc_head_hidden(lr, p.Kr, p.w1t, 0, tid < 32 ? p.b1[tid] : 0.0f, lpart, lhid, tid);
-    sc_head_hidden(lhd, p.off_policy, p.w1t, 1, tid < 32 ? p.b1[32 + tid] : 0.0f, lpart, lhid + 32, tid);
-    sc_head_hidden(lhd + p.off_policy, p.Khd - p.off_policy, p.w1t, 2, tid < 32 ? p.b1[64 + tid] : 0.0f, lpart,
-                   lhid + 64, tid);
+{
+      const float *const in[3] = {lr, lhd, lhd + p.off_policy};
+      const int K[3] = {p.Kr, p.off_policy, p.Khd - p.off_policy};
+      sc_heads_hidden_rs<3, 0>(in, K, p.w1t, p.b1, lpart, lhid, tid);
+    }
     stamp(3);
     // output columns (w2q [8][N2][4]: float4 k4 of column j at (k4 * N2 + j), so a wave-instruction
     // reads 64 consecutive columns' float4s, 1 KiB contiguous), up to three columns per thread per
