@@ -589,7 +589,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     __syncthreads();
     stamp(2);
     // ---- head MLPs: the three hidden layers
-{
+    {
       const float *const in[3] = {lr, lhd, lhd + p.off_policy};
       const int K[3] = {p.Kr, p.off_policy, p.Khd - p.off_policy};
       sc_heads_hidden_rs<3, 0>(in, K, p.w1t, p.b1, lpart, lhid, tid);
