@@ -66,6 +66,12 @@ def parse():
                    help="total CPU-baseline sample over the four variants")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--zero-heads", action="store_true", help="reference zero-init last layers (all-tie search)")
+    p.add_argument("--workload", choices=["cartpole", "breakout"], default="cartpole",
+                   help="cartpole: BASELINE.json config 2 (the headline); breakout: config 5's per-GPU shard "
+                        "(conv MuZeroModel, 4x64x64 frames, 4 actions; 2048 envs = 256 per GPU x 8)")
+    p.add_argument("--secondary", choices=["breakout", "none"], default="breakout",
+                   help="after the headline, also time config 5's sharded collect step (Breakout stand-in env, "
+                        "search + env + recording + trajectory all-gather) and report it in the line's 'config5'")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: the ranks join a gloo group and rank 0 prints who joined")
     return p.parse_args()
@@ -132,35 +138,65 @@ def dry_run(world, rank, local):
         dist.destroy_process_group()
 
 
-def build_model(device, zero_heads, seed):
-    from lightzero_amd.model_mlp import cartpole_muzero_model
-    torch.manual_seed(seed)
-    m = cartpole_muzero_model(random_heads=not zero_heads)
-    # random BatchNorm statistics so eval-mode BN is not the identity
-    g = torch.Generator().manual_seed(seed + 1)
+def _random_bn(m, seed):
+    """random BatchNorm statistics so eval-mode BN is not the identity"""
+    g = torch.Generator().manual_seed(seed)
     for mod in m.modules():
-        if isinstance(mod, torch.nn.BatchNorm1d):
+        if isinstance(mod, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
             with torch.no_grad():
                 mod.running_mean.copy_(torch.randn(mod.running_mean.shape, generator=g) * 0.1)
                 mod.running_var.copy_(torch.rand(mod.running_var.shape, generator=g) * 0.5 + 0.75)
                 mod.weight.copy_(torch.rand(mod.weight.shape, generator=g) * 0.5 + 0.75)
                 mod.bias.copy_(torch.randn(mod.bias.shape, generator=g) * 0.1)
+
+
+def build_model(device, zero_heads, seed):
+    from lightzero_amd.model_mlp import cartpole_muzero_model
+    torch.manual_seed(seed)
+    m = cartpole_muzero_model(random_heads=not zero_heads)
+    _random_bn(m, seed + 1)
     return m.to(device).eval()
+
+
+def build_conv_model(device, seed=0, zero_heads=False):
+    """config 5's network: the restated conv MuZeroModel at Breakout's shapes (atari_muzero_config.py:
+    obs 4x64x64, 4 actions, support 601), random weights (non-zero heads unless zero_heads) and BN stats"""
+    from lightzero_amd.model_conv import atari_muzero_model
+    torch.manual_seed(seed)
+    m = atari_muzero_model(last_linear_layer_init_zero=bool(zero_heads))
+    _random_bn(m, seed + 1)
+    return m.to(device).eval()
+
+
+WORKLOADS = {
+    # name: (actions, observation shape, device env of the collect step)
+    "cartpole": (2, (4,), "cartpole"),
+    "breakout": (4, (4, 64, 64), "breakout"),
+}
+
+
+def synthetic_obs(workload, B, rng):
+    """config 2: N(0,1) [B, 4]; config 5: frames U{0..255}/255 [B, 4, 64, 64]"""
+    if workload == "cartpole":
+        return rng.normal(size=(B, 4)).astype(np.float32)
+    return (rng.integers(0, 256, size=(B, 4, 64, 64)).astype(np.float32) / 255.0).astype(np.float32)
 
 
 class GraphStep:
     """One collect-time search pass (muzero.py:617-690) as one HIP graph (DeviceSearchStep):
-    initial_inference -> Roots.prepare (noise) -> fused search -> distributions / values; the
-    traverse seeds advance on the device every replay."""
+    initial_inference -> Roots.prepare (noise) -> one-launch search -> distributions / values; the
+    traverse seeds advance on the device every replay. workload: config 2 (MLP) or config 5 (conv,
+    BN-folded initial inference + lzm_search_conv)."""
 
-    def __init__(self, B, S, model, device, rng_mode, seed):
+    def __init__(self, B, S, model, device, rng_mode, seed, workload="cartpole"):
         from lightzero_amd.collect import DeviceSearchStep
         rng = np.random.default_rng(seed)
+        A, shape, _ = WORKLOADS[workload]
         self.B, self.S = B, S
-        self.step = DeviceSearchStep(model, B, S, [[0, 1]] * B, (4,), device, noise_weight=0.25, seed=seed,
+        self.step = DeviceSearchStep(model, B, S, [list(range(A))] * B, shape, device, noise_weight=0.25, seed=seed,
                                      rng_mode=rng_mode, graph=True)
-        self.step.set_inputs(obs=torch.from_numpy(rng.normal(size=(B, 4)).astype(np.float32)).to(device),
-                             noises=torch.from_numpy(rng.dirichlet([0.3, 0.3], size=B).astype(np.float32)).to(device))
+        self.step.set_inputs(obs=torch.from_numpy(synthetic_obs(workload, B, rng)).to(device),
+                             noises=torch.from_numpy(rng.dirichlet([0.3] * A, size=B).astype(np.float32)).to(device))
         self.mcts = self.step.mcts
         self.last = None
 
@@ -176,11 +212,15 @@ class CollectStep:
     """One env step of the device collector for every env: search + select_action + CartPole step +
     GameSegment recording, one HIP graph (muzero_collector.py:399-705 per step)."""
 
-    def __init__(self, B, S, model, device, rng_mode, seed):
+    def __init__(self, B, S, model, device, rng_mode, seed, workload="cartpole"):
         from lightzero_amd.collector import DeviceCollector
         self.B, self.S = B, S
+        env = WORKLOADS[workload][2]
+        # CartPole episodes are short (tens of steps): many slots per env; Breakout stand-in episodes
+        # last >= ~17 steps, 400-step limit
+        slots, T = (64, 200) if env == "cartpole" else (8, 400)
         self.col = DeviceCollector(model, B, S, device=device, seed=seed, rng_mode=rng_mode, graph=True,
-                                   episode_slots=64)
+                                   episode_slots=slots, max_episode_steps=T, env=env)
         self.step = self.col.search
         self.mcts = self.step.mcts
         self.last = None
@@ -191,10 +231,12 @@ class CollectStep:
         self.last = (out["distributions"], out["values"], None)
 
     def finish(self, world):
-        """the episodes finished since the last call: packed on the device and, with more than one
-        rank, all-gathered (RCCL) with the step / episode / duration sums (trajectory.py)"""
-        eps, st = self.col.gather_finished()
-        return {"episodes_all_ranks": len(eps), "rows": int(sum(len(e["action_segment"]) + 1 for e in eps)),
+        """the episodes finished since the last call: packed on the device (lzm_episodes_*) and, with
+        more than one rank, all-gathered (RCCL over xGMI) with the step / episode / duration sums
+        (trajectory.py) — the TrajBlocks a learner consumes, no host unpacking"""
+        blocks, st = self.col.gather_blocks(to_host=False)
+        return {"episodes_all_ranks": st["episodes"], "rows": st["rows"], "payload_bytes": st["payload_bytes"],
+                "frame_dtype": str(self.col.rec_frames.dtype).replace("torch.", ""),
                 "total_envstep": st["total_envstep"], "world": world}
 
     def tree(self):
@@ -245,7 +287,7 @@ def kernel_timing(step, n_search=3):
     the mean search depth d-bar from the kernels' own search_len output."""
     from lightzero_amd import mcts_ctree as mc
     mcts = step.mcts
-    names = ("traverse", "decode_backprop", "search_mlp")
+    names = ("traverse", "decode_backprop", "search_mlp", "search_conv")
     orig = {n: getattr(mc.DeviceTree, n) for n in names}
     acc = {n: [] for n in names}
     depth = []
@@ -304,6 +346,20 @@ def mlp_flops_per_sim(H, A, F, V, res=True):
     mac += H * F + F * V               # fc_value_head
     mac += H * F + F * A               # fc_policy_head
     return 2 * mac
+
+
+def conv_flops_per_sim(model, B, device):
+    """(all, matrix) FLOPs of one recurrent_inference row of the conv MuZeroModel (torch
+    FlopCounterMode at batch B: the convolutions are the trunk on the split-bf16 MFMA path, the
+    Linears the head MLPs on the VALU)"""
+    from torch.utils.flop_counter import FlopCounterMode
+    lat = torch.zeros(B, 64, 8, 8, device=device)
+    act = torch.zeros(B, dtype=torch.int64, device=device)
+    with torch.no_grad(), FlopCounterMode(display=False) as fc:
+        model.recurrent_inference(lat, act)
+    per_op = {str(k): v for k, v in fc.get_flop_counts().get("Global", {}).items()}
+    conv = sum(v for k, v in per_op.items() if "convolution" in k)
+    return fc.get_total_flops() / B, conv / B
 
 
 def shard_seed(rank):
@@ -450,6 +506,101 @@ def cpu_reference_search(B, S, model, secs, threads, device=None):
                 return n * B * S / el, n, el
 
 
+def cpu_reference_search_conv(kind, B, S, model, secs, threads, device=None, seed=0):
+    """The reference's search architecture at the conv Atari configs (mcts_ctree.py:228-321 for
+    MuZero / config 5, :696-827 for EfficientZero / config 3): the host tree (the oracle's bit-exact
+    restatement of ctree_muzero / ctree_efficientzero, single-threaded as the reference's ctree), the
+    host gather of latent[x][y] (and of the LSTM state for EZ, zeroed where search_len % 5 == 0), the
+    network through PyTorch and InverseScalarTransform. device=None: the network on torch-CPU with
+    `threads` threads; a GPU device: on the GPU with per-simulation H2D / D2H copies (LightZero with
+    cuda=True). At least one whole search is timed. Returns (sims/s, searches, seconds)."""
+    from oracle.oracle import OracleTree
+    torch.set_num_threads(threads)
+    dev = torch.device("cpu") if device is None else device
+    model = model.to(dev).eval()
+    A = model.action_space_size
+    ez = kind == "ez"
+    scale = 50 if ez else 300
+    rng = np.random.default_rng(seed)
+    obs = torch.from_numpy(synthetic_obs("breakout", B, rng)).to(dev)
+    support = torch.arange(-scale, scale + 1, dtype=torch.float64, device=dev).unsqueeze(0)
+
+    def inv(logits):
+        p = torch.softmax(logits, dim=1)
+        v = p.mul_(support).sum(1, keepdim=True)
+        tmp = (torch.sqrt(1 + 4 * 0.001 * (torch.abs(v) + 1 + 0.001)) - 1) / (2 * 0.001)
+        return (torch.sign(v) * (tmp * tmp - 1)).float().cpu().numpy().reshape(-1)
+
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            out = model.initial_inference(obs)
+            tree = OracleTree(B, A, S, ez=ez)
+            tree.set_delta(np.float32(0.01))
+            noises = rng.dirichlet([0.3] * A, size=B).astype(np.float32)
+            tree.prepare(np.float32(0.25), noises, np.zeros(B, np.float32), out.policy_logits.cpu().numpy(),
+                         np.full(B, -1, np.int32))
+            pool = [out.latent_state.cpu().numpy()]
+            if ez:
+                hpool = [out.reward_hidden_state[0].reshape(B, -1).cpu().numpy()]
+                cpool = [out.reward_hidden_state[1].reshape(B, -1).cpu().numpy()]
+            tp = np.full(B, -1, np.int32)
+            for k in range(S):
+                x, y, a, vtp, slen = tree.traverse(19652, np.float32(1.25), np.float32(0.997), k, tp)
+                lat = torch.from_numpy(np.asarray([pool[ix][iy] for ix, iy in zip(x, y)])).to(dev)
+                act = torch.from_numpy(a.astype(np.int64)).to(dev)
+                if ez:
+                    h = torch.from_numpy(np.asarray([hpool[ix][iy] for ix, iy in zip(x, y)])).to(dev).unsqueeze(0)
+                    c = torch.from_numpy(np.asarray([cpool[ix][iy] for ix, iy in zip(x, y)])).to(dev).unsqueeze(0)
+                    o = model.recurrent_inference(lat, (h, c), act)
+                    reset = (slen % 5 == 0).astype(np.int32)
+                    keep = (1 - reset).astype(np.float32)[:, None]
+                    hpool.append(o.reward_hidden_state[0].reshape(B, -1).cpu().numpy() * keep)
+                    cpool.append(o.reward_hidden_state[1].reshape(B, -1).cpu().numpy() * keep)
+                    pool.append(o.latent_state.cpu().numpy())
+                    tree.backprop(k + 1, np.float32(0.997), inv(o.value_prefix), inv(o.value),
+                                  o.policy_logits.cpu().numpy(), vtp, reset)
+                else:
+                    o = model.recurrent_inference(lat, act)
+                    pool.append(o.latent_state.cpu().numpy())
+                    tree.backprop(k + 1, np.float32(0.997), inv(o.reward), inv(o.value), o.policy_logits.cpu().numpy(),
+                                  vtp)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return n * B * S / el, n, el
+
+
+def cpu_baseline_conv(kind, B, S, model_gpu, secs, device):
+    """CPU baseline of a conv config (3: Pong EZ, 5: Breakout MZ per GPU): BASELINE.md's variants of the
+    bit-exact port — (a)/(b) the tree alone on 1 thread / the CPU share, (c) the reference search
+    architecture with the network on this GPU (one host thread, per-simulation H2D / D2H), (d) the same
+    with the network on torch-CPU over the share. `value` is (d). The conv network costs ≈ 25 MFLOP per
+    simulation, so (c) and (d) time at least one whole 256 x 50 search each."""
+    import copy
+    T = share_threads()
+    A = model_gpu.action_space_size
+    var = {}
+    v, n, el = cpu_tree_only(B, A, S, 1, 0.1 * secs)
+    var["a_tree_only_1t"] = {"value": round(v, 1), "cores": 1, "searches": n, "seconds": round(el, 2)}
+    v, n, el = cpu_tree_only(B, A, S, T, 0.1 * secs)
+    var["b_tree_only_share"] = {"value": round(v, 1), "cores": T, "searches": n, "seconds": round(el, 2)}
+    v, n, el = cpu_reference_search_conv(kind, B, S, model_gpu, 0.3 * secs, 1, device=device)
+    var["c_ref_arch_gpu_net_1t"] = {"value": round(v, 1), "cores": 1, "searches": n, "seconds": round(el, 2),
+                                    "network": "this GPU (PyTorch-ROCm), per-simulation H2D/D2H"}
+    model_cpu = copy.deepcopy(model_gpu).cpu()
+    v, n, el = cpu_reference_search_conv(kind, B, S, model_cpu, 0.5 * secs, T)
+    var["d_ref_arch_cpu_share"] = {"value": round(v, 1), "cores": T, "searches": n, "seconds": round(el, 2),
+                                   "network": f"torch-CPU, {T} threads"}
+    d = var["d_ref_arch_cpu_share"]
+    loop = "mcts_ctree.py:696-827" if kind == "ez" else "mcts_ctree.py:228-321"
+    return {"value": d["value"], "unit": "sims/s", "cores": T, "kind": "port",
+            "sample": f"{d['searches']} full searches (B={B}, S={S}) of the reference search loop ({loop}) over the "
+                      f"oracle's bit-exact ctree restatement, same conv network on torch-CPU with {T} threads, "
+                      f"{d['seconds']}s; variants a-d per BASELINE.md",
+            "variants": var, "host": host_cpu_info()}
+
+
 def load_calibration():
     """The reference-vs-restatement timing ratios measured in the build container, where the
     reference's own ctree may run (tools/cpu_calibration.py -> profiles/cpu_calibration.json);
@@ -491,6 +642,147 @@ def cpu_baseline(B, S, zero_heads, secs, device):
             "variants": var, "host": host_cpu_info(), "calibration": load_calibration()}
 
 
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense BF16 MFMA (MI355X_MICROARCH.md; not the 2:1-sparse figure)
+
+
+def make_step(args, workload, model, device, rank):
+    B, S = args.envs, args.sims
+    if args.path == "fused" and args.step == "graph":
+        return GraphStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload=workload)
+    if args.path == "fused" and args.step == "collect":
+        return CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload=workload)
+    if workload != "cartpole":
+        raise SystemExit("bench: --step python / --path generic are CartPole-only")
+    return GpuStep(B, S, model, device, args.rng, args.graph, seed=shard_seed(rank), fused=args.path == "fused")
+
+
+def timed_run(step, steps, warmup, world, device):
+    """W untimed steps, then K timed ones between barrier + synchronize pairs; collect mode ends the
+    timed region with the trajectory return. Returns (slowest rank's seconds, trajectory summary)."""
+    for _ in range(warmup):
+        step()
+    if hasattr(step, "finish"):
+        step.finish(world)  # (episodes of the warmup steps, untimed)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    # collect mode: the trajectory return ends the timed region (pack the episodes finished in
+    # it on the device, all-gather them over RCCL, sum-reduce the collector statistics)
+    traj = step.finish(world) if hasattr(step, "finish") else None
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return slowest_rank_seconds(time.perf_counter() - t0, world, device), traj
+
+
+def check_step(step, S, fused):
+    """every root received exactly S visits, and no search reported a broken tie-break stream
+    (look-back timeout / draw-table overflow: lzm_check_errors raises)"""
+    dsum = step.last[0].sum(dim=1)
+    assert bool((dsum == S).all()), "visit counts do not sum to num_simulations"
+    tie_errors = step.tree().check_errors()
+    # fused kernels: {integrity errors, ties resolved serially, ties whose depth was published early}
+    sdiag = step.tree().search_diagnostics()[:3] if fused else None
+    return int(sum(tie_errors)), sdiag
+
+
+def conv_roofline(step, model, B, S, device):
+    """config 5's dominant kernel, search_conv_kernel (one launch = B x S simulations): the trunk's
+    convolutions run on the bf16 matrix pipe as split-bf16 (three bf16 terms per f32 operand, six
+    products per f32 product), so the bound is the dense BF16 MFMA peak against 6x the
+    algorithmic conv FLOPs; the f32-equivalent rate and the head MLPs (VALU) ride beside."""
+    ms, dbar = kernel_timing(step)
+    sec = ms["search_conv"] * 1e-3
+    flops, conv = conv_flops_per_sim(model, B, device)
+    mfma = 6.0 * conv * B * S / sec / 1e12
+    f32 = flops * B * S / sec / 1e12
+    return {"bound": "mfma", "compute": "split-bf16 MFMA (v_mfma_f32_16x16x32_bf16, 6 products per f32 product) "
+                                        "for the conv trunk; head MLPs on the fp32 VALU",
+            "kernel": "search_conv_kernel", "achieved": round(mfma, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(mfma / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic("search_conv_kernel"),
+            "alg_flops_per_sim": int(flops), "alg_conv_flops_per_sim": int(conv),
+            "alg_f32_tflops": round(f32, 2), "alg_f32_frac_of_fp32_peak": round(f32 / FP32_PEAK_TFLOPS, 4),
+            "launch_us": round(ms["search_conv"] * 1e3, 1), "sims_per_launch": B * S,
+            "mean_search_len": round(dbar, 3)}
+
+
+def mlp_roofline(step, B, S, device):
+    """config 2's dominant kernel (fused whole-search kernel: one launch = B x S simulations); its
+    algorithmic work is the fp32 network (the launch is a chain of S dependent simulations,
+    so neither peak bounds it; the L2 weight stream is reported beside), or, on the generic path, the
+    tree kernels' HBM bytes"""
+    ms, dbar = kernel_timing(step)
+    if "search_mlp" in ms:
+        flops = B * S * mlp_flops_per_sim(128, 2, 32, 601)
+        hbm = B * (S * 8 * 128 + 2 * 32 * (1 + 2 * (S + 1)))  # latent gather+file per sim, tree slice in/out
+        sec = ms["search_mlp"] * 1e-3
+        achieved = flops / sec / 1e12
+        R = roots_per_workgroup(B, device)
+        from lightzero_amd import _lib
+        resident = int(_lib.load().lzm_search_mlp_kind(B, 2, 128, 32, 601, 1)) == 1
+        if resident:
+            # search_res_kernel streams fc_dynamics[0] (16 slots) and the two support heads
+            # (20 slots each) per simulation, slots of 256 lanes x 16 B (lzm_search_res.h)
+            kname = "search_res_kernel"
+            l2 = B * S * (16 + 20 + 20) * 256 * 16
+        else:
+            kname = "search_mlp_kernel"
+            wbytes = 4 * _lib_kernel_floats()
+            l2 = -(-B // R) * S * wbytes  # every workgroup streams the kernel-layout weights once per simulation
+        # the network runs on the VALU (v_pk_fma_f32 chains on 1 row per workgroup: no M
+        # dimension for a matrix tile), so the bound is the fp32 VALU peak and the MFMA
+        # utilisation of this network step is 0 by design (DESIGN.md §5.0)
+        return {"bound": "valu", "compute": "fp32 VALU (v_pk_fma_f32)", "mfma_utilisation": 0.0,
+                "kernel": kname, "achieved": round(achieved, 3),
+                "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
+                "traffic": pmc_traffic(kname), "alg_flops_per_launch": int(flops),
+                "alg_hbm_bytes_per_launch": int(hbm), "hbm_achieved_GBs": round(hbm / sec / 1e9, 2),
+                "l2_weight_bytes_per_launch": int(l2), "l2_achieved_TBs": round(l2 / sec / 1e12, 3),
+                "l2_peak_TBs": L2_PEAK_TBS, "roots_per_workgroup": R,
+                "launch_us": round(ms["search_mlp"] * 1e3, 1), "sims_per_launch": B * S,
+                "mean_search_len": round(dbar, 3)}
+    byt = algorithmic_bytes(B, 2, 128, 601, dbar)
+    dom = max(ms, key=lambda k: ms[k])
+    achieved = byt[dom] / (ms[dom] * 1e-3) / 1e9
+    return {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+            "alg_bytes_per_launch": int(byt[dom]), "launch_us": round(ms[dom] * 1e3, 2),
+            "kernels_us": {k: round(v * 1e3, 2) for k, v in ms.items()},
+            "mean_search_len": round(dbar, 3)}
+
+
+def workload_name(workload, B, S, world):
+    if workload == "cartpole":
+        return f"CartPole-v0 MuZero search, MuZeroModelMLP (latent 128, support 601), {B} envs x {S} sims per GPU"
+    return (f"Breakout MuZero (BASELINE.json config 5: 2048 envs x {S} sims sharded 8x MI355X), here {world * B} envs "
+            f"= {B} per GPU x {world}; conv MuZeroModel (4x64x64 frames, latent 64x8x8, support 601, 4 actions)")
+
+
+def secondary_breakout(args, world, rank, device):
+    """config 5 beside the headline: every rank runs the Breakout collect step on its own 256-env
+    shard (BN-folded initial inference, one-launch conv search, the stand-in env's step and recording,
+    one HIP graph), and the timed region ends with the trajectory return (device pack + RCCL
+    all-gather of the u8 frames and scalars + statistics sum). Returns the 'config5' object."""
+    B, S = args.envs, args.sims
+    model = build_conv_model(device, seed=0)
+    step = CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload="breakout")
+    el, traj = timed_run(step, args.steps, args.warmup, world, device)
+    tie_errors, sdiag = check_step(step, S, True)
+    out = {"workload": workload_name("breakout", B, S, world), "step": "collect",
+           "value": round(whole_job_rate(B, S, args.steps, world, el), 1), "unit": "sims/s",
+           "ms_per_step": round(el / args.steps * 1e3, 4), "n_gpus": world, "global_envs": world * B,
+           "env_steps_per_s": round(world * B * args.steps / el, 1), "scaling": "weak",
+           "trajectory": traj, "tie_stream_errors": tie_errors, "search_diag": sdiag,
+           "data": "synthetic (random-init conv MuZeroModel; Breakout stand-in env, ALE absent)"}
+    if rank == 0:
+        out["roofline"] = conv_roofline(step, model, B, S, device)
+    return out
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -513,103 +805,42 @@ def main():
     else:
         ranks = [rank_info(rank, local, device)]
     B, S = args.envs, args.sims
-    model = build_model(device, args.zero_heads, seed=0)
-    if args.path == "fused" and args.step == "graph":
-        step = GraphStep(B, S, model, device, args.rng, seed=shard_seed(rank))
-    elif args.path == "fused" and args.step == "collect":
-        step = CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank))
-    else:
-        step = GpuStep(B, S, model, device, args.rng, args.graph, seed=shard_seed(rank), fused=args.path == "fused")
-
-    for _ in range(args.warmup):
-        step()
-    if hasattr(step, "finish"):
-        step.finish(world)  # (episodes of the warmup steps, untimed)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    # collect mode: the trajectory return ends the timed region (pack the episodes finished in
-    # it on the device, all-gather them over RCCL, sum-reduce the collector statistics)
-    traj = step.finish(world) if hasattr(step, "finish") else None
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = slowest_rank_seconds(time.perf_counter() - t0, world, device)
+    wl = args.workload
+    model = build_model(device, args.zero_heads, seed=0) if wl == "cartpole" else \
+        build_conv_model(device, seed=0, zero_heads=args.zero_heads)
+    step = make_step(args, wl, model, device, rank)
+    el, traj = timed_run(step, args.steps, args.warmup, world, device)
     value = whole_job_rate(B, S, args.steps, world, el)
-
-    # sanity: every root received exactly S visits, and no search reported a broken tie-break
-    # stream (look-back timeout / draw-table overflow: lzm_check_errors raises)
-    dsum = step.last[0].sum(dim=1)
-    assert bool((dsum == S).all()), "visit counts do not sum to num_simulations"
-    tie_errors = step.tree().check_errors()
-    # fused kernels: {integrity errors, ties resolved serially, ties whose depth was published early}
-    sdiag = step.tree().search_diagnostics()[:3] if args.path == "fused" else None
+    tie_errors, sdiag = check_step(step, S, args.path == "fused")
 
     roofline = None
     cpu = None
     if rank == 0:
-        ms, dbar = kernel_timing(step)
-        if "search_mlp" in ms:
-            # fused whole-search kernel: one launch = B x S simulations; its algorithmic work is the
-            # fp32 network (the launch is a chain of S dependent simulations, so neither
-            # peak bounds it; the L2 weight stream is reported beside)
-            flops = B * S * mlp_flops_per_sim(128, 2, 32, 601)
-            hbm = B * (S * 8 * 128 + 2 * 32 * (1 + 2 * (S + 1)))  # latent gather+file per sim, tree slice in/out
-            sec = ms["search_mlp"] * 1e-3
-            achieved = flops / sec / 1e12
-            R = roots_per_workgroup(B, device)
-            from lightzero_amd import _lib
-            resident = int(_lib.load().lzm_search_mlp_kind(B, 2, 128, 32, 601, 1)) == 1
-            if resident:
-                # search_res_kernel streams fc_dynamics[0] (16 slots) and the two support heads
-                # (20 slots each) per simulation, slots of 256 lanes x 16 B (lzm_search_res.h)
-                kname = "search_res_kernel"
-                l2 = B * S * (16 + 20 + 20) * 256 * 16
-            else:
-                kname = "search_mlp_kernel"
-                wbytes = 4 * _lib_kernel_floats()
-                l2 = -(-B // R) * S * wbytes  # every workgroup streams the kernel-layout weights once per simulation
-            # the network runs on the VALU (v_pk_fma_f32 chains on 1 row per workgroup: no M
-            # dimension for a matrix tile), so the bound is the fp32 VALU peak and the MFMA
-            # utilisation of this network step is 0 by design
-            roofline = {"bound": "valu", "compute": "fp32 VALU (v_pk_fma_f32)", "mfma_utilisation": 0.0,
-                        "kernel": kname, "achieved": round(achieved, 3),
-                        "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-                        "traffic": pmc_traffic(kname), "alg_flops_per_launch": int(flops),
-                        "alg_hbm_bytes_per_launch": int(hbm), "hbm_achieved_GBs": round(hbm / sec / 1e9, 2),
-                        "l2_weight_bytes_per_launch": int(l2), "l2_achieved_TBs": round(l2 / sec / 1e12, 3),
-                        "l2_peak_TBs": L2_PEAK_TBS, "roots_per_workgroup": R,
-                        "launch_us": round(ms["search_mlp"] * 1e3, 1), "sims_per_launch": B * S,
-                        "mean_search_len": round(dbar, 3)}
-        else:
-            byt = algorithmic_bytes(B, 2, 128, 601, dbar)
-            dom = max(ms, key=lambda k: ms[k])
-            achieved = byt[dom] / (ms[dom] * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                        "alg_bytes_per_launch": int(byt[dom]), "launch_us": round(ms[dom] * 1e3, 2),
-                        "kernels_us": {k: round(v * 1e3, 2) for k, v in ms.items()},
-                        "mean_search_len": round(dbar, 3)}
+        roofline = mlp_roofline(step, B, S, device) if wl == "cartpole" else conv_roofline(step, model, B, S, device)
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(B, S, args.zero_heads, args.cpu_baseline_secs, device)
+            cpu = cpu_baseline(B, S, args.zero_heads, args.cpu_baseline_secs, device) if wl == "cartpole" else \
+                cpu_baseline_conv("mz", B, S, model, args.cpu_baseline_secs, device)
+    config5 = None
+    if wl == "cartpole" and args.secondary == "breakout" and args.path == "fused":
+        del step
+        torch.cuda.empty_cache()
+        config5 = secondary_breakout(args, world, rank, device)
     if rank == 0:
-        line = {"metric": "MCTS simulations/sec (whole node), 256 parallel envs x 50 sims/step",
+        metric = ("MCTS simulations/sec (whole node), 256 parallel envs x 50 sims/step" if wl == "cartpole" else
+                  "MCTS simulations/sec (whole node), Breakout MuZero, 256 envs per GPU x 50 sims/step")
+        line = {"metric": metric,
                 "value": round(value, 1), "unit": "sims/s", "n_gpus": world, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4), "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-                "config": {"workload": "CartPole-v0 MuZero search, MuZeroModelMLP (latent 128, support 601), "
-                                       f"{B} envs x {S} sims per GPU",
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic" if wl == "cartpole" else "synthetic (random-init conv MuZeroModel, synthetic frames)",
+                "config": {"workload": workload_name(wl, B, S, world),
                            "global_batch": world * B, "num_simulations": S, "rng": args.rng,
                            "path": args.path, "step": args.step if args.path == "fused" else "python",
                            "hip_graph": (args.step != "python") if args.path == "fused" else bool(args.graph),
                            "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
-                "tie_stream_errors": int(sum(tie_errors)), "search_diag": sdiag, "ranks": ranks,
-                "trajectory": traj, "roofline": roofline, "cpu_baseline": cpu}
+                "tie_stream_errors": tie_errors, "search_diag": sdiag, "ranks": ranks,
+                "trajectory": traj, "roofline": roofline, "cpu_baseline": cpu, "config5": config5}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -34,7 +34,8 @@ enum lzm_status {
   LZM_ERR_ARG = -1,      /* bad argument (null pointer, size out of range) */
   LZM_ERR_HIP = -2,      /* a HIP runtime call failed */
   LZM_ERR_CAPACITY = -3, /* latent index beyond the reserved simulations: call lzm_reserve */
-  LZM_ERR_STATE = -4     /* call order violated (e.g. backprop before traverse) */
+  LZM_ERR_STATE = -4,    /* call order violated (e.g. backprop before traverse) */
+  LZM_ERR_RESIDENCY = -5 /* a launch that needs its whole grid co-resident was refused; nothing ran */
 };
 
 enum lzm_flags {
@@ -224,6 +225,43 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
                               float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
                               const int64_t *counter, void *stream);
 
+/* The Atari image configs' collect step (BASELINE.json config 5; muzero_collector.py:399-705 with
+ * zoo/atari/envs/atari_lightzero_env.py): one workgroup per env right after the search — select_action
+ * from the root visit counts (policy/utils.py:515-539), record o_t (u8 64x64 frame), a_t, r_t, the
+ * visit counts, root value (and predicted value) into the running episode slot
+ * (ep_count[i] % E of rec_* [n][E][T(+1)]...), step the game, append o_{t+1} to the model's float
+ * observation stack obs [n][4][64][64] (frame / 255, frame_stack_num = 4: game_segment.py:95-127),
+ * auto-reset finished episodes (their final frame goes to slot row L; ep_len / ep_count advance) and
+ * draw the next root's Dirichlet(noise_alpha) noise. The game is a stand-in with Breakout's action set
+ * and frame format (ALE is not installed; csrc/lzm_atari.h). state int32 [n][16], cur u8 [n][4096]
+ * (the newest frame), counter: the device env-step counter. */
+int lzm_atari_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream);
+int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
+                           const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
+                           float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
+                           int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
+                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
+                           const int64_t *counter, void *stream);
+
+/* Device packing of a collector's finished episodes for the trajectory return (SURVEY.md §8(e);
+ * replaces the host loop over envs that builds GameSegments' arrays, muzero_collector.py:612-632, and
+ * feeds the rank all-gather that replaces muzero_collector.py:709-712's DDP path). Episode k of env i
+ * lives in slot k % E; consumed[i] counts the episodes already returned. lzm_episodes_scan (one
+ * workgroup): env_ep_off [n] / env_row_off [n] exclusive prefix sums of the new episodes and their rows
+ * (L + 1 each), totals int64[3] = {episodes, rows, slot overflow (a new count >= E: a returned slot
+ * was overwritten)}. lzm_episodes_pack (one workgroup per env, after the host sized the outputs from
+ * totals): out_index [episodes][3] = (env, L, first row), out_frames [rows][frame_bytes] (o_0..o_L of
+ * each episode, copied from rec_frames [n][E][T+1][frame_bytes]), out_scalars [rows][3 + A (+1)] =
+ * [action | reward | visit counts (A) | root value (| predicted value)] with each episode's row L
+ * zero; then consumed[i] = ep_count[i]. Env-major order, each env's episodes in finishing order. */
+int lzm_episodes_scan(int n, int E, const int32_t *ep_count, const int32_t *consumed, const int32_t *ep_len,
+                      int32_t *env_ep_off, int64_t *env_row_off, int64_t *totals, void *stream);
+int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_bytes, const int32_t *ep_count,
+                      const int32_t *ep_len, int32_t *consumed, const int32_t *env_ep_off, const int64_t *env_row_off,
+                      const void *rec_frames, const int32_t *rec_action, const float *rec_reward,
+                      const int32_t *rec_visits, const float *rec_value, const float *rec_pred, void *out_frames,
+                      float *out_scalars, int64_t *out_index, void *stream);
+
 /* ---- batched AlphaZero for TicTacToe (replaces MCTS.get_next_action,
  * lzero/mcts/ctree/ctree_alphazero/mcts_alphazero.cpp:131-207, called per env from
  * lzero/policy/alphazero.py:266 and :327). B boards are searched together on the device; the caller
@@ -360,7 +398,9 @@ int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_
  * lzm_search_conv with the reward head reading relu(h1 * vp_s + vp_t) (K = H). rec_reset (nullable)
  * is_reset int32 [S][B]. Same results as the generic path (traverse, lzm_conv_trunk_xin_p,
  * lzm_ez_lstm_step, lzm_conv_heads, lzm_decode_backprop) bit for bit. Requires max(B, 2 T) <= the
- * device's CU count, T = ceil(B / 64) * H / 16 (the grid is co-resident). */
+ * device's CU count, T = ceil(B / 64) * H / 16: the grid must be co-resident, so outside a stream
+ * capture it is a cooperative launch; when the runtime (or the occupancy bound) cannot keep it resident
+ * the call returns LZM_ERR_RESIDENCY without running anything and the caller takes the generic path. */
 int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount,
                        float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, float *hpool,
                        float *cpool, int H, int horizon, const float *trunk_w, const float *actmap, int n_dres,

@@ -19,6 +19,7 @@ LZM_ERR_ARG = -1
 LZM_ERR_HIP = -2
 LZM_ERR_CAPACITY = -3
 LZM_ERR_STATE = -4
+LZM_ERR_RESIDENCY = -5
 LZM_TREE_EZ = 1
 LZM_RNG_FAST = 2
 
@@ -90,6 +91,12 @@ SIGNATURES = {
     "lzm_cartpole_reset": [_i, _vp, _vp, _vp, _u32, _vp],
     "lzm_cartpole_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
+    "lzm_atari_reset": [_i, _vp, _vp, _vp, _vp, _u32, _vp],
+    "lzm_atari_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
+    "lzm_episodes_scan": [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_episodes_pack": [_i, _i, _i, _i, _i, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                          _vp, _vp],
     "lzm_az_workspace_bytes": [_i, _i, ctypes.POINTER(_i64)],
     "lzm_az_noise_table": [_d, _i, _vp],
     "lzm_az_set_constants": [_i, _i, _vp, _d, _d, _d, _vp],
@@ -122,6 +129,10 @@ class LzmError(RuntimeError):
     pass
 
 
+class ResidencyError(LzmError):
+    """A launch that needs its whole grid co-resident was refused (LZM_ERR_RESIDENCY); nothing ran."""
+
+
 def load(path=LIB_PATH):
     """Load the library without touching the GPU (symbol table only)."""
     global _lib
@@ -149,6 +160,8 @@ def check(rc, what):
     msg = (_lib.lzm_last_error() or b"").decode(errors="replace")
     if rc == LZM_ERR_ARG:
         raise ValueError(f"{what}: {msg}")
+    if rc == LZM_ERR_RESIDENCY:
+        raise ResidencyError(f"{what}: {msg}")
     raise LzmError(f"{what} failed ({rc}): {msg}")
 
 

@@ -16,7 +16,8 @@ values, root latents and policy logits). `step_counter` counts the steps (device
 """
 import torch
 
-from .initial import fused_initial_or_none
+from .conv_infer import folded_initial_or_none
+from .initial import FusedInitialInference, fused_initial_or_none
 from .mcts_ctree import MuZeroMCTSCtree, _step_net
 from .utils import EasyDict
 
@@ -26,8 +27,12 @@ class DeviceSearchStep:
                  discount_factor=0.997, support_scale=300, seed=0, rng_mode="glibc", graph=True, cfg_extra=None,
                  epilogue=None, fused_initial=True):
         self.model = model.eval()
-        # initial_inference as one HIP launch when the model is a MuZeroModelMLP (lightzero_amd.initial)
-        self.initial = fused_initial_or_none(self.model) if fused_initial else None
+        # initial_inference as one HIP launch when the model is a MuZeroModelMLP (lightzero_amd.initial);
+        # for the conv MuZeroModel family its BatchNorm-folded form (conv_infer.FoldedConvInitial)
+        self.initial = None
+        if fused_initial:
+            self.initial = fused_initial_or_none(self.model) or folded_initial_or_none(self.model)
+        self._weights_key = None
         self.B, self.S = int(num_envs), int(num_simulations)
         self.device = torch.device(device)
         self.noise_weight = float(noise_weight)
@@ -68,8 +73,8 @@ class DeviceSearchStep:
             try:
                 if self.roots is None:
                     self.roots = self.mcts_cls.roots(self.B, self.legal)
-                pool0 = self._root_slot()
-                if self.initial is not None and pool0 is not None:
+                pool0 = self._root_slot() if isinstance(self.initial, FusedInitialInference) else None
+                if pool0 is not None:
                     # one launch: initial_inference into the search's root slot (the search skips its
                     # copy) and the root preparation from the policy logits
                     out = self.initial.initial_inference(
@@ -121,12 +126,21 @@ class DeviceSearchStep:
         with torch.cuda.graph(self.graph):
             self.out = self._body()
 
+    def _weights_version(self):
+        m = self.model
+        return tuple(x._version for x in list(m.parameters()) + list(m.buffers()))
+
     def refresh_weights(self):
         """Re-pack the network for the captured kernels if its parameters changed (e.g. a learner
         update): both caches re-pack IN PLACE, so the captured graph reads the new weights. A graph
-        replay runs no Python, so this host-side version check runs before every replay."""
+        replay runs no Python, so this host-side version check runs before every replay: one cached
+        tuple compare of the model's tensor versions, the caches only when it changed."""
+        key = self._weights_version()
+        if key == self._weights_key:
+            return
+        self._weights_key = key
         if self.initial is not None:
-            self.initial._pack()
+            self.initial.refresh()
         if self.roots is not None and self.roots.tree is not None:
             if self.mcts._fused(self.model, self.roots.tree) is None:
                 # generic path (e.g. a conv model): the folded step network re-folds in place
@@ -140,6 +154,8 @@ class DeviceSearchStep:
         self.build_graph()
         self.refresh_weights()
         self.graph.replay()
+        if self.roots is not None and self.roots.tree is not None:
+            self.roots.tree.searched()
         return self.out
 
     def reset_seed_counter(self):

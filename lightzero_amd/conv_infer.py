@@ -402,6 +402,135 @@ class _Out:
     pass
 
 
+def _basic_blocks(blocks):
+    """DI-engine basic ResBlocks (BN folded) -> [(w1, b1, w2, b2)]"""
+    return [(w1, b1, w2, b2) for (w1, b1), (w2, b2) in _resblocks(blocks)]
+
+
+def fold_representation(model):
+    """The representation network (common.py:369-465, DownSample :164-266) of a conv MuZeroModel /
+    EfficientZeroModel with every eval-mode BatchNorm folded into the convolution in front of it
+    (float64, rounded once to float32). Returns a list of ops for FoldedConvInitial."""
+    rep = model.representation_network
+    if not isinstance(rep.activation, torch.nn.ReLU):
+        raise NotFoldable("ReLU representation network only")
+    ops = []
+    if rep.downsample:
+        ds = rep.downsample_net
+        if not isinstance(ds.norm1, torch.nn.BatchNorm2d):
+            raise NotFoldable("BatchNorm DownSample only")
+        w, b = _fold(ds.conv1.weight, None, ds.norm1)
+        ops.append(("conv_relu", w, b, 2))
+        ops += [("basic",) + blk for blk in _basic_blocks(ds.resblocks1)]
+        db = ds.downsample_block
+        if getattr(db, "res_type", None) != "downsample" or not isinstance(db.act, torch.nn.ReLU):
+            raise NotFoldable("unexpected downsample block")
+        w1, b1 = _fold(db.conv1.weight, None, db.bn1)
+        w2, b2 = _fold(db.conv2.weight, None, db.bn2)
+        ops.append(("down", w1, b1, w2, b2, db.conv3.weight.double()))
+        ops += [("basic",) + blk for blk in _basic_blocks(ds.resblocks2)]
+        ops.append(("avgpool",))
+        ops += [("basic",) + blk for blk in _basic_blocks(ds.resblocks3)]
+        if ds.observation_shape[1] == 96:
+            ops.append(("avgpool",))
+    else:
+        if not isinstance(rep.norm, torch.nn.BatchNorm2d):
+            raise NotFoldable("BatchNorm representation only")
+        w, b = _fold(rep.conv.weight, None, rep.norm)
+        ops.append(("conv_relu", w, b, 1))
+    ops += [("basic",) + blk for blk in _basic_blocks(rep.resblocks)]
+    return [tuple(x.float().contiguous() if torch.is_tensor(x) else x for x in op) for op in ops]
+
+
+class FoldedConvInitial:
+    """initial_inference (muzero_model.py:209-239 / efficientzero_model.py:199-233) of a conv MuZeroModel /
+    EfficientZeroModel with every eval-mode BatchNorm folded: the representation network as convolutions
+    with biases (no BatchNorm launches), then the prediction network exactly as FoldedConvNet folds it
+    (residual blocks, the value | policy 1x1 convs as one, the two hidden Linears as one block-diagonal
+    Linear). Re-folds in place when the module's tensors change. Same outputs as the module within f32
+    rounding (tests/test_conv_fold.py)."""
+
+    def __init__(self, model):
+        self.model = model
+        self.ez = hasattr(model.dynamics_network, "lstm")
+        self._ver = None
+        self.ops = None
+        self.t = None
+        self.refresh()
+
+    def _version(self):
+        m = self.model
+        return tuple(x._version for x in list(m.parameters()) + list(m.buffers()))
+
+    def refresh(self):
+        ver = self._version()
+        if ver == self._ver:
+            return
+        with torch.no_grad():
+            ops = fold_representation(self.model)
+            t = fold_tensors(self.model)
+            if self.ops is None:
+                self.ops, self.t = ops, t
+            else:  # in place: captured graphs keep reading these tensors
+                for old, new in zip(self.ops, ops):
+                    for a, b in zip(old, new):
+                        if torch.is_tensor(a):
+                            a.copy_(b)
+                for k, v in t.items():
+                    self.t[k].copy_(v)
+        self._ver = ver
+
+    @staticmethod
+    def _basic(x, w1, b1, w2, b2):
+        y = F.conv2d(x, w1, b1, padding=1).relu_()
+        return F.conv2d(y, w2, b2, padding=1).add_(x).relu_()
+
+    def initial_inference(self, obs):
+        self.refresh()
+        t = self.t
+        x = obs.float()
+        for op in self.ops:
+            kind = op[0]
+            if kind == "conv_relu":
+                x = F.conv2d(x, op[1], op[2], stride=op[3], padding=1).relu_()
+            elif kind == "basic":
+                x = self._basic(x, *op[1:])
+            elif kind == "down":
+                _, w1, b1, w2, b2, w3 = op
+                y = F.conv2d(x, w1, b1, stride=2, padding=1).relu_()
+                x = F.conv2d(y, w2, b2, padding=1).add_(F.conv2d(x, w3, None, stride=2, padding=1)).relu_()
+            else:  # avgpool (count_include_pad, as nn.AvgPool2d(3, 2, 1))
+                x = F.avg_pool2d(x, kernel_size=3, stride=2, padding=1)
+        latent = x
+        B = latent.shape[0]
+        p = latent
+        i = 0
+        while f"pres{i}_w1" in t:
+            p = self._basic(p, t[f"pres{i}_w1"], t[f"pres{i}_b1"], t[f"pres{i}_w2"], t[f"pres{i}_b2"])
+            i += 1
+        h = F.conv2d(p, t["head_w"], t["head_b"]).relu_().reshape(B, -1)
+        hid = F.linear(h, t["ph_w1"], t["ph_b1"]).relu_()
+        nv = t["v_w2"].shape[1]
+        value = F.linear(hid[:, :nv], t["v_w2"], t["v_b2"])
+        policy = F.linear(hid[:, nv:], t["p_w2"], t["p_b2"])
+        if self.ez:
+            from .model_conv import EZNetworkOutput
+            z = torch.zeros(1, B, self.model.lstm_hidden_size, device=obs.device)
+            return EZNetworkOutput(value, [0. for _ in range(B)], policy, latent, (z, z.clone()))
+        from .model_mlp import MZNetworkOutput
+        return MZNetworkOutput(value, [0. for _ in range(B)], policy, latent)
+
+
+def folded_initial_or_none(model):
+    """FoldedConvInitial for the conv model family, None for anything else"""
+    if not hasattr(model, "latent_hw") or not hasattr(model, "representation_network"):
+        return None
+    try:
+        return FoldedConvInitial(model)
+    except (NotFoldable, AttributeError):
+        return None
+
+
 class FoldedCache:
     """FoldedConvNet per model (None for models it does not recognise); a small LRU keyed by model
     identity, re-folded in place when the model's parameters change (FoldedConvNet.refresh)."""

@@ -31,6 +31,8 @@
 #include "../../include/lzmcts.h"
 #include "lzm_numerics.h"
 #include "lzm_collect.h"
+#include "lzm_atari.h"
+#include "lzm_traj.h"
 #include "lzm_az.h"
 #include "lzm_az_fused.h"
 #include "lzm_tree.h"
@@ -691,6 +693,23 @@ static void set_err(const char *msg) { snprintf(g_err, sizeof(g_err), "%s", msg)
     }                                                                                              \
   } while (0)
 #define LZM_CHECK_LAUNCH() LZM_HIP(hipGetLastError())
+
+// Compute units of the CURRENT device, cached per device ordinal (a process may drive several GPUs,
+// or switch devices between calls: a process-wide static would keep the first device's count).
+static int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  if (dev >= 64) {
+    int n = 0;
+    return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  if (!cache[dev]) {
+    int n = 0;
+    cache[dev] = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n : 256;
+  }
+  return cache[dev];
+}
 
 struct lzm_handle {
   int B, A, flags, sims_cap, cap, depth_cap;
@@ -1459,13 +1478,7 @@ int roots_per_wg(int B) {
     const int r = atoi(e);
     if (r == 1 || r == 2 || r == 4 || r == 8) return r;
   }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = device_cus();
   for (int r = 1; r < 8; r *= 2)
     if ((B + r - 1) / r <= cus) return r;
   return 8;
@@ -1941,6 +1954,81 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
   return LZM_OK;
 }
 
+int lzm_atari_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream) {
+  if (n <= 0 || !state || !steps || !cur || !obs || (((uintptr_t)cur | (uintptr_t)obs) & 15)) {
+    set_err("lzm_atari_reset: bad arguments (16-B aligned frame buffers)");
+    return LZM_ERR_ARG;
+  }
+  hipLaunchKernelGGL(atari_reset_kernel, dim3(n), dim3(kAtThreads), 0, (hipStream_t)stream, n, state, steps, cur, obs,
+                     seed);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
+                           const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
+                           float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
+                           int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
+                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
+                           const int64_t *counter, void *stream) {
+  if (n <= 0 || A <= 0 || A > 64 || T <= 0 || E <= 0 || max_steps <= 0 || !visits || !root_value || !state || !steps ||
+      !cur || !obs || !noises || !rec_frames || !rec_action || !rec_reward || !rec_visits || !rec_value || !ep_len ||
+      !ep_count || !counter || !(temperature > 0.0f) || !(noise_alpha > 0.0f) || (!pred_value) != (!rec_pred) ||
+      (((uintptr_t)cur | (uintptr_t)obs | (uintptr_t)rec_frames) & 15)) {
+    set_err("lzm_atari_collect_step: bad arguments");
+    return LZM_ERR_ARG;
+  }
+  AtariArgs a;
+  a.n = n; a.A = A; a.T = T; a.E = E; a.max_steps = max_steps; a.deterministic = deterministic;
+  a.temperature = temperature; a.noise_alpha = noise_alpha; a.seed = seed; a.counter = counter;
+  a.visits = visits; a.root_value = root_value; a.state = state; a.steps = steps; a.cur = cur; a.obs = obs;
+  a.noises = noises; a.rec_frames = rec_frames; a.rec_action = rec_action; a.rec_reward = rec_reward;
+  a.rec_visits = rec_visits; a.rec_value = rec_value; a.pred_value = pred_value; a.rec_pred = rec_pred;
+  a.ep_len = ep_len; a.ep_count = ep_count;
+  hipLaunchKernelGGL(atari_collect_kernel, dim3(n), dim3(kAtThreads), 0, (hipStream_t)stream, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_episodes_scan(int n, int E, const int32_t *ep_count, const int32_t *consumed, const int32_t *ep_len,
+                      int32_t *env_ep_off, int64_t *env_row_off, int64_t *totals, void *stream) {
+  if (n <= 0 || E <= 0 || !ep_count || !consumed || !ep_len || !env_ep_off || !env_row_off || !totals) {
+    set_err("lzm_episodes_scan: bad arguments");
+    return LZM_ERR_ARG;
+  }
+  hipLaunchKernelGGL(episodes_scan_kernel, dim3(1), dim3(kTrScanThreads), 0, (hipStream_t)stream, n, E, ep_count,
+                     consumed, ep_len, env_ep_off, env_row_off, totals);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_bytes, const int32_t *ep_count,
+                      const int32_t *ep_len, int32_t *consumed, const int32_t *env_ep_off, const int64_t *env_row_off,
+                      const void *rec_frames, const int32_t *rec_action, const float *rec_reward,
+                      const int32_t *rec_visits, const float *rec_value, const float *rec_pred, void *out_frames,
+                      float *out_scalars, int64_t *out_index, void *stream) {
+  if (n <= 0 || E <= 0 || T <= 0 || A <= 0 || frame_bytes <= 0 || !ep_count || !ep_len || !consumed ||
+      !env_ep_off || !env_row_off || !rec_frames || !rec_action || !rec_reward || !rec_visits || !rec_value ||
+      (has_pred && !rec_pred) || !out_frames || !out_scalars || !out_index) {
+    set_err("lzm_episodes_pack: bad arguments");
+    return LZM_ERR_ARG;
+  }
+  PackArgs a;
+  a.n = n; a.E = E; a.T = T; a.A = A; a.W = 3 + A + (has_pred ? 1 : 0); a.has_pred = has_pred ? 1 : 0;
+  a.frame_bytes = frame_bytes; a.ep_count = ep_count; a.ep_len = ep_len; a.env_ep_off = env_ep_off;
+  a.consumed = consumed; a.env_row_off = env_row_off;
+  a.rec_frames = (const uint8_t *)rec_frames; a.rec_action = rec_action; a.rec_reward = rec_reward;
+  a.rec_visits = rec_visits; a.rec_value = rec_value; a.rec_pred = rec_pred;
+  a.out_frames = (uint8_t *)out_frames; a.out_scalars = out_scalars; a.out_index = out_index;
+  if ((frame_bytes & 15) == 0 && (((uintptr_t)rec_frames | (uintptr_t)out_frames) & 15)) {
+    set_err("lzm_episodes_pack: frame buffers must be 16-B aligned when frames are multiples of 16 B");
+    return LZM_ERR_ARG;
+  }
+  hipLaunchKernelGGL(episodes_pack_kernel, dim3(n), dim3(kTrPackThreads), 0, (hipStream_t)stream, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
 }  // extern "C"
 
 // ---- batched AlphaZero (lzm_az.h). One workspace buffer per (B, S), carved here.
@@ -2106,13 +2194,7 @@ int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int3
 // ---- fused AlphaZero search (lzm_az_fused.h)
 static int az_fused_rows(int B) {
   // boards per workgroup: the fewest that keep the grid within one wave of workgroups per CU
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) ? prop.multiProcessorCount
-                                                                                                  : 256;
-  }
+  const int cus = device_cus();
   const char *e = getenv("LZM_AZ_BOARDS_PER_WG");
   if (e && atoi(e) > 0) return atoi(e);
   for (int r : {1, 2, 4}) if ((B + r - 1) / r <= cus) return r;
@@ -2434,13 +2516,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d simulations > reserved %d (lzm_reserve)", S, h->sims_cap);
     return LZM_ERR_CAPACITY;
   }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = device_cus();
   if (h->B > cus || h->B > 256) {
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d roots > min(%d CUs, 256) (one co-resident workgroup per root)",
              h->B, cus);
@@ -2547,19 +2623,13 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
     snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: %d simulations > reserved %d (lzm_reserve)", S, h->sims_cap);
     return LZM_ERR_CAPACITY;
   }
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
+  const int cus = device_cus();
   const int B = h->B, nmb = (B + kLsRows - 1) / kLsRows, T = nmb * (H / kLsUnits), G = std::max(B, 2 * T);
   if (B > 256 || G > cus) {
     snprintf(g_err, sizeof(g_err),
              "lzm_search_conv_ez: %d workgroups (%d roots, %d LSTM tiles x 2) > min(%d CUs) or B > 256 (the grid is "
              "co-resident)", G, B, T, cus);
-    return LZM_ERR_ARG;
+    return LZM_ERR_RESIDENCY;
   }
   int rc = fill_lut(h, pb_c_base, pb_c_init);
   if (rc != LZM_OK) return rc;
@@ -2633,10 +2703,36 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
   p.stamps = stamps ? h->phase : nullptr;
   auto fn = stamps ? (fast ? search_conv_ez_kernel<kBxAhead, true, true> : search_conv_ez_kernel<kBxAhead, false, true>)
                    : (fast ? search_conv_ez_kernel<kBxAhead, true> : search_conv_ez_kernel<kBxAhead, false>);
-  hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e == hipSuccess) {
+  LZM_HIP(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  // The roots wait on LSTM tiles and the tiles on roots inside the launch, so every workgroup must be
+  // resident at once. Occupancy bound first (resident workgroups per CU at this LDS / register use x the
+  // device's CUs), then a COOPERATIVE launch, which the runtime refuses rather than start a grid it
+  // cannot keep resident (e.g. while another kernel holds CUs: a learner on another stream, a second
+  // rank on the same GPU). A refused launch returns LZM_ERR_RESIDENCY and nothing ran: the caller
+  // takes the generic per-simulation path. Inside a stream capture (a HIP graph node cannot carry the
+  // cooperative attribute) the plain launch is used; the captured graph owns its GPU at replay.
+  int per_cu = 0;
+  LZM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, kScThreads, lds));
+  if ((long long)per_cu * cus < G) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: %d workgroups > %d resident (%d per CU x %d CUs)", G,
+             per_cu * cus, per_cu, cus);
+    return LZM_ERR_RESIDENCY;
+  }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  LZM_HIP(hipStreamIsCapturing((hipStream_t)stream, &cap));
+  if (cap != hipStreamCaptureStatusNone) {
     hipLaunchKernelGGL(fn, dim3(G), dim3(kScThreads), lds, (hipStream_t)stream, p);
-    e = hipGetLastError();
+    LZM_CHECK_LAUNCH();
+    return LZM_OK;
+  }
+  void *kargs[] = {(void *)&p};
+  hipError_t e = hipLaunchCooperativeKernel((const void *)fn, dim3(G), dim3(kScThreads), kargs, (unsigned)lds,
+                                            (hipStream_t)stream);
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    (void)hipGetLastError();
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: cooperative launch of %d workgroups refused (not co-resident)",
+             G);
+    return LZM_ERR_RESIDENCY;
   }
   LZM_HIP(e);
   return LZM_OK;

@@ -174,21 +174,23 @@ class _RootsBase:
         if self.tree is None:
             return [[] for _ in range(self.root_num)]
         tr = self.tree.trajectories(self.tree.sims_capacity + 2).cpu().numpy()
+        self.tree.check_once()
         return [[int(a) for a in row if a >= 0] for row in tr]
 
     def get_distributions(self):
         if self.tree is None:
             return [[] for _ in range(self.root_num)]
         d = self.tree.distributions().cpu().numpy()
-        # once per search: a timed-out look-back would leave a wrong tie-break stream.
-        # clear=False: the sticky words stay set for the caller (collector / bench) that owns them
-        self.tree.check_errors(clear=False)
+        # once per search, by whichever getter runs first: a timed-out look-back
+        # would leave a wrong tie-break stream; the words are cleared as they are read
+        self.tree.check_once()
         return [[int(v) for v in row if v >= 0] for row in d]
 
     def get_values(self):
         if self.tree is None:
             return [0.0] * self.root_num
         v = self.tree.values().cpu().numpy()
+        self.tree.check_once()
         return [float(x) for x in v]
 
     def clear(self):
@@ -221,6 +223,7 @@ def _traverse(roots, pb_c_base, pb_c_init, discount_factor, min_max_stats_lst, r
         t.set_reuse(*reuse)
     t.traverse(mm, s, vtp, int(pb_c_base), _f32(pb_c_init), _f32(discount_factor))
     out = torch.stack([t.x, t.y, t.action, t.vtp, t.search_len]).cpu().numpy()
+    t.check_once()  # (already synchronised) this traverse's look-back / draw table intact
     results._search_lens = out[4].tolist()
     results._tree = t
     y = out[1]

@@ -16,8 +16,9 @@ gymnasium is installed here, so:
 - `SyncEnvManager` is the BaseEnvManager surface MuZeroCollector uses (env_num, ready_obs,
   step(actions) -> {env_id: timestep}, reset, launch, close, action_space), stepping in-process
   and auto-resetting finished envs as DI-engine's managers do.
-- `DeviceCartPoleEnvManager` selects MuZeroCollector's device path: the CartPole state lives in
-  HBM and steps inside the collect graph (lzm_collect.h); this object only carries its shape/seed.
+- `DeviceCartPoleEnvManager` / `DeviceBreakoutEnvManager` select MuZeroCollector's device path: the
+  env state lives in HBM and steps inside the collect graph (lzm_collect.h, lzm_atari.h); these
+  objects only carry the env kind, shape and seed.
 """
 import math
 from collections import namedtuple
@@ -139,16 +140,19 @@ class SyncEnvManager:
             self._closed = True
 
 
-class DeviceCartPoleEnvManager:
-    """env_num CartPole-v0 envs resident on the GPU (lzm_cartpole_* kernels): handing one to
+class DeviceEnvManager:
+    """env_num envs resident on the GPU (lightzero_amd.collector.DEVICE_ENVS): handing one to
     MuZeroCollector selects its device path. seed keys the envs' Philox reset streams."""
+    env_kind = None
+    actions = None
+    observation_shape = None
+    frame_stack = 1
 
     def __init__(self, env_num, seed=0, max_episode_steps=200):
         self.env_num = int(env_num)
         self.seed = int(seed)
         self.max_episode_steps = int(max_episode_steps)
-        self.action_space = Discrete(2)
-        self.observation_shape = (4,)
+        self.action_space = Discrete(self.actions)
 
     def launch(self):
         pass
@@ -158,3 +162,24 @@ class DeviceCartPoleEnvManager:
 
     def close(self):
         pass
+
+
+class DeviceCartPoleEnvManager(DeviceEnvManager):
+    """CartPole-v0 (config 2) on the device (lzm_cartpole_* kernels)."""
+    env_kind = "cartpole"
+    actions = 2
+    observation_shape = (4,)
+    frame_stack = 1
+
+
+class DeviceBreakoutEnvManager(DeviceEnvManager):
+    """The Atari image env of config 5 on the device (lzm_atari_* kernels): Breakout's action set and
+    frame format — 4 x 64 x 64 stacked grey frames, one recorded per step — as a stand-in game (ALE
+    is not installed)."""
+    env_kind = "breakout"
+    actions = 4
+    observation_shape = (4, 64, 64)
+    frame_stack = 4
+
+    def __init__(self, env_num, seed=0, max_episode_steps=400):
+        super().__init__(env_num, seed, max_episode_steps)

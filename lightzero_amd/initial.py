@@ -54,6 +54,9 @@ class FusedInitialInference:
         self.flat = None
         self._pack()
 
+    def refresh(self):
+        self._pack()
+
     def _pack(self):
         m = self.model
         ver = tuple(t._version for t in list(m.parameters()) + list(m.buffers()))

@@ -370,7 +370,9 @@ class MuZeroMCTSCtree(object):
                 buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             # the one-launch searches read device seeds / to_play in place (no staging copies)
             in_place = (fz is not None or cz is not None) and rec is None
-            step_in_kernel = step is not None and in_place
+            # the MLP one-launch search runs the collect step's glue in its kernel; the conv one runs
+            # it as two small launches around the search (seed sequence, root outputs)
+            step_in_kernel = step is not None and in_place and fz is not None
             vt = to_play_batch if in_place and _usable_i32(to_play_batch, B, dev) else None
             if vt is None:
                 buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
@@ -389,8 +391,6 @@ class MuZeroMCTSCtree(object):
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
             if cz is not None:
                 # the conv network's whole search in one launch (lzm_search_conv)
-                if step is not None:
-                    raise ValueError("search: step mode is for the MLP one-launch search")
                 cfg = self._cfg
                 new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
                 t.search_conv(cz, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base), float(cfg.pb_c_init),
@@ -421,6 +421,8 @@ class MuZeroMCTSCtree(object):
                           _lib.stream_ptr())
                 if step.get("increment", True):
                     step["count"].add_(1)
+            t.searched()
+            self.last_path = "fused-conv" if cz is not None else ("fused-mlp" if fz is not None else "generic")
             roots._last_minmax = buf.mm
             self.last_record = rec
 
@@ -644,20 +646,31 @@ class EfficientZeroMCTSCtree(object):
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
             cz = self._fused_conv(model, t, shape, Hl)
             if cz is not None:
-                # the conv network's whole search, reward LSTM included, in one launch (lzm_search_conv_ez)
+                # the conv network's whole search, reward LSTM included, in one launch (lzm_search_conv_ez);
+                # the launch needs its whole grid co-resident: when the runtime refuses that (the GPU is
+                # shared with other work), nothing ran and the generic per-simulation path runs instead
                 cfg = self._cfg
                 new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
-                t.search_conv_ez(cz, S, buf.mm, buf.seeds, buf.vtp_in, buf.pool, buf.extra[0], buf.extra[1],
-                                 int(cfg.lstm_horizon_len), int(cfg.pb_c_base), float(cfg.pb_c_init),
-                                 float(np.float32(cfg.discount_factor)),
-                                 bool(cfg.model.get('categorical_distribution', True)), rec=rec)
+                try:
+                    t.search_conv_ez(cz, S, buf.mm, buf.seeds, buf.vtp_in, buf.pool, buf.extra[0], buf.extra[1],
+                                     int(cfg.lstm_horizon_len), int(cfg.pb_c_base), float(cfg.pb_c_init),
+                                     float(np.float32(cfg.discount_factor)),
+                                     bool(cfg.model.get('categorical_distribution', True)), rec=rec)
+                    self.last_path = "fused"
+                except _lib.ResidencyError:
+                    self.residency_fallbacks = getattr(self, "residency_fallbacks", 0) + 1
+                    self.last_path = "generic (co-residency refused)"
+                    self._loop(t, model, buf, S, row, Hl, rec)
             elif graph:
+                self.last_path = "generic"
                 if entry is None:
                     entry = self._capture(t, model, buf, S, row, Hl)
                     self._graphs.put(gkey, entry)
                 entry.replay()
             else:
+                self.last_path = "generic"
                 self._loop(t, model, buf, S, row, Hl, rec)
+            t.searched()
             roots._last_minmax = buf.mm
             self.last_record = rec
 

@@ -78,6 +78,25 @@ class DeviceTree:
         self.search_len = torch.zeros(B, **i32)
         self.is_reset = torch.zeros(B, **i32)
         self.seed_buf = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._unchecked = False  # a search ran whose error words no getter has checked yet
+
+    def searched(self):
+        """mark that a search (or traverse) ran: the next result getter checks the error words once"""
+        self._unchecked = True
+
+    def check_once(self):
+        """check_errors(clear=True) once per search, by whichever result getter runs first: raises
+        LzmError when the search's tie-break stream broke (the words are cleared as they are read, so a
+        pooled tree never carries them into the next owner's searches)"""
+        if self._unchecked:
+            self._unchecked = False
+            self.check_errors(clear=True)
+
+    def reset_errors(self, stream=None):
+        """zero the sticky error words without raising (a recycled handle starts clean); synchronises"""
+        out = (ctypes.c_int32 * 4)()
+        _lib.load().lzm_check_errors(self.h, out, 1, stream_ptr(stream))
+        self._unchecked = False
 
     @property
     def sims_capacity(self):
@@ -136,6 +155,7 @@ class DeviceTree:
 
     def traverse(self, minmax, seed, vtp_in, pb_c_base=19652, pb_c_init=1.25, discount=0.997, stream=None):
         """seed: 1-element device tensor (int32/uint32 bits)."""
+        self._unchecked = True
         call("lzm_traverse", self.h, int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax), ptr(seed),
              ptr(vtp_in), ptr(self.x), ptr(self.y), ptr(self.action), ptr(self.action64), ptr(self.vtp),
              ptr(self.search_len), stream_ptr(stream))
@@ -172,6 +192,7 @@ class DeviceTree:
                    discount=0.997, rec=None, stream=None):
         """One launch for the whole search (lzm_search_mlp); rec: optional _Recorder-like object."""
         r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n)))
+        self._unchecked = True
         call("lzm_search_mlp", self.h, dims["hidden"], dims["head_hidden"], dims["support"], int(dims["res"]),
              ptr(weights), int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax), ptr(seeds),
              ptr(vtp_in), ptr(pool), r("x"), r("action"), r("search_len"), r("decoded"), r("policy_logits"),
@@ -183,6 +204,7 @@ class DeviceTree:
         split-bf16 conv_infer.FoldedConvNet); rec: optional _Recorder-like object."""
         r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n)))
         hp = net.heads
+        self._unchecked = True
         call("lzm_search_conv", self.h, int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax),
              ptr(seeds), ptr(vtp_in), ptr(pool), ptr(net.native), ptr(net.actmap), int(net.n_dres), int(net.n_pres),
              int(net.r_ch), int(net.h_ch), ptr(hp["w1t"]), ptr(hp["b1"]), ptr(hp["w2q"]), ptr(hp["b2"]), int(hp["Kr"]),
@@ -197,6 +219,7 @@ class DeviceTree:
         (with is_reset)."""
         r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n, None)))
         hp, t = net.heads, net.t
+        self._unchecked = True
         call("lzm_search_conv_ez", self.h, int(S), int(pb_c_base), float(pb_c_init), float(discount), ptr(minmax),
              ptr(seeds), ptr(vtp_in), ptr(pool), ptr(hpool), ptr(cpool), int(hpool.shape[2]), int(horizon),
              ptr(net.native), ptr(net.actmap), int(net.n_dres), int(net.n_pres), int(net.r_ch), int(net.h_ch),
@@ -224,6 +247,8 @@ class DeviceTree:
         handle, i.e. when the parity-mode tie-break stream may differ from the reference's.
         Returns the four counters otherwise (all zero)."""
         out = (ctypes.c_int32 * 4)()
+        if clear:
+            self._unchecked = False
         call("lzm_check_errors", self.h, out, int(bool(clear)), stream_ptr(stream))
         return list(out)
 
@@ -293,6 +318,10 @@ class TreePool:
             t = DeviceTree(B, A, max_sims, ez=ez, fast_rng=fast_rng, device=device)
         else:
             t.reserve(max_sims)
+            # the previous owner's sticky error words must not surface in this owner's searches
+            # (ADVICE r03); acquiring happens between searches, never inside a graph capture
+            if not torch.cuda.is_current_stream_capturing():
+                t.reset_errors()
         return t
 
     def release(self, t):

@@ -18,7 +18,7 @@ Two paths behind the one surface:
   `_compute_priorities` (:200-227). With `lightzero_amd.policy.MuZeroCollectPolicy` the search runs
   on the GPU and the noise / action draws come from numpy exactly as the reference draws them: the
   collector's host-parity mode.
-- device path (`env` a `lightzero_amd.envs.DeviceCartPoleEnvManager`, `policy` a
+- device path (`env` a `lightzero_amd.envs.DeviceEnvManager` — CartPole or the Breakout stand-in —, `policy` a
   MuZeroCollectPolicy): every env steps inside one HIP graph per iteration
   (lightzero_amd.collector.DeviceCollector: fused search, action selection, CartPole physics and
   recording on the GPU, Philox streams), the host polls finished episodes, replays the reference's
@@ -37,7 +37,7 @@ import torch
 import torch.distributed as dist
 from scipy.stats import entropy
 
-from ..envs import DeviceCartPoleEnvManager
+from ..envs import DeviceEnvManager
 from ..game_segment import GameSegment
 from .segments import EpisodeSchedule, episode_segments
 
@@ -220,7 +220,8 @@ class MuZeroCollector:
             if self._default_n_episode is None:
                 raise RuntimeError("Please specify collect n_episode")
             n_episode = self._default_n_episode
-        assert n_episode >= self._env_num, "Please make sure n_episode >= env_num{}/{}".format(n_episode, self._env_num)
+        if n_episode < self._env_num:
+            raise AssertionError(f"collect: n_episode ({n_episode}) must be at least the env count ({self._env_num})")
         policy_kwargs = {} if policy_kwargs is None else policy_kwargs
         temperature = policy_kwargs['temperature']
         epsilon = policy_kwargs['epsilon']
@@ -290,7 +291,7 @@ class MuZeroCollector:
                         self._env.reset({env_id: None})
                         self._policy.reset([env_id])
                         self._reset_stat(env_id)
-                        self._logger.info('Env{} returns a abnormal step, its info is {}'.format(env_id, timestep.info))
+                        self._logger.info(f"env {env_id}: abnormal step, reset ({timestep.info})")
                         continue
                     out = policy_output[env_id]
                     obs_t, reward, done = timestep.obs, timestep.reward, timestep.done
@@ -383,9 +384,9 @@ class MuZeroCollector:
     def _device_path(self, collect_with_pure_policy):
         from ..policy import MuZeroCollectPolicy
         cfg = self.policy_config
-        return (isinstance(self._env, DeviceCartPoleEnvManager) and isinstance(self._policy, MuZeroCollectPolicy)
+        return (isinstance(self._env, DeviceEnvManager) and isinstance(self._policy, MuZeroCollectPolicy)
                 and not collect_with_pure_policy and not cfg.eps.eps_greedy_exploration_in_collect
-                and cfg.model.frame_stack_num == 1)
+                and cfg.model.frame_stack_num == self._env.frame_stack)
 
     def _device_collector(self, temperature):
         from ..collector import DeviceCollector
@@ -398,7 +399,8 @@ class MuZeroCollector:
                 temperature=temperature, noise_alpha=cfg.root_dirichlet_alpha, noise_weight=cfg.root_noise_weight,
                 seed=env.seed, rng_mode=cfg.get('device_rng', 'glibc'), graph=True,
                 poll_every=cfg.get('device_poll_every', 4), record_pred=bool(cfg.use_priority),
-                support_scale=cfg.model.support_scale)
+                support_scale=cfg.model.support_scale, env=env.env_kind,
+                categorical_distribution=bool(cfg.model.get('categorical_distribution', True)))
         else:
             self._device.set_temperature(temperature)
         return self._device
@@ -415,14 +417,14 @@ class MuZeroCollector:
         col.restart()
         sched = EpisodeSchedule(n, n_episode)
         pool = []
+        infos = []
         collected_step = 0
         mask = np.ones(col.A, np.int8)
+        t_start = time.perf_counter()
         while not sched.complete:
-            t0 = time.perf_counter()
             for _ in range(col.poll_every):
                 col.step()
             finished = col.pull_new()
-            dt = time.perf_counter() - t0
             for start, i, e in sched.take([(e["env_id"], len(e["action_segment"]), e) for e in finished]):
                 L = len(e["action_segment"])
                 for it, k, seg, prio, d in episode_segments(cfg, self._env.action_space, e["obs_segment"],
@@ -431,8 +433,14 @@ class MuZeroCollector:
                                                             start, mask, -1):
                     pool.append((it, i, k, seg, prio, d))
                 collected_step += L
-                self._episode_info.append({'reward': float(L), 'time': L * dt / (col.poll_every * n), 'step': L,
-                                           'visit_entropy': self._visit_entropy(e["visits"], temperature)})
+                infos.append({'reward': float(L), 'time': 0.0, 'step': L,
+                              'visit_entropy': self._visit_entropy(e["visits"], temperature)})
+        # the loop's wall time is the collect duration (all envs step together on the device); each
+        # counted episode gets the share of it its steps make up, so the per-episode times sum to it
+        wall = time.perf_counter() - t_start
+        for d in infos:
+            d['time'] = wall * d['step'] / max(collected_step, 1)
+        self._episode_info.extend(infos)
         self.last_schedule = sched  # (tests: the counted episodes per env)
         pool.sort(key=lambda x: (x[0], x[1], x[2]))
         for _, _, _, seg, prio, d in pool:

@@ -519,6 +519,39 @@ static void *bench_worker(void *p) {
   return NULL;
 }
 
+/* ---------------------------------------------------------------- diagnostics (tests only) */
+int lzo_get_path_actions(const lzo_tree *t, int i, int32_t *out, int cap) {
+  const int32_t *path = t->path + (size_t)i * t->cap;
+  int np = t->pathlen[i], l, n = 0;
+  for (l = 0; l + 1 < np && n < cap; ++l) {
+    int parent_latent = t->latent[NODE(t, i, path[l])];
+    out[n++] = path[l + 1] - 1 - t->A * parent_latent; /* child_of inverted */
+  }
+  return n;
+}
+
+int lzo_path_scores(const lzo_tree *t, int i, int pb_c_base, float pb_c_init, float disc, int players,
+                    const int32_t *actions, int n, float *out) {
+  int node = 0, is_root = 1, lvl = 0, a, j;
+  float parent_q = 0.0f;
+  while (lvl <= n && t->latent[NODE(t, i, node)] >= 0) {
+    size_t p = NODE(t, i, node);
+    float mean_q = compute_mean_q(t, i, node, is_root, parent_q, disc);
+    is_root = 0;
+    parent_q = mean_q;
+    for (a = 0; a < t->A; ++a) out[(size_t)lvl * t->A + a] = -INFINITY;
+    for (j = 0; j < legal_n(t, i, node); ++j) {
+      a = legal_at(t, i, node, j);
+      out[(size_t)lvl * t->A + a] = ucb_score(t, i, p, NODE(t, i, child_of(t, i, node, a)), mean_q,
+                                              (float)(t->visit[p] - 1), (float)pb_c_base, pb_c_init, disc, players);
+    }
+    if (lvl == n) return lvl + 1;
+    node = child_of(t, i, node, actions[lvl]);
+    lvl += 1;
+  }
+  return lvl;
+}
+
 double lzo_bench_tree_only(int B, int A, int S, int threads, int searches, uint32_t seed) {
   pthread_t th[256];
   bench_arg args[256];

@@ -49,6 +49,13 @@ void lzo_backprop(lzo_tree *t, int current_latent_state_index, float discount, c
 void lzo_get_distributions(const lzo_tree *t, int32_t *out /*[B][A], -1 padded*/);
 void lzo_get_values(const lzo_tree *t, float *out);
 int lzo_get_trajectories(const lzo_tree *t, int32_t *out /*[B][tmax], -1 padded*/, int tmax);
+/* Diagnostics (tests only). lzo_get_path_actions: root i's last traverse path as actions, returns its
+ * length. lzo_path_scores: the pUCT scores cselect_child computes at each level of root i's walk down
+ * `actions` (n of them) in the tree as it stands — the mean-q chain as cbatch_traverse carries it from
+ * parent_q = 0 — out [n + 1][A], -inf for actions not legal at the level; returns the levels written. */
+int lzo_get_path_actions(const lzo_tree *t, int i, int32_t *out, int cap);
+int lzo_path_scores(const lzo_tree *t, int i, int pb_c_base, float pb_c_init, float disc, int players,
+                    const int32_t *actions, int n, float *out);
 
 /* CPU baseline: tree-only search with scripted network responses, envs partitioned over
  * `threads` pthreads (each shard its own batch + RNG stream, i.e. shard-local parity).

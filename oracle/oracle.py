@@ -55,6 +55,11 @@ def lib():
         L.lzo_glibc_rand.argtypes = [ctypes.c_void_p]
         L.lzo_expf_mismatches.restype = ctypes.c_long
         L.lzo_expf_mismatches.argtypes = [ctypes.c_uint32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]
+        L.lzo_get_path_actions.restype = ctypes.c_int
+        L.lzo_get_path_actions.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p, ctypes.c_int]
+        L.lzo_path_scores.restype = ctypes.c_int
+        L.lzo_path_scores.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                      ctypes.c_int, _i32p, ctypes.c_int, _f32p]
         L.lzo_bench_tree_only.restype = ctypes.c_double
         L.lzo_bench_tree_only.argtypes = [ctypes.c_int] * 5 + [ctypes.c_uint32]
         _lib = L
@@ -124,6 +129,21 @@ class OracleTree:
         out = np.zeros(self.B, np.float32)
         lib().lzo_get_values(self._h, out)
         return out
+
+    def path_actions(self, i):
+        """root i's last traverse path as actions (diagnostics)"""
+        out = np.zeros(self.B * 4 + 64, np.int32)
+        n = lib().lzo_get_path_actions(self._h, int(i), out, out.shape[0])
+        return out[:n].copy()
+
+    def path_scores(self, i, actions, pb_c_base=19652, pb_c_init=1.25, discount=0.997, players=1):
+        """the pUCT scores [levels, A] cselect_child computes along root i's walk down `actions`
+        (diagnostics; -inf where an action is not legal)"""
+        acts = np.ascontiguousarray(actions, np.int32)
+        out = np.zeros((len(acts) + 1, self.A), np.float32)
+        n = lib().lzo_path_scores(self._h, int(i), int(pb_c_base), np.float32(pb_c_init), np.float32(discount),
+                                  int(players), acts, len(acts), out)
+        return out[:n]
 
     def trajectories(self, tmax=64):
         out = np.zeros((self.B, tmax), np.int32)

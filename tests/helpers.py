@@ -265,3 +265,21 @@ def az_scripted_pv_torch(state):
     priors = (1 + (7 * h[:, None] + 13 * a[None, :]) % 16).to(torch.float32) / 64.0
     value = ((31 * h) % 129 - 64).to(torch.float32) / 64.0
     return priors, value
+
+
+def tie_list(scores):
+    """cselect_child's order-dependent tie list (cnode.cpp:551-596) over one level's scores, in float32:
+    scan in action order from max_score = FLOAT_MIN (-1e6); a score above the max restarts the list,
+    one within 1e-6 below it joins (non-legal actions carry -inf and never join)."""
+    mx = np.float32(-1e6)
+    eps = np.float32(1e-6)
+    lst = []
+    for a, s in enumerate(np.asarray(scores, np.float32)):
+        if not np.isfinite(s):
+            continue
+        if mx < s:
+            mx = s
+            lst = [a]
+        elif s >= np.float32(mx - eps):
+            lst.append(a)
+    return lst

@@ -64,13 +64,20 @@ def test_single_rank_helpers():
 
 
 # ---------------------------------------------------------------- trajectory all-gather (§8(e))
-N_ENV, E_SLOTS, T_MAX, OBS, ACT = 5, 3, 9, 4, 2
+N_ENV, E_SLOTS, T_MAX, ACT = 5, 3, 9, 2
+# CartPole: one float32 [4] observation per step; Atari (config 5): one u8 [1, 64, 64] grey frame per step
+KINDS = {"vector": ((4,), torch.float32, 1.0), "image": ((1, 64, 64), torch.uint8, 1.0 / 255.0)}
 
 
-def _fake_records(rank):
+def _fake_records(rank, kind="vector"):
     """a rank's collector slots with random contents and a rank-dependent set of finished episodes"""
+    shape, dtype, _ = KINDS[kind]
     g = torch.Generator().manual_seed(100 + rank)
-    rec = dict(obs=torch.randn(N_ENV, E_SLOTS, T_MAX + 1, OBS, generator=g),
+    if dtype == torch.uint8:
+        frames = torch.randint(0, 256, (N_ENV, E_SLOTS, T_MAX + 1) + shape, generator=g, dtype=torch.uint8)
+    else:
+        frames = torch.randn((N_ENV, E_SLOTS, T_MAX + 1) + shape, generator=g)
+    rec = dict(obs=frames,
                action=torch.randint(0, ACT, (N_ENV, E_SLOTS, T_MAX), generator=g, dtype=torch.int32),
                reward=torch.randn(N_ENV, E_SLOTS, T_MAX, generator=g),
                child=torch.randint(0, 30, (N_ENV, E_SLOTS, T_MAX, ACT), generator=g, dtype=torch.int32),
@@ -81,13 +88,15 @@ def _fake_records(rank):
     return rec, eps
 
 
-def _expected(rank):
-    rec, eps = _fake_records(rank)
+def _expected(rank, kind="vector"):
+    rec, eps = _fake_records(rank, kind)
+    scale = KINDS[kind][2]
     out = []
     for i, e, L in eps:
-        out.append(dict(env_id=i, obs=rec["obs"][i, e, :L + 1].numpy(), action=rec["action"][i, e, :L].numpy(),
-                        reward=rec["reward"][i, e, :L].numpy(), child=rec["child"][i, e, :L].numpy(),
-                        value=rec["value"][i, e, :L].numpy()))
+        obs = rec["obs"][i, e, :L + 1].numpy().astype(np.float32)
+        out.append(dict(env_id=i, obs=obs * np.float32(scale) if scale != 1.0 else obs,
+                        action=rec["action"][i, e, :L].numpy(), reward=rec["reward"][i, e, :L].numpy(),
+                        child=rec["child"][i, e, :L].numpy(), value=rec["value"][i, e, :L].numpy()))
     return out
 
 
@@ -95,7 +104,7 @@ def _check_episodes(got, want, rank):
     assert len(got) == len(want)
     for g, w in zip(got, want):
         assert g["rank"] == rank and g["env_id"] == w["env_id"]
-        assert np.array_equal(g["obs_segment"], w["obs"])
+        assert g["obs_segment"].dtype == np.float32 and np.array_equal(g["obs_segment"], w["obs"])
         assert np.array_equal(g["action_segment"], w["action"].astype(np.int64))
         assert np.array_equal(g["reward_segment"], w["reward"])
         assert np.array_equal(g["visits"], w["child"].astype(np.int64))
@@ -106,41 +115,83 @@ def _check_episodes(got, want, rank):
         assert g["to_play_segment"].shape == (len(w["action"]),)
 
 
-def _traj_worker(rank, world, port, out_dir):
-    from lightzero_amd.trajectory import all_gather_packed, allreduce_stats, pack_episodes
+def _pack(rank, kind):
+    from lightzero_amd.trajectory import pack_episodes
+    rec, eps = _fake_records(rank, kind)
+    return pack_episodes(rec["obs"], rec["action"], rec["reward"], rec["child"], rec["value"], eps,
+                         frame_scale=KINDS[kind][2]), eps
+
+
+def _traj_worker(rank, world, port, out_dir, kind):
+    from lightzero_amd.trajectory import all_gather_packed, allreduce_stats
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        rec, eps = _fake_records(rank)
-        packed, index = pack_episodes(rec["obs"], rec["action"], rec["reward"], rec["child"], rec["value"], eps)
-        blocks = all_gather_packed(packed, index)
+        block, eps = _pack(rank, kind)
+        blocks = all_gather_packed(block)
         stats = allreduce_stats(10.0 * (rank + 1), float(len(eps)), 0.25, torch.device("cpu"))
-        np.savez(os.path.join(out_dir, f"r{rank}.npz"), stats=np.array(stats),
-                 **{f"p{r}": p for r, (p, _) in enumerate(blocks)}, **{f"i{r}": i for r, (_, i) in enumerate(blocks)})
+        arrays = {}
+        for r, b in enumerate(blocks):
+            arrays.update({f"f{r}": b.frames, f"s{r}": b.scalars, f"i{r}": b.index, f"c{r}": np.float64(b.frame_scale)})
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), stats=np.array(stats), **arrays)
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_trajectory_all_gather_gloo_world2(tmp_path):
-    from lightzero_amd.trajectory import unpack_episodes
+@pytest.mark.parametrize("kind", ["vector", "image"])
+def test_trajectory_all_gather_gloo_world2(tmp_path, kind):
+    """every rank ends with every rank's episodes — CartPole vectors and config 5's u8 image frames
+    (sent as bytes, unpacked to the reference's float32 frame / 255)"""
+    from lightzero_amd.trajectory import TrajBlock, unpack_episodes
     world = 2
-    mp.spawn(_traj_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_traj_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True)
     for me in range(world):
         r = np.load(tmp_path / f"r{me}.npz")
         for rank in range(world):  # every rank holds every rank's episodes
-            got = unpack_episodes(r[f"p{rank}"], r[f"i{rank}"], OBS, ACT, rank)
-            _check_episodes(got, _expected(rank), rank)
+            blk = TrajBlock(r[f"f{rank}"], r[f"s{rank}"], r[f"i{rank}"], float(r[f"c{rank}"]))
+            assert blk.frames.dtype == (np.uint8 if kind == "image" else np.float32)
+            _check_episodes(unpack_episodes(blk, ACT, rank), _expected(rank, kind), rank)
         n_eps = sum(len(_fake_records(k)[1]) for k in range(world))
         assert tuple(r["stats"]) == (30.0, float(n_eps), 0.5)
 
 
-def test_pack_unpack_round_trip_and_empty():
+@pytest.mark.parametrize("kind", ["vector", "image"])
+def test_pack_unpack_round_trip_and_empty(kind):
     from lightzero_amd.trajectory import pack_episodes, unpack_episodes
-    rec, eps = _fake_records(0)
-    packed, index = pack_episodes(rec["obs"], rec["action"], rec["reward"], rec["child"], rec["value"], eps)
-    assert packed.shape == (sum(L + 1 for _, _, L in eps), OBS + 3 + ACT)
-    _check_episodes(unpack_episodes(packed.numpy(), index.numpy(), OBS, ACT), _expected(0), 0)
-    p0, i0 = pack_episodes(rec["obs"], rec["action"], rec["reward"], rec["child"], rec["value"], [])
-    assert p0.shape == (0, OBS + 3 + ACT) and i0.shape == (0, 3)
-    assert unpack_episodes(p0.numpy(), i0.numpy(), OBS, ACT) == []
+    block, eps = _pack(0, kind)
+    rows = sum(L + 1 for _, _, L in eps)
+    assert block.scalars.shape == (rows, 3 + ACT) and tuple(block.frames.shape) == (rows,) + KINDS[kind][0]
+    _check_episodes(unpack_episodes(block, ACT), _expected(0, kind), 0)
+    rec, _ = _fake_records(0, kind)
+    b0 = pack_episodes(rec["obs"], rec["action"], rec["reward"], rec["child"], rec["value"], [])
+    assert b0.scalars.shape == (0, 3 + ACT) and tuple(b0.index.shape) == (0, 3) and b0.frames.shape[0] == 0
+    assert unpack_episodes(b0, ACT) == []
+
+
+def test_image_episode_segments_frame_stack():
+    """an image episode through the segment cutter: every segment starts with the frame_stack_num
+    window ending at its first frame (the reset frame repeated at the episode start, game_segment.py:
+    95-127) and carries one frame per step after it (muzero_collector.py:305-632)"""
+    from lightzero_amd.trajectory import unpack_episodes
+    from lightzero_amd.utils import EasyDict
+    from lightzero_amd.worker.segments import episode_segments
+    block, eps = _pack(1, "image")
+    ep = max(unpack_episodes(block, ACT), key=lambda e: len(e["action_segment"]))
+    L, fs = len(ep["action_segment"]), 4
+    cfg = EasyDict(dict(game_segment_length=4, num_unroll_steps=2, td_steps=3, discount_factor=0.997,
+                        model=EasyDict(dict(frame_stack_num=fs, action_space_size=ACT, observation_shape=(4, 64, 64),
+                                            image_channel=1))))
+
+    class Space:
+        n = ACT
+    segs = episode_segments(cfg, Space(), ep["obs_segment"], ep["action_segment"], ep["reward_segment"], ep["visits"],
+                            ep["root_value_segment"], None, 0, np.ones(ACT, np.int8), -1)
+    obs = ep["obs_segment"]
+    window = np.concatenate([np.repeat(obs[:1], fs - 1, axis=0), obs])
+    for j, (_, _, seg, _, _) in enumerate(segs):
+        s0, n = 4 * j, len(seg.action_segment)
+        assert seg.obs_segment.shape[1:] == (1, 64, 64)
+        assert np.array_equal(seg.obs_segment[:fs + n], window[s0:s0 + fs + n])
+        assert np.array_equal(seg.action_segment, ep["action_segment"][s0:s0 + n])
+    assert sum(len(s.action_segment) for _, _, s, _, _ in segs) == L

@@ -79,6 +79,7 @@ def run_search(kind, B, S, seed, graph=False, record=True, model=None, mcts=None
                lat0=out.latent_state, hidden0=getattr(out, "reward_hidden_state", None), A=A, scale=scale)
     res["rec"] = None if mcts.last_record is None else mcts.last_record.numpy() | (
         {"is_reset": mcts.last_record.is_reset.cpu().numpy()} if kind == "ez" else {})
+    res["path"] = getattr(mcts, "last_path", None)
     roots.clear()
     return res
 
@@ -164,6 +165,8 @@ def test_fused_conv_search_equals_generic(kind, B, S, rng, zero):
     model = conv_model(kind, 13, zero_heads=zero)
     out = [run_search(kind, B, S, seed=14, model=model, fused=f, rng=rng) for f in (True, False)]
     a, b = out
+    # the one-launch search really ran (EZ: a cooperative launch the runtime accepted)
+    assert a["path"] in ("fused", "fused-conv") and b["path"] == "generic", (a["path"], b["path"])
     for key in ("dist", "values", "traj"):
         assert np.array_equal(a[key], b[key]), key
     for key in ("x", "action", "search_len", "decoded", "policy_logits") + (("is_reset",) if kind == "ez" else ()):
@@ -424,5 +427,13 @@ def test_search_bf16x3_vs_f32_trunk(kind, monkeypatch):
     rate = float(differ.mean())
     print(f"{kind}: roots whose visit counts differ between f32 and bf16x3 trunks: {int(differ.sum())}/{B} ({rate:.3f})")
     assert rate <= 0.1, rate
+    # every root's first divergent walk: a near-tie moved by rounding, or a tie broken at a shifted
+    # position of the glibc stream after an earlier root diverged (tests/divergence.py); reported to
+    # $LZM_REPORT_DIR/divergence_conv_<kind>_bf16x3_vs_f32.json
+    from tests.divergence import attribute, report
+    rep = attribute(res["f32"], res["bf16x3"], B, S, res["f32"]["A"], ez=(kind == "ez"))
+    report(f"conv_{kind}_bf16x3_vs_f32", rep)
+    assert rep["first_divergence_kinds"].get("unexplained", 0) == 0, rep["first_divergences"][:5]
+    assert rep["first_divergence_kinds"].get("tie_draw", 0) == 0
     same = ~differ
     np.testing.assert_allclose(res["bf16x3"]["values"][same], res["f32"]["values"][same], rtol=1e-3, atol=1e-3)

@@ -22,14 +22,16 @@ def _free_port():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(240)
-def test_sharded_device_collect_all_gather_world2(tmp_path):
+@pytest.mark.parametrize("env", ["cartpole", "breakout"])
+def test_sharded_device_collect_all_gather_world2(tmp_path, env):
+    """env: config 2's CartPole shard, or config 5's Breakout shard (conv search, u8 image frames)"""
     world, port = 2, _free_port()
     procs = []
     for rank in range(world):
-        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+        penv = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                    MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "dist_gpu_worker.py"),
-                                       str(tmp_path)], env=env, cwd=REPO))
+                                       str(tmp_path), env], env=penv, cwd=REPO))
     codes = [p.wait(timeout=200) for p in procs]
     assert codes == [0] * world, f"worker exit codes {codes}"
     outs = [np.load(tmp_path / f"out_{r}.npz") for r in range(world)]
@@ -40,6 +42,8 @@ def test_sharded_device_collect_all_gather_world2(tmp_path):
     for r in range(world):
         mine = outs[0]["lens"][outs[0]["ranks"] == r]
         assert np.array_equal(mine, outs[r]["own"]), f"rank {r}'s episodes differ after the all-gather"
+    assert np.array_equal(outs[0]["sums"], outs[1]["sums"])
+    assert tuple(outs[0]["shape"]) == ((1, 64, 64) if env == "breakout" else (4,))
     tot = sum(int(o["envstep"]) for o in outs)
     for o in outs:
         assert int(o["world"]) == world

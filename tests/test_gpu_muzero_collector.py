@@ -112,3 +112,31 @@ def test_device_path_segments_match_restatement(n, n_ep, gsl, prio):
             assert np.all(np.abs(e["obs"][0]) <= 0.05 + 1e-7)
         seen.append(segs[0].obs_segment.copy())
     assert not np.array_equal(seen[0], seen[1])  # the second collect plays fresh episodes
+
+
+def test_device_path_breakout_segments_match_restatement():
+    """config 5's device path through the MuZeroCollector drop-in: the Breakout stand-in env (u8 frames,
+    frame_stack_num 4), episodes cut into segments whose observation windows stack 4 frames — identical
+    to the restatement of the reference's loop fed the same episodes"""
+    import bench
+    from lightzero_amd.envs import DeviceBreakoutEnvManager
+    from lightzero_amd.policy import MuZeroCollectPolicy, policy_config
+    from lightzero_amd.worker import MuZeroCollector
+    n, n_ep = 16, 24
+    cfg = policy_config(num_simulations=8, game_segment_length=12, device=DEV, use_priority=True, n_episode=n,
+                        model=dict(frame_stack_num=4, action_space_size=4, observation_shape=(4, 64, 64),
+                                   image_channel=1, model_type='conv'))
+    model = bench.build_conv_model(DEV, seed=3)
+    col = MuZeroCollector(env=DeviceBreakoutEnvManager(n, seed=7, max_episode_steps=150),
+                          policy=MuZeroCollectPolicy(cfg, model), policy_config=cfg)
+    segs, meta = col.collect(n_episode=n_ep, policy_kwargs=dict(temperature=1.0, epsilon=0.0))
+    eps = _played(col.last_schedule)
+    assert sum(len(e) for e in eps) == n_ep
+    env = EpisodeEnv(eps)
+    ref_segs, ref_meta, _ = ref_collect(cfg, env, EpisodeForward(env), n_ep)
+    _compare(segs, meta, ref_segs, ref_meta)
+    for g in segs:
+        assert g.obs_segment.shape[1:] == (1, 64, 64) and g.obs_segment.dtype == np.float32
+        assert len(g.obs_segment) >= 4 + len(g.action_segment)
+    for e in sum(eps, []):
+        assert (e["visits"].sum(axis=1) == 8).all() and set(np.unique(e["reward"])) <= {0.0, 1.0}

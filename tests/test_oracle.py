@@ -74,3 +74,27 @@ def test_host_search_loop_is_deterministic():
 def test_cpu_baseline_driver_runs():
     secs = lib().lzo_bench_tree_only(64, 2, 10, 2, 1, 1)
     assert secs > 0
+
+
+def test_path_scores_diagnostic_agrees_with_traverse():
+    """oracle.path_scores (the divergence attribution's tool): along every root's traverse path the
+    action taken is in the tie list of the scores the diagnostic recomputes at that level"""
+    from tests.helpers import tie_list
+    tr = random_transcript(24, 16, 3, seed=9, net="rand")
+    B, S, A = 24, 16, 3
+    ot = OracleTree(B, A, S)
+    ot.set_delta(np.float32(0.01))
+    ot.prepare(np.float32(0.25), tr["noises"], tr["root_reward"], tr["root_logits"], np.full(B, -1, np.int32))
+    levels = 0
+    for k in range(S):
+        x, y, a, vtp, slen = ot.traverse(19652, np.float32(1.25), np.float32(0.997), 1000 + k, np.full(B, -1, np.int32))
+        for i in range(B):
+            acts = ot.path_actions(i)
+            assert len(acts) == slen[i] and acts[-1] == a[i]
+            sc = ot.path_scores(i, acts)
+            assert sc.shape[0] == len(acts)  # the leaf below the last action is not expanded yet
+            for lvl, act in enumerate(acts):
+                assert act in tie_list(sc[lvl]), (k, i, lvl)
+                levels += 1
+        ot.backprop(k + 1, np.float32(0.997), tr["resp_reward"][k], tr["resp_value"][k], tr["resp_logits"][k], vtp)
+    assert levels > B * S
