@@ -9,6 +9,8 @@ Restates, from the reference (paths relative to /root/reference):
   lzero/worker/muzero_collector.py:200-301     _compute_priorities, pad_and_save_last_trajectory
   lzero/mcts/buffer/game_segment.py:129-294    append, store_search_stats, pad_over, to_array
   lzero/policy/muzero.py:617-740               _forward_collect (noise, roots, search, select_action)
+  lzero/policy/muzero.py:783-867               _forward_eval (prepare_no_noise, search, argmax)
+  lzero/policy/efficientzero.py:538-656        _forward_collect with the value-prefix tree (is_reset)
   lzero/policy/utils.py:515-539                select_action
 
 `replay_forward` is _forward_collect with the search done by the oracle tree (oracle.OracleTree,
@@ -166,6 +168,61 @@ class ReplayForward:
     def __init__(self, cfg, records):
         self.cfg, self.records, self.k = cfg, records, 0
         self.mismatch = []
+        # EfficientZeroPolicy (efficientzero.py:538-656): the value-prefix tree, is_reset every
+        # lstm_horizon_len levels (mcts_ctree.py:810-816)
+        self.ez = cfg.get('type', 'muzero') == 'efficientzero'
+
+    def _tree_search(self, rec, B, legal, noises, to_play):
+        """the oracle tree replaying the GPU run's recorded search; returns (distributions, values)"""
+        cfg = self.cfg
+        A = max(len(l) for l in legal)
+        S = cfg.num_simulations
+        t = OracleTree(B, A, S, ez=self.ez)
+        lg = np.full((B, A), -1, np.int32)
+        for j, l in enumerate(legal):
+            lg[j, :len(l)] = l
+        t.set_legal(lg, np.array([len(l) for l in legal], np.int32))
+        t.set_delta(VDM)
+        nz = None
+        if noises is not None:
+            nz = np.zeros((B, A), np.float32)
+            for j, z in enumerate(noises):
+                nz[j, :len(z)] = z
+        tp = np.array([int(x) for x in to_play], np.int32)
+        weight = np.float32(cfg.root_noise_weight) if noises is not None else np.float32(0.0)
+        t.prepare(weight, nz, np.asarray(rec.get('reward_roots', np.zeros(B)), np.float32), rec['root_logits'], tp)
+        sr = rec['search']
+        horizon = int(cfg.get('lstm_horizon_len', 5))
+        for s in range(S):
+            x, y, a, vtp, slen = t.traverse(PB_C_BASE, PB_C_INIT, DISC, int(sr['seeds'][s]), tp)
+            if not (np.array_equal(x, sr['x'][s]) and np.array_equal(a, sr['action'][s])
+                    and np.array_equal(slen, sr['search_len'][s])):
+                self.mismatch.append((self.k - 1, 'request', s))
+            is_reset = (slen % horizon == 0).astype(np.int32) if self.ez else None
+            t.backprop(s + 1, DISC, sr['decoded'][s][:, 0], sr['decoded'][s][:, 1], sr['policy_logits'][s], vtp,
+                       is_reset)
+        return t.distributions(), t.values()
+
+    def _check_data(self, data, rec):
+        if not np.array_equal(np.asarray(data, np.float32).reshape(-1), np.asarray(rec['data'], np.float32).reshape(-1)):
+            self.mismatch.append((self.k - 1, 'observations'))
+
+    def eval(self, data, action_mask, to_play, ready_env_id):
+        """_forward_eval (muzero.py:783-867): prepare_no_noise, the search, argmax (no draw)"""
+        rec = self.records[self.k]
+        self.k += 1
+        B = len(ready_env_id)
+        self._check_data(data, rec)
+        legal = [[a for a, m in enumerate(action_mask[j]) if m == 1] for j in range(B)]
+        dist, vals = self._tree_search(rec, B, legal, None, to_play)
+        out = {}
+        for j, env_id in enumerate(ready_env_id):
+            d = [int(v) for v in dist[j][:len(legal[j])]]
+            pos, ent = ref_select_action(d, 1.0, True)
+            out[env_id] = {'action': np.where(np.asarray(action_mask[j]) == 1.0)[0][pos],
+                           'visit_count_distributions': d, 'visit_count_distribution_entropy': ent,
+                           'searched_value': float(vals[j]), 'predicted_value': rec['pred_values'][j]}
+        return out
 
     def __call__(self, data, action_mask, temperature, to_play, epsilon, ready_env_id):
         cfg = self.cfg
@@ -174,35 +231,13 @@ class ReplayForward:
         B = len(ready_env_id)
         assert B == len(rec['root_logits']), (f"forward {self.k - 1}: {B} ready envs, the GPU run had "
                                               f"{len(rec['root_logits'])} (mismatches so far: {self.mismatch[:5]})")
-        if not np.array_equal(np.asarray(data, np.float32), rec['data']):
-            self.mismatch.append((self.k - 1, 'observations'))
+        self._check_data(data, rec)
         legal = [[a for a, m in enumerate(action_mask[j]) if m == 1] for j in range(B)]
         noises = [np.random.dirichlet([cfg.root_dirichlet_alpha] * int(sum(action_mask[j]))).astype(np.float32)
                   .tolist() for j in range(B)]
         if noises != rec['noises']:
             self.mismatch.append((self.k - 1, 'noises'))
-        A = max(len(l) for l in legal)
-        S = cfg.num_simulations
-        t = OracleTree(B, A, S)
-        lg = np.full((B, A), -1, np.int32)
-        for j, l in enumerate(legal):
-            lg[j, :len(l)] = l
-        t.set_legal(lg, np.array([len(l) for l in legal], np.int32))
-        t.set_delta(VDM)
-        nz = np.zeros((B, A), np.float32)
-        for j, z in enumerate(noises):
-            nz[j, :len(z)] = z
-        tp = np.array([int(x) for x in to_play], np.int32)
-        t.prepare(np.float32(cfg.root_noise_weight), nz, np.zeros(B, np.float32), rec['root_logits'], tp)
-        sr = rec['search']
-        for s in range(S):
-            x, y, a, vtp, slen = t.traverse(PB_C_BASE, PB_C_INIT, DISC, int(sr['seeds'][s]), tp)
-            if not (np.array_equal(x, sr['x'][s]) and np.array_equal(a, sr['action'][s])
-                    and np.array_equal(slen, sr['search_len'][s])):
-                self.mismatch.append((self.k - 1, 'request', s))
-            t.backprop(s + 1, DISC, sr['decoded'][s][:, 0], sr['decoded'][s][:, 1], sr['policy_logits'][s], vtp)
-        dist = t.distributions()
-        vals = t.values()
+        dist, vals = self._tree_search(rec, B, legal, noises, to_play)
         out = {}
         for j, env_id in enumerate(ready_env_id):
             d = [int(v) for v in dist[j][:len(legal[j])]]

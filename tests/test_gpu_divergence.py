@@ -59,10 +59,14 @@ def test_fused_vs_torch_network_search_divergence_config2(heads):
     fused = _search(model, True, obs, noises, 5, B, S)
     torch_net = _search(model, False, obs, noises, 5, B, S)
     assert fused["path"] == "fused-mlp" and torch_net["path"] == "generic"
-    rep = attribute(fused, torch_net, B, S, 2)
+    rep = attribute(fused, torch_net, B, S, 2, tau=1e-4)
     report(f"config2_{heads}_heads", rep)
     kinds = rep["first_divergence_kinds"]
     assert kinds.get("unexplained", 0) == 0, rep["first_divergences"][:5]
     # a root whose walk diverges first, with no earlier root diverged, can only do so at a near-tie
     assert kinds.get("tie_draw", 0) == 0, [r for r in rep["first_divergences"] if r["kind"] == "tie_draw"][:3]
     assert (fused["dist"].sum(axis=1) == S).all() and (torch_net["dist"].sum(axis=1) == S).all()
+    # measured (profiles/r04/divergence_config2_*.json): no root's visit counts differ; a few walks part
+    # at near-ties (gaps ~1e-5) and the shared rand() stream then shifts for later roots, but the counts
+    # re-converge. Bound the rate well above that, far below a real divergence.
+    assert rep["rate"] <= 0.02, rep["rate"]

@@ -4,11 +4,19 @@ EfficientZeroModel, 6 actions, LSTM 512, support 101) or MuZeroMCTSCtree (Breako
 MuZeroModel, 4 actions, support 601), random-init weights with non-zero heads, synthetic frames.
 
 Times `searches` full searches (root preparation + search + visit counts, inputs resident in HBM)
-and prints one JSON line with sims/s, the network FLOPs per simulation (torch FlopCounterMode over
-one recurrent_inference at batch B) and the achieved network TFLOP/s against the fp32 MFMA peak.
+and prints one JSON line with sims/s and the network's roofline:
+  - FLOPs per simulation from torch FlopCounterMode over one recurrent_inference at batch B, with the
+    EfficientZero reward LSTM (FlopCounterMode does not see inside nn.LSTM) counted by hand:
+    2 x 4H x (K + H) per row for the gate GEMM (K = reward planes, H = 512);
+  - the matrix work runs split-bf16 (three bf16 terms per f32 operand, SIX bf16 products per f32
+    product) on the bf16 MFMA pipe, so the bound is the dense BF16 peak (2.5 PF)
+    against 6 x the convolution (+ LSTM gate) FLOPs; the f32-equivalent rate is reported beside;
+and, with --cpu-baseline-secs > 0, the CPU baseline of the config (bench.cpu_baseline_conv: the
+reference search loop over the oracle's bit-exact ctree with the same network on torch-CPU over the
+host share, and on this GPU with per-simulation copies; plus the tree alone).
 
     python tools/conv_bench.py --kind ez|mz [--envs 256] [--sims 50] [--searches 5] [--graph 1]
-                               [--precision bf16x3|f32]
+                               [--precision bf16x3|f32] [--cpu-baseline-secs 0]
 """
 import argparse
 import json
@@ -27,9 +35,13 @@ from lightzero_amd.model_conv import atari_efficientzero_model, atari_muzero_mod
 from lightzero_amd.utils import EasyDict  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3
+BF16_PEAK_TFLOPS = 2500.0  # dense (MI355X_MICROARCH.md), not the 2:1-sparse figure
 
 
 def recurrent_flops(model, kind, B, dev):
+    """(all FLOPs, matrix-pipe FLOPs) per simulation row: FlopCounterMode over recurrent_inference
+    (convolutions + Linears) plus, for EfficientZero, the reward LSTM's gate GEMM, which the counter
+    does not see (aten lstm kernels); the matrix-pipe part is the convolutions and the gate GEMM."""
     from torch.utils.flop_counter import FlopCounterMode
     lat = torch.zeros(B, 64, 8, 8, device=dev)
     act = torch.zeros(B, dtype=torch.int64, device=dev)
@@ -39,7 +51,17 @@ def recurrent_flops(model, kind, B, dev):
             model.recurrent_inference(lat, (z, z), act)
         else:
             model.recurrent_inference(lat, act)
-    return fc.get_total_flops() / B
+    per_op = {str(k): v for k, v in fc.get_flop_counts().get("Global", {}).items()}
+    total = fc.get_total_flops() / B
+    matrix = sum(v for k, v in per_op.items() if "convolution" in k) / B
+    if kind == "ez":
+        lstm = model.dynamics_network.lstm
+        H, K = lstm.hidden_size, lstm.input_size
+        gate = 2.0 * 4 * H * (K + H)
+        counted = sum(v for k, v in per_op.items() if "lstm" in k) / B
+        total += gate - counted
+        matrix += gate
+    return total, matrix
 
 
 def main():
@@ -56,6 +78,8 @@ def main():
                     help="the one-launch search (lzm_search_conv / lzm_search_conv_ez) when it applies; 0: the generic path")
     ap.add_argument("--rng", choices=["glibc", "philox"], default="glibc",
                     help="tie-break stream: the reference's glibc rand() (parity) or per-root Philox")
+    ap.add_argument("--cpu-baseline-secs", type=float, default=0.0,
+                    help="> 0: also time the config's CPU baseline (bench.cpu_baseline_conv) for about this long")
     a = ap.parse_args()
     if a.precision:
         os.environ["LZM_CONV_PRECISION"] = a.precision
@@ -104,8 +128,15 @@ def main():
     roots.tree.check_errors()
     fused = (mcts._fused_conv(model, roots.tree, (64, 8, 8)) if a.kind == "mz" else
              mcts._fused_conv(model, roots.tree, (64, 8, 8), model.lstm_hidden_size)) is not None
-    flops = recurrent_flops(model, a.kind, B, dev)
+    flops, matrix = recurrent_flops(model, a.kind, B, dev)
     net_tflops = flops * B * S / dt / 1e12
+    split = precision == "bf16x3"
+    mfma = (6.0 if split else 1.0) * matrix * B * S / dt / 1e12
+    peak = BF16_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS
+    cpu = None
+    if a.cpu_baseline_secs > 0:
+        import bench
+        cpu = bench.cpu_baseline_conv(a.kind, B, S, model, a.cpu_baseline_secs, dev)
     print(json.dumps({
         "metric": "MCTS simulations/sec", "value": B * S / dt, "unit": "sims/s", "ms_per_search": dt * 1e3,
         "config": {"workload": "C3 Pong EfficientZero" if a.kind == "ez" else "C5 Breakout MuZero (per GPU)",
@@ -113,8 +144,12 @@ def main():
                    "path": ("one-launch search (lzm_search_conv%s)" % ("_ez" if a.kind == "ez" else "")) if fused else
                    "generic (HIP tree kernels + PyTorch-ROCm network)", "hip_graph": bool(a.graph) and not fused,
                    "conv_precision": precision, "rng": a.rng},
-        "net_flops_per_sim": flops, "net_tflops_whole_search": net_tflops,
-        "fp32_mfma_peak_tflops": FP32_MFMA_PEAK_TFLOPS, "net_frac_of_peak": net_tflops / FP32_MFMA_PEAK_TFLOPS}))
+        "net_flops_per_sim": flops, "matrix_flops_per_sim": matrix, "net_tflops_whole_search": net_tflops,
+        "roofline": {"bound": "mfma", "pipe": "bf16 MFMA, 6 products per f32 product (split-bf16)" if split else
+                     "f32 MFMA (exact f32)", "achieved": round(mfma, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(mfma / peak, 4), "f32_equivalent_tflops": round(net_tflops, 2),
+                     "f32_equivalent_frac_of_fp32_peak": round(net_tflops / FP32_MFMA_PEAK_TFLOPS, 4)},
+        "cpu_baseline": cpu, "vs_cpu_baseline": (B * S / dt) / cpu["value"] if cpu else None}))
 
 
 if __name__ == "__main__":
