@@ -768,14 +768,17 @@ def secondary_breakout(args, world, rank, device):
     one HIP graph), and the timed region ends with the trajectory return (device pack + RCCL
     all-gather of the u8 frames and scalars + statistics sum). Returns the 'config5' object."""
     B, S = args.envs, args.sims
+    # enough env steps that episodes (tens of steps) finish inside the timed region and the trajectory
+    # return moves real image payloads
+    steps = max(args.steps, 100)
     model = build_conv_model(device, seed=0)
     step = CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload="breakout")
-    el, traj = timed_run(step, args.steps, args.warmup, world, device)
+    el, traj = timed_run(step, steps, args.warmup, world, device)
     tie_errors, sdiag = check_step(step, S, True)
-    out = {"workload": workload_name("breakout", B, S, world), "step": "collect",
-           "value": round(whole_job_rate(B, S, args.steps, world, el), 1), "unit": "sims/s",
-           "ms_per_step": round(el / args.steps * 1e3, 4), "n_gpus": world, "global_envs": world * B,
-           "env_steps_per_s": round(world * B * args.steps / el, 1), "scaling": "weak",
+    out = {"workload": workload_name("breakout", B, S, world), "step": "collect", "steps": steps,
+           "value": round(whole_job_rate(B, S, steps, world, el), 1), "unit": "sims/s",
+           "ms_per_step": round(el / steps * 1e3, 4), "n_gpus": world, "global_envs": world * B,
+           "env_steps_per_s": round(world * B * steps / el, 1), "scaling": "weak",
            "trajectory": traj, "tie_stream_errors": tie_errors, "search_diag": sdiag,
            "data": "synthetic (random-init conv MuZeroModel; Breakout stand-in env, ALE absent)"}
     if rank == 0:

@@ -12,7 +12,8 @@
 // record the u8 frame into the episode slot and shift the model's [4][64][64] float observation stack.
 //
 // The Arcade Learning Environment is not installed (no ROM, no ale_py), so the game is a STAND-IN
-// with Breakout's interface: the minimal action set {NOOP, FIRE, RIGHT, LEFT}, grey 64x64 frames as
+// with Breakout's interface: the minimal action set {NOOP, FIRE, RIGHT, LEFT} (FIRE serves the ball; it is
+// also served after 8 idle steps, so episodes end under any policy), grey 64x64 frames as
 // the reference's wrappers produce (WarpFrame 64x64, grey, scaled to [0, 1]), 6 rows of bricks worth
 // 1 / 4 / 7 points by row pair as ALE scores them (clipped to their sign, as the collector env's
 // ClipRewardWrapper does), one life per episode (EpisodicLifeEnv, the collector setting), truncation
@@ -36,9 +37,10 @@ constexpr int kAtPaddleY = 58, kAtPaddleW = 8, kAtPaddleSpeed = 3;
 constexpr int kAtWall = 2;                  // wall thickness (top, left, right)
 constexpr int kAtSub = 2;                   // ball sub-steps per env step
 constexpr int kAtStateWords = 16;
+constexpr int kAtAutoServe = 8;             // idle steps before the ball is served without FIRE
 
 // state words per env
-enum { AT_PADDLE = 0, AT_BX, AT_BY, AT_VX, AT_VY, AT_IN_PLAY, AT_BRICK0, AT_BRICK1, AT_BRICK2, AT_LIVES };
+enum { AT_PADDLE = 0, AT_BX, AT_BY, AT_VX, AT_VY, AT_IN_PLAY, AT_BRICK0, AT_BRICK1, AT_BRICK2, AT_LIVES, AT_IDLE };
 
 struct AtariArgs {
   int n, A, T, E, max_steps, deterministic;
@@ -87,7 +89,11 @@ __device__ inline float at_step(int32_t *s, int action, PhiloxStream &rs, bool *
   px = px < kAtWall ? kAtWall : (px > kAtHW - kAtWall - kAtPaddleW ? kAtHW - kAtWall - kAtPaddleW : px);
   s[AT_PADDLE] = px;
   if (!s[AT_IN_PLAY]) {
-    if (action != 1) return 0.0f;
+    // served by FIRE, or after kAtAutoServe idle steps (a stand-in convenience: episodes end under any
+    // policy, e.g. an untrained network that never picks FIRE)
+    s[AT_IDLE] += 1;
+    if (action != 1 && s[AT_IDLE] < kAtAutoServe) return 0.0f;
+    s[AT_IDLE] = 0;
     const uint4 r = rs.next();
     s[AT_IN_PLAY] = 1;
     s[AT_BX] = px + kAtPaddleW / 2 - 1;

@@ -16,11 +16,12 @@ BRICK_ROWS, BRICK_COLS, BRICK_Y0, BRICK_H, BRICK_W = 6, 15, 8, 2, 4
 PADDLE_Y, PADDLE_W, PADDLE_SPEED = 58, 8, 3
 WALL = 2
 SUB = 2
+AUTO_SERVE = 8
 FULL_BRICKS = (1 << (BRICK_ROWS * BRICK_COLS)) - 1
 
 
 def new_state(paddle):
-    return dict(paddle=int(paddle), bx=0, by=0, vx=0, vy=0, in_play=0, bricks=FULL_BRICKS, lives=1)
+    return dict(paddle=int(paddle), bx=0, by=0, vx=0, vy=0, in_play=0, bricks=FULL_BRICKS, lives=1, idle=0)
 
 
 def render(s):
@@ -47,8 +48,10 @@ def step(s, action, serve_dir):
     px = min(max(px, WALL), HW - WALL - PADDLE_W)
     s["paddle"] = px
     if not s["in_play"]:
-        if action != 1:
+        s["idle"] += 1
+        if action != 1 and s["idle"] < AUTO_SERVE:
             return s, 0.0, False
+        s["idle"] = 0
         s.update(in_play=1, bx=px + PADDLE_W // 2 - 1, by=PADDLE_Y - 8, vx=serve_dir, vy=-1)
         return s, 0.0, False
     pts, term = 0.0, False
@@ -110,7 +113,8 @@ def replay_episode(frames, actions, rewards, max_steps):
     for t in range(L):
         nxt = []
         for s in cands:
-            dirs = (1, -1) if (not s["in_play"] and int(actions[t]) == 1) else (1,)
+            serve = not s["in_play"] and (int(actions[t]) == 1 or s["idle"] + 1 >= AUTO_SERVE)
+            dirs = (1, -1) if serve else (1,)
             for d in dirs:
                 s1, pts, term = step(s, int(actions[t]), d)
                 r = 1.0 if pts > 0 else 0.0
