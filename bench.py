@@ -403,14 +403,19 @@ def _lib_kernel_floats(H=128, A=2, F=32, V=601, res=1):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch from the committed PMC pass (profiles/pmc_latest.json, written by
-    tools/profile_round.sh on the GPU box): 2 x FETCH_SIZE + WRITE_SIZE, or None."""
+    """HBM bytes per launch from the committed PMC passes (profiles/pmc_latest.json, built by
+    tools/pmc_latest.py from tools/profile_round.sh on the GPU box): 2 x FETCH_SIZE + WRITE_SIZE of
+    that kernel, or None."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    return d.get("traffic_bytes") if kernel.split("<")[0] in d.get("kernel", "") else None
+    base = kernel.split("<")[0]
+    for e in (d.get("kernels") or {}).values():
+        if base in e.get("kernel", "") and e.get("traffic_bytes"):
+            return e["traffic_bytes"]
+    return d.get("traffic_bytes") if base in d.get("kernel", "") else None
 
 
 def algorithmic_bytes(B, A, H, V, dbar):

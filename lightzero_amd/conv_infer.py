@@ -17,9 +17,11 @@ into the convolution or Linear in front of it (in float64, rounded once to float
     the two 1024->32 hidden Linears (+BN) as one block-diagonal 2048->64 Linear, ReLU; the two
     output Linears.
 
-Same outputs as the module within float32 rounding (tests/test_gpu_conv.py); `initial_inference`
-(once per search) is the module's own. Parameters are re-folded in place when the module's
-tensors change (version counters), so captured HIP graphs keep valid pointers.
+Same outputs as the module within float32 rounding (tests/test_gpu_conv.py). `initial_inference`
+(once per env step) is folded the same way by `FoldedConvInitial`: every BatchNorm of the
+representation network folded into its convolution, each convolution + bias (+ residual) + ReLU one
+MIOpen fused launch. Parameters are re-folded in place when the module's tensors change (version
+counters), so captured HIP graphs keep valid pointers.
 
 On the GPU the convolutional trunk (dynamics conv, residual blocks, reward 1x1, prediction blocks,
 head 1x1) is ONE hand-written HIP launch per simulation, one workgroup per env with the
@@ -29,7 +31,9 @@ exact-f32 MFMA kernel stays selectable, precision='f32'): it reads the leaf
 latent straight from the search's latent pool and writes the next latent straight into the next
 pool slot (`step_from_pool`), so the gather and the pool filing kernels disappear too. The head
 MLPs (reward, value, policy; both layers, ReLUs, the EZ value-prefix BatchNorm) are ONE more
-launch (csrc/lzm_heads.h, lzm_conv_heads); the EfficientZero LSTM cell stays a batched GEMM.
+launch (csrc/lzm_heads.h, lzm_conv_heads); the EfficientZero reward LSTM (gate GEMM + cell) one
+split-bf16 launch (csrc/lzm_lstm.h, lzm_ez_lstm_step). The one-launch searches (lzm_search_conv,
+lzm_search_conv_ez) run all of it inside the search kernel.
 """
 import os
 import weakref
@@ -480,25 +484,65 @@ class FoldedConvInitial:
                     self.t[k].copy_(v)
         self._ver = ver
 
+    # MIOpen's fused convolution + bias (+ residual) + ReLU (torch.miopen_convolution_relu /
+    # _add_relu): one launch per convolution instead of a convolution, a bias add / residual add and
+    # a ReLU pass. Checked once per process; the unfused form is kept for CPU tensors and as the
+    # fallback when the fused ops are unavailable.
+    _fused_ok = None
+
+    def _fused(self, x):
+        if not x.is_cuda or not hasattr(torch, "miopen_convolution_relu") or FoldedConvInitial._fused_ok is False:
+            return False
+        if FoldedConvInitial._fused_ok is None:
+            try:
+                w = torch.randn(4, 4, 3, 3, device=x.device)
+                b = torch.randn(4, device=x.device)
+                z = torch.randn(1, 4, 5, 5, device=x.device)
+                xi = torch.randn(1, 4, 5, 5, device=x.device)
+                got = torch.miopen_convolution_add_relu(xi, w, z, 1.0, b, [1, 1], [1, 1], [1, 1], 1)
+                got2 = torch.miopen_convolution_relu(xi, w, b, [1, 1], [1, 1], [1, 1], 1)
+                ref = F.conv2d(xi, w, b, padding=1)
+                FoldedConvInitial._fused_ok = bool(torch.allclose(got, (ref + z).relu(), rtol=1e-4, atol=1e-5) and
+                                                   torch.allclose(got2, ref.relu(), rtol=1e-4, atol=1e-5))
+            except (RuntimeError, TypeError, NotImplementedError):
+                FoldedConvInitial._fused_ok = False
+        return FoldedConvInitial._fused_ok
+
     @staticmethod
-    def _basic(x, w1, b1, w2, b2):
-        y = F.conv2d(x, w1, b1, padding=1).relu_()
-        return F.conv2d(y, w2, b2, padding=1).add_(x).relu_()
+    def _conv_relu(x, w, b, stride, fused):
+        if fused:
+            return torch.miopen_convolution_relu(x, w, b, [stride, stride], [1, 1], [1, 1], 1)
+        return F.conv2d(x, w, b, stride=stride, padding=1).relu_()
+
+    @staticmethod
+    def _conv_add_relu(x, w, z, b, fused):
+        """relu(conv3x3(x, w) + b + z)"""
+        if fused:
+            return torch.miopen_convolution_add_relu(x, w, z, 1.0, b, [1, 1], [1, 1], [1, 1], 1)
+        return F.conv2d(x, w, b, padding=1).add_(z).relu_()
+
+    @classmethod
+    def _basic(cls, x, w1, b1, w2, b2, fused=False):
+        y = cls._conv_relu(x, w1, b1, 1, fused)
+        return cls._conv_add_relu(y, w2, x, b2, fused)
 
     def initial_inference(self, obs):
         self.refresh()
         t = self.t
         x = obs.float()
+        if not x.is_contiguous():
+            x = x.contiguous()
+        fused = self._fused(x)
         for op in self.ops:
             kind = op[0]
             if kind == "conv_relu":
-                x = F.conv2d(x, op[1], op[2], stride=op[3], padding=1).relu_()
+                x = self._conv_relu(x, op[1], op[2], op[3], fused)
             elif kind == "basic":
-                x = self._basic(x, *op[1:])
+                x = self._basic(x, *op[1:], fused=fused)
             elif kind == "down":
                 _, w1, b1, w2, b2, w3 = op
-                y = F.conv2d(x, w1, b1, stride=2, padding=1).relu_()
-                x = F.conv2d(y, w2, b2, padding=1).add_(F.conv2d(x, w3, None, stride=2, padding=1)).relu_()
+                y = self._conv_relu(x, w1, b1, 2, fused)
+                x = self._conv_add_relu(y, w2, F.conv2d(x, w3, None, stride=2, padding=1), b2, fused)
             else:  # avgpool (count_include_pad, as nn.AvgPool2d(3, 2, 1))
                 x = F.avg_pool2d(x, kernel_size=3, stride=2, padding=1)
         latent = x
@@ -506,7 +550,7 @@ class FoldedConvInitial:
         p = latent
         i = 0
         while f"pres{i}_w1" in t:
-            p = self._basic(p, t[f"pres{i}_w1"], t[f"pres{i}_b1"], t[f"pres{i}_w2"], t[f"pres{i}_b2"])
+            p = self._basic(p, t[f"pres{i}_w1"], t[f"pres{i}_b1"], t[f"pres{i}_w2"], t[f"pres{i}_b2"], fused=fused)
             i += 1
         h = F.conv2d(p, t["head_w"], t["head_b"]).relu_().reshape(B, -1)
         hid = F.linear(h, t["ph_w1"], t["ph_b1"]).relu_()

@@ -45,10 +45,21 @@ static_assert(kRTail > 0 && 2 * kRTail <= kRT, "support tail: two lanes per colu
 // float4 slots (each kRT lanes wide) per resident block
 constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlotsPO = 1;
 
+// D-block lane map (every 128 x 128 layer). LZM_RES_D4 = 1 (default): lane l owns the four columns
+// 4 (l >> 3) .. +3 over the K eighth 16 (l & 7) .. +15, so it reads 4 activation float4 per row (all in
+// flight at once) and uses each for 4 columns; the 8 lanes of a column group meet by a 3-step DPP
+// butterfly that leaves column 4 (l >> 3) + ((l & 7) >> 1) in lane pair (l, l ^ 1) (reduce_d4). 0: lane
+// l owns column l >> 1 over K half l & 1 (16 activation float4 per row, read through a shallow
+// software pipeline for lack of registers). Same weights per lane either way.
+#ifndef LZM_RES_D4
+#define LZM_RES_D4 1
+#endif
+
 // Resident weight layout (lzm_mlp_prepare writes it after the generic kernel layout; res_source
 // below is its definition). Every block is [slot][lane] float4, so a wave-instruction of a block
 // is one contiguous 1 KiB read.
-//   D (128 x 128, six of them): slot j, lane l: W[64 (l & 1) + 4 j .. +3][l >> 1]
+//   D (128 x 128, six of them): slot j, lane l: W[16 (l & 7) + 4 (j >> 2) .. +3][4 (l >> 3) + (j & 3)]
+//      (LZM_RES_D4; else W[64 (l & 1) + 4 j .. +3][l >> 1])
 //   RH (128 -> 32 reward head hidden): slot j < 4: W[16 (l & 7) + 4 j ..][l >> 3]
 //   VPH (128 -> 64: [value hidden | policy hidden]): slot j < 8: W[32 (l & 3) + 4 j ..][l >> 2]
 //   S (32 -> 601 support head): slots 0-7: column l, k = 4 j; slots 8-15: column 256 + l;
@@ -116,7 +127,12 @@ __host__ __device__ inline void res_source(int b, size_t d, int A, int *layer, i
   const int j = f4 / kRT, l = f4 % kRT;
   if (b < kRbRH) {
     const int src[6] = {0, 1, 2, 3, 6, 7};
-    *layer = src[b]; *col = l >> 1; *k = 64 * (l & 1) + 4 * j + e;
+    *layer = src[b];
+#if LZM_RES_D4
+    *col = 4 * (l >> 3) + (j & 3); *k = 16 * (l & 7) + 4 * (j >> 2) + e;
+#else
+    *col = l >> 1; *k = 64 * (l & 1) + 4 * j + e;
+#endif
     return;
   }
   switch (b) {
@@ -195,11 +211,56 @@ constexpr int kRRow = kRHid + 4;
 constexpr int kRHalf4 = kRHid / 8 + 1;  // float4 offset of the upper half
 __device__ __forceinline__ int rpad(int c) { return c + ((c >> 6) << 2); }
 
-// Full pre-activation of this lane's column of a 128 x 128 layer (both lanes of a pair get it).
+// The column of a 128 x 128 layer this lane's result holds (both lanes of the pair (l, l ^ 1) hold
+// it; the even lane writes it).
+__device__ __forceinline__ int d_col() {
+#if LZM_RES_D4
+  return 4 * ((int)threadIdx.x >> 3) + (((int)threadIdx.x & 7) >> 1);
+#else
+  return (int)threadIdx.x >> 1;
+#endif
+}
+
+// LZM_RES_D4: the four column partials h0..h3 of the 8 lanes of a column group to full sums —
+// lanes e and 7 - e (row_half_mirror) split the columns {0, 1} / {2, 3}, lanes e and e ^ 2 split the
+// pair, lanes e and e ^ 1 add: column (e >> 1) ends in lanes e, e ^ 1 (the same bits in both: the last
+// add is commutative). A fixed order, so every launch rounds the same way.
+__device__ __forceinline__ float reduce_d4(float h0, float h1, float h2, float h3) {
+  const int e = threadIdx.x & 7;
+  const bool lo = e < 4;
+  float k0 = lo ? h0 : h2, k1 = lo ? h1 : h3;
+  const float s0 = lo ? h2 : h0, s1 = lo ? h3 : h1;
+  k0 += dpp_f<0x141>(s0);
+  k1 += dpp_f<0x141>(s1);
+  const bool q = (e & 2) == 0;
+  float m = q ? k0 : k1;
+  const float snd = q ? k1 : k0;
+  m += dpp_f<0x4E>(snd);
+  return m + dpp_f<0xB1>(m);
+}
+
+// Full pre-activation of this lane's column (d_col) of a 128 x 128 layer.
 template <typename WF>
 __device__ __forceinline__ float dense128(const float *x, WF w) {
+#if LZM_RES_D4
+  const int e = threadIdx.x & 7;
+  const float4 *x4 = reinterpret_cast<const float4 *>(x) + 4 * e + (e >> 2);
+  float4 xv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) xv[j] = x4[j];
+  float a[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) a[c][0] = a[c][1] = a[c][2] = a[c][3] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) fma4(xv[j], w(4 * j + c), a[c]);
+  return reduce_d4((a[0][0] + a[0][1]) + (a[0][2] + a[0][3]), (a[1][0] + a[1][1]) + (a[1][2] + a[1][3]),
+                   (a[2][0] + a[2][1]) + (a[2][2] + a[2][3]), (a[3][0] + a[3][1]) + (a[3][2] + a[3][3]));
+#else
   const float h = dot4<16>(reinterpret_cast<const float4 *>(x) + kRHalf4 * (threadIdx.x & 1), w);
   return h + dpp_f<0xB1>(h);
+#endif
 }
 
 // Logits of one support head (input: 32 floats in LDS; weights: the 20-slot buffer P): lane l
@@ -919,6 +980,34 @@ struct NoSide {
 // 1 KiB wave-load per 16 cycles and four waves share it)
 template <int NR, typename WF, typename SF = NoSide>
 __device__ __forceinline__ void dense128n(const float *x, WF w, float *z, SF side = SF()) {
+#if LZM_RES_D4
+  const int e = threadIdx.x & 7;
+  float4 xv[NR][4];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) xv[r][j] = reinterpret_cast<const float4 *>(x + r * kRRow)[4 * e + (e >> 2) + j];
+  float a[NR][4][4];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a[r][c][0] = a[r][c][1] = a[r][c][2] = a[r][c][3] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      side(4 * j + c);
+      const float4 q = w(4 * j + c);
+#pragma unroll
+      for (int r = 0; r < NR; ++r) fma4(xv[r][j], q, a[r][c]);
+    }
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    z[r] = reduce_d4((a[r][0][0] + a[r][0][1]) + (a[r][0][2] + a[r][0][3]),
+                     (a[r][1][0] + a[r][1][1]) + (a[r][1][2] + a[r][1][3]),
+                     (a[r][2][0] + a[r][2][1]) + (a[r][2][2] + a[r][2][3]),
+                     (a[r][3][0] + a[r][3][1]) + (a[r][3][2] + a[r][3][3]));
+#else
   const int p = threadIdx.x & 1;
   float a[NR][4];
 #pragma unroll
@@ -935,6 +1024,7 @@ __device__ __forceinline__ void dense128n(const float *x, WF w, float *z, SF sid
     const float h = (a[r][0] + a[r][1]) + (a[r][2] + a[r][3]);
     z[r] = h + dpp_f<0xB1>(h);
   }
+#endif
 }
 
 // NH supports decoded together (z[h] = this lane's logits of support h, see support_logits):
@@ -1217,7 +1307,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   res_fetch<kRSlotsRH>(res_blk4(n, kRbRH), wRH);
   res_fetch<kRSlotsVPH>(res_blk4(n, kRbVPH), wVPH);
   res_fetch<kRSlotsPO>(res_blk4(n, kRbPO), wPO);
-  const int cD = tid >> 1, pD = tid & 1, cRH = tid >> 3, pRH = tid & 7, cVP = tid >> 2, pVP = tid & 3, cPO = tid >> 3;
+  const int cD = d_col(), pD = tid & 1, cRH = tid >> 3, pRH = tid & 7, cVP = tid >> 2, pVP = tid & 3, cPO = tid >> 3;
   LZM_ISTAMP(27);
   // biases live in LDS (registers are the scarce resource): the bias blocks are contiguous
   float *BB = reinterpret_cast<float *>(s_bias);

@@ -1,8 +1,9 @@
 """Build profiles/pmc_latest.json from a profile_round.sh output directory: per-dispatch means of
-FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum / TCC_MISS_sum for the bench's dominant kernel, with the
-gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md (x2: 128-B streaming reads tallied at 64 B).
+FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum / TCC_MISS_sum for each named kernel (the bench's dominant
+kernels: search_res_kernel for config 2, search_conv_kernel for config 5), with the gfx950 FETCH_SIZE
+correction of MI355X_MICROARCH.md (x2: 128-B streaming reads tallied at 64 B).
 
-    python tools/pmc_latest.py gpurun_out/prof_<tag> <kernel substring> > profiles/pmc_latest.json
+    python tools/pmc_latest.py gpurun_out/<dir> search_res_kernel search_conv_kernel > profiles/pmc_latest.json
 """
 import csv
 import glob
@@ -12,8 +13,7 @@ import sys
 from collections import defaultdict
 
 
-def main():
-    root, pat = sys.argv[1], sys.argv[2]
+def summarise(root, pat):
     acc, disp, kname = defaultdict(float), defaultdict(set), ""
     for path in sorted(glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(path)):
@@ -28,7 +28,7 @@ def main():
     fetch = 2 * per.get("FETCH_SIZE", 0.0) * 1024
     write = per.get("WRITE_SIZE", 0.0) * 1024
     req = (per.get("TCC_HIT_sum", 0.0) + per.get("TCC_MISS_sum", 0.0))
-    out = {
+    return {
         "kernel": kname,
         "command": "python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline (one rocprofv3 --kernel-trace --pmc pass per group)",
         "per_dispatch": per,
@@ -41,7 +41,11 @@ def main():
                  "streaming-read requests at 64 B) - an upper bound here, the kernel's HBM reads mix 16-B and 4-B "
                  "lanes. TCC_HIT+MISS x 128 B = bytes requested from L2.",
     }
-    print(json.dumps(out, indent=1))
+
+
+def main():
+    root = sys.argv[1]
+    print(json.dumps({"kernels": {pat: summarise(root, pat) for pat in sys.argv[2:]}}, indent=1))
 
 
 if __name__ == "__main__":

@@ -1,9 +1,9 @@
-# GPU: the round's profile set for the fused bench (usage: bash tools/profile_round.sh r01)
-#   kernel trace + stats of the default bench command, the bench line, and PMC passes
-#   (each counter group in its own pass, kernel-trace only: FETCH_SIZE, WRITE_SIZE, TCC hit/miss)
+# GPU: the round's profile set of the default bench command (usage: bash tools/profile_round.sh OUT_DIR)
+#   kernel trace + stats of `bench.py` (the headline config-2 search and config 5's Breakout collect
+#   step), PMC passes (each counter group in its own pass, kernel-trace only: FETCH_SIZE, WRITE_SIZE,
+#   TCC hit/miss), and the full bench line with the CPU baseline.
 set -e
-tag=${1:-r01}
-out=gpurun_out/prof_$tag
+out=${1:-gpurun_out/prof}
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o fused --output-format csv -- \
