@@ -54,6 +54,24 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #ifndef LZM_RES_D4
 #define LZM_RES_D4 1
 #endif
+// LZM_RES_EARLY (experiment, default 0): two barriers fewer per simulation — the walking wave
+// computes the pUCT terms alone (<= 64 expanded nodes) and gathers the leaf's parent latent right
+// after its walk. Measured slower (24.2 vs 24.6 M sims/s): waves 1-3 then issue their fc_dynamics[0]
+// prefetch during wave 0's terms pass instead of during its walk.
+#ifndef LZM_RES_EARLY
+#define LZM_RES_EARLY 0
+#endif
+// LZM_RES_W0SPLIT (default 1): wave 0's fc_dynamics[0] prefetch in four quarters spread over the
+// expand, the backup and the next terms pass instead of one 16-load burst on the critical path (a
+// burst stalls the issuing wave while the vector-memory queue drains).
+#ifndef LZM_RES_W0SPLIT
+#define LZM_RES_W0SPLIT 1
+#endif
+// LZM_RES_H2 (default 1): the [value | policy] head hidden layer (128 -> 64) with two columns per lane
+// over a K eighth (4 activation float4 per lane instead of 8), columns 2 (l >> 3) + {0, 1}.
+#ifndef LZM_RES_H2
+#define LZM_RES_H2 1
+#endif
 
 // Resident weight layout (lzm_mlp_prepare writes it after the generic kernel layout; res_source
 // below is its definition). Every block is [slot][lane] float4, so a wave-instruction of a block
@@ -138,8 +156,13 @@ __host__ __device__ inline void res_source(int b, size_t d, int A, int *layer, i
   switch (b) {
     case kRbRH: *layer = 4; *col = l >> 3; *k = 16 * (l & 7) + 4 * j + e; return;
     case kRbVPH: {
+#if LZM_RES_H2
+      const int c = 2 * (l >> 3) + (j & 1);
+      *layer = c < kRF ? 8 : 10; *col = c < kRF ? c : c - kRF; *k = 16 * (l & 7) + 4 * (j >> 1) + e;
+#else
       const int c = l >> 2;
       *layer = c < kRF ? 8 : 10; *col = c < kRF ? c : c - kRF; *k = 32 * (l & 3) + 4 * j + e;
+#endif
       return;
     }
     case kRbRS: case kRbVS: {
@@ -1308,6 +1331,8 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   res_fetch<kRSlotsVPH>(res_blk4(n, kRbVPH), wVPH);
   res_fetch<kRSlotsPO>(res_blk4(n, kRbPO), wPO);
   const int cD = d_col(), pD = tid & 1, cRH = tid >> 3, pRH = tid & 7, cVP = tid >> 2, pVP = tid & 3, cPO = tid >> 3;
+  (void)cVP;
+  (void)pVP;
   LZM_ISTAMP(27);
   // biases live in LDS (registers are the scarce resource): the bias blocks are contiguous
   float *BB = reinterpret_cast<float *>(s_bias);
@@ -1346,13 +1371,24 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // 0: descend_wave; 1: terms + wave walk; 2: terms + lane walk; 3: descend_slice; 4 (default):
     // terms + descend_small when A <= 2, else as 1
     const int smode = (n.select_mode == 4 && A != 2) ? 1 : n.select_mode;
+    // LZM_RES_EARLY: with at most 64 expanded nodes every term is computed by wave 0, the wave that
+    // walks, so the walk needs no workgroup barrier after the terms (a wave-level fence orders the
+    // LDS writes of its lanes before their reads)
+    const bool w0terms = LZM_RES_EARLY && s_nlat + k <= 64;
     if (smode == 1 || smode == 2 || smode == 4) {
-      __syncthreads();  // the previous simulation's backup (wave 0) is complete
+      __syncthreads();  // the previous simulation's backup (wave 0) and children (wave 1) are complete
+      if (LZM_RES_W0SPLIT && wid == 0 && k > 0) res_fetch<kRSlotsD, 12, 16>(res_blk4(n, kRbD), P);
       if (smode == 4)
         precompute_terms_a2(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, DEC, rleg, nleg);
       else
         precompute_terms(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, smode == 4 ? DEC : nullptr);
-      __syncthreads();
+      if (w0terms) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      } else {
+        __syncthreads();
+      }
     }
     LZM_STAMP(12);
     if (wid != 0 && k > 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // (see the expand)
@@ -1404,6 +1440,18 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+#if LZM_RES_EARLY
+      // gather the leaf's parent latent now, by the walking wave, when the walk's x is final (every
+      // status but 2): the walk's barrier then also orders the gather (one barrier fewer)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's s_status / s_x to the wave
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int stw = __builtin_amdgcn_readfirstlane(s_status);
+      const int x0 = __builtin_amdgcn_readfirstlane(s_x);
+      if (stw != 2 && lane < kRHid / 4)
+        reinterpret_cast<float4 *>(X0)[lane + (lane >= kRHid / 8)] =
+            reinterpret_cast<const float4 *>(p.pool + ((size_t)max(x0, 0) * B + i) * kRHid)[lane];
+#endif
     }
     __syncthreads();
     LZM_STAMP(0);
@@ -1473,11 +1521,14 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       __syncthreads();
     }
     LZM_STAMP(1);
-    // ---- gather the leaf's parent latent: X0 = pool[x][i]
-    if (tid < kRHid / 4)
-      reinterpret_cast<float4 *>(X0)[tid + (tid >= kRHid / 8)] =
-          reinterpret_cast<const float4 *>(p.pool + ((size_t)max(s_x, 0) * B + i) * kRHid)[tid];
-    __syncthreads();
+    // ---- gather the leaf's parent latent: X0 = pool[x][i] (LZM_RES_EARLY: already done by the walk
+    // unless the depth waited for a draw)
+    if (!LZM_RES_EARLY || status == 2) {
+      if (tid < kRHid / 4)
+        reinterpret_cast<float4 *>(X0)[tid + (tid >= kRHid / 8)] =
+            reinterpret_cast<const float4 *>(p.pool + ((size_t)max(s_x, 0) * B + i) * kRHid)[tid];
+      __syncthreads();
+    }
     LZM_STAMP(2);
     unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
     // ---- fc_dynamics[0], latent rows (streamed weights in P): shared by the speculative rows
@@ -1622,6 +1673,33 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int r = 0; r < NR; ++r) {
       float h = dot4<kRSlotsRH>(reinterpret_cast<const float4 *>(T3 + r * kRRow) + 4 * pRH + (pRH >= 4),
                                 [&](int j) { return wRH[j]; });
+#if LZM_RES_H2
+      float u;
+      int cu;
+      {
+        const int e = tid & 7;
+        const float4 *u4 = reinterpret_cast<const float4 *>(U3 + r * kRRow) + 4 * e + (e >> 2);
+        float a0[4] = {0.0f, 0.0f, 0.0f, 0.0f}, a1[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const float4 xv = u4[jj];
+          fma4(xv, wVPH[2 * jj], a0);
+          fma4(xv, wVPH[2 * jj + 1], a1);
+        }
+        const float v0 = (a0[0] + a0[1]) + (a0[2] + a0[3]), v1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+        const bool lo = e < 4;
+        u = lo ? v0 : v1;
+        u += dpp_f<0x141>(lo ? v1 : v0);  // lanes e, 7 - e: the lower half keeps column 0, the upper 1
+        cu = 2 * (tid >> 3) + (lo ? 0 : 1);
+      }
+      h += dpp_f<0xB1>(h);
+      u += dpp_f<0xB1>(u);
+      h += dpp_f<0x4E>(h);
+      u += dpp_f<0x4E>(u);
+      h += dpp_f<0x141>(h);
+      if (pRH == 0) RHo[r * kRF + cRH] = fmaxf(h + BRH[cRH], 0.0f);
+      if ((tid & 3) == 0) HV[r * 2 * kRF + cu] = fmaxf(u + BVP[cu], 0.0f);
+#else
       float u = dot4<kRSlotsVPH>(reinterpret_cast<const float4 *>(U3 + r * kRRow) + 8 * pVP + (pVP >= 2),
                                  [&](int j) { return wVPH[j]; });
       h += dpp_f<0xB1>(h);
@@ -1631,6 +1709,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       h += dpp_f<0x141>(h);
       if (pRH == 0) RHo[r * kRF + cRH] = fmaxf(h + BRH[cRH], 0.0f);
       if (pVP == 0) HV[r * 2 * kRF + cVP] = fmaxf(u + BVP[cVP], 0.0f);
+#endif
     }
     __syncthreads();
     LZM_STAMP(5);
@@ -1691,7 +1770,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // fc_dynamics[0] for the next simulation: wave 0 now, alone on the texture path (16 loads
     // issue in a few hundred cycles), waves 1-3 during the next walk, which only wave 0 runs
     LZM_SUBSTAMP(29);
-    if (wid == 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
+    if (wid == 0) {
+      if (LZM_RES_W0SPLIT)
+        res_fetch<kRSlotsD, 0, 4>(res_blk4(n, kRbD), P);
+      else
+        res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
+    }
     LZM_SUBSTAMP(30);
     // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500): wave 0 files the leaf's own
     // record and backs up; wave 1 meanwhile initialises the leaf's children (disjoint nodes; the
@@ -1704,9 +1788,11 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
       LZM_SUBSTAMP(31);
       expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA, -1, s_exptab, 1);
+      if (LZM_RES_W0SPLIT) res_fetch<kRSlotsD, 4, 8>(res_blk4(n, kRbD), P);
       LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
+      if (LZM_RES_W0SPLIT) res_fetch<kRSlotsD, 8, 12>(res_blk4(n, kRbD), P);
     } else if (wid == 1) {
       expand_wave(t, 0, 0, 0, k + 1, 0.0f, LG + row * kRMaxA, -1, s_exptab, 2);
     }
