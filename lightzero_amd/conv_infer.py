@@ -493,6 +493,8 @@ class FoldedConvInitial:
     def _fused(self, x):
         if not x.is_cuda or not hasattr(torch, "miopen_convolution_relu") or FoldedConvInitial._fused_ok is False:
             return False
+        if os.environ.get("LZM_MIOPEN_FUSED", "1") == "0":  # (A/B: the unfused convolution + ReLU passes)
+            return False
         if FoldedConvInitial._fused_ok is None:
             try:
                 w = torch.randn(4, 4, 3, 3, device=x.device)
@@ -530,7 +532,10 @@ class FoldedConvInitial:
         self.refresh()
         t = self.t
         x = obs.float()
-        if not x.is_contiguous():
+        if os.environ.get("LZM_CONV_CL", "0") == "1" and x.is_cuda:
+            # (experiment) NHWC activations: MIOpen picks its NHWC kernels
+            x = x.contiguous(memory_format=torch.channels_last)
+        elif not x.is_contiguous():
             x = x.contiguous()
         fused = self._fused(x)
         for op in self.ops:
@@ -545,7 +550,7 @@ class FoldedConvInitial:
                 x = self._conv_add_relu(y, w2, F.conv2d(x, w3, None, stride=2, padding=1), b2, fused)
             else:  # avgpool (count_include_pad, as nn.AvgPool2d(3, 2, 1))
                 x = F.avg_pool2d(x, kernel_size=3, stride=2, padding=1)
-        latent = x
+        latent = x.contiguous()
         B = latent.shape[0]
         p = latent
         i = 0
