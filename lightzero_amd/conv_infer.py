@@ -19,8 +19,9 @@ into the convolution or Linear in front of it (in float64, rounded once to float
 
 Same outputs as the module within float32 rounding (tests/test_gpu_conv.py). `initial_inference`
 (once per env step) is folded the same way by `FoldedConvInitial`: every BatchNorm of the
-representation network folded into its convolution, each convolution + bias (+ residual) + ReLU one
-MIOpen fused launch. Parameters are re-folded in place when the module's tensors change (version
+representation network folded into its convolution (bias, residual add and ReLU as separate passes:
+MIOpen's fused convolution + ReLU launch is opt-in, LZM_MIOPEN_FUSED=1, measured 1% slower per
+Breakout step). Parameters are re-folded in place when the module's tensors change (version
 counters), so captured HIP graphs keep valid pointers.
 
 On the GPU the convolutional trunk (dynamics conv, residual blocks, reward 1x1, prediction blocks,
@@ -486,14 +487,14 @@ class FoldedConvInitial:
 
     # MIOpen's fused convolution + bias (+ residual) + ReLU (torch.miopen_convolution_relu /
     # _add_relu): one launch per convolution instead of a convolution, a bias add / residual add and
-    # a ReLU pass. Checked once per process; the unfused form is kept for CPU tensors and as the
-    # fallback when the fused ops are unavailable.
+    # a ReLU pass. Opt-in (LZM_MIOPEN_FUSED=1): measured per Breakout collect-time step 2.863 vs
+    # 2.826 ms unfused (profiles/r04/ab_breakout_miopen.txt). Checked once per process.
     _fused_ok = None
 
     def _fused(self, x):
         if not x.is_cuda or not hasattr(torch, "miopen_convolution_relu") or FoldedConvInitial._fused_ok is False:
             return False
-        if os.environ.get("LZM_MIOPEN_FUSED", "1") == "0":  # (A/B: the unfused convolution + ReLU passes)
+        if os.environ.get("LZM_MIOPEN_FUSED", "0") != "1":
             return False
         if FoldedConvInitial._fused_ok is None:
             try:
@@ -532,10 +533,7 @@ class FoldedConvInitial:
         self.refresh()
         t = self.t
         x = obs.float()
-        if os.environ.get("LZM_CONV_CL", "0") == "1" and x.is_cuda:
-            # (experiment) NHWC activations: MIOpen picks its NHWC kernels
-            x = x.contiguous(memory_format=torch.channels_last)
-        elif not x.is_contiguous():
+        if not x.is_contiguous():
             x = x.contiguous()
         fused = self._fused(x)
         for op in self.ops:
@@ -550,7 +548,7 @@ class FoldedConvInitial:
                 x = self._conv_add_relu(y, w2, F.conv2d(x, w3, None, stride=2, padding=1), b2, fused)
             else:  # avgpool (count_include_pad, as nn.AvgPool2d(3, 2, 1))
                 x = F.avg_pool2d(x, kernel_size=3, stride=2, padding=1)
-        latent = x.contiguous()
+        latent = x
         B = latent.shape[0]
         p = latent
         i = 0

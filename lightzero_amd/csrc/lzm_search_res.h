@@ -61,16 +61,25 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #ifndef LZM_RES_EARLY
 #define LZM_RES_EARLY 0
 #endif
-// LZM_RES_W0SPLIT (default 1): wave 0's fc_dynamics[0] prefetch in four quarters spread over the
-// expand, the backup and the next terms pass instead of one 16-load burst on the critical path (a
-// burst stalls the issuing wave while the vector-memory queue drains).
+// LZM_RES_W0SPLIT (experiment, default 0): wave 0's fc_dynamics[0] prefetch in four quarters spread
+// over the expand, the backup and the next terms pass instead of one 16-load burst after the decode.
+// Measured slower (24.26 vs 24.46 M sims/s, two interleaved runs each, profiles/r04/ab_res.txt).
 #ifndef LZM_RES_W0SPLIT
-#define LZM_RES_W0SPLIT 1
+#define LZM_RES_W0SPLIT 0
 #endif
-// LZM_RES_H2 (default 1): the [value | policy] head hidden layer (128 -> 64) with two columns per lane
-// over a K eighth (4 activation float4 per lane instead of 8), columns 2 (l >> 3) + {0, 1}.
+// LZM_RES_H2 (experiment, default 0): the [value | policy] head hidden layer (128 -> 64) with two
+// columns per lane over a K eighth (4 activation float4 per lane instead of 8), columns
+// 2 (l >> 3) + {0, 1}. Measured slower on top of W0SPLIT (24.14 vs 24.26 M).
 #ifndef LZM_RES_H2
-#define LZM_RES_H2 1
+#define LZM_RES_H2 0
+#endif
+// LZM_RES_SM1 (experiment, default 0): the support decode's softmax with one workgroup barrier — each
+// wave publishes (its max, its sums relative to that max) and every thread rescales the four
+// partials by exp(m_wave - M) — instead of a barrier for the max and another for the sums. Measured
+// slower (23.6 vs 24.14 M on top of W0SPLIT + H2; round 2 measured it even): the four extra expf per
+// thread on the chain cost more than the barrier.
+#ifndef LZM_RES_SM1
+#define LZM_RES_SM1 0
 #endif
 
 // Resident weight layout (lzm_mlp_prepare writes it after the generic kernel layout; res_source
@@ -1056,6 +1065,38 @@ template <int NH>
 __device__ __forceinline__ void support_decode_n(const float (*z)[3], float *red, float *out) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool ok2 = tid < 2 * kRTail && !(tid & 1);
+#if LZM_RES_SM1
+  {
+    const float half = (float)((kRV - 1) / 2);
+    const float j0 = (float)tid - half, j1 = (float)(kRT + tid) - half, j2 = (float)(2 * kRT + (tid >> 1)) - half;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      float m = fmaxf(z[h][0], z[h][1]);
+      if (ok2) m = fmaxf(m, z[h][2]);
+      m = wave_max_dpp(m);
+      const float e0 = expf(z[h][0] - m), e1 = expf(z[h][1] - m), e2 = ok2 ? expf(z[h][2] - m) : 0.0f;
+      float se = (e0 + e1) + e2, sj = (e0 * j0 + e1 * j1) + e2 * j2;
+      se = wave_sum(se);
+      sj = wave_sum(sj);
+      if (lane == 0) {
+        red[12 * h + wid] = m;
+        red[12 * h + 4 + wid] = se;
+        red[12 * h + 8 + wid] = sj;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const float *q = red + 12 * h;
+      const float M = fmaxf(fmaxf(q[0], q[1]), fmaxf(q[2], q[3]));
+      const float f0 = expf(q[0] - M), f1 = expf(q[1] - M), f2 = expf(q[2] - M), f3 = expf(q[3] - M);
+      const float se = (q[4] * f0 + q[5] * f1) + (q[6] * f2 + q[7] * f3);
+      const float sj = (q[8] * f0 + q[9] * f1) + (q[10] * f2 + q[11] * f3);
+      out[h] = h_inverse(sj / se);
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int h = 0; h < NH; ++h) {
     float m = fmaxf(z[h][0], z[h][1]);
@@ -1582,6 +1623,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #else
       dense128n<2>(T1, [&](int j) { return WD1[j * kRT + tid]; }, z);
 #endif
+      LZM_SUBSTAMP(32);
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) NL[r * kRRow + rpad(cD)] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[rpad(cD)];
@@ -1599,6 +1641,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
     __syncthreads();
+    LZM_SUBSTAMP(33);
     if (NR == 1 && late) {
       const unsigned long long w0_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
       if (G <= kRT) {
@@ -1616,6 +1659,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     // the next latent row the rest of the network reads (NR = 1: the late draw's pick)
     const float *NLb = NL + ((NR == 1 && late && s_act == act_r[1]) ? kRRow : 0);
+    LZM_SUBSTAMP(34);
     LZM_STAMP(3);
     // The reward chain (fc_dynamics_2 -> reward head) and the prediction chain (prediction
     // common -> value / policy heads) both start from the next latent: one step per layer pair.
@@ -1628,7 +1672,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rd5, tid * 16, j * kRT * 16, 0);
         P[j] = make_float4(v.x, v.y, v.z, v.w);
       });
+      LZM_SUBSTAMP(35);
       dense128n<NR>(NLb, [&](int j) { return wD4[j]; }, z6);
+      LZM_SUBSTAMP(36);
       if (pD == 0) {
 #pragma unroll
         for (int r = 0; r < NR; ++r) {
@@ -1643,6 +1689,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     {
       float z7[NR], z3[NR];
       dense128n<NR>(U2, [&](int j) { return P[j]; }, z7);
+      LZM_SUBSTAMP(37);
       // the value support head into P (two steps on): half before this layer, half after it (a
       // 20-load burst stalls the wave at issue)
       __builtin_amdgcn_sched_barrier(0);
@@ -1656,6 +1703,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       };
       fetch_vs(0, kRSlotsS / 2);
       dense128n<NR>(T2, [&](int j) { return wD3[j]; }, z3);
+      LZM_SUBSTAMP(38);
       __builtin_amdgcn_sched_barrier(0);
       fetch_vs(kRSlotsS / 2, kRSlotsS);
       if (pD == 0) {
@@ -1667,6 +1715,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
     __syncthreads();
+    LZM_SUBSTAMP(39);
     LZM_STAMP(4);
     // ---- [reward head hidden | (value | policy) head hidden]
 #pragma unroll
