@@ -81,6 +81,18 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #ifndef LZM_RES_SM1
 #define LZM_RES_SM1 0
 #endif
+// LZM_RES_DWIN (experiment, default 0, parity mode): the late draw's rand() value comes from a window
+// of 64 stream positions that wave 1 computes during wave 0's walk (coefficient rows against this
+// simulation's seed state, LaneDraws' arithmetic) around the previous simulation's look-back base,
+// so the draw after the look-back is one LDS read instead of a 31-word coefficient-row round trip
+// to L2. A position outside the window takes glibc_draw (same value either way). Measured: no window
+// misses, the look-back + resolve phase 2.63 K -> 2.35 K cycles per simulation, but the bench even
+// (24.13 vs 24.13 M, profiles/r04/ab_dwin.txt): the roots run as a convoy paced by the look-back
+// flags, so a root that resolves sooner waits longer at its next look-back.
+#ifndef LZM_RES_DWIN
+#define LZM_RES_DWIN 0
+#endif
+constexpr int kDwinBack = 20;  // window [base_prev - kDwinBack, base_prev - kDwinBack + 64)
 
 // Resident weight layout (lzm_mlp_prepare writes it after the generic kernel layout; res_source
 // below is its definition). Every block is [slot][lane] float4, so a wave-instruction of a block
@@ -1268,6 +1280,10 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ WalkState s_walk;
   __shared__ float4 s_mm;
   __shared__ float s_red[12 * 2 * NR];
+  __shared__ uint32_t s_dwin[64];  // LZM_RES_DWIN: draws at stream positions s_dlo + 0..63
+  __shared__ int s_dlo, s_base_prev;
+  if (tid == 0) { s_dlo = -1000000; s_base_prev = 0; }
+  (void)s_base_prev;
   __shared__ uint64_t s_exptab[32];  // glibc_expf's table: expand reads it from LDS (no vmcnt wait
                                      // on the weight prefetch in flight)
   if (threadIdx.x < 32) s_exptab[threadIdx.x] = kExp2fTab[threadIdx.x];
@@ -1433,6 +1449,21 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     LZM_STAMP(12);
     if (wid != 0 && k > 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // (see the expand)
+#if LZM_RES_DWIN
+    // (after the terms pass's barriers, so this simulation's seed state s_z0 is complete)
+    if (RNG != 1 && NR == 1 && !p.fast && n.late_draw && wid == 1 && (smode == 1 || smode == 2 || smode == 4)) {
+      const int lo = max(s_base_prev - kDwinBack, 0);
+      const int q = lo + lane;
+      uint32_t v = 0;
+      if (q < p.coef_positions) {
+        const uint32_t *c = p.coef + (size_t)q * 31;
+#pragma unroll
+        for (int j = 0; j < 31; ++j) v += c[j] * s_z0[j];
+      }
+      s_dwin[lane] = v >> 1;
+      if (lane == 0) s_dlo = lo;
+    }
+#endif
     // ---- selection, part 2: the walk (wave 0, one lane per child)
     if (wid == 0) {
       const float4 mm = s_mm;
@@ -1648,7 +1679,18 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (wid == 0) {
           const int base = lookback_sum_w0(p, k, g, G, epoch);
           if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
-          if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+          if (tid == 0) {
+            const int pos = base + s_tlevel, o = pos - s_dlo;
+            uint32_t rr;
+            if (LZM_RES_DWIN && o >= 0 && o < 64 && pos < p.coef_positions) {
+              rr = s_dwin[o];
+            } else {
+              rr = glibc_draw(p.coef, p.coef_positions, s_z0, pos, p.diag);
+              if (p.phase) s_phase[40] += 1;  // window misses (diagnostics)
+            }
+            s_base_prev = base;
+            resolve_tie(t, A, s_tlevel, s_tmask, rr, &s_act);
+          }
         }
       } else {
         const int base = lookback_sum(p, k, g, G, epoch, s_part);
