@@ -93,6 +93,60 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #define LZM_RES_DWIN 0
 #endif
 constexpr int kDwinBack = 20;  // window [base_prev - kDwinBack, base_prev - kDwinBack + 64)
+// LZM_RES_DWIN2 (default 1, parity mode, A = 2): a tie between visited children (status 2/3: the
+// walk's remaining levels need draws, the zero-init-heads regime at nearly every simulation) waits
+// for its look-back with wave 0 alone (lookback_sum_w0) while wave 1 computes the window of draws
+// around the previous look-back base, so the resumed walk reads its draws from LDS instead of a
+// coefficient-row round trip per lane after the wait (positions outside the window: the rows).
+#ifndef LZM_RES_DWIN2
+#define LZM_RES_DWIN2 1
+#endif
+
+// One wave: the draws at stream positions lo .. lo + 63 of the seed state z0 into win, lo into *dlo.
+__device__ __forceinline__ void dwin_fill(const uint32_t *coef, int npos, const uint32_t *z0, int lo, uint32_t *win,
+                                       int *dlo) {
+  const int lane = threadIdx.x & 63;
+  const int q = lo + lane;
+  uint32_t v = 0;
+  if (q < npos) {
+    const uint32_t *c = coef + (size_t)q * 31;
+#pragma unroll
+    for (int j = 0; j < 31; ++j) v += c[j] * z0[j];
+  }
+  win[lane] = v >> 1;
+  if (lane == 0) *dlo = lo;
+}
+
+// Part `part` (0..2: coefficient words 11 part .. 11 part + 10) of the window's 64 dot products, added
+// to win (the sums are mod 2^32, so the three waves' LDS adds may land in any order); win must be zero
+// before the first add and holds (sum) before the >> 1 of the draw. Eleven loads per lane.
+__device__ __forceinline__ void dwin_add_part(const uint32_t *coef, int npos, const uint32_t *z0, int lo, uint32_t *win,
+                                              int part) {
+  const int lane = threadIdx.x & 63;
+  const int q = lo + lane;
+  const int j0 = 11 * part, j1 = part == 2 ? 31 : j0 + 11;
+  if (q < npos) {
+    const uint32_t *c = coef + (size_t)q * 31;
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 11; ++j)
+      if (j0 + j < j1) v += c[j0 + j] * z0[j0 + j];
+    __hip_atomic_fetch_add(win + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+
+// The draw of this lane's level lo + lane of a resumed walk from the window win[0..64) of stream
+// positions dlo..; *miss when a level below hi lies outside it.
+__device__ __forceinline__ uint32_t window_draw(int npos, int base, int lo, int hi, const uint32_t *win, int dlo,
+                                                bool *miss) {
+  const int lane = threadIdx.x & 63;
+  const int q = base + lo + lane, o = q - dlo;
+  *miss = false;
+  if (lo + lane >= hi || q >= npos) return 0u;
+  if (o >= 0 && o < 64) return win[o] >> 1;
+  *miss = true;
+  return 0u;
+}
 
 // Resident weight layout (lzm_mlp_prepare writes it after the generic kernel layout; res_source
 // below is its definition). Every block is [slot][lane] float4, so a wave-instruction of a block
@@ -1449,20 +1503,11 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     LZM_STAMP(12);
     if (wid != 0 && k > 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // (see the expand)
+    if (LZM_RES_DWIN2 && !LZM_RES_DWIN && RNG != 1 && wid == 1) s_dwin[lane] = 0u;  // (the status-2 window's adds follow a barrier)
 #if LZM_RES_DWIN
     // (after the terms pass's barriers, so this simulation's seed state s_z0 is complete)
-    if (RNG != 1 && NR == 1 && !p.fast && n.late_draw && wid == 1 && (smode == 1 || smode == 2 || smode == 4)) {
-      const int lo = max(s_base_prev - kDwinBack, 0);
-      const int q = lo + lane;
-      uint32_t v = 0;
-      if (q < p.coef_positions) {
-        const uint32_t *c = p.coef + (size_t)q * 31;
-#pragma unroll
-        for (int j = 0; j < 31; ++j) v += c[j] * s_z0[j];
-      }
-      s_dwin[lane] = v >> 1;
-      if (lane == 0) s_dlo = lo;
-    }
+    if (RNG != 1 && NR == 1 && !p.fast && n.late_draw && wid == 1 && (smode == 1 || smode == 2 || smode == 4))
+      dwin_fill(p.coef, p.coef_positions, s_z0, max(s_base_prev - kDwinBack, 0), s_dwin, &s_dlo);
 #endif
     // ---- selection, part 2: the walk (wave 0, one lane per child)
     if (wid == 0) {
@@ -1546,12 +1591,47 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
       LZM_SUBSTAMP(20);
-      const int base = lookback_sum(p, k, g, G, epoch, s_part);
+      // LZM_RES_DWIN2: wave 0 alone waits for the look-back while wave 1 fills the draw window
+      const bool win2 = LZM_RES_DWIN2 && !LZM_RES_DWIN && RNG != 1 && smode == 4 && G <= kRT;
+      int base = 0;
+      if (win2) {
+        if (wid == 0) {
+          base = lookback_sum_w0(p, k, g, G, epoch);
+        } else {
+          const int lo = max(s_base_prev - kDwinBack, 0);
+          dwin_add_part(p.coef, p.coef_positions, s_z0, lo, s_dwin, wid - 1);
+          if (tid == 64) s_dlo = lo;
+        }
+        __syncthreads();
+      } else {
+        base = lookback_sum(p, k, g, G, epoch, s_part);
+      }
       LZM_SUBSTAMP(21);
       if (wid == 0) {
         if (lane == 0) atomicAdd(p.diag + (st == 2 ? 1 : 2), 1);
         WalkState ws = s_walk;
-        const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, ws.len, t.depth_cap, p.diag);
+        // the levels whose draws the resumed walk can read: below the speculated depth (st 3)
+        const int hi = st == 3 ? d0 : t.depth_cap;
+        bool need = true;
+        uint32_t wv = 0u;
+        if (win2) {
+          bool miss;
+          wv = window_draw(p.coef_positions, base, ws.len, hi, s_dwin, s_dlo, &miss);
+          need = __ballot(miss) != 0ull;
+          if (lane == 0) s_base_prev = base;
+          if (p.phase && lane == 0 && need) s_phase[41] += 1;  // window misses (diagnostics)
+        }
+        if (need) {  // (lane_draws' rows)
+          const int q = base + ws.len + lane;
+          wv = 0u;
+          if (ws.len + lane < hi && q < p.coef_positions) {
+            const uint32_t *c = p.coef + (size_t)q * 31;
+#pragma unroll
+            for (int j = 0; j < 31; ++j) wv += c[j] * s_z0[j];
+            wv >>= 1;
+          }
+        }
+        const LaneDraws draw{p.coef, s_z0, p.diag, p.coef_positions, base, ws.len, wv};
         Descent d;
         if (smode == 4)
           d = descend_a2<false>(t, NQ, DEC, CS, s_mm, s_vtp, players, rleg, nleg, draw, nullptr, &ws);
