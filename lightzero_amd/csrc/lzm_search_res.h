@@ -101,6 +101,12 @@ constexpr int kDwinBack = 20;  // window [base_prev - kDwinBack, base_prev - kDw
 #ifndef LZM_RES_DWIN2
 #define LZM_RES_DWIN2 1
 #endif
+// LZM_RES_SPEC_PATH (default 1): a status-3 root (depth speculated over all draw patterns) resolves
+// its path after the look-back from the matching pattern lane's choice bits (speculate_depth_a2) —
+// a pointer chase — instead of re-walking the tie subtree with scores.
+#ifndef LZM_RES_SPEC_PATH
+#define LZM_RES_SPEC_PATH 1
+#endif
 
 // One wave: the draws at stream positions lo .. lo + 63 of the seed state z0 into win, lo into *dlo.
 __device__ __forceinline__ void dwin_fill(const uint32_t *coef, int npos, const uint32_t *z0, int lo, uint32_t *win,
@@ -867,8 +873,16 @@ __device__ inline Descent descend_a2(const TreeView &t, const float2 *nq, const 
 // If all 64 patterns give one depth, the root's draw count is known before any of its draw values:
 // it is published at once and the path is resolved after the look-back (same walk, same bits).
 // Same per-level operations as descend_a2.
+// (LZM_RES_SPEC_PATH: *choice gets bit l = the legal position taken at level w.len + l, *ties bit l
+// when that level was a tie decided by the pattern, *leaf_tie the offset of a final tie between two
+// unexpanded children (its draw picks the leaf; -1: none); *choice = ~0u when the walk is longer than
+// 31 levels past w.len. The path of a walk is then its choice bits: the look-back's draw parities
+// select the lane whose pattern matches, and the path is a pointer chase without the scores.)
 __device__ inline int speculate_depth_a2(const TreeView &t, const float2 *nq, const int *dec, const float4 *cs,
-                                         float4 mm, const int *rleg, int nleg, const WalkState &w, int pattern) {
+                                         float4 mm, const int *rleg, int nleg, const WalkState &w, int pattern,
+                                         uint32_t *choice = nullptr, uint32_t *ties = nullptr, int *leaf_tie = nullptr) {
+  uint32_t ch = 0u, tm = 0u;
+  if (leaf_tie) *leaf_tie = -1;
   const float delta = mm.x - mm.y;
   const bool scale = delta > 0;
   const float div = (delta < mm.z) ? mm.z : delta;
@@ -899,18 +913,25 @@ __device__ inline int speculate_depth_a2(const TreeView &t, const float2 *nq, co
       jsel = (s0 == M) ? 0 : 1;
       tie2 = jsel == 0 && s1 >= M - 0.000001f;
     }
+    const int off = len - w.len;
     if (tie2) {
-      if (__float_as_int(c0.z) < 0 && __float_as_int(c1.z) < 0) return len + 1;  // either way a leaf
+      if (__float_as_int(c0.z) < 0 && __float_as_int(c1.z) < 0) {  // either way a leaf
+        if (choice) { *choice = off < 31 ? ch : ~0u; *ties = tm; *leaf_tie = off; }
+        return len + 1;
+      }
       if (used == 6) return -1;
       jsel = (pattern >> used) & 1;
       ++used;
+      if (off < 31) tm |= 1u << off;
     }
+    if (off < 31) ch |= (uint32_t)jsel << off;
     is_root = false;
     parent_q = mean_q;
     node = base + (jsel ? a1 : a0);
     lat = __float_as_int(jsel ? c1.z : c0.z);
     ++len;
   }
+  if (choice) { *choice = len - w.len <= 31 ? ch : ~0u; *ties = tm; }
   return len;
 }
 
@@ -1579,9 +1600,13 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       // (A == 2), when every draw outcome gives the same depth (speculate_depth_a2), publish it at
       // once so that the roots after this one need not wait for this root's look-back (st = 3).
       int st = 2, d0 = -1;
+      uint32_t sp_choice = ~0u, sp_ties = 0u;
+      int sp_leaf = -1;
       unsigned long long sub_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
       if (smode == 4 && n.spec_depth && wid == 0) {
-        const int de = speculate_depth_a2(t, NQ, DEC, CS, s_mm, rleg, nleg, s_walk, lane);
+        const int de = LZM_RES_SPEC_PATH
+                           ? speculate_depth_a2(t, NQ, DEC, CS, s_mm, rleg, nleg, s_walk, lane, &sp_choice, &sp_ties, &sp_leaf)
+                           : speculate_depth_a2(t, NQ, DEC, CS, s_mm, rleg, nleg, s_walk, lane);
         d0 = __builtin_amdgcn_readfirstlane(de);
         if (d0 >= 0 && __ballot(de != d0) == 0ull) {
           st = 3;
@@ -1633,7 +1658,46 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         const LaneDraws draw{p.coef, s_z0, p.diag, p.coef_positions, base, ws.len, wv};
         Descent d;
-        if (smode == 4)
+        // LZM_RES_SPEC_PATH: the lane whose pattern agrees with the draws' parities at its tie levels
+        // (lane l holds the draw of level ws.len + l); that lane's choice bits are the path
+        int m = -1;
+        uint32_t pch = 0u;
+        if (LZM_RES_SPEC_PATH && st == 3 && smode == 4) {
+          const unsigned long long par = __ballot((wv & 1u) != 0u);
+          const bool ok = sp_choice != ~0u && ((sp_choice ^ (uint32_t)par) & sp_ties) == 0u;
+          const unsigned long long okm = __ballot(ok);
+          if (okm) {
+            m = __ffsll((long long)okm) - 1;
+            pch = (uint32_t)__builtin_amdgcn_readlane((int)sp_choice, m);
+            const int lt = __builtin_amdgcn_readlane(sp_leaf, m);
+            if (lt >= 0) pch = (pch & ~(1u << lt)) | ((uint32_t)(par >> lt) & 1u) << lt;
+          }
+        }
+        if (m >= 0) {
+          int node = ws.node, lat = ws.lat, len = ws.len, plat = ws.plat, last_action = ws.last_action;
+          const int dmax = t.depth_cap - 1;
+          while (lat >= 0 && len < dmax) {
+            const bool root = node == 0;
+            const int j = (int)((pch >> (len - ws.len)) & 1u);
+            const int action = j ? (root ? rleg[1] : 1) : (root ? rleg[0] : 0);
+            const int nnode = 1 + 2 * lat + action;
+            const int nlat = __float_as_int(CS[nnode].z);
+            if (lane == 0) {
+              t.path_act[len] = action;
+              t.path[len + 1] = nnode;
+            }
+            ++len;
+            plat = lat;
+            lat = nlat;
+            node = nnode;
+            last_action = action;
+          }
+          d.len = len;
+          d.x = plat;
+          d.action = last_action;
+          d.vtp = 0;
+          d.leaf = node;
+        } else if (smode == 4)
           d = descend_a2<false>(t, NQ, DEC, CS, s_mm, s_vtp, players, rleg, nleg, draw, nullptr, &ws);
         else
           d = descend_terms<false>(t, NQ, CS, s_mm, s_vtp, players, draw, nullptr, &ws);
