@@ -61,6 +61,12 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #ifndef LZM_RES_EARLY
 #define LZM_RES_EARLY 0
 #endif
+// LZM_RES_EGATHER (default 1): the walking wave gathers the leaf's parent latent X0 itself, right
+// after its walk when x is final (the walk's barrier orders it), or after a status-2 root's draw
+// resolution: the gather phase's own barrier and its dependent load after it go.
+#ifndef LZM_RES_EGATHER
+#define LZM_RES_EGATHER 1
+#endif
 // LZM_RES_W0SPLIT (experiment, default 0): wave 0's fc_dynamics[0] prefetch in four quarters spread
 // over the expand, the backup and the next terms pass instead of one 16-load burst after the decode.
 // Measured slower (24.26 vs 24.46 M sims/s, two interleaved runs each, profiles/r04/ab_res.txt).
@@ -1578,7 +1584,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-#if LZM_RES_EARLY
+#if LZM_RES_EARLY || LZM_RES_EGATHER
       // gather the leaf's parent latent now, by the walking wave, when the walk's x is final (every
       // status but 2): the walk's barrier then also orders the gather (one barrier fewer)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's s_status / s_x to the wave
@@ -1712,6 +1718,12 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             __hip_atomic_store(&p.flags[(size_t)k * G + g], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
+        if (LZM_RES_EGATHER && !LZM_RES_EARLY) {  // X0 by this wave (the barrier below orders it)
+          const int x0 = __builtin_amdgcn_readfirstlane(d.x);
+          if (lane < kRHid / 4)
+            reinterpret_cast<float4 *>(X0)[lane + (lane >= kRHid / 8)] =
+                reinterpret_cast<const float4 *>(p.pool + ((size_t)max(x0, 0) * B + i) * kRHid)[lane];
+        }
       }
       LZM_SUBSTAMP(22);
       __syncthreads();
@@ -1739,7 +1751,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     LZM_STAMP(1);
     // ---- gather the leaf's parent latent: X0 = pool[x][i] (LZM_RES_EARLY: already done by the walk
     // unless the depth waited for a draw)
-    if (!LZM_RES_EARLY || status == 2) {
+    const bool gathered = LZM_RES_EARLY ? status != 2
+                                        : (LZM_RES_EGATHER && (status != 2 || smode == 1 || smode == 4));
+    if (!gathered) {
       if (tid < kRHid / 4)
         reinterpret_cast<float4 *>(X0)[tid + (tid >= kRHid / 8)] =
             reinterpret_cast<const float4 *>(p.pool + ((size_t)max(s_x, 0) * B + i) * kRHid)[tid];
