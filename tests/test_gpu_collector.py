@@ -119,6 +119,6 @@ def test_device_collector_graph_equals_eager():
         for _ in range(20):
             col.step()
         torch.cuda.synchronize()
-        out.append((col.rec_action.cpu().numpy(), col.rec_visits.cpu().numpy(), col.state.cpu().numpy()))
+        out.append((col.rec_action.cpu().numpy(), col.rec_visits.cpu().numpy(), col.env.state.cpu().numpy()))
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)

@@ -2,16 +2,18 @@
 # default bench command (kernel stats, PMC passes, the bench line with its CPU baseline and config 5's
 # sharded collect step), the conv benches with their CPU baselines (Breakout MZ, Pong EZ) and kernel
 # traces, the Philox / zero-heads / collect-mode / config-1 lines, the phase timings.
-# usage: bash tools/gpu_final.sh <tag>
+# usage: bash tools/gpu_final.sh <tag> [--no-tests]
 set -e
 tag=${1:-r04}
 out=gpurun_out/f_$tag
 mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 export LZM_REPORT_DIR="$GRAFT_REPO_ROOT/$out"
-timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $out/gpu_tests.log 2>&1
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
-bash tools/profile_round.sh $out/prof
+if [ "$2" != "--no-tests" ]; then  # (--no-tests: the second half after tools/gpu_final_a.sh)
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread > $out/gpu_tests.log 2>&1
+  timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1
+  bash tools/profile_round.sh $out/prof
+fi
 for k in mz ez; do
   timeout -k 10 300 python tools/conv_bench.py --kind $k --cpu-baseline-secs 30 > $out/conv_$k.json 2>$out/conv_$k.err
 done
