@@ -67,6 +67,19 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #ifndef LZM_RES_EGATHER
 #define LZM_RES_EGATHER 1
 #endif
+// LZM_RES_RD5E (experiment): where fc_prediction_common[1]'s weight slots are fetched into the stream
+// buffer P. 0 (default): one slot per slot of the fc_dynamics_2[0] layer (its `side` hook); 1: waves
+// 1-3 right after fc_dynamics[1] (they idle through wave 0's look-back), wave 0 as in 0; 2: every wave
+// there. Measured 24.0 (0) vs 23.5 (1) vs 23.2 M (2) sims/s (profiles/r04/ab_rd5e_seedw1.txt).
+#ifndef LZM_RES_RD5E
+#define LZM_RES_RD5E 0
+#endif
+// LZM_RES_SEEDW1 (default 1): this simulation's glibc seed state (s_z0, read only after the walk) is
+// computed by wave 1 during wave 0's walk instead of by wave 0 before the terms pass's barrier:
+// +0.8% with random and with zero-init heads (profiles/r04/ab_rd5e_seedw1.txt).
+#ifndef LZM_RES_SEEDW1
+#define LZM_RES_SEEDW1 1
+#endif
 // LZM_RES_W0SPLIT (experiment, default 0): wave 0's fc_dynamics[0] prefetch in four quarters spread
 // over the expand, the backup and the next terms pass instead of one 16-load burst after the decode.
 // Measured slower (24.26 vs 24.46 M sims/s, two interleaved runs each, profiles/r04/ab_res.txt).
@@ -1504,7 +1517,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   for (int k = 0; k < p.S; ++k) {
     const uint32_t seed = s_seeds[k];
-    if (!p.fast) seed_state_parallel(seed, s_pow, s_z0);
+    if (!LZM_RES_SEEDW1 && !p.fast) seed_state_parallel(seed, s_pow, s_z0);
     // ---- selection, part 1: every expanded node's walk-independent pUCT terms (all threads)
     // 0: descend_wave; 1: terms + wave walk; 2: terms + lane walk; 3: descend_slice; 4 (default):
     // terms + descend_small when A <= 2, else as 1
@@ -1530,6 +1543,20 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     LZM_STAMP(12);
     if (wid != 0 && k > 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // (see the expand)
+    if (LZM_RES_SEEDW1 && !p.fast && wid == 1) {  // (the post-walk barrier orders s_z0 for its readers)
+      const uint32_t sd = seed == 0 ? 1u : seed;
+      if (sd < 0x7fffffffu) {
+        if (lane < 31) {
+          unsigned long long x = (unsigned long long)sd * s_pow[lane];
+          unsigned long long r = (x & 0x7fffffffull) + (x >> 31);
+          r = (r & 0x7fffffffull) + (r >> 31);
+          if (r >= 0x7fffffffull) r -= 0x7fffffffull;
+          s_z0[lane] = (uint32_t)r;
+        }
+      } else if (lane == 0) {
+        glibc_seed_state(seed, s_z0);
+      }
+    }
     if (LZM_RES_DWIN2 && !LZM_RES_DWIN && RNG != 1 && wid == 1) s_dwin[lane] = 0u;  // (the status-2 window's adds follow a barrier)
 #if LZM_RES_DWIN
     // (after the terms pass's barriers, so this simulation's seed state s_z0 is complete)
@@ -1829,6 +1856,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int r = 0; r < NR; ++r) NL[r * kRRow + rpad(cD)] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[rpad(cD)];
       }
     }
+    if (LZM_RES_RD5E == 2 || (LZM_RES_RD5E == 1 && wid != 0)) res_fetch<kRSlotsD>(res_blk4(n, kRbD + 5), P);
     __syncthreads();
     LZM_SUBSTAMP(33);
     if (NR == 1 && late) {
@@ -1868,10 +1896,15 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       float z2[NR], z6[NR];
       // fc_prediction_common[1] into P (used by the next pair), one slot per slot of this layer
       const __amdgpu_buffer_rsrc_t rd5 = wave_rsrc(res_blk4(n, kRbD + 5), kRSlotsD * kRT * 16);
-      dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2, [&](int j) {
-        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rd5, tid * 16, j * kRT * 16, 0);
-        P[j] = make_float4(v.x, v.y, v.z, v.w);
-      });
+      if (LZM_RES_RD5E == 2 || (LZM_RES_RD5E == 1 && wid != 0)) {
+        (void)rd5;
+        dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2);
+      } else {
+        dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2, [&](int j) {
+          const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rd5, tid * 16, j * kRT * 16, 0);
+          P[j] = make_float4(v.x, v.y, v.z, v.w);
+        });
+      }
       LZM_SUBSTAMP(35);
       dense128n<NR>(NLb, [&](int j) { return wD4[j]; }, z6);
       LZM_SUBSTAMP(36);
