@@ -1,0 +1,12 @@
+# Final build of round 4 (after LZM_RES_SEEDW1; the closing set in the parent directory is the build
+# before it — conv kernels unchanged since). Two gpurun calls:
+#   gpu_tests.log, smoke.log, kernel_stats.csv <- bash tools/gpu_final_a.sh r04b (236 passed; smoke
+#       bit-exact; rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 3 --no-cpu-baseline;
+#       the first --pmc pass then printed nothing for 180 s on that box and the call was ended, so the
+#       PMC summary stays the closing set's: ../pmc.json, same kernels' memory traffic)
+#   bench.json, bench_zero_heads.json, bench_philox.json, bench_collect.json, phase_timing*.txt <-
+python3 bench.py
+python bench.py --no-cpu-baseline --secondary none --zero-heads
+python bench.py --no-cpu-baseline --secondary none --rng philox
+python bench.py --step collect --secondary none --no-cpu-baseline
+python tools/phase_timing.py; python tools/phase_timing.py --zero-heads
