@@ -54,25 +54,11 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #ifndef LZM_RES_D4
 #define LZM_RES_D4 1
 #endif
-// LZM_RES_EARLY (experiment, default 0): two barriers fewer per simulation — the walking wave
-// computes the pUCT terms alone (<= 64 expanded nodes) and gathers the leaf's parent latent right
-// after its walk. Measured slower (24.2 vs 24.6 M sims/s): waves 1-3 then issue their fc_dynamics[0]
-// prefetch during wave 0's terms pass instead of during its walk.
-#ifndef LZM_RES_EARLY
-#define LZM_RES_EARLY 0
-#endif
 // LZM_RES_EGATHER (default 1): the walking wave gathers the leaf's parent latent X0 itself, right
 // after its walk when x is final (the walk's barrier orders it), or after a status-2 root's draw
 // resolution: the gather phase's own barrier and its dependent load after it go.
 #ifndef LZM_RES_EGATHER
 #define LZM_RES_EGATHER 1
-#endif
-// LZM_RES_RD5E (experiment): where fc_prediction_common[1]'s weight slots are fetched into the stream
-// buffer P. 0 (default): one slot per slot of the fc_dynamics_2[0] layer (its `side` hook); 1: waves
-// 1-3 right after fc_dynamics[1] (they idle through wave 0's look-back), wave 0 as in 0; 2: every wave
-// there. Measured 24.0 (0) vs 23.5 (1) vs 23.2 M (2) sims/s (profiles/r04/ab_rd5e_seedw1.txt).
-#ifndef LZM_RES_RD5E
-#define LZM_RES_RD5E 0
 #endif
 // LZM_RES_SEEDW1 (default 1): this simulation's glibc seed state (s_z0, read only after the walk) is
 // computed by wave 1 during wave 0's walk instead of by wave 0 before the terms pass's barrier:
@@ -80,38 +66,11 @@ constexpr int kRSlotsD = 16, kRSlotsRH = 4, kRSlotsVPH = 8, kRSlotsS = 20, kRSlo
 #ifndef LZM_RES_SEEDW1
 #define LZM_RES_SEEDW1 1
 #endif
-// LZM_RES_W0SPLIT (experiment, default 0): wave 0's fc_dynamics[0] prefetch in four quarters spread
-// over the expand, the backup and the next terms pass instead of one 16-load burst after the decode.
-// Measured slower (24.26 vs 24.46 M sims/s, two interleaved runs each, profiles/r04/ab_res.txt).
-#ifndef LZM_RES_W0SPLIT
-#define LZM_RES_W0SPLIT 0
-#endif
-// LZM_RES_H2 (experiment, default 0): the [value | policy] head hidden layer (128 -> 64) with two
-// columns per lane over a K eighth (4 activation float4 per lane instead of 8), columns
-// 2 (l >> 3) + {0, 1}. Measured slower on top of W0SPLIT (24.14 vs 24.26 M).
-#ifndef LZM_RES_H2
-#define LZM_RES_H2 0
-#endif
-// LZM_RES_SM1 (experiment, default 0): the support decode's softmax with one workgroup barrier — each
-// wave publishes (its max, its sums relative to that max) and every thread rescales the four
-// partials by exp(m_wave - M) — instead of a barrier for the max and another for the sums. Measured
-// slower (23.6 vs 24.14 M on top of W0SPLIT + H2; round 2 measured it even): the four extra expf per
-// thread on the chain cost more than the barrier.
-#ifndef LZM_RES_SM1
-#define LZM_RES_SM1 0
-#endif
-// LZM_RES_DWIN (experiment, default 0, parity mode): the late draw's rand() value comes from a window
-// of 64 stream positions that wave 1 computes during wave 0's walk (coefficient rows against this
-// simulation's seed state, LaneDraws' arithmetic) around the previous simulation's look-back base,
-// so the draw after the look-back is one LDS read instead of a 31-word coefficient-row round trip
-// to L2. A position outside the window takes glibc_draw (same value either way). Measured: no window
-// misses, the look-back + resolve phase 2.63 K -> 2.35 K cycles per simulation, but the bench even
-// (24.13 vs 24.13 M, profiles/r04/ab_dwin.txt): the roots run as a convoy paced by the look-back
-// flags, so a root that resolves sooner waits longer at its next look-back.
-#ifndef LZM_RES_DWIN
-#define LZM_RES_DWIN 0
-#endif
-constexpr int kDwinBack = 20;  // window [base_prev - kDwinBack, base_prev - kDwinBack + 64)
+// Measured and removed in round 4 (DESIGN.md §9 gives each A/B): wave 0 computing the pUCT terms
+// alone with an early latent gather, wave 0's fc_dynamics[0] prefetch in quarters, a two-column
+// value / policy head hidden layer, a one-barrier support softmax, the late draw from a window of
+// draws built during the walk, fc_prediction_common[1] prefetched during the look-back.
+constexpr int kDwinBack = 20;  // draw window [base_prev - kDwinBack, base_prev - kDwinBack + 64)
 // LZM_RES_DWIN2 (default 1, parity mode, A = 2): a tie between visited children (status 2/3: the
 // walk's remaining levels need draws, the zero-init-heads regime at nearly every simulation) waits
 // for its look-back with wave 0 alone (lookback_sum_w0) while wave 1 computes the window of draws
@@ -126,21 +85,6 @@ constexpr int kDwinBack = 20;  // window [base_prev - kDwinBack, base_prev - kDw
 #ifndef LZM_RES_SPEC_PATH
 #define LZM_RES_SPEC_PATH 1
 #endif
-
-// One wave: the draws at stream positions lo .. lo + 63 of the seed state z0 into win, lo into *dlo.
-__device__ __forceinline__ void dwin_fill(const uint32_t *coef, int npos, const uint32_t *z0, int lo, uint32_t *win,
-                                       int *dlo) {
-  const int lane = threadIdx.x & 63;
-  const int q = lo + lane;
-  uint32_t v = 0;
-  if (q < npos) {
-    const uint32_t *c = coef + (size_t)q * 31;
-#pragma unroll
-    for (int j = 0; j < 31; ++j) v += c[j] * z0[j];
-  }
-  win[lane] = v >> 1;
-  if (lane == 0) *dlo = lo;
-}
 
 // Part `part` (0..2: coefficient words 11 part .. 11 part + 10) of the window's 64 dot products, added
 // to win (the sums are mod 2^32, so the three waves' LDS adds may land in any order); win must be zero
@@ -256,13 +200,8 @@ __host__ __device__ inline void res_source(int b, size_t d, int A, int *layer, i
   switch (b) {
     case kRbRH: *layer = 4; *col = l >> 3; *k = 16 * (l & 7) + 4 * j + e; return;
     case kRbVPH: {
-#if LZM_RES_H2
-      const int c = 2 * (l >> 3) + (j & 1);
-      *layer = c < kRF ? 8 : 10; *col = c < kRF ? c : c - kRF; *k = 16 * (l & 7) + 4 * (j >> 1) + e;
-#else
       const int c = l >> 2;
       *layer = c < kRF ? 8 : 10; *col = c < kRF ? c : c - kRF; *k = 32 * (l & 3) + 4 * j + e;
-#endif
       return;
     }
     case kRbRS: case kRbVS: {
@@ -1171,38 +1110,6 @@ template <int NH>
 __device__ __forceinline__ void support_decode_n(const float (*z)[3], float *red, float *out) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool ok2 = tid < 2 * kRTail && !(tid & 1);
-#if LZM_RES_SM1
-  {
-    const float half = (float)((kRV - 1) / 2);
-    const float j0 = (float)tid - half, j1 = (float)(kRT + tid) - half, j2 = (float)(2 * kRT + (tid >> 1)) - half;
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      float m = fmaxf(z[h][0], z[h][1]);
-      if (ok2) m = fmaxf(m, z[h][2]);
-      m = wave_max_dpp(m);
-      const float e0 = expf(z[h][0] - m), e1 = expf(z[h][1] - m), e2 = ok2 ? expf(z[h][2] - m) : 0.0f;
-      float se = (e0 + e1) + e2, sj = (e0 * j0 + e1 * j1) + e2 * j2;
-      se = wave_sum(se);
-      sj = wave_sum(sj);
-      if (lane == 0) {
-        red[12 * h + wid] = m;
-        red[12 * h + 4 + wid] = se;
-        red[12 * h + 8 + wid] = sj;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      const float *q = red + 12 * h;
-      const float M = fmaxf(fmaxf(q[0], q[1]), fmaxf(q[2], q[3]));
-      const float f0 = expf(q[0] - M), f1 = expf(q[1] - M), f2 = expf(q[2] - M), f3 = expf(q[3] - M);
-      const float se = (q[4] * f0 + q[5] * f1) + (q[6] * f2 + q[7] * f3);
-      const float sj = (q[8] * f0 + q[9] * f1) + (q[10] * f2 + q[11] * f3);
-      out[h] = h_inverse(sj / se);
-    }
-    return;
-  }
-#endif
 #pragma unroll
   for (int h = 0; h < NH; ++h) {
     float m = fmaxf(z[h][0], z[h][1]);
@@ -1374,10 +1281,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ WalkState s_walk;
   __shared__ float4 s_mm;
   __shared__ float s_red[12 * 2 * NR];
-  __shared__ uint32_t s_dwin[64];  // LZM_RES_DWIN: draws at stream positions s_dlo + 0..63
+  __shared__ uint32_t s_dwin[64];  // LZM_RES_DWIN2: draw sums at stream positions s_dlo + 0..63
   __shared__ int s_dlo, s_base_prev;
   if (tid == 0) { s_dlo = -1000000; s_base_prev = 0; }
-  (void)s_base_prev;
   __shared__ uint64_t s_exptab[32];  // glibc_expf's table: expand reads it from LDS (no vmcnt wait
                                      // on the weight prefetch in flight)
   if (threadIdx.x < 32) s_exptab[threadIdx.x] = kExp2fTab[threadIdx.x];
@@ -1482,8 +1388,6 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   res_fetch<kRSlotsVPH>(res_blk4(n, kRbVPH), wVPH);
   res_fetch<kRSlotsPO>(res_blk4(n, kRbPO), wPO);
   const int cD = d_col(), pD = tid & 1, cRH = tid >> 3, pRH = tid & 7, cVP = tid >> 2, pVP = tid & 3, cPO = tid >> 3;
-  (void)cVP;
-  (void)pVP;
   LZM_ISTAMP(27);
   // biases live in LDS (registers are the scarce resource): the bias blocks are contiguous
   float *BB = reinterpret_cast<float *>(s_bias);
@@ -1522,24 +1426,13 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // 0: descend_wave; 1: terms + wave walk; 2: terms + lane walk; 3: descend_slice; 4 (default):
     // terms + descend_small when A <= 2, else as 1
     const int smode = (n.select_mode == 4 && A != 2) ? 1 : n.select_mode;
-    // LZM_RES_EARLY: with at most 64 expanded nodes every term is computed by wave 0, the wave that
-    // walks, so the walk needs no workgroup barrier after the terms (a wave-level fence orders the
-    // LDS writes of its lanes before their reads)
-    const bool w0terms = LZM_RES_EARLY && s_nlat + k <= 64;
     if (smode == 1 || smode == 2 || smode == 4) {
       __syncthreads();  // the previous simulation's backup (wave 0) and children (wave 1) are complete
-      if (LZM_RES_W0SPLIT && wid == 0 && k > 0) res_fetch<kRSlotsD, 12, 16>(res_blk4(n, kRbD), P);
       if (smode == 4)
         precompute_terms_a2(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, DEC, rleg, nleg);
       else
         precompute_terms(t, s_nlat + k, L2N, NQ, CS, s_mm, players, p.disc, smode == 4 ? DEC : nullptr);
-      if (w0terms) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      } else {
-        __syncthreads();
-      }
+      __syncthreads();
     }
     LZM_STAMP(12);
     if (wid != 0 && k > 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);  // (see the expand)
@@ -1557,12 +1450,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         glibc_seed_state(seed, s_z0);
       }
     }
-    if (LZM_RES_DWIN2 && !LZM_RES_DWIN && RNG != 1 && wid == 1) s_dwin[lane] = 0u;  // (the status-2 window's adds follow a barrier)
-#if LZM_RES_DWIN
-    // (after the terms pass's barriers, so this simulation's seed state s_z0 is complete)
-    if (RNG != 1 && NR == 1 && !p.fast && n.late_draw && wid == 1 && (smode == 1 || smode == 2 || smode == 4))
-      dwin_fill(p.coef, p.coef_positions, s_z0, max(s_base_prev - kDwinBack, 0), s_dwin, &s_dlo);
-#endif
+    if (LZM_RES_DWIN2 && RNG != 1 && wid == 1) s_dwin[lane] = 0u;  // (the status-2 window's adds follow a barrier)
     // ---- selection, part 2: the walk (wave 0, one lane per child)
     if (wid == 0) {
       const float4 mm = s_mm;
@@ -1611,7 +1499,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                                __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-#if LZM_RES_EARLY || LZM_RES_EGATHER
+#if LZM_RES_EGATHER
       // gather the leaf's parent latent now, by the walking wave, when the walk's x is final (every
       // status but 2): the walk's barrier then also orders the gather (one barrier fewer)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // lane 0's s_status / s_x to the wave
@@ -1650,7 +1538,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
       LZM_SUBSTAMP(20);
       // LZM_RES_DWIN2: wave 0 alone waits for the look-back while wave 1 fills the draw window
-      const bool win2 = LZM_RES_DWIN2 && !LZM_RES_DWIN && RNG != 1 && smode == 4 && G <= kRT;
+      const bool win2 = LZM_RES_DWIN2 && RNG != 1 && smode == 4 && G <= kRT;
       int base = 0;
       if (win2) {
         if (wid == 0) {
@@ -1745,7 +1633,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             __hip_atomic_store(&p.flags[(size_t)k * G + g], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (LZM_RES_EGATHER && !LZM_RES_EARLY) {  // X0 by this wave (the barrier below orders it)
+        if (LZM_RES_EGATHER) {  // X0 by this wave (the barrier below orders it)
           const int x0 = __builtin_amdgcn_readfirstlane(d.x);
           if (lane < kRHid / 4)
             reinterpret_cast<float4 *>(X0)[lane + (lane >= kRHid / 8)] =
@@ -1776,10 +1664,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       __syncthreads();
     }
     LZM_STAMP(1);
-    // ---- gather the leaf's parent latent: X0 = pool[x][i] (LZM_RES_EARLY: already done by the walk
-    // unless the depth waited for a draw)
-    const bool gathered = LZM_RES_EARLY ? status != 2
-                                        : (LZM_RES_EGATHER && (status != 2 || smode == 1 || smode == 4));
+    // ---- gather the leaf's parent latent: X0 = pool[x][i] (LZM_RES_EGATHER: already done by the
+    // walking wave)
+    const bool gathered = LZM_RES_EGATHER && (status != 2 || smode == 1 || smode == 4);
     if (!gathered) {
       if (tid < kRHid / 4)
         reinterpret_cast<float4 *>(X0)[tid + (tid >= kRHid / 8)] =
@@ -1856,7 +1743,6 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int r = 0; r < NR; ++r) NL[r * kRRow + rpad(cD)] = fmaxf(z[r] + BD[kRHid + cD], 0.0f) + X0[rpad(cD)];
       }
     }
-    if (LZM_RES_RD5E == 2 || (LZM_RES_RD5E == 1 && wid != 0)) res_fetch<kRSlotsD>(res_blk4(n, kRbD + 5), P);
     __syncthreads();
     LZM_SUBSTAMP(33);
     if (NR == 1 && late) {
@@ -1865,18 +1751,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (wid == 0) {
           const int base = lookback_sum_w0(p, k, g, G, epoch);
           if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
-          if (tid == 0) {
-            const int pos = base + s_tlevel, o = pos - s_dlo;
-            uint32_t rr;
-            if (LZM_RES_DWIN && o >= 0 && o < 64 && pos < p.coef_positions) {
-              rr = s_dwin[o];
-            } else {
-              rr = glibc_draw(p.coef, p.coef_positions, s_z0, pos, p.diag);
-              if (p.phase) s_phase[40] += 1;  // window misses (diagnostics)
-            }
-            s_base_prev = base;
-            resolve_tie(t, A, s_tlevel, s_tmask, rr, &s_act);
-          }
+          if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
         }
       } else {
         const int base = lookback_sum(p, k, g, G, epoch, s_part);
@@ -1896,15 +1771,10 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       float z2[NR], z6[NR];
       // fc_prediction_common[1] into P (used by the next pair), one slot per slot of this layer
       const __amdgpu_buffer_rsrc_t rd5 = wave_rsrc(res_blk4(n, kRbD + 5), kRSlotsD * kRT * 16);
-      if (LZM_RES_RD5E == 2 || (LZM_RES_RD5E == 1 && wid != 0)) {
-        (void)rd5;
-        dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2);
-      } else {
-        dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2, [&](int j) {
-          const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rd5, tid * 16, j * kRT * 16, 0);
-          P[j] = make_float4(v.x, v.y, v.z, v.w);
-        });
-      }
+      dense128n<NR>(NLb, [&](int j) { return WD2[j * kRT + tid]; }, z2, [&](int j) {
+        const f32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rd5, tid * 16, j * kRT * 16, 0);
+        P[j] = make_float4(v.x, v.y, v.z, v.w);
+      });
       LZM_SUBSTAMP(35);
       dense128n<NR>(NLb, [&](int j) { return wD4[j]; }, z6);
       LZM_SUBSTAMP(36);
@@ -1955,33 +1825,6 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     for (int r = 0; r < NR; ++r) {
       float h = dot4<kRSlotsRH>(reinterpret_cast<const float4 *>(T3 + r * kRRow) + 4 * pRH + (pRH >= 4),
                                 [&](int j) { return wRH[j]; });
-#if LZM_RES_H2
-      float u;
-      int cu;
-      {
-        const int e = tid & 7;
-        const float4 *u4 = reinterpret_cast<const float4 *>(U3 + r * kRRow) + 4 * e + (e >> 2);
-        float a0[4] = {0.0f, 0.0f, 0.0f, 0.0f}, a1[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const float4 xv = u4[jj];
-          fma4(xv, wVPH[2 * jj], a0);
-          fma4(xv, wVPH[2 * jj + 1], a1);
-        }
-        const float v0 = (a0[0] + a0[1]) + (a0[2] + a0[3]), v1 = (a1[0] + a1[1]) + (a1[2] + a1[3]);
-        const bool lo = e < 4;
-        u = lo ? v0 : v1;
-        u += dpp_f<0x141>(lo ? v1 : v0);  // lanes e, 7 - e: the lower half keeps column 0, the upper 1
-        cu = 2 * (tid >> 3) + (lo ? 0 : 1);
-      }
-      h += dpp_f<0xB1>(h);
-      u += dpp_f<0xB1>(u);
-      h += dpp_f<0x4E>(h);
-      u += dpp_f<0x4E>(u);
-      h += dpp_f<0x141>(h);
-      if (pRH == 0) RHo[r * kRF + cRH] = fmaxf(h + BRH[cRH], 0.0f);
-      if ((tid & 3) == 0) HV[r * 2 * kRF + cu] = fmaxf(u + BVP[cu], 0.0f);
-#else
       float u = dot4<kRSlotsVPH>(reinterpret_cast<const float4 *>(U3 + r * kRRow) + 8 * pVP + (pVP >= 2),
                                  [&](int j) { return wVPH[j]; });
       h += dpp_f<0xB1>(h);
@@ -1991,7 +1834,6 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       h += dpp_f<0x141>(h);
       if (pRH == 0) RHo[r * kRF + cRH] = fmaxf(h + BRH[cRH], 0.0f);
       if (pVP == 0) HV[r * 2 * kRF + cVP] = fmaxf(u + BVP[cVP], 0.0f);
-#endif
     }
     __syncthreads();
     LZM_STAMP(5);
@@ -2052,12 +1894,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // fc_dynamics[0] for the next simulation: wave 0 now, alone on the texture path (16 loads
     // issue in a few hundred cycles), waves 1-3 during the next walk, which only wave 0 runs
     LZM_SUBSTAMP(29);
-    if (wid == 0) {
-      if (LZM_RES_W0SPLIT)
-        res_fetch<kRSlotsD, 0, 4>(res_blk4(n, kRbD), P);
-      else
-        res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
-    }
+    if (wid == 0) res_fetch<kRSlotsD>(res_blk4(n, kRbD), P);
     LZM_SUBSTAMP(30);
     // ---- expand + backup (cbatch_backpropagate, cnode.cpp:480-500): wave 0 files the leaf's own
     // record and backs up; wave 1 meanwhile initialises the leaf's children (disjoint nodes; the
@@ -2070,11 +1907,9 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int l = 0; l < len; ++l) vtp = (vtp == 1) ? 2 : 1;
       LZM_SUBSTAMP(31);
       expand_wave(t, 0, leaf, vtp, k + 1, rdec, LG + row * kRMaxA, -1, s_exptab, 1);
-      if (LZM_RES_W0SPLIT) res_fetch<kRSlotsD, 4, 8>(res_blk4(n, kRbD), P);
       LZM_STAMP(14);
       if (lane == 0) L2N[s_nlat + k] = leaf;  // the leaf now holds latent k + 1 (= s_nlat + k)
       backup_wave(t, 0, 0, 1, &s_mm, vtp, vdec, p.disc);
-      if (LZM_RES_W0SPLIT) res_fetch<kRSlotsD, 8, 12>(res_blk4(n, kRbD), P);
     } else if (wid == 1) {
       expand_wave(t, 0, 0, 0, k + 1, 0.0f, LG + row * kRMaxA, -1, s_exptab, 2);
     }
