@@ -1,4 +1,4 @@
-# Final build of round 4 (after LZM_RES_SEEDW1; the closing set in the parent directory is the build
+# Final build of round 4 (after LZM_RES_SEEDW1 and the removal of the off-by-default experiment paths; the closing set in the parent directory is the build
 # before it — conv kernels unchanged since). Two gpurun calls:
 #   gpu_tests.log, smoke.log, kernel_stats.csv <- bash tools/gpu_final_a.sh r04b (236 passed; smoke
 #       bit-exact; rocprofv3 --kernel-trace --stats of bench.py --steps 20 --warmup 3 --no-cpu-baseline;
@@ -10,3 +10,5 @@ python bench.py --no-cpu-baseline --secondary none --zero-heads
 python bench.py --no-cpu-baseline --secondary none --rng philox
 python bench.py --step collect --secondary none --no-cpu-baseline
 python tools/phase_timing.py; python tools/phase_timing.py --zero-heads
+# gpu_tests.log, smoke.log, bench_nobaseline.json re-run on the final code (after the cleanup):
+#   bash tools/gpu.sh gpurun_out/f_r04d alltests smoke bench:--no-cpu-baseline,--secondary,none  (236 passed)
