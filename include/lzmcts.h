@@ -262,6 +262,13 @@ int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_by
                       const int32_t *rec_visits, const float *rec_value, const float *rec_pred, void *out_frames,
                       float *out_scalars, int64_t *out_index, void *stream);
 
+/* The BatchNorm-folded conv representation network's epilogue in one pass (conv_infer.FoldedConvInitial,
+ * replacing torch's bias broadcast add, residual add and ReLU passes after each MIOpen convolution,
+ * lzero/model/common.py:164-265): y[n][c][p] = max((y[n][c][p] + bias[c]) + z[n][c][p], 0) in place,
+ * z nullable (no residual), relu 0 keeps the sum. y, z contiguous [N][C][HW], HW % 4 == 0, 16-B
+ * aligned. The same float additions in the same order as the torch passes (the same bits). */
+int lzm_bias_add_relu(float *y, const float *bias, const float *z, int N, int C, int HW, int relu, void *stream);
+
 /* ---- batched AlphaZero for TicTacToe (replaces MCTS.get_next_action,
  * lzero/mcts/ctree/ctree_alphazero/mcts_alphazero.cpp:131-207, called per env from
  * lzero/policy/alphazero.py:266 and :327). B boards are searched together on the device; the caller

@@ -512,17 +512,30 @@ class FoldedConvInitial:
         return FoldedConvInitial._fused_ok
 
     @staticmethod
-    def _conv_relu(x, w, b, stride, fused):
+    def _epilogue(y, b, z=None, relu=True):
+        """y = relu((y + b) + z) in place: on the GPU one HIP pass (lzm_bias_add_relu) instead of
+        torch's bias, residual and ReLU passes (the same float additions, the same bits)"""
+        if y.is_cuda:
+            _lib.call("lzm_bias_add_relu", _lib.ptr(y), _lib.ptr(b), None if z is None else _lib.ptr(z),
+                      y.shape[0], y.shape[1], y.shape[2] * y.shape[3], 1 if relu else 0, _lib.stream_ptr())
+            return y
+        y = y + b.reshape(1, -1, 1, 1)
+        if z is not None:
+            y = y.add_(z)
+        return y.relu_() if relu else y
+
+    @classmethod
+    def _conv_relu(cls, x, w, b, stride, fused):
         if fused:
             return torch.miopen_convolution_relu(x, w, b, [stride, stride], [1, 1], [1, 1], 1)
-        return F.conv2d(x, w, b, stride=stride, padding=1).relu_()
+        return cls._epilogue(F.conv2d(x, w, None, stride=stride, padding=1).contiguous(), b)
 
-    @staticmethod
-    def _conv_add_relu(x, w, z, b, fused):
+    @classmethod
+    def _conv_add_relu(cls, x, w, z, b, fused):
         """relu(conv3x3(x, w) + b + z)"""
         if fused:
             return torch.miopen_convolution_add_relu(x, w, z, 1.0, b, [1, 1], [1, 1], [1, 1], 1)
-        return F.conv2d(x, w, b, padding=1).add_(z).relu_()
+        return cls._epilogue(F.conv2d(x, w, None, padding=1).contiguous(), b, z.contiguous())
 
     @classmethod
     def _basic(cls, x, w1, b1, w2, b2, fused=False):
@@ -555,7 +568,7 @@ class FoldedConvInitial:
         while f"pres{i}_w1" in t:
             p = self._basic(p, t[f"pres{i}_w1"], t[f"pres{i}_b1"], t[f"pres{i}_w2"], t[f"pres{i}_b2"], fused=fused)
             i += 1
-        h = F.conv2d(p, t["head_w"], t["head_b"]).relu_().reshape(B, -1)
+        h = self._epilogue(F.conv2d(p, t["head_w"], None).contiguous(), t["head_b"]).reshape(B, -1)
         hid = F.linear(h, t["ph_w1"], t["ph_b1"]).relu_()
         nv = t["v_w2"].shape[1]
         value = F.linear(hid[:, :nv], t["v_w2"], t["v_b2"])

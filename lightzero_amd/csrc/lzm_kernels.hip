@@ -2002,6 +2002,39 @@ int lzm_episodes_scan(int n, int E, const int32_t *ep_count, const int32_t *cons
   return LZM_OK;
 }
 
+// the conv representation network's per-convolution epilogue (include/lzmcts.h lzm_bias_add_relu):
+// one float4 per thread, HBM-bound (one read of y (and z), one write)
+__global__ __launch_bounds__(256) void bias_add_relu_kernel(float4 *__restrict__ y, const float *__restrict__ bias,
+                                                            const float4 *__restrict__ z, int C, int HW4, long long n4,
+                                                            int relu) {
+  const long long q = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= n4) return;
+  const float b = bias[(int)((q / HW4) % C)];
+  float4 v = y[q];
+  v.x += b; v.y += b; v.z += b; v.w += b;
+  if (z) {
+    const float4 r = z[q];
+    v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+  }
+  if (relu) {
+    v.x = fmaxf(v.x, 0.0f); v.y = fmaxf(v.y, 0.0f); v.z = fmaxf(v.z, 0.0f); v.w = fmaxf(v.w, 0.0f);
+  }
+  y[q] = v;
+}
+
+int lzm_bias_add_relu(float *y, const float *bias, const float *z, int N, int C, int HW, int relu, void *stream) {
+  if (!y || !bias || N <= 0 || C <= 0 || HW <= 0 || HW % 4 || ((uintptr_t)y & 15) || ((uintptr_t)z & 15)) {
+    set_err("lzm_bias_add_relu: bad arguments (HW % 4 == 0, 16-B aligned rows)");
+    return LZM_ERR_ARG;
+  }
+  const long long n4 = (long long)N * C * (HW / 4);
+  hipLaunchKernelGGL(bias_add_relu_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     reinterpret_cast<float4 *>(y), bias, reinterpret_cast<const float4 *>(z), C, HW / 4, n4,
+                     relu ? 1 : 0);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
 int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_bytes, const int32_t *ep_count,
                       const int32_t *ep_len, int32_t *consumed, const int32_t *env_ep_off, const int64_t *env_row_off,
                       const void *rec_frames, const int32_t *rec_action, const float *rec_reward,
