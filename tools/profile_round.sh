@@ -11,7 +11,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o fused --outp
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $out/pmc_$i -o pmc --output-format csv -- \
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $set -d $out/pmc_$i -o pmc --output-format csv -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > $out/pmc_$i.log 2>&1
 done
 timeout -k 10 300 python3 bench.py > $out/bench.json 2>&1
