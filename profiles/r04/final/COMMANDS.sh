@@ -12,3 +12,7 @@ python bench.py --step collect --secondary none --no-cpu-baseline
 python tools/phase_timing.py; python tools/phase_timing.py --zero-heads
 # gpu_tests.log, smoke.log, bench_nobaseline.json re-run on the final code (after the cleanup):
 #   bash tools/gpu.sh gpurun_out/f_r04d alltests smoke bench:--no-cpu-baseline,--secondary,none  (236 passed)
+# Closing set on the final code (after the fused representation-network epilogue):
+#   bash tools/gpu_final_a.sh r04e -> gpu_tests.log (236 passed), smoke.log, kernel_stats.csv, pmc.json
+#   (three --pmc passes, tools/pmc_latest.py), bench.json (bench.py defaults: CPU baseline, config 5 object),
+#   divergence_*.json
