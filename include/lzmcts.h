@@ -348,6 +348,15 @@ int lzm_conv_trunk_prepare_p(int precision, int n_dres, int n_pres, int r_ch, in
 int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
                      const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
                      float *out_latent, float *out_r, float *out_h, void *stream);
+/* The conv representation network's 8 x 8 tail on the same split-bf16 trunk kernel (no dynamics conv,
+ * no reward 1x1): in [B][64][8][8] (the DownSample's output after its last average pool) through
+ * n_blocks residual blocks -> out_latent [B][64 * 64] (the initial latent), then n_pres prediction
+ * blocks and the head 1x1 (+ ReLU) -> out_h [B][h_ch * 64]. Replaces those layers of
+ * conv_infer.FoldedConvInitial (lzero/model/common.py:369-465 representation blocks, :568-640
+ * prediction trunk). Weights: lzm_conv_trunk_prepare_p(LZM_CONV_BF16X3, n_blocks, n_pres, 1, h_ch, raw)
+ * with a zero dynamics conv and a zero 1-channel reward 1x1 in raw. */
+int lzm_conv_resnet8_p(int B, int n_blocks, int n_pres, int h_ch, const float *weights, const float *in,
+                       float *out_latent, float *out_h, void *stream);
 /* lzm_conv_trunk_p writing the EfficientZero LSTM input row directly (mcts_ctree.py:776-790 +
  * efficientzero_model.py:551-556: nn.LSTM over [reward planes | leaf hidden state]): row b of xin
  * (xin_stride floats, >= r_ch*64 + H) gets the reward planes at [0, r_ch*64) and, when hpool

@@ -96,6 +96,7 @@ SIGNATURES = {
                                _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
     "lzm_episodes_scan": [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_bias_add_relu": [_vp, _vp, _vp, _i, _i, _i, _i, _vp],
+    "lzm_conv_resnet8_p": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "lzm_episodes_pack": [_i, _i, _i, _i, _i, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp, _vp],
     "lzm_az_workspace_bytes": [_i, _i, ctypes.POINTER(_i64)],

@@ -461,6 +461,7 @@ class FoldedConvInitial:
         self._ver = None
         self.ops = None
         self.t = None
+        self.native = None  # lzm_conv_resnet8_p weights of the 8 x 8 tail (GPU, 64 x 8 x 8 latents)
         self.refresh()
 
     def _version(self):
@@ -483,7 +484,55 @@ class FoldedConvInitial:
                             a.copy_(b)
                 for k, v in t.items():
                     self.t[k].copy_(v)
+            self._pack_native()
         self._ver = ver
+
+    def _tail_start(self):
+        """index of the first op after the representation's last average pool when every op from there
+        on is a 64-channel residual block at 8 x 8 (the split-bf16 trunk's shape), else None"""
+        pools = [i for i, op in enumerate(self.ops) if op[0] == "avgpool"]
+        if not pools or tuple(self.model.latent_hw) != (8, 8):
+            return None
+        i0 = pools[-1] + 1
+        tail = self.ops[i0:]
+        if not tail or any(op[0] != "basic" or tuple(op[1].shape) != (64, 64, 3, 3) or tuple(op[3].shape) != (64, 64, 3, 3)
+                           for op in tail):
+            return None
+        return i0
+
+    def _pack_native(self):
+        """the 8 x 8 tail (representation blocks, prediction blocks, head 1x1) as one lzm_conv_resnet8_p
+        launch on the split-bf16 trunk kernel (LZM_CONV_INIT_NATIVE=0: the MIOpen convolutions)"""
+        t = self.t
+        dev = t["head_w"].device
+        i0 = self._tail_start()
+        n_pres = 0
+        while f"pres{n_pres}_w1" in t:
+            n_pres += 1
+        h_ch = int(t["head_w"].shape[0])
+        if dev.type != "cuda" or i0 is None or h_ch > 32 or os.environ.get("LZM_CONV_INIT_NATIVE", "1") == "0" \
+                or len(self.ops) - i0 > 8 or n_pres > 8:
+            return
+        z = torch.zeros(64 * 64 * 9 + 64 + 1, dtype=torch.float32, device=dev)
+        parts = [z[:64 * 64 * 9]]
+        for op in self.ops[i0:]:
+            parts += [op[1], op[2], op[3], op[4]]
+        parts += [z[64 * 64 * 9:]]  # a zero 1-channel reward 1x1 (weights, bias): not run
+        for i in range(n_pres):
+            parts += [t[f"pres{i}_w1"], t[f"pres{i}_b1"], t[f"pres{i}_w2"], t[f"pres{i}_b2"]]
+        parts += [t["head_w"], t["head_b"]]
+        raw = np.ascontiguousarray(torch.cat([q.reshape(-1).float() for q in parts]).cpu().numpy(), dtype=np.float32)
+        L = _lib.load()
+        nb = len(self.ops) - i0
+        host = np.zeros(L.lzm_conv_trunk_floats_p(nb, n_pres, 1), np.float32)
+        _lib.check(L.lzm_conv_trunk_prepare_p(1, nb, n_pres, 1, h_ch, raw.ctypes.data, host.ctypes.data),
+                   "lzm_conv_trunk_prepare_p")
+        blob = torch.from_numpy(host).to(dev)
+        if self.native is None:
+            self.native = blob
+        else:
+            self.native.copy_(blob)  # in place: captured graphs keep reading it
+        self.tail = (i0, nb, n_pres, h_ch)
 
     # MIOpen's fused convolution + bias (+ residual) + ReLU (torch.miopen_convolution_relu /
     # _add_relu): one launch per convolution instead of a convolution, a bias add / residual add and
@@ -549,7 +598,8 @@ class FoldedConvInitial:
         if not x.is_contiguous():
             x = x.contiguous()
         fused = self._fused(x)
-        for op in self.ops:
+        native = self.native is not None and x.is_cuda
+        for op in (self.ops[:self.tail[0]] if native else self.ops):
             kind = op[0]
             if kind == "conv_relu":
                 x = self._conv_relu(x, op[1], op[2], op[3], fused)
@@ -561,14 +611,23 @@ class FoldedConvInitial:
                 x = self._conv_add_relu(y, w2, F.conv2d(x, w3, None, stride=2, padding=1), b2, fused)
             else:  # avgpool (count_include_pad, as nn.AvgPool2d(3, 2, 1))
                 x = F.avg_pool2d(x, kernel_size=3, stride=2, padding=1)
-        latent = x
-        B = latent.shape[0]
-        p = latent
-        i = 0
-        while f"pres{i}_w1" in t:
-            p = self._basic(p, t[f"pres{i}_w1"], t[f"pres{i}_b1"], t[f"pres{i}_w2"], t[f"pres{i}_b2"], fused=fused)
-            i += 1
-        h = self._epilogue(F.conv2d(p, t["head_w"], None).contiguous(), t["head_b"]).reshape(B, -1)
+        B = x.shape[0]
+        if native:
+            # the 8 x 8 tail in one launch: representation blocks -> latent, prediction blocks, head 1x1
+            _, nb, n_pres, h_ch = self.tail
+            x = x.contiguous()
+            latent = torch.empty_like(x)
+            h = torch.empty((B, h_ch * 64), dtype=torch.float32, device=x.device)
+            _lib.call("lzm_conv_resnet8_p", B, nb, n_pres, h_ch, _lib.ptr(self.native), _lib.ptr(x),
+                      _lib.ptr(latent), _lib.ptr(h), _lib.stream_ptr())
+        else:
+            latent = x
+            p = latent
+            i = 0
+            while f"pres{i}_w1" in t:
+                p = self._basic(p, t[f"pres{i}_w1"], t[f"pres{i}_b1"], t[f"pres{i}_w2"], t[f"pres{i}_b2"], fused=fused)
+                i += 1
+            h = self._epilogue(F.conv2d(p, t["head_w"], None).contiguous(), t["head_b"]).reshape(B, -1)
         hid = F.linear(h, t["ph_w1"], t["ph_b1"]).relu_()
         nv = t["v_w2"].shape[1]
         value = F.linear(hid[:, :nv], t["v_w2"], t["v_b2"])

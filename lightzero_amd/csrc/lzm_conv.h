@@ -69,6 +69,8 @@ struct ConvTrunkArgs {
   int r_stride;          // floats per out_r row (r_ch * 64, or the EfficientZero LSTM input row)
   const float *hpool;    // nullable: EfficientZero LSTM hidden-state pool [.][B][H]; row x[b] of env b
   int H;                 // is copied to out_r[b][r_ch * 64 ..] (the [r | h] LSTM input row, no gather launch)
+  int skip_dyn;          // 1: no dynamics conv — the input runs straight into the residual blocks, and no
+                         // reward 1x1 (lzm_conv_resnet8_p: the representation network's 8 x 8 tail)
 };
 
 // [r | h] LSTM input row: the leaf's hidden state after the reward planes (every thread calls it)
@@ -502,8 +504,9 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const int n3 = 1 + 2 * a.n_dres + 2 * a.n_pres;
   auto layer_w = [&](int i) { return a.w + bx_layer_off(L, a.n_dres, i); };
   auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * 3 * 64; };
+  const int i0 = a.skip_dyn ? 1 : 0;  // the first layer run (skip_dyn: the first residual block's)
   BxRing<AHEAD> ring;
-  bx_prefetch<18, AHEAD, DIAG>(ring, wave_stream(a.w + L.dyn), lane);
+  bx_prefetch<18, AHEAD, DIAG>(ring, wave_stream(layer_w(i0)), lane);
   // the input latent: this lane's 16 values in registers (the dynamics residual, exact f32) ...
   const float *src = a.pool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
   float xres[16];
@@ -520,7 +523,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 #pragma unroll
     for (int t = 0; t < 4; ++t) in4[t] = bxf4{xres[4 * t], xres[4 * t + 1], xres[4 * t + 2], xres[4 * t + 3]};
     const float4 no_am[4] = {};
-    bx_epilogue3<0, 4, false>(in4, buf(0), 0.f, false, no_am, xres, false, false, lane, c);
+    bx_epilogue3<0, 4, false>(in4, buf(i0 & 1), 0.f, false, no_am, xres, false, false, lane, c);
   }
   for (int k = tid; k < 2 * 3 * 36 * 8; k += kCvThreads) {  // [buffer][term][border position][16-B chunk]
     const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
@@ -528,7 +531,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     bx_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
   }
   __syncthreads();
-  for (int i = 0; i < n3; ++i) {
+  for (int i = i0; i < n3; ++i) {
     const float *w = layer_w(i);
     const bool second = i > 0 && ((i - 1) & 1);  // a block's second conv: + residual, new block input
     // epilogue operands first (vmcnt counts in order: they must not queue behind the next prefetch)
@@ -549,7 +552,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         *reinterpret_cast<float4 *>(dst + 16 * t) = float4{xres[4 * t], xres[4 * t + 1], xres[4 * t + 2], xres[4 * t + 3]};
-      if (wv < 2)
+      if (!a.skip_dyn && wv < 2)
         bx_conv1_layer<DIAG>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_stride,
                              lane, wv);
     }

@@ -2463,7 +2463,7 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
   ConvTrunkArgs a;
   a.B = B; a.n_dres = n_dres; a.n_pres = n_pres; a.r_ch = r_ch; a.h_ch = h_ch; a.w = weights; a.actmap = actmap;
   a.pool = pool; a.x = x; a.action = action; a.out_latent = out_latent; a.out_r = out_r; a.out_h = out_h;
-  a.r_stride = xin_stride; a.hpool = hpool; a.H = hpool ? H : 0;
+  a.r_stride = xin_stride; a.hpool = hpool; a.H = hpool ? H : 0; a.skip_dyn = 0;
   if (bx && cwaves == 8 && diag == 0 && ahead == kBxAhead)
     hipLaunchKernelGGL(conv_trunk_bx2_kernel<kBxAhead>, dim3(B), dim3(kBx2Threads), lds_bx2, (hipStream_t)stream, a);
   else if (bx)
@@ -2479,6 +2479,27 @@ int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int
                      float *out_r, float *out_h, void *stream) {
   return lzm_conv_trunk_xin_p(precision, B, n_dres, n_pres, r_ch, h_ch, weights, actmap, pool, x, action, out_latent,
                               out_r, r_ch * 64, nullptr, 0, out_h, stream);
+}
+
+int lzm_conv_resnet8_p(int B, int n_blocks, int n_pres, int h_ch, const float *weights, const float *in,
+                       float *out_latent, float *out_h, void *stream) {
+  if (B <= 0 || n_blocks < 1 || lzm_conv_trunk_floats_p(n_blocks, n_pres, LZM_CONV_BF16X3) < 0 || h_ch < 1 ||
+      h_ch > 32 || !weights || !in || !out_latent || !out_h || (((uintptr_t)weights | (uintptr_t)in) & 15)) {
+    set_err("lzm_conv_resnet8_p: bad arguments (1..8 blocks, 1..32 head channels, 16-byte aligned weights / input)");
+    return LZM_ERR_ARG;
+  }
+  static hipError_t attr_err = hipFuncSetAttribute((const void *)conv_trunk_bx_kernel<kBxAhead, 0>,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   (int)(2 * kBxBuf * sizeof(uint16_t)));
+  LZM_HIP(attr_err);
+  ConvTrunkArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = B; a.n_dres = n_blocks; a.n_pres = n_pres; a.r_ch = 0; a.h_ch = h_ch; a.w = weights;
+  a.pool = in; a.out_latent = out_latent; a.out_h = out_h; a.skip_dyn = 1;
+  hipLaunchKernelGGL((conv_trunk_bx_kernel<kBxAhead, 0>), dim3(B), dim3(kCvThreads), 2 * kBxBuf * sizeof(uint16_t),
+                     (hipStream_t)stream, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
 }
 
 int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,

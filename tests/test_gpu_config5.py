@@ -155,7 +155,8 @@ def test_breakout_graph_step_equals_eager():
 
 def test_folded_initial_inference_matches_module_on_gpu():
     """the BN-folded representation + prediction (conv_infer.FoldedConvInitial) vs the module, f32
-    tolerance, on the GPU (MIOpen convolutions) for both conv families"""
+    tolerance, on the GPU (MIOpen convolutions with the lzm_bias_add_relu epilogue, the 8 x 8 tail on
+    the split-bf16 trunk, lzm_conv_resnet8_p) for both conv families"""
     from lightzero_amd.conv_infer import FoldedConvInitial
     from lightzero_amd.model_conv import atari_efficientzero_model
     torch.manual_seed(1)
