@@ -16,3 +16,8 @@ python tools/phase_timing.py; python tools/phase_timing.py --zero-heads
 #   bash tools/gpu_final_a.sh r04e -> gpu_tests.log (236 passed), smoke.log, kernel_stats.csv, pmc.json
 #   (three --pmc passes, tools/pmc_latest.py), bench.json (bench.py defaults: CPU baseline, config 5 object),
 #   divergence_*.json
+# Closing set on the final code (after the native 8x8 representation tail), two steps in one call:
+#   bash tools/gpu_final_a.sh r04f -> gpu_tests.log (236 passed), smoke.log, kernel_stats.csv, pmc.json, bench.json
+#   bash tools/gpu.sh gpurun_out/f_r04f bench:--workload,breakout,--no-cpu-baseline
+#        bench:--workload,breakout,--no-cpu-baseline,--step,collect -> bench_breakout_search_step.json,
+#        bench_breakout_collect_step.json
