@@ -119,3 +119,22 @@ def test_lstm_gate_fragments_recover_f32_weights():
     unit = 16 * nb_ + 4 * w_ + (n >> 2)
     want = W.astype(np.float64)[(n & 3) * H + unit, 32 * j_ + 8 * (l_ >> 4) + e_]
     np.testing.assert_allclose(rec, want, rtol=2.0 ** -23, atol=0)
+
+
+def test_representation_entry_points_validate_arguments_on_the_host():
+    """lzm_bias_add_relu / lzm_conv_resnet8_p (conv_infer.FoldedConvInitial's kernels) refuse bad
+    shapes and alignments before any HIP call (status LZM_ERR_ARG, no launch, no GPU needed)"""
+    import ctypes
+    L = _lib.load()
+    err = -1  # LZM_ERR_ARG
+    buf = ctypes.create_string_buffer(64 + 16)
+    base = ctypes.addressof(buf)
+    p16 = ctypes.c_void_p((base + 15) & ~15)  # 16-B aligned
+    p4 = ctypes.c_void_p(((base + 15) & ~15) + 4)  # misaligned
+    assert L.lzm_bias_add_relu(None, p16, None, 1, 1, 4, 1, None) == err
+    assert L.lzm_bias_add_relu(p16, p16, None, 1, 1, 6, 1, None) == err  # HW % 4
+    assert L.lzm_bias_add_relu(p4, p16, None, 1, 1, 4, 1, None) == err  # alignment
+    assert L.lzm_conv_resnet8_p(1, 0, 1, 16, p16, p16, p16, p16, None) == err  # no residual block
+    assert L.lzm_conv_resnet8_p(1, 9, 1, 16, p16, p16, p16, p16, None) == err  # more than 8
+    assert L.lzm_conv_resnet8_p(1, 2, 1, 33, p16, p16, p16, p16, None) == err  # head channels
+    assert L.lzm_conv_resnet8_p(1, 2, 1, 16, p16, p4, p16, p16, None) == err  # input alignment
