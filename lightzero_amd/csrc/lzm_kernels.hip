@@ -316,28 +316,24 @@ __device__ inline float wave_support_expectation_reg(const float *row, int V, bo
 #pragma unroll
     for (int q = 0; q < NPL; ++q)
       if (lane + 64 * q < V) acc += x[q] * ((float)(lane + 64 * q) - half);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+    acc = xor_sum(acc);
     return acc;
   }
   float mx = -INFINITY;
 #pragma unroll
   for (int q = 0; q < NPL; ++q)
     if (lane + 64 * q < V) mx = fmaxf(mx, x[q]);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+  mx = xor_max(mx);
   float sum = 0.0f;
 #pragma unroll
   for (int q = 0; q < NPL; ++q)
     if (lane + 64 * q < V) sum += expf(x[q] - mx);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  sum = xor_sum(sum);
   float acc = 0.0f;
 #pragma unroll
   for (int q = 0; q < NPL; ++q)
     if (lane + 64 * q < V) acc += (expf(x[q] - mx) / sum) * ((float)(lane + 64 * q) - half);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  acc = xor_sum(acc);
   return acc;
 }
 
@@ -356,22 +352,18 @@ __device__ inline float wave_support_expectation_loop(const float *row, int V, b
   if (!softmax) {
     float acc = 0.0f;
     for (int j = lane; j < V; j += 64) acc += row[j] * ((float)j - half);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+    acc = xor_sum(acc);
     return acc;
   }
   float mx = -INFINITY;
   for (int j = lane; j < V; j += 64) mx = fmaxf(mx, row[j]);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+  mx = xor_max(mx);
   float sum = 0.0f;
   for (int j = lane; j < V; j += 64) sum += expf(row[j] - mx);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  sum = xor_sum(sum);
   float acc = 0.0f;
   for (int j = lane; j < V; j += 64) acc += (expf(row[j] - mx) / sum) * ((float)j - half);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  acc = xor_sum(acc);
   return acc;
 }
 
@@ -387,13 +379,11 @@ __device__ inline float wave_row_sum(const float *row, int V) {
 #pragma unroll
     for (int q = 0; q < 10; ++q)
       if (lane + 64 * q < V) s += x[q];
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+    s = xor_sum(s);
     return s;
   }
   for (int j = lane; j < V; j += 64) s += row[j];
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) s += __shfl_xor(s, d, 64);
+  s = xor_sum(s);
   return s;
 }
 

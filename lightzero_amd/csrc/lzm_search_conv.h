@@ -124,9 +124,7 @@ __device__ __forceinline__ int sc_lookback_finish(const ConvSearchArgs &p, int k
     }
     base += (int)(v[u] & 0xffffffffu);
   }
-#pragma unroll
-  for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
-  return base;
+  return xor_sum(base);
 }
 
 __device__ __forceinline__ int sc_lookback(const ConvSearchArgs &p, int k, int b, unsigned long long epoch, int lane) {
@@ -162,11 +160,7 @@ __device__ __forceinline__ float sc_decode_row(const float *row, int V, float *r
       rs += x[q];
       mx = fmaxf(mx, x[q]);
     }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) {
-    rs += __shfl_xor(rs, d, 64);
-    mx = fmaxf(mx, __shfl_xor(mx, d, 64));
-  }
+  xor_sum_max(rs, mx);
   *raw_sum = rs;
   float e[NPL], sum = 0.0f;
 #pragma unroll
@@ -174,15 +168,12 @@ __device__ __forceinline__ float sc_decode_row(const float *row, int V, float *r
     e[q] = lane + 64 * q < V ? expf(x[q] - mx) : 0.0f;
     if (lane + 64 * q < V) sum += e[q];
   }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  sum = xor_sum(sum);
   float acc = 0.0f;
 #pragma unroll
   for (int q = 0; q < NPL; ++q)
     if (lane + 64 * q < V) acc += (e[q] / sum) * ((float)(lane + 64 * q) - half);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
-  return acc;
+  return xor_sum(acc);
 }
 
 // Output columns [jlo, jhi) of the three head layers (w2q [8][N2][4]: float4 k4 of column j at
@@ -444,8 +435,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   if (tid < 64) {  // players (cnode.cpp:776-781), every load in flight at once
     int m = INT_MIN;
     for (int q = tid; q < B; q += 64) m = max(m, p.vtp_in[q]);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+    m = xor_max(m);
     if (tid == 0) s_players = (m == -1) ? 1 : 2;
   }
   __syncthreads();
@@ -788,8 +778,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   if (tid < 64) {  // players (cnode.cpp:776-781), every load in flight at once
     int m = INT_MIN;
     for (int q = tid; q < B; q += 64) m = max(m, p.vtp_in[q]);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+    m = xor_max(m);
     if (tid == 0) s_players = (m == -1) ? 1 : 2;
   }
   __syncthreads();

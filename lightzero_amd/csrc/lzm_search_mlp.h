@@ -511,16 +511,13 @@ __device__ inline float wave_expect_lds(const float *row, int V) {
   const float half = (float)((V - 1) / 2);
   float mx = -INFINITY;
   for (int j = lane; j < V; j += 64) mx = fmaxf(mx, row[j]);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) mx = fmaxf(mx, __shfl_xor(mx, d, 64));
+  mx = xor_max(mx);
   float sum = 0.0f;
   for (int j = lane; j < V; j += 64) sum += expf(row[j] - mx);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  sum = xor_sum(sum);
   float acc = 0.0f;
   for (int j = lane; j < V; j += 64) acc += (expf(row[j] - mx) / sum) * ((float)j - half);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  acc = xor_sum(acc);
   return acc;
 }
 
@@ -702,8 +699,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
     // players (cnode.cpp:776-781) by wave 0, every load in flight at once
     int m = INT_MIN;
     for (int q = tid; q < B; q += 64) m = max(m, p.vtp_in[q]);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+    m = xor_max(m);
     if (tid == 0) s_players = (m == -1) ? 1 : 2;
   }
   __syncthreads();
@@ -790,8 +786,7 @@ __global__ __launch_bounds__(kThreads) void search_mlp_kernel(SearchArgs p) {
           }
           sum += (int)(v & 0xffffffffu);
         }
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+        sum = xor_sum(sum);
         if (tid == 0) s_base = sum;
       }
       __syncthreads();

@@ -1174,8 +1174,7 @@ __device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, uns
     }
     sum += (int)(v & 0xffffffffu);
   }
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  sum = xor_sum(sum);
   if (lane == 0) part[threadIdx.x >> 6] = sum;
   __syncthreads();
   return (part[0] + part[1]) + (part[2] + part[3]);
@@ -1338,8 +1337,7 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // loads in flight (a serial loop over B was ~30 K cycles of the launch)
     int m = INT_MIN;
     for (int q = lane; q < B; q += 64) m = max(m, p.vtp_in[q]);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+    m = xor_max(m);
     if (lane == 0) s_players = (m == -1) ? 1 : 2;
   }
   uint32_t *s_seeds = reinterpret_cast<uint32_t *>(smem + L.misc);

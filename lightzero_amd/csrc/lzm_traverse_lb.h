@@ -60,8 +60,7 @@ __device__ inline unsigned long long traverse_lb_setup(const TraverseLbArgs &p, 
   const int ep = tid == 0 ? (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
   int m = INT_MIN;
   for (int q = tid; q < p.t.B; q += blockDim.x) m = max(m, p.vtp_in[q]);
-#pragma unroll
-  for (int d = 32; d > 0; d >>= 1) m = max(m, __shfl_xor(m, d, 64));
+  m = xor_max(m);
   if (lane == 0) s_wmax[tid >> 6] = m;
   if (tid < 31) s_pow[tid] = pw;
   if (tid == 0) *s_epoch = ep;
@@ -109,8 +108,7 @@ __device__ inline void traverse_lb_root(const TraverseLbArgs &p, int i, const ui
       }
       base += (int)(v & 0xffffffffu);
     }
-#pragma unroll
-    for (int s = 32; s > 0; s >>= 1) base += __shfl_xor(base, s, 64);
+    base = xor_sum(base);
     const uint32_t *coef = p.coef;
     const int npos = p.coef_positions;
     int32_t *diag = p.err + 1;

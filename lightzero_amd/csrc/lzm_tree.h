@@ -222,6 +222,77 @@ __device__ __forceinline__ float dpp_f(float v) {
 __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
+
+// The value of lane (lane ^ D) for a wave-wide xor butterfly step, without the LDS crossbar
+// (__shfl_xor is a ds_bpermute: a dependent LDS round trip per step): D = 1, 2 quad_perm DPP; 4 two
+// row shifts (row_shl:4 reads lane + 4, row_shr:4 lane - 4); 8 row_ror:8; 16, 32 the gfx950
+// permlane swaps (with both operands v, each lane holds itself and its partner). The same pairs as
+// __shfl_xor(v, D, 64), so a butterfly reduction built on it gives the same bits (measured: the
+// Breakout / Pong one-launch searches +1% / +3% from their decodes).
+template <int D>
+__device__ __forceinline__ int xor_partner(int v) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (D == 1) {
+    return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);
+  } else if constexpr (D == 2) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);
+  } else if constexpr (D == 4) {
+    const int up = __builtin_amdgcn_update_dpp(0, v, 0x104, 0xF, 0xF, false);
+    const int dn = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+    return (lane & 4) ? dn : up;
+  } else if constexpr (D == 8) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);
+  } else if constexpr (D == 16) {
+    const auto pr = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((lane & 16) ? pr[0] : pr[1]);
+  } else {
+    static_assert(D == 32, "xor step");
+    const auto pr = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((lane & 32) ? pr[0] : pr[1]);
+  }
+}
+template <int D>
+__device__ __forceinline__ float xor_partner(float v) {
+  return __int_as_float(xor_partner<D>(__float_as_int(v)));
+}
+// sum / max over the wave in __shfl_xor butterfly order d = 32, 16, .., 1 (same bits); every lane
+// of the wave must be active
+template <typename T>
+__device__ __forceinline__ T xor_sum(T v) {
+  v += xor_partner<32>(v);
+  v += xor_partner<16>(v);
+  v += xor_partner<8>(v);
+  v += xor_partner<4>(v);
+  v += xor_partner<2>(v);
+  v += xor_partner<1>(v);
+  return v;
+}
+__device__ __forceinline__ float xor_max(float v) {
+  v = fmaxf(v, xor_partner<32>(v));
+  v = fmaxf(v, xor_partner<16>(v));
+  v = fmaxf(v, xor_partner<8>(v));
+  v = fmaxf(v, xor_partner<4>(v));
+  v = fmaxf(v, xor_partner<2>(v));
+  v = fmaxf(v, xor_partner<1>(v));
+  return v;
+}
+__device__ __forceinline__ int xor_max(int v) {
+  v = max(v, xor_partner<32>(v));
+  v = max(v, xor_partner<16>(v));
+  v = max(v, xor_partner<8>(v));
+  v = max(v, xor_partner<4>(v));
+  v = max(v, xor_partner<2>(v));
+  v = max(v, xor_partner<1>(v));
+  return v;
+}
+// sum and max together (independent chains interleaved)
+__device__ __forceinline__ void xor_sum_max(float &s, float &m) {
+#define LZM_XOR_STEP(D)                 \
+  s += xor_partner<D>(s);               \
+  m = fmaxf(m, xor_partner<D>(m));
+  LZM_XOR_STEP(32) LZM_XOR_STEP(16) LZM_XOR_STEP(8) LZM_XOR_STEP(4) LZM_XOR_STEP(2) LZM_XOR_STEP(1)
+#undef LZM_XOR_STEP
+}
 // max over the wave (rows of 16 by DPP, then the four row results by readlane)
 __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, dpp_f<0xB1>(v));
