@@ -167,9 +167,7 @@ __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
     __shared__ float s_sum[kHdEnvs][kHdThreads / 64];
 #pragma unroll
     for (int e = 0; e < kHdEnvs; ++e) {
-      float v = rsum[e];
-#pragma unroll
-      for (int d = 32; d > 0; d >>= 1) v += __shfl_xor(v, d, 64);
+      const float v = xor_sum(rsum[e]);
       if ((tid & 63) == 0) s_sum[e][tid >> 6] = v;
     }
     __syncthreads();
