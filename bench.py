@@ -12,7 +12,9 @@ Multi-GPU: one process per GPU. Under torchrun the ranks come from the environme
 fresh interpreters, the parent never touches the GPU). Every rank searches its own 256 envs (envs
 are independent trees: weak scaling, no collective in the data path). value = all ranks' sims /
 the slowest rank's time. `--step collect` runs the device collector per rank and ends the timed
-region with the trajectory return (device pack + RCCL all-gather + statistics sum, trajectory.py).
+region with the trajectory return (device pack + the flat byte buffer gathered to the learner rank
+over RCCL, or all-gathered with --traj all_gather + statistics sum, trajectory.py); with one GPU the
+collectives still run, in a one-rank RCCL group (--rccl-world1).
 `--dry-run` checks the launch on gloo without a GPU.
 
 Extra objects on the JSON line:
@@ -72,6 +74,12 @@ def parse():
     p.add_argument("--secondary", choices=["breakout", "none"], default="breakout",
                    help="after the headline, also time config 5's sharded collect step (Breakout stand-in env, "
                         "search + env + recording + trajectory all-gather) and report it in the line's 'config5'")
+    p.add_argument("--traj", choices=["gather", "all_gather"], default="gather",
+                   help="collect steps' trajectory return: gather = to the learner rank 0 alone (each rank sends its "
+                        "flat byte buffer once, point to point); all_gather = to every rank")
+    p.add_argument("--rccl-world1", type=int, default=1,
+                   help="N = 1: still run under a one-rank RCCL process group, so the collect steps' trajectory "
+                        "return and statistics all-reduce go through RCCL as on the 8-GPU node (0: no group)")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: the ranks join a gloo group and rank 0 prints who joined")
     return p.parse_args()
@@ -212,9 +220,10 @@ class CollectStep:
     """One env step of the device collector for every env: search + select_action + CartPole step +
     GameSegment recording, one HIP graph (muzero_collector.py:399-705 per step)."""
 
-    def __init__(self, B, S, model, device, rng_mode, seed, workload="cartpole"):
+    def __init__(self, B, S, model, device, rng_mode, seed, workload="cartpole", dst=0):
         from lightzero_amd.collector import DeviceCollector
         self.B, self.S = B, S
+        self.dst = dst  # trajectory return: gather to rank dst (None: all-gather)
         env = WORKLOADS[workload][2]
         # CartPole episodes are short (tens of steps): many slots per env; Breakout stand-in episodes
         # last >= ~17 steps, 400-step limit
@@ -231,13 +240,20 @@ class CollectStep:
         self.last = (out["distributions"], out["values"], None)
 
     def finish(self, world):
-        """the episodes finished since the last call: packed on the device (lzm_episodes_*) and, with
-        more than one rank, all-gathered (RCCL over xGMI) with the step / episode / duration sums
-        (trajectory.py) — the TrajBlocks a learner consumes, no host unpacking"""
-        blocks, st = self.col.gather_blocks(to_host=False)
-        return {"episodes_all_ranks": st["episodes"], "rows": st["rows"], "payload_bytes": st["payload_bytes"],
+        """the episodes finished since the last call: packed on the device (lzm_episodes_*) and, under a
+        process group, returned over it (RCCL over xGMI: gathered to the learner rank, or all-gathered)
+        with the step / episode / duration sums (trajectory.py) — the TrajBlocks a learner consumes, no
+        host unpacking"""
+        blocks, st = self.col.gather_blocks(to_host=False, dst=self.dst)
+        c = st["collective"]
+        return {"episodes_received": st["episodes"], "episodes_all_ranks": int(st["total_episodes"]),
+                "rows_received": st["rows"], "payload_bytes_received": st["payload_bytes"],
                 "frame_dtype": str(self.col.rec_frames.dtype).replace("torch.", ""),
-                "total_envstep": st["total_envstep"], "world": world}
+                "total_envstep": st["total_envstep"], "world": world,
+                "backend": c["backend"] if c else None, "mode": c["mode"] if c else None,
+                "collective_ms": round(c["ms"], 3) if c else None,
+                "wire_bytes_sent": c["bytes_sent"] if c else None,
+                "wire_bytes_received": c["bytes_received"] if c else None}
 
     def tree(self):
         return self.col.search.roots.tree
@@ -368,9 +384,9 @@ def shard_seed(rank):
 
 
 def slowest_rank_seconds(elapsed, world, device):
-    """The job's time is the slowest rank's (max-reduce; the only collective: envs are
-    independent trees, nothing crosses ranks in the data path)."""
-    if world == 1:
+    """The job's time is the slowest rank's (max-reduce over the process group when one is initialised;
+    envs are independent trees, nothing crosses ranks in the search's data path)."""
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         return elapsed
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -655,7 +671,8 @@ def make_step(args, workload, model, device, rank):
     if args.path == "fused" and args.step == "graph":
         return GraphStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload=workload)
     if args.path == "fused" and args.step == "collect":
-        return CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload=workload)
+        return CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload=workload,
+                           dst=0 if args.traj == "gather" else None)
     if workload != "cartpole":
         raise SystemExit("bench: --step python / --path generic are CartPole-only")
     return GpuStep(B, S, model, device, args.rng, args.graph, seed=shard_seed(rank), fused=args.path == "fused")
@@ -676,7 +693,7 @@ def timed_run(step, steps, warmup, world, device):
     for _ in range(steps):
         step()
     # collect mode: the trajectory return ends the timed region (pack the episodes finished in
-    # it on the device, all-gather them over RCCL, sum-reduce the collector statistics)
+    # it on the device, return them over RCCL, sum-reduce the collector statistics)
     traj = step.finish(world) if hasattr(step, "finish") else None
     torch.cuda.synchronize()
     if world > 1:
@@ -770,14 +787,15 @@ def workload_name(workload, B, S, world):
 def secondary_breakout(args, world, rank, device):
     """config 5 beside the headline: every rank runs the Breakout collect step on its own 256-env
     shard (BN-folded initial inference, one-launch conv search, the stand-in env's step and recording,
-    one HIP graph), and the timed region ends with the trajectory return (device pack + RCCL
-    all-gather of the u8 frames and scalars + statistics sum). Returns the 'config5' object."""
+    one HIP graph), and the timed region ends with the trajectory return (device pack + the u8 frames and
+    scalars to the learner over RCCL + statistics sum). Returns the 'config5' object."""
     B, S = args.envs, args.sims
     # enough env steps that episodes (tens of steps) finish inside the timed region and the trajectory
     # return moves real image payloads
     steps = max(args.steps, 100)
     model = build_conv_model(device, seed=0)
-    step = CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload="breakout")
+    step = CollectStep(B, S, model, device, args.rng, seed=shard_seed(rank), workload="breakout",
+                       dst=0 if args.traj == "gather" else None)
     el, traj = timed_run(step, steps, args.warmup, world, device)
     tie_errors, sdiag = check_step(step, S, True)
     out = {"workload": workload_name("breakout", B, S, world), "step": "collect", "steps": steps,
@@ -802,9 +820,20 @@ def main():
         print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; reporting n_gpus={world}", file=sys.stderr)
     if args.dry_run:
         return dry_run(world, rank, local)
+    rccl1 = None
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif args.rccl_world1:
+        # one-rank RCCL group (a private in-memory store: no rendezvous), so the collect steps' trajectory
+        # return runs the 8-GPU node's RCCL calls; the headline search has no collective in its timed region
+        torch.cuda.set_device(local)
+        try:
+            dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                                    device_id=torch.device("cuda", local))
+            rccl1 = "nccl"
+        except Exception as e:  # keep the headline: report the failure in the line
+            rccl1 = f"failed: {type(e).__name__}: {e}"[:300]
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     if world > 1:
@@ -847,10 +876,12 @@ def main():
                            "hip_graph": (args.step != "python") if args.path == "fused" else bool(args.graph),
                            "heads": "zero" if args.zero_heads else "random",
                            "parallelism": f"env-sharded x{world}"},
+                "process_group": (dist.get_backend() if dist.is_initialized() else None) if rccl1 is None
+                else {"world1": rccl1},
                 "tie_stream_errors": tie_errors, "search_diag": sdiag, "ranks": ranks,
                 "trajectory": traj, "roofline": roofline, "cpu_baseline": cpu, "config5": config5}
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

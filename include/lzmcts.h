@@ -202,6 +202,14 @@ int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream);
  * prefetch, reduction, store, support decode), 1 barrier. out_host holds 64 counters. */
 int lzm_debug_phase_cycles(lzm_handle *h, uint64_t *out_host, int reset);
 int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*/, int n, void *stream);
+/* Process teardown: synchronises the device and frees the library's process-wide device buffers (the
+ * decode's verdict scratch, debug tables) while the runtime is intact. Destroy live handles first; later
+ * calls re-allocate what they need. lightzero_amd runs it from an atexit hook. */
+int lzm_shutdown(void);
+/* The wave butterflies of the search kernels (DPP / permlane xor_partner, xor_sum, xor_max) beside the
+ * __shfl_xor (ds_bpermute) forms they replace, on one wave of in float[64]; out float[16][64] (rows:
+ * partner D = 1..32, __shfl_xor D = 1..32, xor_sum, shfl sum, xor_max, shfl max). Tests only. */
+int lzm_debug_xor(const float *in, float *out, void *stream);
 
 /* ---- Device collect loop, CartPole-v0 (lzero/worker/muzero_collector.py
  * :399-705, zoo/classic_control/cartpole/envs/cartpole_lightzero_env.py) ----
@@ -216,14 +224,16 @@ int lzm_debug_philox(const uint32_t *ctr_key /*[n][6]*/, uint32_t *out /*[n][4]*
  * store_search_stats does), step the env (gymnasium CartPole equations in float64, truncation at
  * max_steps), auto-reset finished episodes (ep_len[n][E], ep_count[n]) and write the next root's
  * obs and Dirichlet(noise_alpha) noises float[n][A]. `counter` (int64, device) keys this step's
- * Philox streams; the caller advances it. pred_value / rec_pred: both or neither. */
+ * Philox streams; the caller advances it. pred_value / rec_pred: both or neither. ep_return float[n][E]
+ * (nullable): each finished episode's return, the env's eval_episode_return (the reward sum, 1 per step;
+ * muzero_collector.py:596-603 logs it). */
 int lzm_cartpole_reset(int n, double *state, int32_t *steps, float *obs, uint32_t seed, void *stream);
 int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
                               const float *pred_value, double *state, int32_t *steps, float *obs, float *noises,
                               float noise_alpha, float temperature, int deterministic, float *rec_obs,
                               int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
-                              float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
-                              const int64_t *counter, void *stream);
+                              float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
+                              uint32_t seed, const int64_t *counter, void *stream);
 
 /* The Atari image configs' collect step (BASELINE.json config 5; muzero_collector.py:399-705 with
  * zoo/atari/envs/atari_lightzero_env.py): one workgroup per env right after the search — select_action
@@ -234,14 +244,16 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
  * auto-reset finished episodes (their final frame goes to slot row L; ep_len / ep_count advance) and
  * draw the next root's Dirichlet(noise_alpha) noise. The game is a stand-in with Breakout's action set
  * and frame format (ALE is not installed; csrc/lzm_atari.h). state int32 [n][16], cur u8 [n][4096]
- * (the newest frame), counter: the device env-step counter. */
+ * (the newest frame), counter: the device env-step counter. ep_return float[n][E] (nullable): each finished
+ * episode's UNCLIPPED score (eval_episode_return, muzero_collector.py:596-603; the recorded rewards are
+ * clipped). */
 int lzm_atari_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream);
 int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
                            const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
                            float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
                            int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
-                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
-                           const int64_t *counter, void *stream);
+                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
+                           uint32_t seed, const int64_t *counter, void *stream);
 
 /* Device packing of a collector's finished episodes for the trajectory return (SURVEY.md §8(e);
  * replaces the host loop over envs that builds GameSegments' arrays, muzero_collector.py:612-632, and
@@ -253,14 +265,16 @@ int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, co
  * totals): out_index [episodes][3] = (env, L, first row), out_frames [rows][frame_bytes] (o_0..o_L of
  * each episode, copied from rec_frames [n][E][T+1][frame_bytes]), out_scalars [rows][3 + A (+1)] =
  * [action | reward | visit counts (A) | root value (| predicted value)] with each episode's row L
- * zero; then consumed[i] = ep_count[i]. Env-major order, each env's episodes in finishing order. */
+ * zero but for its reward column, which holds ep_return [n][E] of the slot (nullable: 0); then
+ * consumed[i] = ep_count[i]. Env-major order, each env's episodes in finishing order. */
 int lzm_episodes_scan(int n, int E, const int32_t *ep_count, const int32_t *consumed, const int32_t *ep_len,
                       int32_t *env_ep_off, int64_t *env_row_off, int64_t *totals, void *stream);
 int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_bytes, const int32_t *ep_count,
                       const int32_t *ep_len, int32_t *consumed, const int32_t *env_ep_off, const int64_t *env_row_off,
                       const void *rec_frames, const int32_t *rec_action, const float *rec_reward,
-                      const int32_t *rec_visits, const float *rec_value, const float *rec_pred, void *out_frames,
-                      float *out_scalars, int64_t *out_index, void *stream);
+                      const int32_t *rec_visits, const float *rec_value, const float *rec_pred,
+                      const float *ep_return, void *out_frames, float *out_scalars, int64_t *out_index,
+                      void *stream);
 
 /* The BatchNorm-folded conv representation network's epilogue in one pass (conv_infer.FoldedConvInitial,
  * replacing torch's bias broadcast add, residual add and ReLU passes after each MIOpen convolution,
@@ -414,9 +428,11 @@ int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base, float pb_
  * lzm_search_conv with the reward head reading relu(h1 * vp_s + vp_t) (K = H). rec_reset (nullable)
  * is_reset int32 [S][B]. Same results as the generic path (traverse, lzm_conv_trunk_xin_p,
  * lzm_ez_lstm_step, lzm_conv_heads, lzm_decode_backprop) bit for bit. Requires max(B, 2 T) <= the
- * device's CU count, T = ceil(B / 64) * H / 16: the grid must be co-resident, so outside a stream
- * capture it is a cooperative launch; when the runtime (or the occupancy bound) cannot keep it resident
- * the call returns LZM_ERR_RESIDENCY without running anything and the caller takes the generic path. */
+ * device's CU count, T = ceil(B / 64) * H / 16: the grid must be co-resident. When the static bound
+ * (occupancy per CU x CUs; LZM_RESIDENCY_CUS=<n> caps the CU count, for tests) cannot hold it the call
+ * returns LZM_ERR_RESIDENCY without running anything and the caller takes the generic path; otherwise it
+ * is a plain launch (eager or captured), whose bounded hand-off waits count a timeout in the tree's
+ * error word when other work on the GPU keeps part of the grid from running. */
 int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_base, float pb_c_init, float discount,
                        float *minmax, const uint32_t *seeds, const int32_t *vtp_in, float *latent_pool, float *hpool,
                        float *cpool, int H, int horizon, const float *trunk_w, const float *actmap, int n_dres,

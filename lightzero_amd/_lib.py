@@ -6,8 +6,10 @@ point raises. torch is imported first so that the library binds to the HIP runti
 already loaded (same soname, libamdhip64.so.7), and torch streams / device pointers are
 valid inside it.
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
@@ -87,18 +89,20 @@ SIGNATURES = {
     "lzm_debug_expf": [_vp, _vp, _i64, _vp],
     "lzm_debug_glibc_rand": [_u32, _i, _vp, _vp],
     "lzm_debug_philox": [_vp, _vp, _i, _vp],
+    "lzm_debug_xor": [_vp, _vp, _vp],
+    "lzm_shutdown": [],
     "lzm_debug_phase_cycles": [_vp, _vp, _i],
     "lzm_cartpole_reset": [_i, _vp, _vp, _vp, _u32, _vp],
     "lzm_cartpole_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp,
-                                  _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
+                                  _vp, _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
     "lzm_atari_reset": [_i, _vp, _vp, _vp, _vp, _u32, _vp],
     "lzm_atari_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp,
-                               _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
+                               _vp, _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
     "lzm_episodes_scan": [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_bias_add_relu": [_vp, _vp, _vp, _i, _i, _i, _i, _vp],
     "lzm_conv_resnet8_p": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
     "lzm_episodes_pack": [_i, _i, _i, _i, _i, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                          _vp, _vp],
+                          _vp, _vp, _vp],
     "lzm_az_workspace_bytes": [_i, _i, ctypes.POINTER(_i64)],
     "lzm_az_noise_table": [_d, _i, _vp],
     "lzm_az_set_constants": [_i, _i, _vp, _d, _d, _d, _vp],
@@ -135,6 +139,33 @@ class ResidencyError(LzmError):
     """A launch that needs its whole grid co-resident was refused (LZM_ERR_RESIDENCY); nothing ran."""
 
 
+# objects owning device memory allocated by the library (tree handles, ...): closed by the exit hook
+_owners = weakref.WeakSet()
+
+
+def register_owner(obj):
+    """obj.close() releases its library resources; called at process exit before the runtime's teardown"""
+    _owners.add(obj)
+
+
+def _teardown():
+    """atexit (runs before the interpreter finalises and before any C-level exit handler): close the live
+    handles, wait for the device and free the library's static buffers, so nothing of the library is left
+    for the HIP runtime's (or a profiler's) exit-time teardown to release (profiles/r05/README.md)."""
+    if _lib is None:
+        return
+    for o in list(_owners):
+        try:
+            o.close()
+        except Exception:
+            pass
+    try:
+        if torch.cuda.is_initialized():
+            _lib.lzm_shutdown()
+    except Exception:
+        pass
+
+
 def load(path=LIB_PATH):
     """Load the library without touching the GPU (symbol table only)."""
     global _lib
@@ -148,6 +179,7 @@ def load(path=LIB_PATH):
         fn.argtypes = args
         fn.restype = _RESTYPE.get(name, ctypes.c_int)
     _lib = L
+    atexit.register(_teardown)
     return L
 
 

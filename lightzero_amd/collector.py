@@ -37,7 +37,8 @@ import torch.distributed as dist
 from . import _lib
 from ._lib import call, ptr, stream_ptr
 from .collect import DeviceSearchStep
-from .trajectory import TrajBlock, all_gather_packed, allreduce_stats, scalar_width, unpack_episodes
+from .trajectory import TrajBlock, all_gather_packed, allreduce_stats, gather_packed, scalar_width, unpack_episodes, \
+    wire_bytes
 
 
 class CartPoleDevice:
@@ -64,7 +65,8 @@ class CartPoleDevice:
              ptr(pred), ptr(self.state), ptr(self.steps), ptr(c.search.obs), ptr(c.search.noises),
              float(c.noise_alpha), float(c.temperature), int(c.deterministic), ptr(c.rec_frames),
              ptr(c.rec_action), ptr(c.rec_reward), ptr(c.rec_visits), ptr(c.rec_value), ptr(c.rec_pred),
-             ptr(c.ep_len), ptr(c.ep_count), int(c.T), c.seed, ptr(c.search.step_counter), stream_ptr())
+             ptr(c.ep_len), ptr(c.ep_count), ptr(c.ep_return), int(c.T), c.seed, ptr(c.search.step_counter),
+             stream_ptr())
 
 
 class BreakoutDevice:
@@ -94,7 +96,8 @@ class BreakoutDevice:
              ptr(pred), ptr(self.state), ptr(self.steps), ptr(self.cur), ptr(c.search.obs), ptr(c.search.noises),
              float(c.noise_alpha), float(c.temperature), int(c.deterministic), ptr(c.rec_frames),
              ptr(c.rec_action), ptr(c.rec_reward), ptr(c.rec_visits), ptr(c.rec_value), ptr(c.rec_pred),
-             ptr(c.ep_len), ptr(c.ep_count), int(c.T), c.seed, ptr(c.search.step_counter), stream_ptr())
+             ptr(c.ep_len), ptr(c.ep_count), ptr(c.ep_return), int(c.T), c.seed, ptr(c.search.step_counter),
+             stream_ptr())
 
 
 DEVICE_ENVS = {"cartpole": CartPoleDevice, "breakout": BreakoutDevice}
@@ -134,6 +137,9 @@ class DeviceCollector:
         self._epoch = 0
         self.ep_len = torch.zeros((n, E), dtype=torch.int32, device=dev)
         self.ep_count = torch.zeros(n, dtype=torch.int32, device=dev)
+        # each finished episode's return (the env's eval_episode_return: CartPole's reward sum, the Atari
+        # game's unclipped score), carried in the packed block's row L (trajectory.py)
+        self.ep_return = torch.zeros((n, E), dtype=torch.float32, device=dev)
         # device packing state (lzm_episodes_*): episodes returned per env, offsets, totals
         self._consumed_dev = torch.zeros(n, dtype=torch.int32, device=dev)
         self._ep_off = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -199,6 +205,7 @@ class DeviceCollector:
         self.search.noises.copy_(noise)
         self.ep_count.zero_()
         self.ep_len.zero_()
+        self.ep_return.zero_()
         self._consumed_dev.zero_()
         self._consumed = np.zeros(self.n, dtype=np.int64)
         self._gathered_at = getattr(self, "envstep", 0)
@@ -224,63 +231,78 @@ class DeviceCollector:
             if new.sum() >= n_episode:
                 return time.perf_counter() - t0
 
-    def collect(self, n_episode, group=None):
+    def collect(self, n_episode, group=None, dst=None):
         """Step until `n_episode` new episodes have finished on this rank; returns (episodes, stats).
 
-        With an initialised torch.distributed process group of more than one rank (one collector
-        per GPU, env-sharded), every rank's finished episodes are packed on its device and
-        all-gathered (lightzero_amd.trajectory, RCCL over xGMI), and the step / episode / duration
-        statistics are sum-reduced (muzero_collector.py:709-712): every rank returns the episodes
-        of all ranks, each tagged with its `rank`."""
+        Under an initialised torch.distributed process group (one collector per GPU, env-sharded)
+        every rank's finished episodes are packed on its device and returned over the group
+        (lightzero_amd.trajectory, RCCL over xGMI): to every rank (dst=None: all-gather) or to the
+        learner rank `dst` alone (gather-to-learner; the other ranks get no episodes back), each tagged
+        with its `rank`; the step / episode / duration statistics are sum-reduced on every rank
+        (muzero_collector.py:709-712)."""
         steps0 = self.envstep
         el = self._poll_until(n_episode)
-        blocks, stats = self._return_blocks(self.envstep - steps0, el, group)
+        blocks, stats = self._return_blocks(self.envstep - steps0, el, group, dst=dst)
         return self._unpack(blocks, stats)
 
-    def collect_blocks(self, n_episode, group=None, to_host=False):
-        """collect() without the host unpacking: (every rank's TrajBlock in rank order, stats) — what a
+    def collect_blocks(self, n_episode, group=None, to_host=False, dst=None):
+        """collect() without the host unpacking: (the returned TrajBlocks in rank order, stats) — what a
         learner consumes directly (device tensors with to_host=False)."""
         steps0 = self.envstep
         el = self._poll_until(n_episode)
-        return self._return_blocks(self.envstep - steps0, el, group, to_host)
+        return self._return_blocks(self.envstep - steps0, el, group, to_host, dst=dst)
 
-    def gather_finished(self, group=None):
+    def gather_finished(self, group=None, dst=None):
         """The episodes finished since the last collect / gather, without stepping: packed on the
-        device and, under a process group of more than one rank, all-gathered with the statistics
-        sum-reduced (as collect does). Returns (episodes, stats)."""
-        blocks, stats = self.gather_blocks(group, to_host=True)
+        device and returned over the process group as collect does. Returns (episodes, stats)."""
+        blocks, stats = self.gather_blocks(group, to_host=True, dst=dst)
         return self._unpack(blocks, stats)
 
-    def gather_blocks(self, group=None, to_host=False):
+    def gather_blocks(self, group=None, to_host=False, dst=None):
         """gather_finished() without the host unpacking: (TrajBlocks in rank order, stats)."""
         steps = self.envstep - getattr(self, "_gathered_at", 0)
-        return self._return_blocks(steps, 0.0, group, to_host)
+        return self._return_blocks(steps, 0.0, group, to_host, dst=dst)
 
     def _world(self, group):
-        return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        """the group's size when a process group is initialised (its collectives then carry the return, even
+        with one rank), else 0"""
+        return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 0
 
-    def _return_blocks(self, steps, el, group, to_host=True):
+    def _return_blocks(self, steps, el, group, to_host=True, dst=None):
+        self._check_search()
         block = self.pack_new()
         self._gathered_at = self.envstep
         world = self._world(group)
-        if world > 1:
+        coll = None
+        if world >= 1:
             rank = dist.get_rank(group)
-            blocks = all_gather_packed(block, group, to_host=to_host)
+            torch.cuda.synchronize(self.dev)
+            t0 = time.perf_counter()
+            if dst is None:
+                blocks = all_gather_packed(block, group, to_host=to_host)
+            else:
+                blocks = gather_packed(block, int(dst), group, to_host=to_host)
             tot_steps, tot_eps, tot_secs = allreduce_stats(steps, block.num_episodes, el, self.dev, group)
+            torch.cuda.synchronize(self.dev)
+            mine = wire_bytes(block)
+            coll = dict(backend=str(dist.get_backend(group)), mode="all_gather" if dst is None else f"gather(dst={dst})",
+                        ms=(time.perf_counter() - t0) * 1e3, bytes_sent=mine,
+                        bytes_received=sum(wire_bytes(b) for r, b in enumerate(blocks) if r != rank))
         else:
             rank = 0
+            world = 1
             blocks = [block.numpy() if to_host else block]
             tot_steps, tot_eps, tot_secs = steps, block.num_episodes, el
         stats = dict(envstep=steps, seconds=el, env_steps_per_s=steps / el if el else None,
                      sims_per_s=steps * self.S / el if el else None, rank=rank, world=world,
                      total_envstep=tot_steps, total_episodes=tot_eps, total_duration=tot_secs,
                      episodes=sum(b.num_episodes for b in blocks), rows=sum(b.rows for b in blocks),
-                     payload_bytes=sum(b.nbytes for b in blocks))
+                     payload_bytes=sum(b.nbytes for b in blocks), collective=coll)
         return blocks, stats
 
     def _unpack(self, blocks, stats):
         episodes = [e for r, b in enumerate(blocks) for e in unpack_episodes(b, self.A, r)]
-        stats = dict(stats, episode_returns=[float(e["reward_segment"].sum()) for e in episodes])
+        stats = dict(stats, episode_returns=[float(e["episode_return"]) for e in episodes])
         return episodes, stats
 
     def pack_new(self):
@@ -304,12 +326,12 @@ class DeviceCollector:
             call("lzm_episodes_pack", n, E, self.T, self.A, int(has_pred), fbytes, ptr(self.ep_count), ptr(self.ep_len),
                  ptr(self._consumed_dev), ptr(self._ep_off), ptr(self._row_off), ptr(self.rec_frames),
                  ptr(self.rec_action), ptr(self.rec_reward), ptr(self.rec_visits), ptr(self.rec_value),
-                 ptr(self.rec_pred), ptr(frames), ptr(scalars), ptr(index), stream_ptr())
+                 ptr(self.rec_pred), ptr(self.ep_return), ptr(frames), ptr(scalars), ptr(index), stream_ptr())
         self._consumed = snap[4:].astype(np.int64)  # lzm_episodes_pack sets consumed = ep_count on the device
         return TrajBlock(frames, scalars, index, self.env.frame_scale)
 
     def pull_new(self):
         """The episodes finished since the last pull, on the host (one device pack + one copy):
         episode dicts in env order, each env's episodes in finishing order."""
-        self.search.roots.tree.check_errors()  # the fused searches' tie-break stream intact, as collect()
+        self._check_search()  # as collect() / gather_blocks()
         return unpack_episodes(self.pack_new(), self.A)

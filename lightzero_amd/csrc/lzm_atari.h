@@ -40,7 +40,8 @@ constexpr int kAtStateWords = 16;
 constexpr int kAtAutoServe = 8;             // idle steps before the ball is served without FIRE
 
 // state words per env
-enum { AT_PADDLE = 0, AT_BX, AT_BY, AT_VX, AT_VY, AT_IN_PLAY, AT_BRICK0, AT_BRICK1, AT_BRICK2, AT_LIVES, AT_IDLE };
+// (AT_SCORE: the episode's unclipped points so far, the env's eval_episode_return)
+enum { AT_PADDLE = 0, AT_BX, AT_BY, AT_VX, AT_VY, AT_IN_PLAY, AT_BRICK0, AT_BRICK1, AT_BRICK2, AT_LIVES, AT_IDLE, AT_SCORE };
 
 struct AtariArgs {
   int n, A, T, E, max_steps, deterministic;
@@ -63,6 +64,7 @@ struct AtariArgs {
   float *rec_pred;             // [n][E][T] (nullable)
   int32_t *ep_len;             // [n][E]
   int32_t *ep_count;           // [n]
+  float *ep_return;            // [n][E] unclipped score of the finished episode in each slot (nullable)
 };
 
 __device__ inline bool at_brick(const int32_t *s, int r, int c) {
@@ -244,13 +246,17 @@ __global__ void __launch_bounds__(kAtThreads) atari_collect_kernel(AtariArgs p) 
     for (int k = 0; k < kAtStateWords; ++k) s1[k] = p.state[(size_t)i * kAtStateWords + k];
     PhiloxStream rg{p.seed, (uint32_t)i, (uint32_t)step, (uint32_t)(step >> 32), 6u, 0u};
     bool terminated = false;
-    // ClipRewardWrapper (the collector env's clip_rewards=True, atari_lightzero_env.py:57): sign(points)
-    const float reward = at_step(s1, action, rg, &terminated) > 0.0f ? 1.0f : 0.0f;
+    // ClipRewardWrapper (the collector env's clip_rewards=True, atari_lightzero_env.py:57): sign(points);
+    // the unclipped points add up to the episode's return, the env's eval_episode_return
+    const float points = at_step(s1, action, rg, &terminated);
+    s1[AT_SCORE] += (int32_t)points;
+    const float reward = points > 0.0f ? 1.0f : 0.0f;
     const int nt = t + 1;
     const bool done = terminated || nt >= p.max_steps;
     if (t < p.T) p.rec_reward[slot * p.T + t] = reward;
     if (done) {
       p.ep_len[slot] = nt;
+      if (p.ep_return) p.ep_return[slot] = (float)s1[AT_SCORE];
       p.ep_count[i] += 1;
       PhiloxStream rr{p.seed, (uint32_t)i, (uint32_t)step, (uint32_t)(step >> 32), 3u, 0u};
       at_reset(s0, rr);

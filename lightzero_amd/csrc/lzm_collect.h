@@ -42,6 +42,7 @@ struct CollectArgs {
   float *rec_pred;             // [n][E][T] (nullable)
   int32_t *ep_len;             // [n][E] length of the finished episode in each slot
   int32_t *ep_count;           // [n] finished episodes (slot of the running one = ep_count % E)
+  float *ep_return;            // [n][E] return of the finished episode in each slot (nullable)
 };
 
 // uniform in (0, 1) from one Philox output word (53-bit double from two words)
@@ -171,6 +172,8 @@ __global__ void cartpole_collect_kernel(CollectArgs p) {
     if (nt <= p.T)
       for (int j = 0; j < 4; ++j) p.rec_obs[(slot * (p.T + 1) + nt) * 4 + j] = (float)s[j];
     p.ep_len[slot] = nt;
+    // eval_episode_return (cartpole_lightzero_env.py: the sum of the env's rewards, 1 per step)
+    if (p.ep_return) p.ep_return[slot] = (float)nt;
     p.ep_count[i] += 1;
     PhiloxStream rr{p.seed, (uint32_t)i, (uint32_t)step, (uint32_t)(step >> 32), 3u, 0u};
     cartpole_reset(s, rr);

@@ -609,6 +609,31 @@ __global__ void debug_expf_kernel(const float *x, float *out, long long n) {
     out[e] = glibc_expf(x[e]);
 }
 
+// lzm_debug_xor: the DPP / permlane butterfly helpers (lzm_tree.h xor_partner / xor_sum / xor_max) beside
+// the ds_bpermute __shfl_xor they replace, one 64-lane wave; rows of out [16][64]:
+//   0-5 xor_partner<1..32>, 6-11 __shfl_xor(v, 1..32), 12 xor_sum, 13 the __shfl_xor butterfly sum,
+//   14 xor_max, 15 the __shfl_xor butterfly max
+__global__ void __launch_bounds__(64) debug_xor_kernel(const float *in, float *out) {
+  const int l = threadIdx.x;
+  const float v = in[l];
+  out[0 * 64 + l] = xor_partner<1>(v);
+  out[1 * 64 + l] = xor_partner<2>(v);
+  out[2 * 64 + l] = xor_partner<4>(v);
+  out[3 * 64 + l] = xor_partner<8>(v);
+  out[4 * 64 + l] = xor_partner<16>(v);
+  out[5 * 64 + l] = xor_partner<32>(v);
+  for (int k = 0; k < 6; ++k) out[(6 + k) * 64 + l] = __shfl_xor(v, 1 << k, 64);
+  out[12 * 64 + l] = xor_sum(v);
+  float s = v, m = v;
+  for (int d = 32; d >= 1; d >>= 1) {
+    s += __shfl_xor(s, d, 64);
+    m = fmaxf(m, __shfl_xor(m, d, 64));
+  }
+  out[13 * 64 + l] = s;
+  out[14 * 64 + l] = xor_max(v);
+  out[15 * 64 + l] = m;
+}
+
 __global__ void debug_philox_kernel(const uint32_t *ck, uint32_t *out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1225,6 +1250,7 @@ int lzm_decode_backprop_traverse(lzm_handle *h, int cur, float discount, float *
 
 static int32_t *g_scratch_flag = nullptr;
 static int g_scratch_parts = 0;
+static uint32_t *g_debug_jm = nullptr;  // lzm_debug_glibc_rand's jump matrices
 static std::mutex g_scratch_mu;
 
 int lzm_inverse_scalar_transform(const float *logits, int rows, int V, int categorical, float *out, void *stream) {
@@ -1293,9 +1319,31 @@ int lzm_debug_philox(const uint32_t *ck, uint32_t *out, int n, void *stream) {
   return LZM_OK;
 }
 
+// Process teardown (lightzero_amd registers it with atexit, before the interpreter finalises): wait for the
+// device, then free the library's process-wide device buffers while the HIP runtime (and a profiler's
+// hooks) are still in place, instead of leaving them to the runtime's own exit-time teardown. Live handles
+// are destroyed by their owners first (lzm_destroy).
+int lzm_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_scratch_mu);
+  LZM_HIP(hipDeviceSynchronize());
+  if (g_scratch_flag) LZM_HIP(hipFree(g_scratch_flag));
+  g_scratch_flag = nullptr;
+  g_scratch_parts = 0;
+  if (g_debug_jm) LZM_HIP(hipFree(g_debug_jm));
+  g_debug_jm = nullptr;
+  return LZM_OK;
+}
+
+int lzm_debug_xor(const float *in, float *out, void *stream) {
+  if (!in || !out) return LZM_ERR_ARG;
+  hipLaunchKernelGGL(debug_xor_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, in, out);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
 int lzm_debug_glibc_rand(uint32_t seed, int n, int32_t *out, void *stream) {
   if (!out || n <= 0) return LZM_ERR_ARG;
-  static uint32_t *jm = nullptr;
+  uint32_t *&jm = g_debug_jm;
   {
     std::lock_guard<std::mutex> lk(g_scratch_mu);
     if (!jm) {
@@ -1924,8 +1972,8 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
                               const float *pred_value, double *state, int32_t *steps, float *obs, float *noises,
                               float noise_alpha, float temperature, int deterministic, float *rec_obs,
                               int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
-                              float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
-                              const int64_t *counter, void *stream) {
+                              float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
+                              uint32_t seed, const int64_t *counter, void *stream) {
   if (n <= 0 || A <= 0 || A > 64 || T <= 0 || E <= 0 || !visits || !root_value || !state || !steps || !obs ||
       !noises || !rec_obs || !rec_action || !rec_reward || !rec_visits || !rec_value || !ep_len || !ep_count ||
       !counter || !(temperature > 0.0f) || !(noise_alpha > 0.0f) || (!pred_value) != (!rec_pred)) {
@@ -1938,7 +1986,7 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
   a.visits = visits; a.root_value = root_value; a.state = state; a.steps = steps; a.obs = obs; a.noises = noises;
   a.rec_obs = rec_obs; a.rec_action = rec_action; a.rec_reward = rec_reward; a.rec_visits = rec_visits;
   a.rec_value = rec_value; a.pred_value = pred_value; a.rec_pred = rec_pred; a.ep_len = ep_len;
-  a.ep_count = ep_count;
+  a.ep_count = ep_count; a.ep_return = ep_return;
   hipLaunchKernelGGL(cartpole_collect_kernel, dim3((n + 127) / 128), dim3(128), 0, (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
@@ -1959,8 +2007,8 @@ int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, co
                            const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
                            float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
                            int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
-                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, int max_steps, uint32_t seed,
-                           const int64_t *counter, void *stream) {
+                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
+                           uint32_t seed, const int64_t *counter, void *stream) {
   if (n <= 0 || A <= 0 || A > 64 || T <= 0 || E <= 0 || max_steps <= 0 || !visits || !root_value || !state || !steps ||
       !cur || !obs || !noises || !rec_frames || !rec_action || !rec_reward || !rec_visits || !rec_value || !ep_len ||
       !ep_count || !counter || !(temperature > 0.0f) || !(noise_alpha > 0.0f) || (!pred_value) != (!rec_pred) ||
@@ -1974,7 +2022,7 @@ int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, co
   a.visits = visits; a.root_value = root_value; a.state = state; a.steps = steps; a.cur = cur; a.obs = obs;
   a.noises = noises; a.rec_frames = rec_frames; a.rec_action = rec_action; a.rec_reward = rec_reward;
   a.rec_visits = rec_visits; a.rec_value = rec_value; a.pred_value = pred_value; a.rec_pred = rec_pred;
-  a.ep_len = ep_len; a.ep_count = ep_count;
+  a.ep_len = ep_len; a.ep_count = ep_count; a.ep_return = ep_return;
   hipLaunchKernelGGL(atari_collect_kernel, dim3(n), dim3(kAtThreads), 0, (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
@@ -2028,8 +2076,9 @@ int lzm_bias_add_relu(float *y, const float *bias, const float *z, int N, int C,
 int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_bytes, const int32_t *ep_count,
                       const int32_t *ep_len, int32_t *consumed, const int32_t *env_ep_off, const int64_t *env_row_off,
                       const void *rec_frames, const int32_t *rec_action, const float *rec_reward,
-                      const int32_t *rec_visits, const float *rec_value, const float *rec_pred, void *out_frames,
-                      float *out_scalars, int64_t *out_index, void *stream) {
+                      const int32_t *rec_visits, const float *rec_value, const float *rec_pred,
+                      const float *ep_return, void *out_frames, float *out_scalars, int64_t *out_index,
+                      void *stream) {
   if (n <= 0 || E <= 0 || T <= 0 || A <= 0 || frame_bytes <= 0 || !ep_count || !ep_len || !consumed ||
       !env_ep_off || !env_row_off || !rec_frames || !rec_action || !rec_reward || !rec_visits || !rec_value ||
       (has_pred && !rec_pred) || !out_frames || !out_scalars || !out_index) {
@@ -2041,7 +2090,7 @@ int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_by
   a.frame_bytes = frame_bytes; a.ep_count = ep_count; a.ep_len = ep_len; a.env_ep_off = env_ep_off;
   a.consumed = consumed; a.env_row_off = env_row_off;
   a.rec_frames = (const uint8_t *)rec_frames; a.rec_action = rec_action; a.rec_reward = rec_reward;
-  a.rec_visits = rec_visits; a.rec_value = rec_value; a.rec_pred = rec_pred;
+  a.rec_visits = rec_visits; a.rec_value = rec_value; a.rec_pred = rec_pred; a.ep_return = ep_return;
   a.out_frames = (uint8_t *)out_frames; a.out_scalars = out_scalars; a.out_index = out_index;
   if ((frame_bytes & 15) == 0 && (((uintptr_t)rec_frames | (uintptr_t)out_frames) & 15)) {
     set_err("lzm_episodes_pack: frame buffers must be 16-B aligned when frames are multiples of 16 B");
@@ -2667,7 +2716,10 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
     snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: %d simulations > reserved %d (lzm_reserve)", S, h->sims_cap);
     return LZM_ERR_CAPACITY;
   }
-  const int cus = device_cus();
+  // LZM_RESIDENCY_CUS=<n> caps the CU count this check assumes (tests: force the refusal)
+  int cus = device_cus();
+  if (const char *ov = getenv("LZM_RESIDENCY_CUS"))
+    if (atoi(ov) > 0) cus = std::min(cus, atoi(ov));
   const int B = h->B, nmb = (B + kLsRows - 1) / kLsRows, T = nmb * (H / kLsUnits), G = std::max(B, 2 * T);
   if (B > 256 || G > cus) {
     snprintf(g_err, sizeof(g_err),
@@ -2749,12 +2801,15 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
                    : (fast ? search_conv_ez_kernel<kBxAhead, true> : search_conv_ez_kernel<kBxAhead, false>);
   LZM_HIP(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // The roots wait on LSTM tiles and the tiles on roots inside the launch, so every workgroup must be
-  // resident at once. Occupancy bound first (resident workgroups per CU at this LDS / register use x the
-  // device's CUs), then a COOPERATIVE launch, which the runtime refuses rather than start a grid it
-  // cannot keep resident (e.g. while another kernel holds CUs: a learner on another stream, a second
-  // rank on the same GPU). A refused launch returns LZM_ERR_RESIDENCY and nothing ran: the caller
-  // takes the generic per-simulation path. Inside a stream capture (a HIP graph node cannot carry the
-  // cooperative attribute) the plain launch is used; the captured graph owns its GPU at replay.
+  // resident at once. The check is static: resident workgroups per CU at this LDS / register use (the
+  // occupancy API) x the CUs must cover the grid, else LZM_ERR_RESIDENCY and nothing ran (the caller takes
+  // the generic per-simulation path). It cannot see other work on the GPU (a learner on another stream, a
+  // second rank on the same GPU): every hand-off wait in the kernel is bounded and a timeout is counted in
+  // the tree's error word (lzm_check_errors raises), never a hang. The launch is a plain one, eager and
+  // captured alike: the cooperative launch it replaced applies the same static occupancy check (it is
+  // not a residency guarantee against other streams), cannot be captured into a HIP graph, and its
+  // runtime state was the one difference from the MuZero conv search in the EZ trace that faulted in
+  // exit() after rocprofv3 finalised (profiles/r05/README.md).
   int per_cu = 0;
   LZM_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void *)fn, kScThreads, lds));
   if ((long long)per_cu * cus < G) {
@@ -2762,23 +2817,8 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
              per_cu * cus, per_cu, cus);
     return LZM_ERR_RESIDENCY;
   }
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  LZM_HIP(hipStreamIsCapturing((hipStream_t)stream, &cap));
-  if (cap != hipStreamCaptureStatusNone) {
-    hipLaunchKernelGGL(fn, dim3(G), dim3(kScThreads), lds, (hipStream_t)stream, p);
-    LZM_CHECK_LAUNCH();
-    return LZM_OK;
-  }
-  void *kargs[] = {(void *)&p};
-  hipError_t e = hipLaunchCooperativeKernel((const void *)fn, dim3(G), dim3(kScThreads), kargs, (unsigned)lds,
-                                            (hipStream_t)stream);
-  if (e == hipErrorCooperativeLaunchTooLarge) {
-    (void)hipGetLastError();
-    snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: cooperative launch of %d workgroups refused (not co-resident)",
-             G);
-    return LZM_ERR_RESIDENCY;
-  }
-  LZM_HIP(e);
+  hipLaunchKernelGGL(fn, dim3(G), dim3(kScThreads), lds, (hipStream_t)stream, p);
+  LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
 

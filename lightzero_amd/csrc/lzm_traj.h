@@ -10,7 +10,9 @@
 //   episodes_pack_kernel  one workgroup per env: its episodes' index entries (env, L, first row), the
 //                         frames of each episode as ONE contiguous copy (slot rows 0..L are adjacent in
 //                         rec_frames [n][E][T+1][frame]), the scalar rows [action | reward | visits (A) |
-//                         root value (| predicted value)] with row L zero, and consumed[i] = ep_count[i].
+//                         root value (| predicted value)] with row L zero except its reward column, which
+//                         carries the episode's return (the env's eval_episode_return; 0 when the
+//                         collector records none), and consumed[i] = ep_count[i].
 // Env-major order, each env's episodes in finishing order — the order of the host loop it replaces.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -80,6 +82,7 @@ struct PackArgs {
   const int32_t *rec_visits;   // [n][E][T][A]
   const float *rec_value;      // [n][E][T]
   const float *rec_pred;       // [n][E][T] (nullable)
+  const float *ep_return;      // [n][E] (nullable)
   uint8_t *out_frames;         // [rows][frame_bytes]
   float *out_scalars;          // [rows][W]
   int64_t *out_index;          // [n_ep][3]
@@ -112,11 +115,12 @@ __global__ void __launch_bounds__(kTrPackThreads) episodes_pack_kernel(PackArgs 
     } else {
       for (int64_t q = tid; q < nbytes; q += kTrPackThreads) dst[q] = src[q];
     }
-    // scalar rows (row L: zeros)
+    // scalar rows (row L: zeros, the episode's return in the reward column)
     for (int t = tid; t <= L; t += kTrPackThreads) {
       float *o = p.out_scalars + (size_t)(row + t) * p.W;
       if (t == L) {
         for (int c = 0; c < p.W; ++c) o[c] = 0.0f;
+        if (p.ep_return) o[1] = p.ep_return[slot];
         continue;
       }
       const size_t s = slot * p.T + t;

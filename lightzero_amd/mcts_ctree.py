@@ -647,8 +647,9 @@ class EfficientZeroMCTSCtree(object):
             cz = self._fused_conv(model, t, shape, Hl)
             if cz is not None:
                 # the conv network's whole search, reward LSTM included, in one launch (lzm_search_conv_ez);
-                # the launch needs its whole grid co-resident: when the runtime refuses that (the GPU is
-                # shared with other work), nothing ran and the generic per-simulation path runs instead
+                # the launch needs its whole grid co-resident: when the occupancy bound refuses it, nothing
+                # ran and the generic per-simulation path runs instead — eagerly only: inside a stream
+                # capture the refusal is raised (the caller captures a different graph, not a fallback)
                 cfg = self._cfg
                 new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
                 try:
@@ -658,6 +659,8 @@ class EfficientZeroMCTSCtree(object):
                                      bool(cfg.model.get('categorical_distribution', True)), rec=rec)
                     self.last_path = "fused"
                 except _lib.ResidencyError:
+                    if torch.cuda.is_current_stream_capturing():
+                        raise
                     self.residency_fallbacks = getattr(self, "residency_fallbacks", 0) + 1
                     self.last_path = "generic (co-residency refused)"
                     self._loop(t, model, buf, S, row, Hl, rec)

@@ -66,6 +66,7 @@ class DeviceTree:
         with torch.cuda.device(self.device):
             call("lzm_create", self.B, self.A, int(max_sims), flags, ctypes.byref(h))
         self.h = h
+        _lib.register_owner(self)  # closed at exit before the runtime's own teardown
         self.generation = 0
         self._pb_c = (19652, 1.25)  # lzm_create builds the table for the reference defaults
         i32 = dict(dtype=torch.int32, device=self.device)

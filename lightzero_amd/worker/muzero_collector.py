@@ -384,7 +384,9 @@ class MuZeroCollector:
     def _device_path(self, collect_with_pure_policy):
         from ..policy import MuZeroCollectPolicy
         cfg = self.policy_config
-        return (isinstance(self._env, DeviceEnvManager) and isinstance(self._policy, MuZeroCollectPolicy)
+        # MuZero policies only: the device collector's search step is MuZero's (an EfficientZero
+        # policy, a MuZeroCollectPolicy subclass, keeps the host path with its value-prefix / LSTM search)
+        return (isinstance(self._env, DeviceEnvManager) and type(self._policy) is MuZeroCollectPolicy
                 and not collect_with_pure_policy and not cfg.eps.eps_greedy_exploration_in_collect
                 and cfg.model.frame_stack_num == self._env.frame_stack)
 
@@ -433,7 +435,9 @@ class MuZeroCollector:
                                                             start, mask, -1):
                     pool.append((it, i, k, seg, prio, d))
                 collected_step += L
-                infos.append({'reward': float(L), 'time': 0.0, 'step': L,
+                # the env's eval_episode_return (muzero_collector.py:596-603): the unclipped game score
+                # for Atari, the reward sum for CartPole (recorded on the device, lzm_*_collect_step)
+                infos.append({'reward': float(e["episode_return"]), 'time': 0.0, 'step': L,
                               'visit_entropy': self._visit_entropy(e["visits"], temperature)})
         # the loop's wall time is the collect duration (all envs step together on the device); each
         # counted episode gets the share of it its steps make up, so the per-episode times sum to it

@@ -101,18 +101,19 @@ def paddle_from_frame(frame):
     return int(xs[0]) + WALL
 
 
-def replay_episode(frames, actions, rewards, max_steps):
-    """frames u8 [L + 1, 64, 64] (o_0 .. o_L), actions [L], rewards [L] (clipped, as recorded).
+def replay_episode(frames, actions, rewards, max_steps, episode_return=None):
+    """frames u8 [L + 1, 64, 64] (o_0 .. o_L), actions [L], rewards [L] (clipped, as recorded), and
+    optionally the recorded episode return (the unclipped score, the env's eval_episode_return).
     Re-derives the episode; returns None when it matches the game, else a message."""
     frames = np.asarray(frames).reshape(-1, HW, HW)
     L = len(actions)
     s0 = new_state(paddle_from_frame(frames[0]))
     if not np.array_equal(render(s0), frames[0]):
         return "first frame is not a reset frame"
-    cands = [s0]
+    cands = [(s0, 0.0)]  # (game state, unclipped points so far)
     for t in range(L):
         nxt = []
-        for s in cands:
+        for s, score in cands:
             serve = not s["in_play"] and (int(actions[t]) == 1 or s["idle"] + 1 >= AUTO_SERVE)
             dirs = (1, -1) if serve else (1,)
             for d in dirs:
@@ -125,10 +126,12 @@ def replay_episode(frames, actions, rewards, max_steps):
                     continue
                 if last and not (term or t + 1 >= max_steps):
                     continue
-                nxt.append(s1)
+                nxt.append((s1, score + pts))
         if not nxt:
             return f"step {t}: no game state reproduces frame {t + 1} / reward {rewards[t]}"
         # identical candidates collapse
-        uniq = {tuple(sorted(c.items())): c for c in nxt}
+        uniq = {(tuple(sorted(c.items())), sc): (c, sc) for c, sc in nxt}
         cands = list(uniq.values())
+    if episode_return is not None and not any(sc == float(episode_return) for _, sc in cands):
+        return f"episode return {episode_return} is not the game's score {sorted({sc for _, sc in cands})}"
     return None

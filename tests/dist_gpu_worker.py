@@ -16,6 +16,7 @@ from lightzero_amd.collector import DeviceCollector  # noqa: E402
 def main():
     out_dir = sys.argv[1]
     env = sys.argv[2] if len(sys.argv) > 2 else "cartpole"
+    dst = 0 if len(sys.argv) > 3 and sys.argv[3] == "gather" else None  # gather-to-learner: rank 0 receives
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -28,8 +29,14 @@ def main():
             model = bench.build_conv_model(dev, seed=0)
             col = DeviceCollector(model, 16, 8, device=dev, seed=bench.shard_seed(rank), graph=True, poll_every=4,
                                   episode_slots=8, max_episode_steps=150, env="breakout")
-        col.collect(n_episode=4)  # warm-up collect (all-gathered too)
-        eps_all, st_all = col.collect(n_episode=4, group=None)
+        col.collect(n_episode=4, dst=dst)  # warm-up collect (returned over the group too)
+        eps_all, st_all = col.collect(n_episode=4, group=None, dst=dst)
+        if dst is not None and rank != dst:
+            assert eps_all == [] and st_all["collective"]["bytes_received"] == 0
+            np.savez(os.path.join(out_dir, f"out_{rank}.npz"), sent=st_all["collective"]["bytes_sent"],
+                     envstep=st_all["envstep"], total_envstep=st_all["total_envstep"],
+                     total_episodes=st_all["total_episodes"], world=st_all["world"])
+            return
         ranks = np.array([e["rank"] for e in eps_all], np.int64)
         lens = np.array([len(e["action_segment"]) for e in eps_all], np.int64)
         own = np.array([len(e["action_segment"]) for e in eps_all if e["rank"] == rank], np.int64)

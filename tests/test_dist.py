@@ -122,13 +122,19 @@ def _pack(rank, kind):
                          frame_scale=KINDS[kind][2]), eps
 
 
-def _traj_worker(rank, world, port, out_dir, kind):
-    from lightzero_amd.trajectory import all_gather_packed, allreduce_stats
+def _traj_worker(rank, world, port, out_dir, kind, mode="all_gather"):
+    from lightzero_amd.trajectory import all_gather_packed, allreduce_stats, gather_packed
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         block, eps = _pack(rank, kind)
-        blocks = all_gather_packed(block)
+        if mode == "all_gather":
+            blocks = all_gather_packed(block)
+        else:  # gather-to-learner: rank 0 alone receives
+            blocks = gather_packed(block, dst=0)
+            assert (len(blocks) == world) if rank == 0 else (blocks == [])
+            if rank == 0:
+                assert blocks[0] is not None and blocks[0].rows == block.rows
         stats = allreduce_stats(10.0 * (rank + 1), float(len(eps)), 0.25, torch.device("cpu"))
         arrays = {}
         for r, b in enumerate(blocks):
@@ -139,21 +145,45 @@ def _traj_worker(rank, world, port, out_dir, kind):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["all_gather", "gather"])
 @pytest.mark.parametrize("kind", ["vector", "image"])
-def test_trajectory_all_gather_gloo_world2(tmp_path, kind):
-    """every rank ends with every rank's episodes — CartPole vectors and config 5's u8 image frames
-    (sent as bytes, unpacked to the reference's float32 frame / 255)"""
+def test_trajectory_return_gloo_world2(tmp_path, kind, mode):
+    """all_gather: every rank ends with every rank's episodes; gather: the learner (rank 0) alone does —
+    CartPole vectors and config 5's u8 image frames (one flat byte buffer per rank on the wire, unpacked
+    to the reference's float32 frame / 255); the statistics are summed on every rank"""
     from lightzero_amd.trajectory import TrajBlock, unpack_episodes
     world = 2
-    mp.spawn(_traj_worker, args=(world, _free_port(), str(tmp_path), kind), nprocs=world, join=True)
+    mp.spawn(_traj_worker, args=(world, _free_port(), str(tmp_path), kind, mode), nprocs=world, join=True)
     for me in range(world):
         r = np.load(tmp_path / f"r{me}.npz")
-        for rank in range(world):  # every rank holds every rank's episodes
+        n_eps = sum(len(_fake_records(k)[1]) for k in range(world))
+        assert tuple(r["stats"]) == (30.0, float(n_eps), 0.5)
+        if mode == "gather" and me != 0:
+            assert "f0" not in r.files  # nothing received off the learner
+            continue
+        for rank in range(world):  # every receiving rank holds every rank's episodes
             blk = TrajBlock(r[f"f{rank}"], r[f"s{rank}"], r[f"i{rank}"], float(r[f"c{rank}"]))
             assert blk.frames.dtype == (np.uint8 if kind == "image" else np.float32)
             _check_episodes(unpack_episodes(blk, ACT, rank), _expected(rank, kind), rank)
-        n_eps = sum(len(_fake_records(k)[1]) for k in range(world))
-        assert tuple(r["stats"]) == (30.0, float(n_eps), 0.5)
+
+
+@pytest.mark.parametrize("kind", ["vector", "image"])
+def test_flat_wire_buffer_round_trip(kind):
+    """flatten_block / unflatten_block: the block's three arrays in one 16-byte-aligned byte buffer and
+    back, bit for bit (and the empty block)"""
+    from lightzero_amd.trajectory import flatten_block, unflatten_block, wire_bytes
+    for rank in (0, 1):
+        block, _ = _pack(rank, kind)
+        buf = flatten_block(block)
+        assert buf.dtype == torch.uint8 and buf.numel() == wire_bytes(block)
+        b2 = unflatten_block(buf, block.rows, block.num_episodes, tuple(block.frames.shape[1:]), block.frames.dtype,
+                             block.scalars.shape[1], block.frame_scale)
+        assert torch.equal(b2.frames, block.frames) and torch.equal(b2.scalars, block.scalars)
+        assert torch.equal(b2.index, block.index.to(torch.int64))
+    rec, _ = _fake_records(0, kind)
+    from lightzero_amd.trajectory import pack_episodes
+    b0 = pack_episodes(rec["obs"], rec["action"], rec["reward"], rec["child"], rec["value"], [])
+    assert flatten_block(b0).numel() == 0
 
 
 @pytest.mark.parametrize("kind", ["vector", "image"])

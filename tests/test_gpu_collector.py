@@ -27,8 +27,8 @@ def _raw_step(n, visits, state, steps, obs, counter, temperature=1.0, determinis
     value = torch.zeros(n, device=DEV)
     call("lzm_cartpole_collect_step", n, A, T, E, ptr(visits), ptr(value), None, ptr(state), ptr(steps), ptr(obs),
          ptr(noises), 0.3, float(temperature), int(deterministic), ptr(rec["obs"]), ptr(rec["action"]),
-         ptr(rec["reward"]), ptr(rec["child"]), ptr(rec["value"]), None, ptr(rec["ep_len"]), ptr(rec["ep_count"]), T,
-         seed, ptr(counter), stream_ptr())
+         ptr(rec["reward"]), ptr(rec["child"]), ptr(rec["value"]), None, ptr(rec["ep_len"]), ptr(rec["ep_count"]), None,
+         T, seed, ptr(counter), stream_ptr())
     return rec, noises
 
 

@@ -43,8 +43,9 @@ def test_breakout_episodes_replay_through_the_restated_game():
         assert 1 <= L <= col.T and set(np.unique(actions)) <= {0, 1, 2, 3}
         assert set(np.unique(rewards)) <= {0.0, 1.0}  # ClipRewardWrapper
         assert (sc[:L, 2:6].sum(axis=1) == col.S).all()  # root visit counts of an S-simulation search
-        assert (sc[L] == 0).all()
-        msg = breakout_synth.replay_episode(fr, actions, rewards, col.T)
+        # row L: zeros but for the reward column, the episode's unclipped score (eval_episode_return)
+        assert sc[L, 0] == 0 and (sc[L, 2:] == 0).all() and sc[L, 1] >= rewards.sum()
+        msg = breakout_synth.replay_episode(fr, actions, rewards, col.T, episode_return=sc[L, 1])
         assert msg is None, f"env {env_id} episode of {L} steps: {msg}"
 
 
@@ -81,7 +82,7 @@ def test_device_pack_equals_torch_pack(env):
         todo = [(i, k % col.E, int(ln[i, k % col.E])) for i in range(col.n) for k in range(int(col._consumed[i]),
                                                                                         int(counts[i]))]
         ref = pack_episodes(col.rec_frames, col.rec_action, col.rec_reward, col.rec_visits, col.rec_value, todo,
-                            col.rec_pred, col.env.frame_scale)
+                            col.rec_pred, col.env.frame_scale, ep_return=col.ep_return)
         got = col.pack_new()
         assert got.num_episodes == len(todo)
         np.testing.assert_array_equal(got.index.cpu().numpy(), ref.index.numpy())

@@ -165,7 +165,7 @@ def test_fused_conv_search_equals_generic(kind, B, S, rng, zero):
     model = conv_model(kind, 13, zero_heads=zero)
     out = [run_search(kind, B, S, seed=14, model=model, fused=f, rng=rng) for f in (True, False)]
     a, b = out
-    # the one-launch search really ran (EZ: a cooperative launch the runtime accepted)
+    # the one-launch search really ran (EZ: the co-residency bound accepted the grid)
     assert a["path"] in ("fused", "fused-conv") and b["path"] == "generic", (a["path"], b["path"])
     for key in ("dist", "values", "traj"):
         assert np.array_equal(a[key], b[key]), key
@@ -437,3 +437,38 @@ def test_search_bf16x3_vs_f32_trunk(kind, monkeypatch):
     assert rep["first_divergence_kinds"].get("tie_draw", 0) == 0
     same = ~differ
     np.testing.assert_allclose(res["bf16x3"]["values"][same], res["f32"]["values"][same], rtol=1e-3, atol=1e-3)
+
+
+def test_ez_residency_refusal_falls_back_to_generic_with_same_results(monkeypatch):
+    """lzm_search_conv_ez refuses a grid its static co-residency bound cannot hold (LZM_RESIDENCY_CUS caps
+    the CU count it assumes) with LZM_ERR_RESIDENCY before running anything; EfficientZeroMCTSCtree.search
+    then runs the generic path eagerly: the same visit counts, values and trajectories. Inside a stream
+    capture the refusal is raised instead."""
+    from lightzero_amd import _lib
+    from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree
+    from lightzero_amd.utils import EasyDict
+    B, S = 48, 10
+    model = conv_model("ez", 21)
+    a = run_search("ez", B, S, seed=22, model=model, record=False)
+    assert a["path"] == "fused"
+    monkeypatch.setenv("LZM_RESIDENCY_CUS", "8")
+    cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5,
+                        model=dict(support_scale=50, categorical_distribution=True)))
+    mcts = EfficientZeroMCTSCtree(cfg)
+    b = run_search("ez", B, S, seed=22, model=model, record=False, mcts=mcts)
+    assert b["path"] == "generic (co-residency refused)" and mcts.residency_fallbacks == 1
+    for key in ("dist", "values", "traj"):
+        assert np.array_equal(a[key], b[key]), key
+    # captured: raised, not a fallback inside the capture
+    roots = EfficientZeroMCTSCtree.roots(B, [list(range(6))] * B)
+    roots.prepare_no_noise([0.0] * B, a["logits0"].tolist(), [-1] * B)
+    seeds = torch.arange(S, dtype=torch.int32, device=DEV)
+    to_play = torch.full((B,), -1, dtype=torch.int32, device=DEV)
+    roots.tree.reserve(S)  # (no allocation or host copy inside the capture)
+    roots.tree.set_pb_c(19652, 1.25)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with pytest.raises(_lib.ResidencyError):
+        with torch.cuda.graph(g):
+            mcts.search(roots, model, a["lat0"], a["hidden0"], to_play, seeds=seeds)
+    assert mcts.residency_fallbacks == 1

@@ -20,21 +20,41 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.gpu
-@pytest.mark.timeout(240)
-@pytest.mark.parametrize("env", ["cartpole", "breakout"])
-def test_sharded_device_collect_all_gather_world2(tmp_path, env):
-    """env: config 2's CartPole shard, or config 5's Breakout shard (conv search, u8 image frames)"""
+def _run_world2(tmp_path, env, mode):
     world, port = 2, _free_port()
     procs = []
     for rank in range(world):
         penv = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                     MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "dist_gpu_worker.py"),
-                                       str(tmp_path), env], env=penv, cwd=REPO))
+                                       str(tmp_path), env, mode], env=penv, cwd=REPO))
     codes = [p.wait(timeout=200) for p in procs]
     assert codes == [0] * world, f"worker exit codes {codes}"
-    outs = [np.load(tmp_path / f"out_{r}.npz") for r in range(world)]
+    return [np.load(tmp_path / f"out_{r}.npz") for r in range(world)]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+def test_sharded_device_collect_gather_to_learner_world2(tmp_path):
+    """gather-to-learner (config 5's Breakout shard): rank 0 receives both ranks' episodes, rank 1 none;
+    the summed statistics count exactly the episodes the learner received"""
+    outs = _run_world2(tmp_path, "breakout", "gather")
+    r0, r1 = outs
+    assert set(r0["ranks"].tolist()) == {0, 1} and np.all(np.diff(r0["ranks"]) >= 0)
+    assert np.array_equal(r0["lens"][r0["ranks"] == 0], r0["own"])
+    assert int(r1["sent"]) > 0 and tuple(r0["shape"]) == (1, 64, 64)
+    for o in outs:
+        assert int(o["world"]) == 2 and int(o["total_episodes"]) == len(r0["ranks"])
+        assert int(o["total_envstep"]) == int(r0["envstep"]) + int(r1["envstep"])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("env", ["cartpole", "breakout"])
+def test_sharded_device_collect_all_gather_world2(tmp_path, env):
+    """env: config 2's CartPole shard, or config 5's Breakout shard (conv search, u8 image frames)"""
+    world = 2
+    outs = _run_world2(tmp_path, env, "all_gather")
     # every rank holds the same gathered set: both ranks' episodes, in rank order
     assert np.array_equal(outs[0]["ranks"], outs[1]["ranks"]) and np.array_equal(outs[0]["lens"], outs[1]["lens"])
     assert set(outs[0]["ranks"].tolist()) == set(range(world))

@@ -110,6 +110,9 @@ def test_device_path_segments_match_restatement(n, n_ep, gsl, prio):
         for e in sum(eps, []):
             assert (e["visits"].sum(axis=1) == 12).all() and (e["reward"] == 1.0).all()
             assert np.all(np.abs(e["obs"][0]) <= 0.05 + 1e-7)
+        # the logged episode return is CartPole's reward sum (eval_episode_return), one per counted episode
+        info = col._episode_info[-n_ep:]
+        assert [d['reward'] for d in info] == [float(d['step']) for d in info]
         seen.append(segs[0].obs_segment.copy())
     assert not np.array_equal(seen[0], seen[1])  # the second collect plays fresh episodes
 
@@ -140,3 +143,14 @@ def test_device_path_breakout_segments_match_restatement():
         assert len(g.obs_segment) >= 4 + len(g.action_segment)
     for e in sum(eps, []):
         assert (e["visits"].sum(axis=1) == 8).all() and set(np.unique(e["reward"])) <= {0.0, 1.0}
+    # the logged reward is each counted episode's UNCLIPPED score (eval_episode_return), as replayed
+    # through the restated game; the clipped rewards only count the scoring steps
+    from oracle import breakout_synth
+    counted = [e for r in col.last_schedule.played for e in r]
+    info = col._episode_info[-n_ep:]
+    assert sorted(d['reward'] for d in info) == sorted(float(e["episode_return"]) for e in counted)
+    for e in counted:
+        fr = np.rint(e["obs_segment"] * 255).astype(np.uint8)
+        assert e["episode_return"] >= e["reward_segment"].sum()
+        assert breakout_synth.replay_episode(fr, e["action_segment"], e["reward_segment"], 150,
+                                             episode_return=e["episode_return"]) is None

@@ -79,6 +79,28 @@ def test_device_philox_known_answers():
                             [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]]
 
 
+def test_dpp_butterflies_equal_shfl_xor():
+    """lzm_tree.h's DPP / permlane xor_partner<D> picks lane ^ D for all 64 lanes and every D, and
+    xor_sum / xor_max give the same bits as the __shfl_xor (ds_bpermute) butterflies they replaced"""
+    rng = np.random.default_rng(7)
+    for case in range(4):
+        v = rng.normal(size=64).astype(np.float32) * np.float32(10.0 ** (case - 1))
+        if case == 3:
+            v[::3] = np.float32(-0.0)
+        x = torch.from_numpy(v).to(DEV)
+        out = torch.empty((16, 64), dtype=torch.float32, device=DEV)
+        call("lzm_debug_xor", ptr(x), ptr(out), stream_ptr())
+        o = out.cpu().numpy()
+        lanes = np.arange(64)
+        for k in range(6):
+            want = v[lanes ^ (1 << k)]
+            assert np.array_equal(o[k].view(np.uint32), want.view(np.uint32)), f"xor_partner<{1 << k}>"
+            assert np.array_equal(o[6 + k].view(np.uint32), want.view(np.uint32)), f"__shfl_xor {1 << k}"
+        assert np.array_equal(o[12].view(np.uint32), o[13].view(np.uint32)), "xor_sum"
+        assert np.array_equal(o[14].view(np.uint32), o[15].view(np.uint32)), "xor_max"
+        assert (o[14] == v.max()).all()
+
+
 def torch_inverse_scalar_transform(logits, support_size, eps=0.001):
     """fp32 restatement of InverseScalarTransform.__call__ (scaling_transform.py:118-128)."""
     s = logits.sum(dim=1, keepdim=True)

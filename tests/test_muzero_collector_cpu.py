@@ -186,3 +186,19 @@ def test_game_segment_surface():
     assert g.child_visit_segment.dtype == object  # ragged
     assert g.obs_segment.shape == (6, 4) and g.reward_segment.shape == (4,)
     assert torch is not None
+
+
+def test_device_path_routes_plain_muzero_policies_only():
+    """a DeviceEnvManager selects the device collector for a MuZero policy only: an EfficientZero policy
+    (a MuZeroCollectPolicy subclass) keeps the host loop with its value-prefix / LSTM search"""
+    from lightzero_amd.envs import DeviceBreakoutEnvManager
+    from lightzero_amd.policy import EfficientZeroCollectPolicy, MuZeroCollectPolicy
+    cfg = policy_config(num_simulations=4, device='cpu',
+                        model=dict(frame_stack_num=4, action_space_size=4, observation_shape=(4, 64, 64),
+                                   image_channel=1, model_type='conv'))
+    model = torch.nn.Linear(1, 1)  # (routing only: no forward)
+    env = DeviceBreakoutEnvManager(4, seed=1)
+    for cls, device_path in ((MuZeroCollectPolicy, True), (EfficientZeroCollectPolicy, False)):
+        col = MuZeroCollector(env=env, policy=cls(cfg, model), policy_config=cfg)
+        assert col._device_path(False) is device_path, cls.__name__
+        assert col._device_path(True) is False  # collect_with_pure_policy: the host loop
