@@ -80,6 +80,9 @@ def parse():
     p.add_argument("--rccl-world1", type=int, default=1,
                    help="N = 1: still run under a one-rank RCCL process group, so the collect steps' trajectory "
                         "return and statistics all-reduce go through RCCL as on the 8-GPU node (0: no group)")
+    p.add_argument("--configs", default="1,3,4",
+                   help="with one GPU, also time these BASELINE.json configs into the line ('config1', 'config3', "
+                        "'config4' objects, each with its roofline and CPU baseline); 'none' skips them")
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: the ranks join a gloo group and rank 0 prints who joined")
     return p.parse_args()
@@ -176,10 +179,22 @@ def build_conv_model(device, seed=0, zero_heads=False):
     return m.to(device).eval()
 
 
+def build_ez_model(device, seed=0, zero_heads=False):
+    """config 3's network: the restated conv EfficientZeroModel at Pong's shapes (atari_efficientzero_config.py:
+    obs 4x64x64, 6 actions, LSTM 512, support 101), random weights (non-zero heads unless zero_heads) and BN
+    stats"""
+    from lightzero_amd.model_conv import atari_efficientzero_model
+    torch.manual_seed(seed)
+    m = atari_efficientzero_model(last_linear_layer_init_zero=bool(zero_heads))
+    _random_bn(m, seed + 1)
+    return m.to(device).eval()
+
+
 WORKLOADS = {
-    # name: (actions, observation shape, device env of the collect step)
-    "cartpole": (2, (4,), "cartpole"),
-    "breakout": (4, (4, 64, 64), "breakout"),
+    # name: (actions, observation shape, device env of the collect step, support_scale)
+    "cartpole": (2, (4,), "cartpole", 300),
+    "breakout": (4, (4, 64, 64), "breakout", 300),
+    "pong": (6, (4, 64, 64), None, 50),
 }
 
 
@@ -187,22 +202,23 @@ def synthetic_obs(workload, B, rng):
     """config 2: N(0,1) [B, 4]; config 5: frames U{0..255}/255 [B, 4, 64, 64]"""
     if workload == "cartpole":
         return rng.normal(size=(B, 4)).astype(np.float32)
-    return (rng.integers(0, 256, size=(B, 4, 64, 64)).astype(np.float32) / 255.0).astype(np.float32)
+    return (rng.integers(0, 256, size=(B, 4, 64, 64)).astype(np.float32) / 255.0).astype(np.float32)  # (Atari)
 
 
 class GraphStep:
-    """One collect-time search pass (muzero.py:617-690) as one HIP graph (DeviceSearchStep):
-    initial_inference -> Roots.prepare (noise) -> one-launch search -> distributions / values; the
-    traverse seeds advance on the device every replay. workload: config 2 (MLP) or config 5 (conv,
-    BN-folded initial inference + lzm_search_conv)."""
+    """One collect-time search pass (muzero.py:617-690; efficientzero.py:538-656) as one HIP graph
+    (DeviceSearchStep): initial_inference -> Roots.prepare (noise) -> one-launch search -> distributions /
+    values; the traverse seeds advance on the device every replay. workload: config 2 / 1 (MLP), config 5
+    (conv MuZero: BN-folded initial inference + lzm_search_conv) or config 3 ("pong": conv EfficientZero,
+    + lzm_search_conv_ez with the reward LSTM)."""
 
     def __init__(self, B, S, model, device, rng_mode, seed, workload="cartpole"):
         from lightzero_amd.collect import DeviceSearchStep
         rng = np.random.default_rng(seed)
-        A, shape, _ = WORKLOADS[workload]
+        A, shape, _, scale = WORKLOADS[workload]
         self.B, self.S = B, S
         self.step = DeviceSearchStep(model, B, S, [list(range(A))] * B, shape, device, noise_weight=0.25, seed=seed,
-                                     rng_mode=rng_mode, graph=True)
+                                     rng_mode=rng_mode, graph=True, support_scale=scale)
         self.step.set_inputs(obs=torch.from_numpy(synthetic_obs(workload, B, rng)).to(device),
                              noises=torch.from_numpy(rng.dirichlet([0.3] * A, size=B).astype(np.float32)).to(device))
         self.mcts = self.step.mcts
@@ -303,7 +319,7 @@ def kernel_timing(step, n_search=3):
     the mean search depth d-bar from the kernels' own search_len output."""
     from lightzero_amd import mcts_ctree as mc
     mcts = step.mcts
-    names = ("traverse", "decode_backprop", "search_mlp", "search_conv")
+    names = ("traverse", "decode_backprop", "search_mlp", "search_conv", "search_conv_ez")
     orig = {n: getattr(mc.DeviceTree, n) for n in names}
     acc = {n: [] for n in names}
     depth = []
@@ -365,17 +381,30 @@ def mlp_flops_per_sim(H, A, F, V, res=True):
 
 
 def conv_flops_per_sim(model, B, device):
-    """(all, matrix) FLOPs of one recurrent_inference row of the conv MuZeroModel (torch
-    FlopCounterMode at batch B: the convolutions are the trunk on the split-bf16 MFMA path, the
-    Linears the head MLPs on the VALU)"""
+    """(all, matrix-pipe) FLOPs of one recurrent_inference row of the conv MuZeroModel / EfficientZeroModel
+    (torch FlopCounterMode at batch B: the convolutions are the trunk on the split-bf16 MFMA path, the
+    Linears the head MLPs on the VALU). EfficientZero's reward LSTM, which the counter does not see inside
+    nn.LSTM, is counted by hand as its gate GEMM, 2 x 4H x (K + H) per row (K = reward planes, H = 512),
+    on the matrix pipe too (lzm_ez_lstm_step)."""
     from torch.utils.flop_counter import FlopCounterMode
     lat = torch.zeros(B, 64, 8, 8, device=device)
     act = torch.zeros(B, dtype=torch.int64, device=device)
+    ez = hasattr(model.dynamics_network, "lstm")
     with torch.no_grad(), FlopCounterMode(display=False) as fc:
-        model.recurrent_inference(lat, act)
+        if ez:
+            z = torch.zeros(1, B, model.lstm_hidden_size, device=device)
+            model.recurrent_inference(lat, (z, z), act)
+        else:
+            model.recurrent_inference(lat, act)
     per_op = {str(k): v for k, v in fc.get_flop_counts().get("Global", {}).items()}
-    conv = sum(v for k, v in per_op.items() if "convolution" in k)
-    return fc.get_total_flops() / B, conv / B
+    total = fc.get_total_flops() / B
+    matrix = sum(v for k, v in per_op.items() if "convolution" in k) / B
+    if ez:
+        lstm = model.dynamics_network.lstm
+        gate = 2.0 * 4 * lstm.hidden_size * (lstm.input_size + lstm.hidden_size)
+        total += gate - sum(v for k, v in per_op.items() if "lstm" in k) / B
+        matrix += gate
+    return total, matrix
 
 
 def shard_seed(rank):
@@ -713,22 +742,26 @@ def check_step(step, S, fused):
 
 
 def conv_roofline(step, model, B, S, device):
-    """config 5's dominant kernel, search_conv_kernel (one launch = B x S simulations): the trunk's
-    convolutions run on the bf16 matrix pipe as split-bf16 (three bf16 terms per f32 operand, six
-    products per f32 product), so the bound is the dense BF16 MFMA peak against 6x the
-    algorithmic conv FLOPs; the f32-equivalent rate and the head MLPs (VALU) ride beside."""
+    """configs 5 / 3: the dominant kernel, search_conv_kernel / search_conv_ez_kernel (one launch = B x S
+    simulations): the trunk's convolutions (and EZ's LSTM gate GEMM) run on the bf16 matrix pipe as
+    split-bf16 (three bf16 terms per f32 operand, six products per f32 product), so the
+    bound is the dense BF16 MFMA peak against 6x the algorithmic matrix FLOPs; the f32-equivalent rate
+    and the head MLPs (VALU) ride beside."""
     ms, dbar = kernel_timing(step)
-    sec = ms["search_conv"] * 1e-3
+    ez = "search_conv_ez" in ms
+    key, kname = ("search_conv_ez", "search_conv_ez_kernel") if ez else ("search_conv", "search_conv_kernel")
+    sec = ms[key] * 1e-3
     flops, conv = conv_flops_per_sim(model, B, device)
     mfma = 6.0 * conv * B * S / sec / 1e12
     f32 = flops * B * S / sec / 1e12
     return {"bound": "mfma", "compute": "split-bf16 MFMA (v_mfma_f32_16x16x32_bf16, 6 products per f32 product) "
-                                        "for the conv trunk; head MLPs on the fp32 VALU",
-            "kernel": "search_conv_kernel", "achieved": round(mfma, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(mfma / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic("search_conv_kernel"),
+                                        "for the conv trunk" + (" and the LSTM gate GEMM" if ez else "") +
+                                        "; head MLPs on the fp32 VALU",
+            "kernel": kname, "achieved": round(mfma, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(mfma / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(kname),
             "alg_flops_per_sim": int(flops), "alg_conv_flops_per_sim": int(conv),
             "alg_f32_tflops": round(f32, 2), "alg_f32_frac_of_fp32_peak": round(f32 / FP32_PEAK_TFLOPS, 4),
-            "launch_us": round(ms["search_conv"] * 1e3, 1), "sims_per_launch": B * S,
+            "launch_us": round(ms[key] * 1e3, 1), "sims_per_launch": B * S,
             "mean_search_len": round(dbar, 3)}
 
 
@@ -809,6 +842,186 @@ def secondary_breakout(args, world, rank, device):
     return out
 
 
+# ---------------------------------------------------------------------------------- configs 1, 3, 4
+AZ_LINES = ((0, 1, 2), (3, 4, 5), (6, 7, 8), (0, 3, 6), (1, 4, 7), (2, 5, 8), (0, 4, 8), (2, 4, 6))
+
+
+def az_boards(n, seed, max_moves=4):
+    """config 4's synthetic positions: n TicTacToe boards, each reached by
+    k ~ U{0..max_moves} random legal moves from the empty board (player 1 first), none terminal; returns
+    (boards int32 [n, 9] with 0 empty / 1 / 2, start_player_index int32 [n]: 0 = player 1 to move)"""
+    rng = np.random.default_rng(seed)
+    boards, starts = [], []
+    while len(boards) < n:
+        b = np.zeros(9, np.int32)
+        p = 1
+        for _ in range(int(rng.integers(0, max_moves + 1))):
+            b[int(rng.choice(np.flatnonzero(b == 0)))] = p
+            p = 3 - p
+        if any(b[i] and b[i] == b[j] == b[k] for i, j, k in AZ_LINES) or not (b == 0).any():
+            continue
+        boards.append(b)
+        starts.append(p - 1)
+    return np.stack(boards), np.asarray(starts, np.int32)
+
+
+def load_calibration_key(name):
+    """a reference-vs-port timing ratio measured in the build container (tools/cpu_calibration.py)"""
+    try:
+        with open(os.path.join(REPO, "profiles", "cpu_calibration.json")) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline_ptree(B, S, secs):
+    """config 1's CPU baseline: the reference's own architecture for it — the pure-Python tree (ptree_mz.py,
+    mcts_ptree.py:92-194) restated transcript-exact in oracle/ptree_port.py ("port"), MuZeroModelMLP on
+    torch-CPU, 1 thread, for about `secs` (tools/ptree_bench.py)"""
+    from tools.ptree_bench import run
+    torch.set_num_threads(1)
+    v, n, el = run(B, S, secs, False)
+    cal = None
+    try:
+        with open(os.path.join(REPO, "profiles", "ptree_calibration.json")) as f:
+            cal = {"ref_over_port_time": json.load(f)["ref_over_port_time"]}
+    except (OSError, ValueError, KeyError):
+        pass
+    return {"value": round(v, 1), "unit": "sims/s", "cores": 1, "kind": "port",
+            "sample": f"{n} searches (B={B}, S={S}) of the ptree search loop over oracle/ptree_port.py (transcript-"
+                      f"exact restatement of ptree_mz.py), MuZeroModelMLP on torch-CPU, 1 thread, {el:.1f}s",
+            "host": host_cpu_info(), "calibration": cal}
+
+
+def cpu_baseline_az(model, boards, starts, S, secs):
+    """config 4's CPU baseline: the reference AlphaZero search architecture (policy/alphazero.py:239-265,
+    371-380: one tree per board, the network called per leaf, batch 1) over the bit-exact restatement of
+    mcts_alphazero.cpp (oracle/az_oracle.py, "port") with the same AlphaZeroModel on torch-CPU, 1 thread,
+    boards in order until about `secs`"""
+    import copy
+    from oracle import az_oracle
+    torch.set_num_threads(1)
+    net = copy.deepcopy(model).cpu().eval()
+    table = az_oracle.noise_table(0.3)
+
+    def pv(board, legal):
+        b = np.asarray(board).reshape(3, 3)
+        me = 1 if (b == 1).sum() == (b == 2).sum() else 2  # player 1 moved first from the empty board
+        x = np.stack([(b == me), (b == 3 - me), np.full((3, 3), me)]).astype(np.float32) / 2
+        with torch.no_grad():
+            probs, value = net.compute_policy_value(torch.from_numpy(x).unsqueeze(0))
+        p = probs.squeeze(0).numpy()
+        return {int(a): float(p[a]) for a in legal}, float(value.item())
+
+    n, t0 = 0, time.perf_counter()
+    while True:
+        az_oracle.search(boards[n % len(boards)], int(starts[n % len(boards)]), S, pv, True, table=table)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= secs:
+            break
+    return {"value": round(n * S / el, 1), "unit": "sims/s", "cores": 1, "kind": "port",
+            "sample": f"{n} board searches x {S} sims of the reference's per-board search with per-leaf network "
+                      f"calls over oracle/az_oracle.py (restatement of mcts_alphazero.cpp), AlphaZeroModel on "
+                      f"torch-CPU, 1 thread, {el:.1f}s",
+            "host": host_cpu_info(), "calibration": load_calibration_key("az")}
+
+
+def config1(args, device, cpu):
+    """BASELINE.json config 1's shape (8 envs x 25 sims, CartPole MuZero MLP): the reference runs it on the
+    CPU with its pure-Python tree; here the same collect-time search as the headline on the GPU"""
+    B, S = 8, 25
+    model = build_model(device, args.zero_heads, seed=0)
+    step = GraphStep(B, S, model, device, args.rng, seed=shard_seed(0))
+    steps = max(args.steps, 50)
+    el, _ = timed_run(step, steps, args.warmup, 1, device)
+    tie, sdiag = check_step(step, S, True)
+    out = {"workload": f"CartPole-v0 MuZero (BASELINE.json config 1 shape), {B} envs x {S} sims, MuZeroModelMLP",
+           "value": round(B * S * steps / el, 1), "unit": "sims/s", "ms_per_step": round(el / steps * 1e3, 4),
+           "steps": steps, "n_gpus": 1, "dtype": "f32", "tie_stream_errors": tie, "search_diag": sdiag,
+           "roofline": mlp_roofline(step, B, S, device)}
+    if cpu:
+        out["cpu_baseline"] = cpu_baseline_ptree(B, S, 0.15 * args.cpu_baseline_secs)
+    return out
+
+
+def config3(args, device, cpu):
+    """BASELINE.json config 3: Pong EfficientZero, 256 envs x 50 sims on one GPU, as the collect-time step
+    (efficientzero.py:538-656): BN-folded conv initial inference (the representation network included),
+    root preparation, the one-launch EZ search with the reward LSTM, root outputs — one HIP graph"""
+    B, S = args.envs, args.sims
+    model = build_ez_model(device, seed=0, zero_heads=args.zero_heads)
+    step = GraphStep(B, S, model, device, args.rng, seed=shard_seed(0), workload="pong")
+    steps = max(args.steps, 20)
+    el, _ = timed_run(step, steps, args.warmup, 1, device)
+    tie, sdiag = check_step(step, S, True)
+    out = {"workload": f"Atari Pong EfficientZero (BASELINE.json config 3), {B} envs x {S} sims, conv "
+                       f"EfficientZeroModel (4x64x64 frames, latent 64x8x8, LSTM 512, support 101, 6 actions)",
+           "step": "collect-time search (initial inference + prepare + search + root outputs)",
+           "value": round(B * S * steps / el, 1), "unit": "sims/s", "ms_per_step": round(el / steps * 1e3, 4),
+           "steps": steps, "n_gpus": 1, "dtype": "f32 (convolutions as split-bf16 MFMA)",
+           "search_path": step.mcts.last_path, "tie_stream_errors": tie, "search_diag": sdiag,
+           "data": "synthetic (random-init conv EfficientZeroModel, synthetic frames)",
+           "roofline": conv_roofline(step, model, B, S, device)}
+    if cpu:
+        out["cpu_baseline"] = cpu_baseline_conv("ez", B, S, model, 0.5 * args.cpu_baseline_secs, device)
+    return out
+
+
+def config4(args, device, cpu):
+    """BASELINE.json config 4: TicTacToe AlphaZero self-play, 512 boards x 100 sims on one GPU: the whole
+    batched search (roots with the reference's noise, 100 simulations with the AlphaZeroModel in the
+    kernel, the final action draw) as one lzm_az_search_fused launch per step"""
+    from torch.utils.flop_counter import FlopCounterMode
+    from lightzero_amd.alphazero import AlphaZeroMCTS, FusedAZNet
+    from lightzero_amd.model_az import tictactoe_alphazero_model
+    B, S = 512, 100
+    torch.manual_seed(0)
+    model = tictactoe_alphazero_model().to(device).eval()
+    boards, starts = az_boards(B, 0)
+    db = torch.from_numpy(boards).to(device)
+    ds = torch.from_numpy(starts).to(device)
+    m = AlphaZeroMCTS(9, S, 19652, 1.25, 0.3, 0.25, device=device)
+    fnet = FusedAZNet(model)
+    steps = max(args.steps, 20)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            m.search_fused(db, ds, fnet, 1.0, True)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record()  # (the launch stream: torch's current stream, as every lzm_* call)
+        for _ in range(steps):
+            m.search_fused(db, ds, fnet, 1.0, True)
+        e1.record()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+    visits = m.last_visits(B)
+    assert bool((visits.sum(dim=1) == S).all()), "AlphaZero root visits do not sum to num_simulations"
+    with torch.no_grad(), FlopCounterMode(display=False) as fc:
+        model.compute_policy_value(torch.zeros(B, 3, 3, 3, device=device))
+    per_op = {str(k): v for k, v in fc.get_flop_counts().get("Global", {}).items()}
+    flops = fc.get_total_flops() / B
+    conv = sum(v for k, v in per_op.items() if "convolution" in k) / B
+    sec = e0.elapsed_time(e1) * 1e-3 / steps
+    ach = conv * B * S / sec / 1e12
+    out = {"workload": f"TicTacToe AlphaZero self-play (BASELINE.json config 4), {B} boards x {S} sims, "
+                       f"AlphaZeroModel (1 residual block x 16 channels)",
+           "value": round(B * S * steps / el, 1), "unit": "sims/s", "ms_per_step": round(el / steps * 1e3, 4),
+           "steps": steps, "n_gpus": 1, "dtype": "f32", "data": "synthetic (random-init AlphaZeroModel, random "
+                                                                "legal positions)",
+           "roofline": {"bound": "mfma", "compute": "exact f32 MFMA (v_mfma_f32_16x16x4_f32) for the convolutions, "
+                                                    "heads on the VALU",
+                        "kernel": "az_search_fused_kernel", "achieved": round(ach, 3), "peak": FP32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 5),
+                        "traffic": pmc_traffic("az_search_fused_kernel"), "alg_flops_per_sim": int(flops),
+                        "alg_conv_flops_per_sim": int(conv), "launch_us": round(sec * 1e6, 1),
+                        "sims_per_launch": B * S}}
+    if cpu:
+        out["cpu_baseline"] = cpu_baseline_az(model, boards, starts, S, 0.2 * args.cpu_baseline_secs)
+    return out
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -862,6 +1075,17 @@ def main():
         del step
         torch.cuda.empty_cache()
         config5 = secondary_breakout(args, world, rank, device)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            config5["cpu_baseline"] = cpu_baseline_conv("mz", args.envs, args.sims, build_conv_model(device, seed=0),
+                                                        0.5 * args.cpu_baseline_secs, device)
+    extra = {}
+    wanted = [c for c in args.configs.split(",") if c and c != "none"]
+    if wl == "cartpole" and args.path == "fused" and world == 1:
+        # the single-GPU configs of BASELINE.json beside the headline (the SCALE runs, N > 1, skip them)
+        for c in wanted:
+            fn = {"1": config1, "3": config3, "4": config4}[c]
+            torch.cuda.empty_cache()
+            extra[f"config{c}"] = fn(args, device, not args.no_cpu_baseline)
     if rank == 0:
         metric = ("MCTS simulations/sec (whole node), 256 parallel envs x 50 sims/step" if wl == "cartpole" else
                   "MCTS simulations/sec (whole node), Breakout MuZero, 256 envs per GPU x 50 sims/step")
@@ -879,7 +1103,7 @@ def main():
                 "process_group": (dist.get_backend() if dist.is_initialized() else None) if rccl1 is None
                 else {"world1": rccl1},
                 "tie_stream_errors": tie_errors, "search_diag": sdiag, "ranks": ranks,
-                "trajectory": traj, "roofline": roofline, "cpu_baseline": cpu, "config5": config5}
+                "trajectory": traj, "roofline": roofline, "cpu_baseline": cpu, "config5": config5, **extra}
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

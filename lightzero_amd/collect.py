@@ -2,9 +2,12 @@
 
 MuZeroPolicy._forward_collect (lzero/policy/muzero.py:617-690) runs, per env step:
 initial_inference -> Roots.prepare (Dirichlet-mixed root priors) -> MuZeroMCTSCtree.search ->
-get_distributions / get_values. `DeviceSearchStep` runs exactly that sequence on device tensors
-and captures it as ONE HIP graph, so a step costs one graph launch: no Python glue, no host copies
-between the network, the root preparation and the fused search. The traverse seeds (the
+get_distributions / get_values; EfficientZeroPolicy._forward_collect (efficientzero.py:538-656) the
+same with the value-prefix roots and the initial inference's reward_hidden_state (LSTM (c, h), zeros)
+handed to EfficientZeroMCTSCtree.search. `DeviceSearchStep` runs exactly that sequence on device
+tensors — for a MuZero model or, picked from the model (a dynamics network with an LSTM), an
+EfficientZero one — and captures it as ONE HIP graph, so a step costs one graph launch: no Python
+glue, no host copies between the network, the root preparation and the fused search. The traverse seeds (the
 reference's per-call srand(tv_usec) values) are derived on the device from a replay counter,
 usec_k = (1000003 * seed + n) mod 10^6 for the n-th traverse of the run (the SequentialSeeds rule
 of tests and bench), so every replay is a fresh search.
@@ -18,7 +21,7 @@ import torch
 
 from .conv_infer import folded_initial_or_none
 from .initial import FusedInitialInference, fused_initial_or_none
-from .mcts_ctree import MuZeroMCTSCtree, _step_net
+from .mcts_ctree import EfficientZeroMCTSCtree, MuZeroMCTSCtree, _step_net
 from .utils import EasyDict
 
 
@@ -36,12 +39,17 @@ class DeviceSearchStep:
         self.B, self.S = int(num_envs), int(num_simulations)
         self.device = torch.device(device)
         self.noise_weight = float(noise_weight)
+        # EfficientZero models (value prefix + reward LSTM): EfficientZeroMCTSCtree with the policy's
+        # lstm_horizon_len (efficientzero.py default 5)
+        self.ez = hasattr(getattr(model, "dynamics_network", None), "lstm")
         cfg = dict(num_simulations=self.S, discount_factor=float(discount_factor), device=self.device,
                    model=dict(support_scale=int(support_scale), categorical_distribution=True))
+        if self.ez:
+            cfg["lstm_horizon_len"] = 5
         cfg.update(cfg_extra or {})
-        self.mcts_cls = MuZeroMCTSCtree
+        self.mcts_cls = EfficientZeroMCTSCtree if self.ez else MuZeroMCTSCtree
         self.rng_mode = rng_mode
-        self.mcts = MuZeroMCTSCtree(EasyDict(cfg))
+        self.mcts = self.mcts_cls(EasyDict(cfg))
         self.legal = [list(l) for l in legal_actions]
         self.A = max(len(l) for l in self.legal)
         dev = self.device
@@ -91,9 +99,13 @@ class DeviceSearchStep:
                 dist = torch.empty((self.B, t.A), dtype=torch.int32, device=self.device)
                 values = torch.empty(self.B, dtype=torch.float32, device=self.device)
                 # (an epilogue reads the counter of this step: it advances after the epilogue)
-                self.mcts.search(self.roots, self.model, out.latent_state, self.to_play,
-                                 step=dict(count=self._count, base=self._base, dist=dist, values=values,
-                                           increment=self.epilogue is None))
+                stp = dict(count=self._count, base=self._base, dist=dist, values=values,
+                           increment=self.epilogue is None)
+                if self.ez:  # the roots' LSTM state: the initial inference's reward_hidden_state (zeros)
+                    self.mcts.search(self.roots, self.model, out.latent_state, out.reward_hidden_state, self.to_play,
+                                     step=stp)
+                else:
+                    self.mcts.search(self.roots, self.model, out.latent_state, self.to_play, step=stp)
                 res = dict(distributions=dist, values=values, latent_state=out.latent_state,
                            policy_logits=out.policy_logits, value_logits=out.value)
                 if self.epilogue is not None:
@@ -142,8 +154,9 @@ class DeviceSearchStep:
         if self.initial is not None:
             self.initial.refresh()
         if self.roots is not None and self.roots.tree is not None:
-            if self.mcts._fused(self.model, self.roots.tree) is None:
-                # generic path (e.g. a conv model): the folded step network re-folds in place
+            fused = getattr(self.mcts, "_fused", None)  # (MuZero's packed-MLP one-launch search)
+            if fused is None or fused(self.model, self.roots.tree) is None:
+                # conv models (MuZero or EfficientZero): the folded step network re-folds in place
                 _step_net(self.mcts, self.model)
 
     def step(self):

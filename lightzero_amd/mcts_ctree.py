@@ -609,8 +609,10 @@ class EfficientZeroMCTSCtree(object):
 
     def search(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
                reward_hidden_state_roots: List[Any], to_play_batch: Union[int, List[Any]],
-               seeds: torch.Tensor = None) -> None:
-        """seeds: optional device int32 [num_simulations] traverse seeds (see MuZeroMCTSCtree.search)."""
+               seeds: torch.Tensor = None, step: dict = None) -> None:
+        """seeds: optional device int32 [num_simulations] traverse seeds; step: the collect step's glue
+        (lightzero_amd.collect: device seeds from a step counter, root outputs into device tensors, the
+        counter advanced) — both as in MuZeroMCTSCtree.search, here as small launches around the search."""
         with torch.no_grad():
             model.eval()
             t = roots.tree
@@ -639,7 +641,11 @@ class EfficientZeroMCTSCtree(object):
             buf.extra[0][0].copy_(hc0)
             buf.extra[1][0].copy_(hh0)
             buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
-            buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
+            if step is not None:  # seeds (base + count * S + k) mod 10^6 on the device
+                _lib.call("lzm_seed_sequence", _lib.ptr(step["count"]), int(step["base"]), S, _lib.ptr(buf.seeds),
+                          _lib.stream_ptr())
+            else:
+                buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
             if getattr(self, "record", False):
                 rec = _Recorder(S, B, t.A, dev)
                 rec.is_reset = torch.zeros((S, B), dtype=torch.int32, device=dev)
@@ -673,6 +679,11 @@ class EfficientZeroMCTSCtree(object):
             else:
                 self.last_path = "generic"
                 self._loop(t, model, buf, S, row, Hl, rec)
+            if step is not None:
+                _lib.call("lzm_get_root_outputs", t.h, _lib.ptr(step["dist"]), _lib.ptr(step["values"]),
+                          _lib.stream_ptr())
+                if step.get("increment", True):
+                    step["count"].add_(1)
             t.searched()
             roots._last_minmax = buf.mm
             self.last_record = rec

@@ -39,29 +39,10 @@ BF16_PEAK_TFLOPS = 2500.0  # dense (MI355X_MICROARCH.md), not the 2:1-sparse fig
 
 
 def recurrent_flops(model, kind, B, dev):
-    """(all FLOPs, matrix-pipe FLOPs) per simulation row: FlopCounterMode over recurrent_inference
-    (convolutions + Linears) plus, for EfficientZero, the reward LSTM's gate GEMM, which the counter
-    does not see (aten lstm kernels); the matrix-pipe part is the convolutions and the gate GEMM."""
-    from torch.utils.flop_counter import FlopCounterMode
-    lat = torch.zeros(B, 64, 8, 8, device=dev)
-    act = torch.zeros(B, dtype=torch.int64, device=dev)
-    with torch.no_grad(), FlopCounterMode(display=False) as fc:
-        if kind == "ez":
-            z = torch.zeros(1, B, model.lstm_hidden_size, device=dev)
-            model.recurrent_inference(lat, (z, z), act)
-        else:
-            model.recurrent_inference(lat, act)
-    per_op = {str(k): v for k, v in fc.get_flop_counts().get("Global", {}).items()}
-    total = fc.get_total_flops() / B
-    matrix = sum(v for k, v in per_op.items() if "convolution" in k) / B
-    if kind == "ez":
-        lstm = model.dynamics_network.lstm
-        H, K = lstm.hidden_size, lstm.input_size
-        gate = 2.0 * 4 * H * (K + H)
-        counted = sum(v for k, v in per_op.items() if "lstm" in k) / B
-        total += gate - counted
-        matrix += gate
-    return total, matrix
+    """(all FLOPs, matrix-pipe FLOPs) per simulation row (bench.conv_flops_per_sim: FlopCounterMode over
+    recurrent_inference plus, for EfficientZero, the reward LSTM's gate GEMM counted by hand)"""
+    import bench
+    return bench.conv_flops_per_sim(model, B, dev)
 
 
 def main():

@@ -14,9 +14,12 @@ can be read as reference numbers:
               host tree + MuZeroModelMLP on torch-CPU + InverseScalarTransform + list glue) with the
               reference's ctree and with the oracle, same threads.
 
+  az        : config 4, the per-board AlphaZero search with per-leaf network calls over the reference's
+              mcts_alphazero and over the port (oracle/az_oracle.py), 1 thread (--az: this entry only).
+
 Writes profiles/cpu_calibration.json with time ratios reference / port (> 1: the port is faster).
 
-    bash oracle/build_ref.sh && python tools/cpu_calibration.py
+    bash oracle/build_ref.sh && python tools/cpu_calibration.py [--az]
 """
 import glob
 import importlib.util
@@ -126,7 +129,62 @@ def ref_arch_ref(mod, B, S, model_cpu, secs, threads):
                 return n * B * S / el, n, el
 
 
+def az_calibration(secs=6.0):
+    """config 4: the reference's compiled mcts_alphazero (oracle/_ref) vs the port (oracle/az_oracle.py), each
+    driving the same AlphaZeroModel on torch-CPU per leaf (bench.cpu_baseline_az's loop), 1 thread, the same
+    boards; returns the "az" entry (time ratio reference / port)"""
+    paths = sorted(glob.glob(os.path.join(REPO, "oracle", "_ref", "mcts_alphazero*.so")))
+    if not paths:
+        sys.exit("oracle/_ref missing: run oracle/build_ref.sh first (build container only)")
+    spec = importlib.util.spec_from_file_location("mcts_alphazero", paths[0])
+    az = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(az)
+    from lightzero_amd.model_az import tictactoe_alphazero_model
+    from oracle.tictactoe import SimTicTacToe
+    torch.set_num_threads(1)
+    torch.manual_seed(0)
+    net = tictactoe_alphazero_model().eval()
+    boards, starts = bench.az_boards(64, 0)
+    S = 100
+
+    def pv(e):
+        legal = e.legal_actions
+        _, scaled = e.current_state()
+        with torch.no_grad():
+            probs, value = net.compute_policy_value(torch.from_numpy(scaled).float().unsqueeze(0))
+        return dict(zip(legal, probs.squeeze(0)[legal].numpy())), value.item()
+
+    def ref_rate():
+        mcts = az.MCTS(9, S, 19652, 1.25, 0.3, 0.25, SimTicTacToe(scale=True))
+        n, t0 = 0, time.perf_counter()
+        while True:
+            b, st = boards[n % len(boards)], starts[n % len(boards)]
+            mcts.get_next_action(dict(start_player_index=int(st), init_state=b.reshape(3, 3).astype(np.int32),
+                                      katago_policy_init=False, katago_game_state=None), pv, 1.0, True)
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return n * S / el
+
+    vr, vp = [], []
+    for _ in range(2):
+        vr.append(ref_rate())
+        vp.append(bench.cpu_baseline_az(net, boards, starts, S, secs)["value"])
+    return {"ref_sims_per_s": round(max(vr), 1), "port_sims_per_s": round(max(vp), 1), "threads": 1,
+            "loop": "per-board search, AlphaZeroModel on torch-CPU called per leaf (policy/alphazero.py:371-380)",
+            "ref_over_port_time": round(max(vp) / max(vr), 3)}
+
+
 def main():
+    if "--az" in sys.argv:  # refresh the config-4 entry only
+        out = os.path.join(REPO, "profiles", "cpu_calibration.json")
+        with open(out) as f:
+            res = json.load(f)
+        res["az"] = az_calibration()
+        with open(out, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res["az"], indent=1))
+        return
     mod = load_ref()
     B, S, A = 256, 50, 2
     tab = scripted(B, S, A)
@@ -150,6 +208,7 @@ def main():
     res["ref_arch"] = {"ref_sims_per_s": round(max(vr), 1), "port_sims_per_s": round(max(vp), 1),
                        "threads": threads, "network": "MuZeroModelMLP on torch-CPU"}
     res["ref_over_port_time_ref_arch"] = round(max(vp) / max(vr), 3)
+    res["az"] = az_calibration()
     out = os.path.join(REPO, "profiles", "cpu_calibration.json")
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
