@@ -268,6 +268,12 @@ class DeviceCollector:
         with one rank), else 0"""
         return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 0
 
+    def _check_search(self):
+        """the fused searches' tie-break stream intact (lzm_check_errors raises) before their episodes leave"""
+        roots = self.search.roots
+        if roots is not None and roots.tree is not None:
+            roots.tree.check_errors()
+
     def _return_blocks(self, steps, el, group, to_host=True, dst=None):
         self._check_search()
         block = self.pack_new()

@@ -1,0 +1,326 @@
+// lzm_repr.h — the representation network's downsampling stages of the Atari configs (BASELINE.json configs 3
+// and 5) on the split-bf16 matrix path: initial_inference's DownSample (lzero/model/common.py:164-265), with
+// every eval-mode BatchNorm folded into the convolution in front of it (lightzero_amd/conv_infer.py):
+//
+//   L1  y = relu(conv3x3_s2(obs, W1) + b1)                         obs [C <= 7][64][64] -> [32][32][32]
+//   L2  t = relu(conv3x3(y) + b)          L3  y = relu(conv3x3(t) + b + y)           (resblocks1)
+//   L4  d = relu(conv3x3_s2(y, W1) + b1), s = conv3x3_s2(y, W3)    [32][32][32] -> 2 x [64][16][16]
+//   L5  x = relu(conv3x3(d, W2) + b2 + s)                          (the downsample block)
+//   L6  t = relu(conv3x3(x) + b)          L7  x = relu(conv3x3(t) + b + x)           (resblocks2)
+//   avg_pool 3x3 / 2 (pad 1, count_include_pad) -> [64][8][8] NCHW, the 8 x 8 tail's input (lzm_conv_resnet8_p)
+//
+// One launch per convolution, activations NHWC f32 in HBM (the whole [B][32][32][32] stage is 33 MB at B = 256:
+// it stays in the Infinity Cache between layers). Each convolution is an implicit GEMM: rows = out channels
+// (the MFMA A operand: the folded weights, held in REGISTERS for the whole launch), columns = output pixels
+// (the B operand: read from an LDS image of the input halo), K = 9 taps x in-channels in chunks of 32, on
+// v_mfma_f32_16x16x32_bf16 with every f32 operand split into three bf16 terms (six products per K: f32-level
+// error, the trunk's scheme, lzm_conv.h). A persistent grid (one 4-wave workgroup per CU) walks 64-pixel
+// output tiles; the next tile's halo is loaded into registers before the current tile's MFMAs and written to
+// the other LDS buffer after them.
+//
+// LDS image of a halo, per bf16 term: [channel group g = 8 channels][position][8 bf16], a group's plane padded
+// to a multiple of 16 positions. A B-fragment read (lane: pixel l & 15 of a 16-pixel tile, channel group
+// g0 + (l >> 4)) touches 16 consecutive positions per group, so every ds_read_b128 lane group hits 16
+// distinct 16-B bank slots. Stride-2 convolutions store the halo's even and odd columns apart, which makes
+// their reads consecutive too. The first layer (C <= 7 input channels, NCHW) stages an im2col tile instead:
+// K = tap * C + channel, zero-padded to 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lzm_conv.h"
+
+namespace lzm {
+
+constexpr int kRpThreads = 256;
+
+struct ReprConvArgs {
+  int B, ntiles, cin_obs;  // cin_obs: first layer's input channels (MODE 2)
+  const float *in;         // NHWC [B][HIN][HIN][CIN] (MODE 2: NCHW obs [B][cin_obs][64][64])
+  const float *w;          // fragments [out tile][chunk][term][lane][8 bf16] (repr_pack)
+  const float *bias;       // [COUT] (MODE 1: [64], the first half's)
+  const float *res;        // nullable: NHWC residual of the output's shape
+  float *out;              // NHWC [B][HOUT][HOUT][COUT] (MODE 1: the first 64 channels)
+  float *out2;             // MODE 1: the shortcut's 64 channels, NHWC
+};
+
+// Geometry of one layer: WOUT-wide output rows, 64-pixel tiles of TR rows; halo HR x HC (bordered), LDS row
+// pitch ROWP (stride 2: even columns, then odd ones), group plane NPP positions (a multiple of 16).
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+struct ReprGeom {
+  static constexpr int TR = 64 / WOUT;
+  static constexpr int HR = MODE == 2 ? 1 : (TR - 1) * STRIDE + 3;
+  static constexpr int HC = MODE == 2 ? 64 : (WOUT - 1) * STRIDE + 3;
+  static constexpr int HC2 = (HC + 1) / 2;
+  static constexpr int ROWP = STRIDE == 2 && MODE != 2 ? 2 * HC2 : HC;
+  static constexpr int NP = HR * ROWP;
+  static constexpr int NPP = (NP + 15) / 16 * 16;
+  static constexpr int CG = MODE == 2 ? 8 : CIN / 8;                  // channel groups (MODE 2: 64 K / 8)
+  static constexpr int NCH = MODE == 2 ? 2 : 9 * (CIN / 32);          // K chunks of 32
+  static constexpr int OT = COUT / 16;                                // out-channel tiles
+  static constexpr int OTW = OT >= 4 ? OT / 4 : 1;                    // per wave
+  static constexpr int PTW = OT >= 4 ? 4 : 2;                         // pixel tiles per wave
+  static constexpr int TERM = CG * NPP * 8;                           // bf16 per term image
+  static constexpr int BUF = 3 * TERM;                                // bf16 per halo buffer
+  static constexpr int ITEMS = MODE == 2 ? 64 * 8 : HR * HC * CG;     // (position, group) staging items
+  static constexpr int IPT = (ITEMS + kRpThreads - 1) / kRpThreads;  // per thread
+  static constexpr int PPW = MODE == 2 ? 64 : 64 / CG;                // positions per wave-instruction
+};
+
+// the LDS position of halo (row hr, bordered column hc)
+template <class G, int STRIDE>
+__device__ __forceinline__ int rp_pos(int hr, int hc) {
+  if constexpr (STRIDE == 2) return hr * G::ROWP + (hc & 1) * G::HC2 + (hc >> 1);
+  else return hr * G::ROWP + hc;
+}
+
+// staging item q of a tile -> (LDS position, channel group); false past the last item
+template <class G, int STRIDE, int MODE>
+__device__ __forceinline__ bool rp_item(int q, int &hr, int &hc, int &g) {
+  if (q >= G::ITEMS) return false;
+  const int lin = (q >> 6) * G::PPW + (q & 63) % G::PPW;
+  g = (q & 63) / G::PPW;
+  if constexpr (MODE == 2) {
+    hr = 0;
+    hc = q & 63;  // pixel of the tile
+    g = q >> 6;
+    return true;
+  }
+  hr = lin / G::HC;
+  hc = lin % G::HC;
+  return true;
+}
+
+// load this thread's staging items of tile `tile` into registers (8 f32 per item)
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+__device__ __forceinline__ void rp_load(const ReprConvArgs &a, int tile, float4 (&v)[ReprGeom<CIN, COUT, STRIDE, WOUT, MODE>::IPT][2]) {
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
+  constexpr int HIN = WOUT * STRIDE;
+  constexpr int TPI = (WOUT / G::TR);  // tiles per image (square output: WOUT rows)
+  const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
+#pragma unroll
+  for (int i = 0; i < G::IPT; ++i) {
+    int hr, hc, g;
+    v[i][0] = v[i][1] = float4{0.f, 0.f, 0.f, 0.f};
+    if (!rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g)) continue;
+    if constexpr (MODE == 2) {
+      // im2col: pixel hc of the tile (row r0 + hc / 32, column hc % 32), K = 8 g .. 8 g + 7 = tap * C + c
+      const int oy = r0 + (hc >> 5), ox = hc & 31;
+      float e[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j, tap = k / a.cin_obs, c = k % a.cin_obs;
+        const int iy = 2 * oy + tap / 3 - 1, ix = 2 * ox + tap % 3 - 1;
+        e[j] = (tap < 9 && iy >= 0 && iy < 64 && ix >= 0 && ix < 64)
+                   ? a.in[(((int64_t)b * a.cin_obs + c) * 64 + iy) * 64 + ix] : 0.f;
+      }
+      v[i][0] = float4{e[0], e[1], e[2], e[3]};
+      v[i][1] = float4{e[4], e[5], e[6], e[7]};
+    } else {
+      const int iy = r0 * STRIDE - 1 + hr, ix = hc - 1;
+      if (iy >= 0 && iy < HIN && ix >= 0 && ix < HIN) {
+        const float4 *src = reinterpret_cast<const float4 *>(a.in + (((int64_t)b * HIN + iy) * HIN + ix) * CIN + 8 * g);
+        v[i][0] = src[0];
+        v[i][1] = src[1];
+      }
+    }
+  }
+}
+
+// split the loaded items into the three bf16 term images of an LDS halo buffer
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+__device__ __forceinline__ void rp_store(uint16_t *buf, const float4 (&v)[ReprGeom<CIN, COUT, STRIDE, WOUT, MODE>::IPT][2]) {
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  typedef float f8 __attribute__((ext_vector_type(8)));
+#pragma unroll
+  for (int i = 0; i < G::IPT; ++i) {
+    int hr, hc, g;
+    if (!rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g)) continue;
+    const int pos = MODE == 2 ? hc : rp_pos<G, STRIDE>(hr, hc);
+    const f8 x = f8{v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w};
+    const b8 h = __builtin_convertvector(x, b8);
+    const f8 r1 = x - __builtin_convertvector(h, f8);
+    const b8 m = __builtin_convertvector(r1, b8);
+    const b8 l = __builtin_convertvector(r1 - __builtin_convertvector(m, f8), b8);
+    const int o = (g * G::NPP + pos) * 8;
+    *reinterpret_cast<b8 *>(buf + o) = h;
+    *reinterpret_cast<b8 *>(buf + G::TERM + o) = m;
+    *reinterpret_cast<b8 *>(buf + 2 * G::TERM + o) = l;
+  }
+}
+
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+__global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void repr_conv_kernel(
+    ReprConvArgs a) {
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
+  extern __shared__ uint4 rp_lds4[];
+  uint16_t *lds = reinterpret_cast<uint16_t *>(rp_lds4);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // this wave's out-channel tiles ot0 .. ot0 + OTW - 1 and pixel tiles pt0 .. pt0 + PTW - 1
+  const int ot0 = G::OT >= 4 ? wv * G::OTW : (wv & 1);
+  const int pt0 = G::OT >= 4 ? 0 : 2 * (wv >> 1);
+  // the weights of those out tiles, all K, three terms: registers for the whole launch
+  uint4 wr[G::OTW][G::NCH][3];
+#pragma unroll
+  for (int o = 0; o < G::OTW; ++o)
+#pragma unroll
+    for (int s = 0; s < G::NCH; ++s)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        wr[o][s][q] = reinterpret_cast<const uint4 *>(a.w)[(((ot0 + o) * G::NCH + s) * 3 + q) * 64 + lane];
+  // per out tile: bias (none for the dual layer's shortcut half), output tensor and channel
+  constexpr int COUT_T = MODE == 1 ? COUT / 2 : COUT;  // channels of one output tensor
+  constexpr int HOUT = WOUT, TPI = HOUT / G::TR;
+  float4 bias[G::OTW];
+#pragma unroll
+  for (int o = 0; o < G::OTW; ++o) {
+    const int ch = 16 * (ot0 + o) + 4 * (lane >> 4);
+    const bool sc = MODE == 1 && ch >= COUT_T;
+    bias[o] = sc ? float4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4 *>(a.bias + ch);
+  }
+  float4 v[G::IPT][2];
+  int tile = blockIdx.x;
+  if (tile < a.ntiles) {
+    rp_load<CIN, COUT, STRIDE, WOUT, MODE>(a, tile, v);
+    rp_store<CIN, COUT, STRIDE, WOUT, MODE>(lds, v);
+  }
+  __syncthreads();
+  for (int it = 0; tile < a.ntiles; ++it, tile += gridDim.x) {
+    const uint16_t *cur = lds + (it & 1) * G::BUF;
+    const int nxt = tile + gridDim.x;
+    if (nxt < a.ntiles) rp_load<CIN, COUT, STRIDE, WOUT, MODE>(a, nxt, v);  // in flight during the MFMAs
+    bxf4 acc[G::OTW][G::PTW];
+#pragma unroll
+    for (int o = 0; o < G::OTW; ++o)
+#pragma unroll
+      for (int p = 0; p < G::PTW; ++p) acc[o][p] = bxf4{0.f, 0.f, 0.f, 0.f};
+    // lane's pixel in pixel tile p: 16 (pt0 + p) + (lane & 15) -> output row / column within the tile
+#pragma unroll
+    for (int s = 0; s < G::NCH; ++s) {
+      const int tap = MODE == 2 ? 0 : s / (CIN / 32), j = MODE == 2 ? s : s % (CIN / 32);
+      const int dy = tap / 3, dx = tap % 3, g = 4 * j + (lane >> 4);
+      uint4 x[G::PTW][3];
+#pragma unroll
+      for (int p = 0; p < G::PTW; ++p) {
+        const int px = 16 * (pt0 + p) + (lane & 15);
+        int pos;
+        if constexpr (MODE == 2) pos = px;
+        else pos = rp_pos<G, STRIDE>((px / WOUT) * STRIDE + dy, (px % WOUT) * STRIDE + dx);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          x[p][q] = *reinterpret_cast<const uint4 *>(cur + q * G::TERM + (g * G::NPP + pos) * 8);
+      }
+      // small terms first: w_l x_h, w_h x_l, w_m x_m, w_m x_h, w_h x_m, w_h x_h
+#pragma unroll
+      for (int o = 0; o < G::OTW; ++o) {
+        const uint4(&w)[3] = wr[o][s];
+#pragma unroll
+        for (int p = 0; p < G::PTW; ++p) {
+          bxf4 c = acc[o][p];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[2]), bx_as(x[p][0]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(x[p][2]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(x[p][1]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(x[p][0]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(x[p][1]), c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(x[p][0]), c, 0, 0, 0);
+          acc[o][p] = c;
+        }
+      }
+    }
+    // epilogue: acc[o][p][r] = out channel 16 (ot0 + o) + 4 (lane >> 4) + r at pixel 16 (pt0 + p) + (lane & 15)
+    const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
+#pragma unroll
+    for (int o = 0; o < G::OTW; ++o) {
+      int ch = 16 * (ot0 + o) + 4 * (lane >> 4);
+      const bool sc = MODE == 1 && ch >= COUT_T;
+      float *dst = sc ? a.out2 : a.out;
+      if (sc) ch -= COUT_T;
+#pragma unroll
+      for (int p = 0; p < G::PTW; ++p) {
+        const int px = 16 * (pt0 + p) + (lane & 15);
+        const int64_t e = (((int64_t)b * HOUT + r0 + px / WOUT) * WOUT + px % WOUT) * COUT_T + ch;
+        float4 y = float4{acc[o][p][0] + bias[o].x, acc[o][p][1] + bias[o].y, acc[o][p][2] + bias[o].z,
+                          acc[o][p][3] + bias[o].w};
+        if (!sc) {
+          if (a.res) {
+            const float4 rr = *reinterpret_cast<const float4 *>(a.res + e);
+            y.x += rr.x; y.y += rr.y; y.z += rr.z; y.w += rr.w;
+          }
+          y.x = fmaxf(y.x, 0.f); y.y = fmaxf(y.y, 0.f); y.z = fmaxf(y.z, 0.f); y.w = fmaxf(y.w, 0.f);
+        }
+        *reinterpret_cast<float4 *>(dst + e) = y;
+      }
+    }
+    if (nxt < a.ntiles) rp_store<CIN, COUT, STRIDE, WOUT, MODE>(lds + ((it + 1) & 1) * G::BUF, v);
+    __syncthreads();
+  }
+}
+
+// avg_pool2d(3, 2, padding 1, count_include_pad) of NHWC [B][16][16][64] -> NCHW [B][64][8][8]
+__global__ __launch_bounds__(256) void repr_avgpool_kernel(const float *__restrict__ in, float *__restrict__ out, int B) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (b, c, y, x) of the output, x fastest
+  if (q >= (int64_t)B * 64 * 64) return;
+  const int x = (int)(q & 7), y = (int)((q >> 3) & 7), c = (int)((q >> 6) & 63);
+  const int64_t b = q >> 12;
+  float s = 0.f;
+  for (int dy = -1; dy <= 1; ++dy) {
+    const int iy = 2 * y + dy;
+    if (iy < 0 || iy >= 16) continue;
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int ix = 2 * x + dx;
+      if (ix < 0 || ix >= 16) continue;
+      s += in[((b * 16 + iy) * 16 + ix) * 64 + c];
+    }
+  }
+  out[q] = s / 9.0f;
+}
+
+// ---- host side: packing
+// A-operand fragments of one convolution: W [cout][cin][3][3] (folded) -> [out tile][chunk][term][lane][8 bf16],
+// lane -> out channel 16 tile + (lane & 15), K = 8 (lane >> 4) + e within the chunk; chunk s = tap * (cin / 32)
+// + j with K -> in channel 32 j + ..., or (first layer, cin <= 7) chunk s with K = 32 s + ... = tap * cin + c.
+// Two weights stacked (the dual layer: W [64] then W3 [64]) give cout = 128.
+inline void repr_pack(const float *W, int cout, int cin, bool im2col, float *outf) {
+  uint16_t *out = reinterpret_cast<uint16_t *>(outf);
+  const int nch = im2col ? 2 : 9 * (cin / 32);
+  for (int ot = 0; ot < cout / 16; ++ot)
+    for (int s = 0; s < nch; ++s)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int e = 0; e < 8; ++e) {
+          const int co = 16 * ot + (lane & 15), k = 8 * (lane >> 4) + e;
+          float wv = 0.f;
+          if (im2col) {
+            const int kk = 32 * s + k, tap = kk / cin, c = kk % cin;
+            if (tap < 9) wv = W[(co * cin + c) * 9 + tap];
+          } else {
+            const int tap = s / (cin / 32), c = 32 * (s % (cin / 32)) + k;
+            wv = W[(co * cin + c) * 9 + tap];
+          }
+          uint16_t t[3];
+          bx_split(wv, t[0], t[1], t[2]);
+          for (int q = 0; q < 3; ++q) out[(((ot * nch + s) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+        }
+}
+
+// packed blob layout (floats): one entry per layer, fragments then the bias
+struct ReprLayout {
+  int w1, b1, r1w1, r1b1, r1w2, r1b2, dw, db1, dw2, db2, r2w1, r2b1, r2w2, r2b2, total;
+};
+inline int repr_frag_floats(int cout, int nch) { return cout / 16 * nch * 3 * 64 * 4; }
+inline ReprLayout repr_layout() {
+  ReprLayout L;
+  int o = 0;
+  auto take = [&](int n) { const int r = o; o += (n + 3) & ~3; return r; };
+  L.w1 = take(repr_frag_floats(32, 2)); L.b1 = take(32);
+  L.r1w1 = take(repr_frag_floats(32, 9)); L.r1b1 = take(32);
+  L.r1w2 = take(repr_frag_floats(32, 9)); L.r1b2 = take(32);
+  L.dw = take(repr_frag_floats(128, 9)); L.db1 = take(64);
+  L.dw2 = take(repr_frag_floats(64, 18)); L.db2 = take(64);
+  L.r2w1 = take(repr_frag_floats(64, 18)); L.r2b1 = take(64);
+  L.r2w2 = take(repr_frag_floats(64, 18)); L.r2b2 = take(64);
+  L.total = o;
+  return L;
+}
+
+}  // namespace lzm

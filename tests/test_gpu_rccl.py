@@ -46,13 +46,13 @@ def test_breakout_collect_blocks_over_rccl(rccl_group, dst):
     all-reduced on the device, and the stats name the backend and the collective's time"""
     from lightzero_amd.trajectory import pack_episodes
     col = _collector()
-    for _ in range(24):
+    for _ in range(80):  # (stand-in Breakout episodes last tens of steps)
         col.step()
     counts = col.ep_count.cpu().numpy().astype(np.int64)
     ln = col.ep_len.cpu().numpy()
     todo = [(i, k % col.E, int(ln[i, k % col.E])) for i in range(col.n) for k in range(int(col._consumed[i]),
                                                                                     int(counts[i]))]
-    assert todo, "no finished episodes after 24 steps"
+    assert todo, "no finished episodes after 80 steps"
     ref = pack_episodes(col.rec_frames, col.rec_action, col.rec_reward, col.rec_visits, col.rec_value, todo,
                         col.rec_pred, col.env.frame_scale, ep_return=col.ep_return)
     blocks, st = col.gather_blocks(to_host=False, dst=dst)
@@ -64,7 +64,7 @@ def test_breakout_collect_blocks_over_rccl(rccl_group, dst):
     c = st["collective"]
     assert c["backend"] == "nccl" and c["ms"] > 0 and c["bytes_sent"] > 0
     assert c["mode"] == ("all_gather" if dst is None else "gather(dst=0)")
-    assert st["world"] == 1 and st["total_episodes"] == len(todo) and st["total_envstep"] == 24 * col.n
+    assert st["world"] == 1 and st["total_episodes"] == len(todo) and st["total_envstep"] == 80 * col.n
 
 
 def test_rccl_all_gather_packed_and_gather_packed_device_dtypes(rccl_group):
