@@ -101,6 +101,10 @@ SIGNATURES = {
     "lzm_episodes_scan": [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_bias_add_relu": [_vp, _vp, _vp, _i, _i, _i, _i, _vp],
     "lzm_conv_resnet8_p": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "lzm_repr_floats": [],
+    "lzm_repr_prepare": [_i, _vp, _vp],
+    "lzm_repr_workspace_floats": [_i],
+    "lzm_repr_downsample": [_i, _i, _vp, _vp, _vp, _vp, _vp],
     "lzm_episodes_pack": [_i, _i, _i, _i, _i, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp],
     "lzm_az_workspace_bytes": [_i, _i, ctypes.POINTER(_i64)],
@@ -126,7 +130,8 @@ _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c
             "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64,
             "lzm_conv_trunk_floats": ctypes.c_int64, "lzm_conv_trunk_floats_p": ctypes.c_int64,
             "lzm_ez_lstm_frag_floats": ctypes.c_int64, "lzm_ez_lstm_workspace_bytes": ctypes.c_int64,
-            "lzm_error_word": ctypes.c_void_p}
+            "lzm_error_word": ctypes.c_void_p, "lzm_repr_floats": ctypes.c_int64,
+            "lzm_repr_workspace_floats": ctypes.c_int64}
 
 _lib = None
 

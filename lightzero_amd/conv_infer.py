@@ -462,6 +462,8 @@ class FoldedConvInitial:
         self.ops = None
         self.t = None
         self.native = None  # lzm_conv_resnet8_p weights of the 8 x 8 tail (GPU, 64 x 8 x 8 latents)
+        self.repr_native = None  # lzm_repr_downsample weights of the DownSample stages before the tail
+        self._repr_ws = {}
         self.refresh()
 
     def _version(self):
@@ -533,6 +535,47 @@ class FoldedConvInitial:
         else:
             self.native.copy_(blob)  # in place: captured graphs keep reading it
         self.tail = (i0, nb, n_pres, h_ch)
+        self._pack_repr(L, dev, i0)
+
+    def _pack_repr(self, L, dev, i0):
+        """the DownSample stages in front of the tail (conv 3x3/2 -> 32, a 32-channel block, the downsample block,
+        a 64-channel block, avg pool: common.py:164-265 at 64 x 64 frames) as lzm_repr_downsample's split-bf16
+        launches (csrc/lzm_repr.h); LZM_REPR_NATIVE=0: MIOpen convolutions"""
+        ops = self.ops[:i0]
+        kinds = [op[0] for op in ops]
+        obs = tuple(self.model.representation_network.downsample_net.observation_shape) \
+            if getattr(self.model.representation_network, "downsample", False) else None
+        if kinds != ["conv_relu", "basic", "down", "basic", "avgpool"] or obs is None or tuple(obs[1:]) != (64, 64) \
+                or not 1 <= obs[0] <= 7 or os.environ.get("LZM_REPR_NATIVE", "1") == "0":
+            return
+        c1, b1, d, b2 = ops[0], ops[1], ops[2], ops[3]
+        shapes = [(c1[1], (32, obs[0], 3, 3)), (b1[1], (32, 32, 3, 3)), (b1[3], (32, 32, 3, 3)), (d[1], (64, 32, 3, 3)),
+                  (d[3], (64, 64, 3, 3)), (d[5], (64, 32, 3, 3)), (b2[1], (64, 64, 3, 3)), (b2[3], (64, 64, 3, 3))]
+        if any(tuple(w.shape) != sh for w, sh in shapes) or c1[3] != 2:
+            return
+        parts = [c1[1], c1[2], b1[1], b1[2], b1[3], b1[4], d[1], d[2], d[3], d[4], d[5], b2[1], b2[2], b2[3], b2[4]]
+        raw = np.ascontiguousarray(torch.cat([q.reshape(-1).float() for q in parts]).cpu().numpy(), dtype=np.float32)
+        host = np.zeros(L.lzm_repr_floats(), np.float32)
+        _lib.check(L.lzm_repr_prepare(int(obs[0]), raw.ctypes.data, host.ctypes.data), "lzm_repr_prepare")
+        blob = torch.from_numpy(host).to(dev)
+        if self.repr_native is None:
+            self.repr_native = blob
+            self.repr_cin = int(obs[0])
+        else:
+            self.repr_native.copy_(blob)
+
+    def _downsample_native(self, x):
+        """obs [B, C, 64, 64] -> [B, 64, 8, 8] through lzm_repr_downsample (workspace kept per B: captured graphs
+        hold its address)"""
+        B = x.shape[0]
+        ws = self._repr_ws.get(B)
+        if ws is None:
+            ws = torch.empty(int(_lib.load().lzm_repr_workspace_floats(B)), dtype=torch.float32, device=x.device)
+            self._repr_ws[B] = ws
+        out = torch.empty((B, 64, 8, 8), dtype=torch.float32, device=x.device)
+        _lib.call("lzm_repr_downsample", B, self.repr_cin, _lib.ptr(self.repr_native), _lib.ptr(x), _lib.ptr(ws),
+                  _lib.ptr(out), _lib.stream_ptr())
+        return out
 
     # MIOpen's fused convolution + bias (+ residual) + ReLU (torch.miopen_convolution_relu /
     # _add_relu): one launch per convolution instead of a convolution, a bias add / residual add and
@@ -599,7 +642,11 @@ class FoldedConvInitial:
             x = x.contiguous()
         fused = self._fused(x)
         native = self.native is not None and x.is_cuda
-        for op in (self.ops[:self.tail[0]] if native else self.ops):
+        pre = self.ops[:self.tail[0]] if native else self.ops
+        if native and self.repr_native is not None and tuple(x.shape[1:]) == (self.repr_cin, 64, 64):
+            x = self._downsample_native(x)  # the DownSample stages in front of the tail, split-bf16 launches
+            pre = []
+        for op in pre:
             kind = op[0]
             if kind == "conv_relu":
                 x = self._conv_relu(x, op[1], op[2], op[3], fused)

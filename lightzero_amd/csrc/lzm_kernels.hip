@@ -39,6 +39,7 @@
 #include "lzm_search_mlp.h"
 #include "lzm_search_res.h"
 #include "lzm_conv.h"
+#include "lzm_repr.h"
 #include "lzm_heads.h"
 #include "lzm_lstm.h"
 #include "lzm_initial.h"
@@ -2537,6 +2538,92 @@ int lzm_conv_resnet8_p(int B, int n_blocks, int n_pres, int h_ch, const float *w
   a.pool = in; a.out_latent = out_latent; a.out_h = out_h; a.skip_dyn = 1;
   hipLaunchKernelGGL((conv_trunk_bx_kernel<kBxAhead, 0>), dim3(B), dim3(kCvThreads), 2 * kBxBuf * sizeof(uint16_t),
                      (hipStream_t)stream, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+// ---- the representation network's DownSample stages (lzm_repr.h)
+int64_t lzm_repr_floats(void) { return repr_layout().total; }
+
+int lzm_repr_prepare(int cin, const float *raw, float *out) {
+  if (cin < 1 || cin * 9 > 64 || !raw || !out) {
+    set_err("lzm_repr_prepare: 1..7 observation channels and buffers");
+    return LZM_ERR_ARG;
+  }
+  const ReprLayout L = repr_layout();
+  memset(out, 0, sizeof(float) * (size_t)L.total);
+  const float *r = raw;
+  auto bias = [&](int off, int n) { memcpy(out + off, r, n * sizeof(float)); r += n; };
+  repr_pack(r, 32, cin, true, out + L.w1); r += 32 * cin * 9; bias(L.b1, 32);
+  repr_pack(r, 32, 32, false, out + L.r1w1); r += 32 * 32 * 9; bias(L.r1b1, 32);
+  repr_pack(r, 32, 32, false, out + L.r1w2); r += 32 * 32 * 9; bias(L.r1b2, 32);
+  // the downsample block: conv1 (64) and the shortcut conv3 (64) stacked as one 128-channel layer
+  std::vector<float> dual((size_t)128 * 32 * 9);
+  memcpy(dual.data(), r, sizeof(float) * 64 * 32 * 9); r += 64 * 32 * 9;
+  bias(L.db1, 64);
+  const float *w2 = r; r += 64 * 64 * 9;
+  bias(L.db2, 64);
+  memcpy(dual.data() + 64 * 32 * 9, r, sizeof(float) * 64 * 32 * 9); r += 64 * 32 * 9;
+  repr_pack(dual.data(), 128, 32, false, out + L.dw);
+  repr_pack(w2, 64, 64, false, out + L.dw2);
+  repr_pack(r, 64, 64, false, out + L.r2w1); r += 64 * 64 * 9; bias(L.r2b1, 64);
+  repr_pack(r, 64, 64, false, out + L.r2w2); r += 64 * 64 * 9; bias(L.r2b2, 64);
+  return LZM_OK;
+}
+
+int64_t lzm_repr_workspace_floats(int B) { return B <= 0 ? -1 : (int64_t)B * (2 * 32 * 32 * 32 + 2 * 16 * 16 * 64); }
+
+}  // extern "C"
+
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+static int repr_launch(const ReprConvArgs &a, hipStream_t s) {
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
+  const size_t lds = 2 * (size_t)G::BUF * sizeof(uint16_t) + (G::KS == 2 ? 8 * 64 * 8 * sizeof(float) : 0);
+  static hipError_t attr = hipFuncSetAttribute((const void *)repr_conv_kernel<CIN, COUT, STRIDE, WOUT, MODE>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  LZM_HIP(attr);
+  const int grid = std::min(a.ntiles, device_cus());
+  hipLaunchKernelGGL((repr_conv_kernel<CIN, COUT, STRIDE, WOUT, MODE>), dim3(grid), dim3(kRpThreads), lds, s, a);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+extern "C" {
+
+int lzm_repr_downsample(int B, int cin, const float *w, const float *obs, float *ws, float *out, void *stream) {
+  if (B <= 0 || cin < 1 || cin * 9 > 64 || !w || !obs || !ws || !out ||
+      (((uintptr_t)w | (uintptr_t)ws | (uintptr_t)out) & 15)) {
+    set_err("lzm_repr_downsample: bad arguments (1..7 observation channels, 16-byte aligned weights / workspace)");
+    return LZM_ERR_ARG;
+  }
+  const ReprLayout L = repr_layout();
+  hipStream_t s = (hipStream_t)stream;
+  float *A0 = ws, *A1 = ws + (size_t)B * 32768, *D0 = ws + (size_t)B * 65536, *D1 = D0 + (size_t)B * 16384;
+  ReprConvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.B = B; a.cin_obs = cin;
+  int rc;
+  // L1: obs (NCHW 64 x 64) -> A0 [32][32][32]
+  a.ntiles = B * 16; a.in = obs; a.w = w + L.w1; a.bias = w + L.b1; a.res = nullptr; a.out = A0;
+  if ((rc = repr_launch<32, 32, 2, 32, 2>(a, s)) != LZM_OK) return rc;
+  // resblocks1: A0 -> A1 -> A0 (+ A0)
+  a.in = A0; a.w = w + L.r1w1; a.bias = w + L.r1b1; a.out = A1;
+  if ((rc = repr_launch<32, 32, 1, 32, 0>(a, s)) != LZM_OK) return rc;
+  a.in = A1; a.w = w + L.r1w2; a.bias = w + L.r1b2; a.res = A0; a.out = A0;
+  if ((rc = repr_launch<32, 32, 1, 32, 0>(a, s)) != LZM_OK) return rc;
+  // the downsample block: A0 -> D0 = relu(conv1 + b1), D1 = conv3 (shortcut); D1 = relu(conv2(D0) + b2 + D1)
+  a.ntiles = B * 4; a.in = A0; a.w = w + L.dw; a.bias = w + L.db1; a.res = nullptr; a.out = D0; a.out2 = D1;
+  if ((rc = repr_launch<32, 128, 2, 16, 1>(a, s)) != LZM_OK) return rc;
+  a.in = D0; a.w = w + L.dw2; a.bias = w + L.db2; a.res = D1; a.out = D1; a.out2 = nullptr;
+  if ((rc = repr_launch<64, 64, 1, 16, 0>(a, s)) != LZM_OK) return rc;
+  // resblocks2: D1 -> D0 -> D1 (+ D1)
+  a.in = D1; a.w = w + L.r2w1; a.bias = w + L.r2b1; a.res = nullptr; a.out = D0;
+  if ((rc = repr_launch<64, 64, 1, 16, 0>(a, s)) != LZM_OK) return rc;
+  a.in = D0; a.w = w + L.r2w2; a.bias = w + L.r2b2; a.res = D1; a.out = D1;
+  if ((rc = repr_launch<64, 64, 1, 16, 0>(a, s)) != LZM_OK) return rc;
+  // avg pool -> out NCHW [B][64][8][8]
+  const long long n = (long long)B * 4096;
+  hipLaunchKernelGGL(repr_avgpool_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, D1, out, B);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }

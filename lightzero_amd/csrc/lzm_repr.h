@@ -32,7 +32,7 @@
 
 namespace lzm {
 
-constexpr int kRpThreads = 256;
+constexpr int kRpThreads = 512;  // 8 waves: two per SIMD
 
 struct ReprConvArgs {
   int B, ntiles, cin_obs;  // cin_obs: first layer's input channels (MODE 2)
@@ -58,13 +58,19 @@ struct ReprGeom {
   static constexpr int CG = MODE == 2 ? 8 : CIN / 8;                  // channel groups (MODE 2: 64 K / 8)
   static constexpr int NCH = MODE == 2 ? 2 : 9 * (CIN / 32);          // K chunks of 32
   static constexpr int OT = COUT / 16;                                // out-channel tiles
-  static constexpr int OTW = OT >= 4 ? OT / 4 : 1;                    // per wave
-  static constexpr int PTW = OT >= 4 ? 4 : 2;                         // pixel tiles per wave
+  // 8 waves, one out tile each: 2 out tiles -> a pixel tile per wave; 4 -> all 4 pixel tiles over half of K
+  // (KS = 2: K split, partial sums exchanged through LDS); 8 -> all 4 pixel tiles, all of K
+  static constexpr int KS = OT == 4 ? 2 : 1;
+  static constexpr int PTW = OT == 2 ? 1 : 4;                         // pixel tiles per wave
+  static constexpr int NCW = NCH / KS;                                // K chunks per wave
+  static_assert(OT == 2 || OT == 4 || OT == 8, "out tiles");
+  static_assert(NCH % KS == 0, "K split");
   static constexpr int TERM = CG * NPP * 8;                           // bf16 per term image
   static constexpr int BUF = 3 * TERM;                                // bf16 per halo buffer
-  static constexpr int ITEMS = MODE == 2 ? 64 * 8 : HR * HC * CG;     // (position, group) staging items
-  static constexpr int IPT = (ITEMS + kRpThreads - 1) / kRpThreads;  // per thread
   static constexpr int PPW = MODE == 2 ? 64 : 64 / CG;                // positions per wave-instruction
+  // staging items (position, group): 64 per wave-instruction, PPW consecutive positions x CG groups
+  static constexpr int ITEMS = MODE == 2 ? 64 * 8 : (HR * HC + PPW - 1) / PPW * 64;
+  static constexpr int IPT = (ITEMS + kRpThreads - 1) / kRpThreads;  // per thread
 };
 
 // the LDS position of halo (row hr, bordered column hc)
@@ -78,20 +84,33 @@ __device__ __forceinline__ int rp_pos(int hr, int hc) {
 template <class G, int STRIDE, int MODE>
 __device__ __forceinline__ bool rp_item(int q, int &hr, int &hc, int &g) {
   if (q >= G::ITEMS) return false;
-  const int lin = (q >> 6) * G::PPW + (q & 63) % G::PPW;
-  g = (q & 63) / G::PPW;
   if constexpr (MODE == 2) {
     hr = 0;
     hc = q & 63;  // pixel of the tile
     g = q >> 6;
     return true;
   }
+  // lanes: PPW consecutive halo positions (global: whole NHWC rows, coalesced; LDS: distinct bank slots per
+  // 8-lane write group) x the CG channel groups
+  const int lin = (q >> 6) * G::PPW + (q & 63) % G::PPW;
+  if (lin >= G::HR * G::HC) return false;
+  g = (q & 63) / G::PPW;
   hr = lin / G::HC;
   hc = lin % G::HC;
   return true;
 }
 
-// load this thread's staging items of tile `tile` into registers (8 f32 per item)
+// x where ok, else +0 (a bit mask: no select of addresses for the compiler to turn into a scratch array)
+__device__ __forceinline__ float4 rp_keep(bool ok, float4 x) {
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  return float4{__uint_as_float(__float_as_uint(x.x) & m), __uint_as_float(__float_as_uint(x.y) & m),
+                __uint_as_float(__float_as_uint(x.z) & m), __uint_as_float(__float_as_uint(x.w) & m)};
+}
+
+// load this thread's staging items of tile `tile` into registers (8 f32 per item). Branch-free: every item
+// loads from a clamped in-bounds address and selects zero where it lies outside the image (the halo border),
+// so the registers stay registers (no private-array stores under divergent control flow) and the loads stay
+// in flight until rp_store
 template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
 __device__ __forceinline__ void rp_load(const ReprConvArgs &a, int tile, float4 (&v)[ReprGeom<CIN, COUT, STRIDE, WOUT, MODE>::IPT][2]) {
   typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
@@ -100,9 +119,8 @@ __device__ __forceinline__ void rp_load(const ReprConvArgs &a, int tile, float4 
   const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
 #pragma unroll
   for (int i = 0; i < G::IPT; ++i) {
-    int hr, hc, g;
-    v[i][0] = v[i][1] = float4{0.f, 0.f, 0.f, 0.f};
-    if (!rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g)) continue;
+    int hr = 0, hc = 0, g = 0;
+    const bool item = rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g);
     if constexpr (MODE == 2) {
       // im2col: pixel hc of the tile (row r0 + hc / 32, column hc % 32), K = 8 g .. 8 g + 7 = tap * C + c
       const int oy = r0 + (hc >> 5), ox = hc & 31;
@@ -111,18 +129,19 @@ __device__ __forceinline__ void rp_load(const ReprConvArgs &a, int tile, float4 
       for (int j = 0; j < 8; ++j) {
         const int k = 8 * g + j, tap = k / a.cin_obs, c = k % a.cin_obs;
         const int iy = 2 * oy + tap / 3 - 1, ix = 2 * ox + tap % 3 - 1;
-        e[j] = (tap < 9 && iy >= 0 && iy < 64 && ix >= 0 && ix < 64)
-                   ? a.in[(((int64_t)b * a.cin_obs + c) * 64 + iy) * 64 + ix] : 0.f;
+        const bool ok = item && tap < 9 && iy >= 0 && iy < 64 && ix >= 0 && ix < 64;
+        const float x = a.in[ok ? (((int64_t)b * a.cin_obs + c) * 64 + iy) * 64 + ix : 0];
+        e[j] = __uint_as_float(__float_as_uint(x) & (ok ? 0xffffffffu : 0u));
       }
       v[i][0] = float4{e[0], e[1], e[2], e[3]};
       v[i][1] = float4{e[4], e[5], e[6], e[7]};
     } else {
       const int iy = r0 * STRIDE - 1 + hr, ix = hc - 1;
-      if (iy >= 0 && iy < HIN && ix >= 0 && ix < HIN) {
-        const float4 *src = reinterpret_cast<const float4 *>(a.in + (((int64_t)b * HIN + iy) * HIN + ix) * CIN + 8 * g);
-        v[i][0] = src[0];
-        v[i][1] = src[1];
-      }
+      const bool ok = item && iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
+      const float4 *src = reinterpret_cast<const float4 *>(
+          a.in + (ok ? (((int64_t)b * HIN + iy) * HIN + ix) * CIN + 8 * g : 0));
+      v[i][0] = rp_keep(ok, src[0]);
+      v[i][1] = rp_keep(ok, src[1]);
     }
   }
 }
@@ -151,34 +170,32 @@ __device__ __forceinline__ void rp_store(uint16_t *buf, const float4 (&v)[ReprGe
 }
 
 template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
-__global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void repr_conv_kernel(
+__global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void repr_conv_kernel(
     ReprConvArgs a) {
   typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
   extern __shared__ uint4 rp_lds4[];
   uint16_t *lds = reinterpret_cast<uint16_t *>(rp_lds4);
+  float *xscr = reinterpret_cast<float *>(lds + 2 * G::BUF);  // K-split partial sums
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // this wave's out-channel tiles ot0 .. ot0 + OTW - 1 and pixel tiles pt0 .. pt0 + PTW - 1
-  const int ot0 = G::OT >= 4 ? wv * G::OTW : (wv & 1);
-  const int pt0 = G::OT >= 4 ? 0 : 2 * (wv >> 1);
-  // the weights of those out tiles, all K, three terms: registers for the whole launch
-  uint4 wr[G::OTW][G::NCH][3];
+  // this wave's out tile, first pixel tile and K half
+  const int ot = G::OT == 2 ? (wv & 1) : (G::OT == 4 ? (wv & 3) : wv);
+  const int pt0 = G::OT == 2 ? (wv >> 1) : 0;
+  const int kh = G::KS == 2 ? (wv >> 2) : 0;
+  // the weights of that out tile over its K chunks, three terms: registers for the whole launch
+  uint4 wr[G::NCW][3];
 #pragma unroll
-  for (int o = 0; o < G::OTW; ++o)
+  for (int s = 0; s < G::NCW; ++s)
 #pragma unroll
-    for (int s = 0; s < G::NCH; ++s)
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        wr[o][s][q] = reinterpret_cast<const uint4 *>(a.w)[(((ot0 + o) * G::NCH + s) * 3 + q) * 64 + lane];
-  // per out tile: bias (none for the dual layer's shortcut half), output tensor and channel
+    for (int q = 0; q < 3; ++q)
+      wr[s][q] = reinterpret_cast<const uint4 *>(a.w)[((ot * G::NCH + kh * G::NCW + s) * 3 + q) * 64 + lane];
+  // out channels 4 (lane >> 4) .. + 3 of the tile; the dual layer's upper half is the shortcut (no bias)
   constexpr int COUT_T = MODE == 1 ? COUT / 2 : COUT;  // channels of one output tensor
   constexpr int HOUT = WOUT, TPI = HOUT / G::TR;
-  float4 bias[G::OTW];
-#pragma unroll
-  for (int o = 0; o < G::OTW; ++o) {
-    const int ch = 16 * (ot0 + o) + 4 * (lane >> 4);
-    const bool sc = MODE == 1 && ch >= COUT_T;
-    bias[o] = sc ? float4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4 *>(a.bias + ch);
-  }
+  int ch = 16 * ot + 4 * (lane >> 4);
+  const bool sc = MODE == 1 && ch >= COUT_T;
+  float *dst = sc ? a.out2 : a.out;
+  if (sc) ch -= COUT_T;
+  const float4 bias = sc ? float4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4 *>(a.bias + ch);
   float4 v[G::IPT][2];
   int tile = blockIdx.x;
   if (tile < a.ntiles) {
@@ -190,17 +207,15 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     const uint16_t *cur = lds + (it & 1) * G::BUF;
     const int nxt = tile + gridDim.x;
     if (nxt < a.ntiles) rp_load<CIN, COUT, STRIDE, WOUT, MODE>(a, nxt, v);  // in flight during the MFMAs
-    bxf4 acc[G::OTW][G::PTW];
+    bxf4 acc[G::PTW];
 #pragma unroll
-    for (int o = 0; o < G::OTW; ++o)
-#pragma unroll
-      for (int p = 0; p < G::PTW; ++p) acc[o][p] = bxf4{0.f, 0.f, 0.f, 0.f};
-    // lane's pixel in pixel tile p: 16 (pt0 + p) + (lane & 15) -> output row / column within the tile
-#pragma unroll
-    for (int s = 0; s < G::NCH; ++s) {
-      const int tap = MODE == 2 ? 0 : s / (CIN / 32), j = MODE == 2 ? s : s % (CIN / 32);
+    for (int p = 0; p < G::PTW; ++p) acc[p] = bxf4{0.f, 0.f, 0.f, 0.f};
+    // B fragments of chunk s for the wave's pixel tiles (lane: pixel 16 (pt0 + p) + (lane & 15) of the tile,
+    // output row px / WOUT, column px % WOUT; channel group 4 j + (lane >> 4))
+    auto load_x = [&](int s, uint4 (&x)[G::PTW][3]) {
+      const int sg = kh * G::NCW + s;  // chunk within the layer's K
+      const int tap = MODE == 2 ? 0 : sg / (CIN / 32), j = MODE == 2 ? sg : sg % (CIN / 32);
       const int dy = tap / 3, dx = tap % 3, g = 4 * j + (lane >> 4);
-      uint4 x[G::PTW][3];
 #pragma unroll
       for (int p = 0; p < G::PTW; ++p) {
         const int px = 16 * (pt0 + p) + (lane & 15);
@@ -211,46 +226,65 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         for (int q = 0; q < 3; ++q)
           x[p][q] = *reinterpret_cast<const uint4 *>(cur + q * G::TERM + (g * G::NPP + pos) * 8);
       }
-      // small terms first: w_l x_h, w_h x_l, w_m x_m, w_m x_h, w_h x_m, w_h x_h
+    };
+    // software pipeline: chunk s + 1's LDS reads issued before chunk s's MFMAs (the scheduling barrier keeps
+    // the compiler from hoisting every chunk's reads to the top, which would need 9 x the fragment registers)
+    uint4 xa[G::PTW][3], xb[G::PTW][3];
+    load_x(0, xa);
 #pragma unroll
-      for (int o = 0; o < G::OTW; ++o) {
-        const uint4(&w)[3] = wr[o][s];
+    for (int s = 0; s < G::NCW; ++s) {
+      uint4(&xc)[G::PTW][3] = (s & 1) ? xb : xa;
+      uint4(&xn)[G::PTW][3] = (s & 1) ? xa : xb;
+      if (s + 1 < G::NCW) load_x(s + 1, xn);
+      const uint4(&w)[3] = wr[s];
 #pragma unroll
-        for (int p = 0; p < G::PTW; ++p) {
-          bxf4 c = acc[o][p];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[2]), bx_as(x[p][0]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(x[p][2]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(x[p][1]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(x[p][0]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(x[p][1]), c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(x[p][0]), c, 0, 0, 0);
-          acc[o][p] = c;
+      for (int p = 0; p < G::PTW; ++p) {
+        // small terms first: w_l x_h, w_h x_l, w_m x_m, w_m x_h, w_h x_m, w_h x_h
+        bxf4 c = acc[p];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[2]), bx_as(xc[p][0]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][2]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(xc[p][1]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(xc[p][0]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][1]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][0]), c, 0, 0, 0);
+        acc[p] = c;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // K split: the K-half-0 wave finishes pixel tiles 0-1, the K-half-1 wave tiles 2-3; each hands the other
+    // its partial sums of the other two through LDS
+    if constexpr (G::KS == 2) {
+      float4 *mine = reinterpret_cast<float4 *>(xscr + ((ot * 2 + (1 - kh)) * 64 + lane) * 8);
+      const bxf4 g0 = kh ? acc[0] : acc[2], g1 = kh ? acc[1] : acc[3];
+      mine[0] = float4{g0[0], g0[1], g0[2], g0[3]};
+      mine[1] = float4{g1[0], g1[1], g1[2], g1[3]};
+      __syncthreads();
+      const float4 *theirs = reinterpret_cast<const float4 *>(xscr + ((ot * 2 + kh) * 64 + lane) * 8);
+      const float4 q0 = theirs[0], q1 = theirs[1];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float4 q = (p & 1) ? q1 : q0;
+        if ((p >> 1) == kh) {
+          acc[p][0] += q.x; acc[p][1] += q.y; acc[p][2] += q.z; acc[p][3] += q.w;
         }
       }
     }
-    // epilogue: acc[o][p][r] = out channel 16 (ot0 + o) + 4 (lane >> 4) + r at pixel 16 (pt0 + p) + (lane & 15)
+    // epilogue: acc[p][r] = out channel ch + r at pixel 16 (pt0 + p) + (lane & 15)
     const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
 #pragma unroll
-    for (int o = 0; o < G::OTW; ++o) {
-      int ch = 16 * (ot0 + o) + 4 * (lane >> 4);
-      const bool sc = MODE == 1 && ch >= COUT_T;
-      float *dst = sc ? a.out2 : a.out;
-      if (sc) ch -= COUT_T;
-#pragma unroll
-      for (int p = 0; p < G::PTW; ++p) {
-        const int px = 16 * (pt0 + p) + (lane & 15);
-        const int64_t e = (((int64_t)b * HOUT + r0 + px / WOUT) * WOUT + px % WOUT) * COUT_T + ch;
-        float4 y = float4{acc[o][p][0] + bias[o].x, acc[o][p][1] + bias[o].y, acc[o][p][2] + bias[o].z,
-                          acc[o][p][3] + bias[o].w};
-        if (!sc) {
-          if (a.res) {
-            const float4 rr = *reinterpret_cast<const float4 *>(a.res + e);
-            y.x += rr.x; y.y += rr.y; y.z += rr.z; y.w += rr.w;
-          }
-          y.x = fmaxf(y.x, 0.f); y.y = fmaxf(y.y, 0.f); y.z = fmaxf(y.z, 0.f); y.w = fmaxf(y.w, 0.f);
+    for (int p = 0; p < G::PTW; ++p) {
+      if (G::KS == 2 && (p >> 1) != kh) continue;  // (the K-split partner's tiles)
+      const int px = 16 * (pt0 + p) + (lane & 15);
+      const int64_t e = (((int64_t)b * HOUT + r0 + px / WOUT) * WOUT + px % WOUT) * COUT_T + ch;
+      float4 y = float4{acc[p][0] + bias.x, acc[p][1] + bias.y, acc[p][2] + bias.z, acc[p][3] + bias.w};
+      if (!sc) {
+        if (a.res) {
+          const float4 rr = *reinterpret_cast<const float4 *>(a.res + e);
+          y.x += rr.x; y.y += rr.y; y.z += rr.z; y.w += rr.w;
         }
-        *reinterpret_cast<float4 *>(dst + e) = y;
+        y.x = fmaxf(y.x, 0.f); y.y = fmaxf(y.y, 0.f); y.z = fmaxf(y.z, 0.f); y.w = fmaxf(y.w, 0.f);
       }
+      *reinterpret_cast<float4 *>(dst + e) = y;
     }
     if (nxt < a.ntiles) rp_store<CIN, COUT, STRIDE, WOUT, MODE>(lds + ((it + 1) & 1) * G::BUF, v);
     __syncthreads();

@@ -142,7 +142,8 @@ def _flat_layout(rows: int, n_ep: int, frame_bytes: int, W: int):
 
 
 def _frame_bytes(block: TrajBlock) -> int:
-    return int(np.prod(tuple(block.frames.shape[1:]), dtype=np.int64)) * block.frames.element_size()
+    f = block.frames
+    return int(np.prod(tuple(f.shape[1:]), dtype=np.int64)) * (f.element_size() if torch.is_tensor(f) else f.itemsize)
 
 
 def flatten_block(block: TrajBlock, device=None) -> torch.Tensor:

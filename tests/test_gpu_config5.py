@@ -187,3 +187,44 @@ def test_bench_breakout_workload_line(tmp_path):
     assert "Breakout MuZero" in line["config"]["workload"] and line["value"] > 0
     assert line["roofline"]["kernel"] == "search_conv_kernel" and line["roofline"]["bound"] == "mfma"
     assert line["tie_stream_errors"] == 0 and line["trajectory"]["frame_dtype"] == "uint8"
+
+
+@pytest.mark.parametrize("kind", ["mz", "ez"])
+def test_native_downsample_matches_float64_reference(kind):
+    """lzm_repr_downsample (the DownSample stages on split-bf16 MFMA, csrc/lzm_repr.h) vs the same BN-folded
+    convolutions in float64 on the CPU: conv 3x3/2 -> 32, the 32-channel block, the downsample block with its
+    3x3/2 shortcut, the 64-channel block, avg pool. Tolerance: the split keeps f32-level error — 2e-5 of the
+    layer's magnitude (relative to max |ref|) and rtol 1e-4 elementwise."""
+    import torch.nn.functional as F
+    from lightzero_amd.conv_infer import FoldedConvInitial
+    from lightzero_amd.model_conv import atari_efficientzero_model
+    if kind == "mz":
+        m = _conv_model(4)
+    else:
+        torch.manual_seed(4)
+        m = atari_efficientzero_model(last_linear_layer_init_zero=False)
+        bench._random_bn(m, 5)
+        m = m.to(DEV).eval()
+    fi = FoldedConvInitial(m)
+    assert fi.repr_native is not None
+    B = 37  # tiles of several images per workgroup, a ragged last round
+    obs = torch.rand(B, 4, 64, 64, device=DEV)
+    with torch.no_grad():
+        got = fi._downsample_native(obs).cpu().double()
+    x = obs.cpu().double()
+    ops = [tuple(t.cpu().double() if torch.is_tensor(t) else t for t in op) for op in fi.ops[:fi.tail[0]]]
+    for op in ops:
+        if op[0] == "conv_relu":
+            x = F.conv2d(x, op[1], op[2], stride=op[3], padding=1).relu()
+        elif op[0] == "basic":
+            y = F.conv2d(x, op[1], op[2], padding=1).relu()
+            x = (F.conv2d(y, op[3], op[4], padding=1) + x).relu()
+        elif op[0] == "down":
+            y = F.conv2d(x, op[1], op[2], stride=2, padding=1).relu()
+            x = (F.conv2d(y, op[3], op[4], padding=1) + F.conv2d(x, op[5], None, stride=2, padding=1)).relu()
+        else:
+            x = F.avg_pool2d(x, 3, 2, 1)
+    assert got.shape == x.shape == (B, 64, 8, 8)
+    err = (got - x).abs()
+    assert float(err.max()) <= 2e-5 * float(x.abs().max()), float(err.max() / x.abs().max())
+    torch.testing.assert_close(got, x, rtol=1e-4, atol=2e-5 * float(x.abs().max()))
