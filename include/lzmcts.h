@@ -403,7 +403,9 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
  * b2[Vr+Vv+A] as packed by lightzero_amd.conv_infer; outputs reward [B][Vr], value [B][Vv],
  * policy [B][A]. norm_words (nullable, int32 [2 * ceil(B / 2)]): also write ensure_softmax's
  * verdict for the reward and value rows (scaling_transform.py:36-62) in the layout
- * lzm_decode_backprop reads after lzm_set_norm_words, so it launches no check of its own. */
+ * lzm_decode_backprop reads after lzm_set_norm_words, so it launches no check of its own. r = NULL: the
+ * prediction heads only (value, policy; initial_inference's prediction network, common.py:854-881): Kr,
+ * r_scale / r_shift, reward and norm_words are not read. */
 int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const float *r_scale, const float *r_shift,
                    const float *hd, const float *w1t, const float *b1, const float *w2t, const float *b2, int Vr,
                    int Vv, int A, float *reward, float *value, float *policy, int32_t *norm_words, void *stream);

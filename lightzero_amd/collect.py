@@ -19,7 +19,7 @@ values, root latents and policy logits). `step_counter` counts the steps (device
 """
 import torch
 
-from .conv_infer import folded_initial_or_none
+from .conv_infer import FoldedConvInitial, folded_initial_or_none
 from .initial import FusedInitialInference, fused_initial_or_none
 from .mcts_ctree import EfficientZeroMCTSCtree, MuZeroMCTSCtree, _step_net
 from .utils import EasyDict
@@ -90,7 +90,10 @@ class DeviceSearchStep:
                         prepare=dict(roots=self.roots, noise_weight=self.noise_weight, noises=self.noises,
                                      rewards=self.rewards, to_play=self.to_play))
                 else:
-                    out = (self.initial or self.model).initial_inference(self.obs)
+                    if isinstance(self.initial, FoldedConvInitial):  # the latent straight into the root slot
+                        out = self.initial.initial_inference(self.obs, latent_out=self._root_slot())
+                    else:
+                        out = (self.initial or self.model).initial_inference(self.obs)
                     self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
                                               self.to_play)
                 # the seeds (from the step counter), fresh min-max bounds, the root outputs and the

@@ -126,6 +126,33 @@ def fold_tensors(model):
     return {k: v.float().contiguous() for k, v in t.items()}
 
 
+def pack_heads(t, hv):
+    """lzm_conv_heads layouts (csrc/lzm_heads.h) of the folded head MLPs (fold_tensors' t; hv: value head
+    channels), or None if they do not fit the kernel: w1t [3][8][32][32][4] over the three hidden layers
+    (reward from r, value / policy from the value / policy planes), w2t [32][Vr + Vv + A] (and w2q [8][N2][4],
+    k4-major float4s, for the one-launch search lzm_search_conv)."""
+    rw1, vw1 = t["rh_w1"], t["ph_w1"]
+    Kr, fv = rw1.shape[1], hv * 64
+    Khd = vw1.shape[1]
+    fp = Khd - fv
+    if rw1.shape[0] != 32 or vw1.shape[0] != 64 or Kr > 1024 or fv > 1024 or fp > 1024 or fp <= 0 \
+            or Kr % 4 or fv % 4 or Khd > 2048:
+        return None
+    dev = rw1.device
+    W = torch.zeros(96, 1024, dtype=torch.float32, device=dev)
+    W[0:32, :Kr] = rw1
+    W[32:64, :fv] = vw1[:32, :fv]
+    W[64:96, :fp] = vw1[32:, fv:]
+    w1t = W.reshape(3, 32, 8, 32, 4).permute(0, 2, 3, 1, 4).contiguous()  # [head][part][k4][col][4]
+    b1 = torch.cat([t["rh_b1"], t["ph_b1"]]).contiguous()
+    w2c = torch.cat([t["rh_w2"], t["v_w2"], t["p_w2"]], dim=0)  # [N2][32]
+    w2t = w2c.t().contiguous()
+    w2q = w2c.reshape(-1, 8, 4).permute(1, 0, 2).contiguous()  # [8][N2][4] (the one-launch search)
+    b2 = torch.cat([t["rh_b2"], t["v_b2"], t["p_b2"]]).contiguous()
+    return dict(w1t=w1t, b1=b1, w2t=w2t, w2q=w2q, b2=b2, Kr=Kr, Khd=Khd, off_policy=fv, Vr=t["rh_w2"].shape[0],
+                Vv=t["v_w2"].shape[0], A=t["p_w2"].shape[0])
+
+
 class FoldedConvNet:
     """recurrent_inference of a conv MuZeroModel / EfficientZeroModel with every BN folded."""
 
@@ -227,31 +254,7 @@ class FoldedConvNet:
         return torch.from_numpy(host).to(W.device)
 
     def _pack_heads(self):
-        """lzm_conv_heads layouts (csrc/lzm_heads.h) of the folded head MLPs, or None if they do
-        not fit the kernel: w1t [3][8][32][32][4] over the three hidden layers (reward from r,
-        value / policy from the value / policy planes), w2t [32][Vr + Vv + A] (and w2q [8][N2][4],
-        k4-major float4s, for the one-launch search lzm_search_conv)."""
-        t = self.t
-        rw1, vw1 = t["rh_w1"], t["ph_w1"]
-        Kr, fv = rw1.shape[1], self.hv * 64
-        Khd = vw1.shape[1]
-        fp = Khd - fv
-        if rw1.shape[0] != 32 or vw1.shape[0] != 64 or Kr > 1024 or fv > 1024 or fp > 1024 or fp <= 0 \
-                or Kr % 4 or fv % 4 or Khd > 2048:
-            return None
-        dev = rw1.device
-        W = torch.zeros(96, 1024, dtype=torch.float32, device=dev)
-        W[0:32, :Kr] = rw1
-        W[32:64, :fv] = vw1[:32, :fv]
-        W[64:96, :fp] = vw1[32:, fv:]
-        w1t = W.reshape(3, 32, 8, 32, 4).permute(0, 2, 3, 1, 4).contiguous()  # [head][part][k4][col][4]
-        b1 = torch.cat([t["rh_b1"], t["ph_b1"]]).contiguous()
-        w2c = torch.cat([t["rh_w2"], t["v_w2"], t["p_w2"]], dim=0)  # [N2][32]
-        w2t = w2c.t().contiguous()
-        w2q = w2c.reshape(-1, 8, 4).permute(1, 0, 2).contiguous()  # [8][N2][4] (the one-launch search)
-        b2 = torch.cat([t["rh_b2"], t["v_b2"], t["p_b2"]]).contiguous()
-        return dict(w1t=w1t, b1=b1, w2t=w2t, w2q=w2q, b2=b2, Kr=Kr, Khd=Khd, off_policy=fv, Vr=t["rh_w2"].shape[0],
-                    Vv=t["v_w2"].shape[0], A=t["p_w2"].shape[0])
+        return pack_heads(self.t, self.hv)
 
     def _trunk(self, pool, x, action, out_latent):
         """lzm_conv_trunk: (reward planes [B, r_ch*64], head planes [B, h_ch*64]); next latent -> out_latent"""
@@ -536,6 +539,14 @@ class FoldedConvInitial:
             self.native.copy_(blob)  # in place: captured graphs keep reading it
         self.tail = (i0, nb, n_pres, h_ch)
         self._pack_repr(L, dev, i0)
+        # the value / policy MLPs after the tail as one lzm_conv_heads launch (prediction heads only)
+        heads = pack_heads(t, self.model.prediction_network.conv1x1_value.out_channels)
+        if getattr(self, "heads", None) is None or heads is None:
+            self.heads = heads
+        else:
+            for k, v in heads.items():
+                if torch.is_tensor(v):
+                    self.heads[k].copy_(v)  # in place: captured graphs keep reading them
 
     def _pack_repr(self, L, dev, i0):
         """the DownSample stages in front of the tail (conv 3x3/2 -> 32, a 32-channel block, the downsample block,
@@ -634,7 +645,9 @@ class FoldedConvInitial:
         y = cls._conv_relu(x, w1, b1, 1, fused)
         return cls._conv_add_relu(y, w2, x, b2, fused)
 
-    def initial_inference(self, obs):
+    def initial_inference(self, obs, latent_out=None):
+        """latent_out: optional [B, 64, 8, 8] f32 tensor the native tail writes the latent into (the search's
+        root pool slot: no copy)"""
         self.refresh()
         t = self.t
         x = obs.float()
@@ -663,10 +676,21 @@ class FoldedConvInitial:
             # the 8 x 8 tail in one launch: representation blocks -> latent, prediction blocks, head 1x1
             _, nb, n_pres, h_ch = self.tail
             x = x.contiguous()
-            latent = torch.empty_like(x)
+            latent = latent_out if latent_out is not None and tuple(latent_out.shape) == tuple(x.shape) \
+                and latent_out.is_contiguous() else torch.empty_like(x)
             h = torch.empty((B, h_ch * 64), dtype=torch.float32, device=x.device)
             _lib.call("lzm_conv_resnet8_p", B, nb, n_pres, h_ch, _lib.ptr(self.native), _lib.ptr(x),
                       _lib.ptr(latent), _lib.ptr(h), _lib.stream_ptr())
+            hp = getattr(self, "heads", None)
+            if hp is not None and h.shape[1] == hp["Khd"]:
+                # the value / policy MLPs in one launch (lzm_conv_heads, prediction heads only)
+                value = torch.empty((B, hp["Vv"]), dtype=torch.float32, device=x.device)
+                policy = torch.empty((B, hp["A"]), dtype=torch.float32, device=x.device)
+                P = _lib.ptr
+                _lib.call("lzm_conv_heads", B, 0, hp["Khd"], hp["off_policy"], None, None, None, P(h), P(hp["w1t"]),
+                          P(hp["b1"]), P(hp["w2t"]), P(hp["b2"]), hp["Vr"], hp["Vv"], hp["A"], None, P(value),
+                          P(policy), None, _lib.stream_ptr())
+                return self._output(value, policy, latent, B, obs.device)
         else:
             latent = x
             p = latent
@@ -679,9 +703,12 @@ class FoldedConvInitial:
         nv = t["v_w2"].shape[1]
         value = F.linear(hid[:, :nv], t["v_w2"], t["v_b2"])
         policy = F.linear(hid[:, nv:], t["p_w2"], t["p_b2"])
+        return self._output(value, policy, latent, B, obs.device)
+
+    def _output(self, value, policy, latent, B, dev):
         if self.ez:
             from .model_conv import EZNetworkOutput
-            z = torch.zeros(1, B, self.model.lstm_hidden_size, device=obs.device)
+            z = torch.zeros(1, B, self.model.lstm_hidden_size, device=dev)
             return EZNetworkOutput(value, [0. for _ in range(B)], policy, latent, (z, z.clone()))
         from .model_mlp import MZNetworkOutput
         return MZNetworkOutput(value, [0. for _ in range(B)], policy, latent)

@@ -44,6 +44,7 @@ struct HeadsArgs {
   float *reward, *value, *policy;      // [B][Vr], [B][Vv], [B][A]
   int32_t *norm_words;                 // optional: ensure_softmax verdict words (see below)
   int norm_nparts;                     // norm_parts(B) word pairs the consumer ANDs
+  int head0;                           // first head of the grid's y range (1: prediction heads only)
 };
 
 __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
@@ -52,7 +53,7 @@ __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
   __shared__ float s_hid[kHdEnvs][32];
   float *s_in = reinterpret_cast<float *>(s_in4);
   const int tid = threadIdx.x;
-  const int head = blockIdx.y;
+  const int head = blockIdx.y + p.head0;
   const int e0 = blockIdx.x * kHdEnvs;
   const int ne = min(kHdEnvs, p.B - e0);
   const int K = p.K[head];

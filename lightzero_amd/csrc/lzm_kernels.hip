@@ -2641,11 +2641,13 @@ extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const floa
                               const float *r_shift, const float *hd, const float *w1t, const float *b1,
                               const float *w2t, const float *b2, int Vr, int Vv, int A, float *reward, float *value,
                               float *policy, int32_t *norm_words, void *stream) {
-  if (B <= 0 || Kr <= 0 || Kr > kHdRMax || Khd <= 0 || Khd > kHdHMax || off_policy <= 0 || off_policy >= Khd ||
-      Khd - off_policy > kHdKMax || off_policy > kHdKMax || Vr <= 0 || Vv <= 0 || A <= 0 || Vr > kHdCols * kHdThreads || Vv > kHdCols * kHdThreads ||
-      A > kHdCols * kHdThreads || !r || !hd || !w1t ||
-      !b1 || !w2t || !b2 || !reward || !value || !policy || (!r_scale) != (!r_shift) || ((uintptr_t)w1t & 15) ||
-      (Kr & 3) || (Khd & 3) || (off_policy & 3)) {
+  // r == NULL: the prediction heads only (value, policy: initial_inference), reward / norm_words unused
+  const bool pred_only = !r;
+  if (B <= 0 || (!pred_only && (Kr <= 0 || Kr > kHdRMax || (Kr & 3) || !reward)) || Khd <= 0 || Khd > kHdHMax ||
+      off_policy <= 0 || off_policy >= Khd || Khd - off_policy > kHdKMax || off_policy > kHdKMax || Vr <= 0 ||
+      Vv <= 0 || A <= 0 || Vr > kHdCols * kHdThreads || Vv > kHdCols * kHdThreads || A > kHdCols * kHdThreads ||
+      !hd || !w1t || !b1 || !w2t || !b2 || !value || !policy || (!r_scale) != (!r_shift) || ((uintptr_t)w1t & 15) ||
+      (Khd & 3) || (off_policy & 3)) {
     set_err("lzm_conv_heads: bad arguments (Kr <= 1024, head planes <= 2048, K per head <= 1024, supports <= 768, 16-B aligned w1t)");
     return LZM_ERR_ARG;
   }
@@ -2658,8 +2660,10 @@ extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const floa
   p.w1t = w1t; p.b1 = b1; p.w2t = w2t; p.b2 = b2;
   p.Vr = Vr; p.Vv = Vv; p.A = A;
   p.reward = reward; p.value = value; p.policy = policy;
-  p.norm_words = norm_words; p.norm_nparts = norm_parts(B);
-  hipLaunchKernelGGL(conv_heads_kernel, dim3((B + kHdEnvs - 1) / kHdEnvs, 3), dim3(kHdThreads), 0, (hipStream_t)stream, p);
+  p.norm_words = pred_only ? nullptr : norm_words; p.norm_nparts = norm_parts(B);
+  p.head0 = pred_only ? 1 : 0;
+  hipLaunchKernelGGL(conv_heads_kernel, dim3((B + kHdEnvs - 1) / kHdEnvs, pred_only ? 2 : 3), dim3(kHdThreads), 0,
+                     (hipStream_t)stream, p);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }

@@ -637,7 +637,8 @@ class EfficientZeroMCTSCtree(object):
             entry = self._graphs.get(gkey, model, t) if graph else None
             buf = entry.buf if entry is not None else (_SearchBuffers() if graph else self._buf).get(
                 B, S, shape, dev, extra=(Hl, Hl))
-            buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
+            if lat0.data_ptr() != buf.pool[0].data_ptr():  # (the collect step writes it in place)
+                buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             buf.extra[0][0].copy_(hc0)
             buf.extra[1][0].copy_(hh0)
             buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
