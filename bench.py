@@ -448,9 +448,9 @@ def _lib_kernel_floats(H=128, A=2, F=32, V=601, res=1):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch from the committed PMC passes (profiles/pmc_latest.json, built by
-    tools/pmc_latest.py from tools/profile_round.sh on the GPU box): 2 x FETCH_SIZE + WRITE_SIZE of
-    that kernel, or None."""
+    """HBM bytes per launch from the COMMITTED PMC passes (profiles/pmc_latest.json, built by
+    tools/pmc_latest.py from tools/profile_round.sh on the GPU box), not measured in this run: 2 x FETCH_SIZE +
+    WRITE_SIZE of that kernel, or None."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(path))
@@ -458,9 +458,18 @@ def pmc_traffic(kernel):
         return None
     base = kernel.split("<")[0]
     for e in (d.get("kernels") or {}).values():
-        if base in e.get("kernel", "") and e.get("traffic_bytes"):
+        if e.get("kernel", "").split("(")[0].split("<")[0].endswith(base) and e.get("traffic_bytes"):
             return e["traffic_bytes"]
-    return d.get("traffic_bytes") if base in d.get("kernel", "") else None
+    return None
+
+
+def pmc_source():
+    """where roofline.traffic comes from: the committed PMC file, its pass directory, build date and head"""
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", "pmc_latest.json")))
+    except (OSError, ValueError):
+        return None
+    return dict({"file": "profiles/pmc_latest.json", "measured_in_this_run": False}, **(d.get("source") or {}))
 
 
 def algorithmic_bytes(B, A, H, V, dbar):
@@ -759,6 +768,7 @@ def conv_roofline(step, model, B, S, device):
                                         "; head MLPs on the fp32 VALU",
             "kernel": kname, "achieved": round(mfma, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(mfma / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(kname),
+            "traffic_source": pmc_source(),
             "alg_flops_per_sim": int(flops), "alg_conv_flops_per_sim": int(conv),
             "alg_f32_tflops": round(f32, 2), "alg_f32_frac_of_fp32_peak": round(f32 / FP32_PEAK_TFLOPS, 4),
             "launch_us": round(ms[key] * 1e3, 1), "sims_per_launch": B * S,
@@ -794,7 +804,7 @@ def mlp_roofline(step, B, S, device):
         return {"bound": "valu", "compute": "fp32 VALU (v_pk_fma_f32)", "mfma_utilisation": 0.0,
                 "kernel": kname, "achieved": round(achieved, 3),
                 "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-                "traffic": pmc_traffic(kname), "alg_flops_per_launch": int(flops),
+                "traffic": pmc_traffic(kname), "traffic_source": pmc_source(), "alg_flops_per_launch": int(flops),
                 "alg_hbm_bytes_per_launch": int(hbm), "hbm_achieved_GBs": round(hbm / sec / 1e9, 2),
                 "l2_weight_bytes_per_launch": int(l2), "l2_achieved_TBs": round(l2 / sec / 1e12, 3),
                 "l2_peak_TBs": L2_PEAK_TBS, "roots_per_workgroup": R,
@@ -1014,7 +1024,8 @@ def config4(args, device, cpu):
                                                     "heads on the VALU",
                         "kernel": "az_search_fused_kernel", "achieved": round(ach, 3), "peak": FP32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(ach / FP32_PEAK_TFLOPS, 5),
-                        "traffic": pmc_traffic("az_search_fused_kernel"), "alg_flops_per_sim": int(flops),
+                        "traffic": pmc_traffic("az_search_fused_kernel"), "traffic_source": pmc_source(),
+                        "alg_flops_per_sim": int(flops),
                         "alg_conv_flops_per_sim": int(conv), "launch_us": round(sec * 1e6, 1),
                         "sims_per_launch": B * S}}
     if cpu:

@@ -2603,8 +2603,8 @@ int lzm_repr_downsample(int B, int cin, const float *w, const float *obs, float 
   memset(&a, 0, sizeof(a));
   a.B = B; a.cin_obs = cin;
   int rc;
-  // L1: obs (NCHW 64 x 64) -> A0 [32][32][32]
-  a.ntiles = B * 16; a.in = obs; a.w = w + L.w1; a.bias = w + L.b1; a.res = nullptr; a.out = A0;
+  // L1: obs (NCHW 64 x 64) -> A0 [32][32][32] (128-pixel tiles: 8 per image)
+  a.ntiles = B * 8; a.in = obs; a.w = w + L.w1; a.bias = w + L.b1; a.res = nullptr; a.out = A0;
   if ((rc = repr_launch<32, 32, 2, 32, 2>(a, s)) != LZM_OK) return rc;
   // resblocks1: A0 -> A1 -> A0 (+ A0)
   a.in = A0; a.w = w + L.r1w1; a.bias = w + L.r1b1; a.out = A1;
@@ -2622,8 +2622,7 @@ int lzm_repr_downsample(int B, int cin, const float *w, const float *obs, float 
   a.in = D0; a.w = w + L.r2w2; a.bias = w + L.r2b2; a.res = D1; a.out = D1;
   if ((rc = repr_launch<64, 64, 1, 16, 0>(a, s)) != LZM_OK) return rc;
   // avg pool -> out NCHW [B][64][8][8]
-  const long long n = (long long)B * 4096;
-  hipLaunchKernelGGL(repr_avgpool_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, D1, out, B);
+  hipLaunchKernelGGL(repr_avgpool_kernel, dim3(B), dim3(256), 0, s, D1, out, B);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
@@ -2678,7 +2677,8 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
                                int off_policy, int Vr, int Vv, int categorical, int32_t *rec_x, int32_t *rec_a,
                                int32_t *rec_len, float *rec_decoded, float *rec_logits, void *stream) {
   const int S = num_simulations;
-  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !trunk_w || !actmap || !w1t || !b1 || !w2q || !b2 ||
+  if (!h || !minmax || (!seeds && !h->step_count) || !vtp_in || !latent_pool || !trunk_w || !actmap || !w1t || !b1 ||
+      !w2q || !b2 ||
       S <= 0) {
     set_err("lzm_search_conv: null argument or no simulations");
     return LZM_ERR_ARG;
@@ -2727,6 +2727,8 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
   p.flags = h->lb_flags; p.epoch = h->epoch; p.err = h->err; p.sdiag = h->search_diag; p.fast = fast ? 1 : 0;
   p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
+  p.step_count = h->step_count; p.step_base = h->step_base; p.step_inc = h->step_inc; p.step_fresh = h->step_fresh;
+  p.step_delta = h->step_delta; p.out_dist = h->step_dist; p.out_values = h->step_vals;
   // dynamic LDS plan (float offsets, 16-B aligned): the two split-bf16 activation buffers first
   size_t o = (size_t)2 * kBxBuf / 2;
   p.off_stat = (int)o; o += (size_t)h->cap * 4;
@@ -2781,7 +2783,8 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
                                   int32_t *rec_len, float *rec_decoded, float *rec_logits, int32_t *rec_reset,
                                   void *stream) {
   const int S = num_simulations;
-  if (!h || !minmax || !seeds || !vtp_in || !latent_pool || !hpool || !cpool || !trunk_w || !actmap || !lstm_frag ||
+  if (!h || !minmax || (!seeds && !h->step_count) || !vtp_in || !latent_pool || !hpool || !cpool || !trunk_w ||
+      !actmap || !lstm_frag ||
       !lstm_bias || !vp_s || !vp_t || !w1t || !b1 || !w2q || !b2 || S <= 0) {
     set_err("lzm_search_conv_ez: null argument or no simulations");
     return LZM_ERR_ARG;
@@ -2853,6 +2856,8 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
   p.coef = h->coef; p.coef_positions = h->coef_positions; p.pow16807 = h->pow16807;
   p.flags = h->lb_flags; p.epoch = h->epoch; p.err = h->err; p.sdiag = h->search_diag; p.fast = fast ? 1 : 0;
   p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
+  p.step_count = h->step_count; p.step_base = h->step_base; p.step_inc = h->step_inc; p.step_fresh = h->step_fresh;
+  p.step_delta = h->step_delta; p.out_dist = h->step_dist; p.out_values = h->step_vals;
   p.rec_reset = rec_reset;
   p.xin = wsf; p.h1g = wsf + f_xin; p.kpart = wsf + f_xin + f_h1;
   p.xflags = wsl; p.tflags = wsl + (size_t)S * B; p.pflags = wsl + (size_t)S * B + (size_t)S * T;

@@ -48,9 +48,11 @@ struct ReprConvArgs {
 // pitch ROWP (stride 2: even columns, then odd ones), group plane NPP positions (a multiple of 16).
 template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
 struct ReprGeom {
-  static constexpr int TR = 64 / WOUT;
+  // output pixels per tile: 128 for the 32-channel layers (two pixel tiles per wave), 64 otherwise
+  static constexpr int PX = COUT == 32 ? 128 : 64;
+  static constexpr int TR = PX / WOUT;
   static constexpr int HR = MODE == 2 ? 1 : (TR - 1) * STRIDE + 3;
-  static constexpr int HC = MODE == 2 ? 64 : (WOUT - 1) * STRIDE + 3;
+  static constexpr int HC = MODE == 2 ? PX : (WOUT - 1) * STRIDE + 3;
   static constexpr int HC2 = (HC + 1) / 2;
   static constexpr int ROWP = STRIDE == 2 && MODE != 2 ? 2 * HC2 : HC;
   static constexpr int NP = HR * ROWP;
@@ -61,7 +63,7 @@ struct ReprGeom {
   // 8 waves, one out tile each: 2 out tiles -> a pixel tile per wave; 4 -> all 4 pixel tiles over half of K
   // (KS = 2: K split, partial sums exchanged through LDS); 8 -> all 4 pixel tiles, all of K
   static constexpr int KS = OT == 4 ? 2 : 1;
-  static constexpr int PTW = OT == 2 ? 1 : 4;                         // pixel tiles per wave
+  static constexpr int PTW = OT == 2 ? PX / 64 : PX / 16;             // pixel tiles per wave
   static constexpr int NCW = NCH / KS;                                // K chunks per wave
   static_assert(OT == 2 || OT == 4 || OT == 8, "out tiles");
   static_assert(NCH % KS == 0, "K split");
@@ -69,7 +71,7 @@ struct ReprGeom {
   static constexpr int BUF = 3 * TERM;                                // bf16 per halo buffer
   static constexpr int PPW = MODE == 2 ? 64 : 64 / CG;                // positions per wave-instruction
   // staging items (position, group): 64 per wave-instruction, PPW consecutive positions x CG groups
-  static constexpr int ITEMS = MODE == 2 ? 64 * 8 : (HR * HC + PPW - 1) / PPW * 64;
+  static constexpr int ITEMS = MODE == 2 ? PX * 8 : (HR * HC + PPW - 1) / PPW * 64;
   static constexpr int IPT = (ITEMS + kRpThreads - 1) / kRpThreads;  // per thread
 };
 
@@ -86,8 +88,8 @@ __device__ __forceinline__ bool rp_item(int q, int &hr, int &hc, int &g) {
   if (q >= G::ITEMS) return false;
   if constexpr (MODE == 2) {
     hr = 0;
-    hc = q & 63;  // pixel of the tile
-    g = q >> 6;
+    hc = q % G::PX;  // pixel of the tile
+    g = q / G::PX;
     return true;
   }
   // lanes: PPW consecutive halo positions (global: whole NHWC rows, coalesced; LDS: distinct bank slots per
@@ -122,8 +124,8 @@ __device__ __forceinline__ void rp_load(const ReprConvArgs &a, int tile, float4 
     int hr = 0, hc = 0, g = 0;
     const bool item = rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g);
     if constexpr (MODE == 2) {
-      // im2col: pixel hc of the tile (row r0 + hc / 32, column hc % 32), K = 8 g .. 8 g + 7 = tap * C + c
-      const int oy = r0 + (hc >> 5), ox = hc & 31;
+      // im2col: pixel hc of the tile (row r0 + hc / WOUT, column hc % WOUT), K = 8 g .. 8 g + 7 = tap * C + c
+      const int oy = r0 + hc / WOUT, ox = hc % WOUT;
       float e[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // this wave's out tile, first pixel tile and K half
   const int ot = G::OT == 2 ? (wv & 1) : (G::OT == 4 ? (wv & 3) : wv);
-  const int pt0 = G::OT == 2 ? (wv >> 1) : 0;
+  const int pt0 = G::OT == 2 ? (wv >> 1) * G::PTW : 0;
   const int kh = G::KS == 2 ? (wv >> 2) : 0;
   // the weights of that out tile over its K chunks, three terms: registers for the whole launch
   uint4 wr[G::NCW][3];
@@ -207,6 +209,18 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const uint16_t *cur = lds + (it & 1) * G::BUF;
     const int nxt = tile + gridDim.x;
     if (nxt < a.ntiles) rp_load<CIN, COUT, STRIDE, WOUT, MODE>(a, nxt, v);  // in flight during the MFMAs
+    const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
+    // the epilogue's residual, issued now (its latency hides behind the MFMAs): one float4 per pixel tile this
+    // wave finishes (K split: 2, the tiles 2 kh + j), none for the dual layer
+    constexpr int NRES = MODE == 1 ? 1 : (G::KS == 2 ? 2 : G::PTW);
+    float4 rres[NRES];
+#pragma unroll
+    for (int j = 0; j < NRES; ++j) {
+      const int p = G::KS == 2 ? 2 * kh + j : j;
+      const int px = 16 * (pt0 + p) + (lane & 15);
+      const int64_t e = (((int64_t)b * HOUT + r0 + px / WOUT) * WOUT + px % WOUT) * COUT_T + ch;
+      rres[j] = (MODE != 1 && a.res) ? *reinterpret_cast<const float4 *>(a.res + e) : float4{0.f, 0.f, 0.f, 0.f};
+    }
     bxf4 acc[G::PTW];
 #pragma unroll
     for (int p = 0; p < G::PTW; ++p) acc[p] = bxf4{0.f, 0.f, 0.f, 0.f};
@@ -270,7 +284,6 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       }
     }
     // epilogue: acc[p][r] = out channel ch + r at pixel 16 (pt0 + p) + (lane & 15)
-    const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
 #pragma unroll
     for (int p = 0; p < G::PTW; ++p) {
       if (G::KS == 2 && (p >> 1) != kh) continue;  // (the K-split partner's tiles)
@@ -279,7 +292,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       float4 y = float4{acc[p][0] + bias.x, acc[p][1] + bias.y, acc[p][2] + bias.z, acc[p][3] + bias.w};
       if (!sc) {
         if (a.res) {
-          const float4 rr = *reinterpret_cast<const float4 *>(a.res + e);
+          const float4 rr = rres[MODE == 1 ? 0 : (G::KS == 2 ? (p & 1) : p)];
           y.x += rr.x; y.y += rr.y; y.z += rr.z; y.w += rr.w;
         }
         y.x = fmaxf(y.x, 0.f); y.y = fmaxf(y.y, 0.f); y.z = fmaxf(y.z, 0.f); y.w = fmaxf(y.w, 0.f);
@@ -291,23 +304,36 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 }
 
-// avg_pool2d(3, 2, padding 1, count_include_pad) of NHWC [B][16][16][64] -> NCHW [B][64][8][8]
+// avg_pool2d(3, 2, padding 1, count_include_pad) of NHWC [B][16][16][64] -> NCHW [B][64][8][8]: one workgroup per
+// image, the 64 KiB image staged through LDS (coalesced float4 reads; positions padded to 65 floats so the
+// pooling reads of consecutive output columns fall in different banks), NCHW written coalesced
 __global__ __launch_bounds__(256) void repr_avgpool_kernel(const float *__restrict__ in, float *__restrict__ out, int B) {
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (b, c, y, x) of the output, x fastest
-  if (q >= (int64_t)B * 64 * 64) return;
-  const int x = (int)(q & 7), y = (int)((q >> 3) & 7), c = (int)((q >> 6) & 63);
-  const int64_t b = q >> 12;
-  float s = 0.f;
-  for (int dy = -1; dy <= 1; ++dy) {
-    const int iy = 2 * y + dy;
-    if (iy < 0 || iy >= 16) continue;
-    for (int dx = -1; dx <= 1; ++dx) {
-      const int ix = 2 * x + dx;
-      if (ix < 0 || ix >= 16) continue;
-      s += in[((b * 16 + iy) * 16 + ix) * 64 + c];
-    }
+  __shared__ float img[256 * 65];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float4 *src = reinterpret_cast<const float4 *>(in + (size_t)b * 16384);
+#pragma unroll 4
+  for (int q = tid; q < 4096; q += 256) {
+    const float4 v = src[q];
+    float *d = img + (q >> 4) * 65 + (q & 15) * 4;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
   }
-  out[q] = s / 9.0f;
+  __syncthreads();
+  float *dst = out + (size_t)b * 4096;
+#pragma unroll 4
+  for (int o = tid; o < 4096; o += 256) {
+    const int c = o >> 6, y = (o >> 3) & 7, x = o & 7;
+    float s = 0.f;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = 2 * y + dy;
+      if (iy < 0 || iy >= 16) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ix = 2 * x + dx;
+        if (ix < 0 || ix >= 16) continue;
+        s += img[(iy * 16 + ix) * 65 + c];
+      }
+    }
+    dst[o] = s / 9.0f;
+  }
 }
 
 // ---- host side: packing

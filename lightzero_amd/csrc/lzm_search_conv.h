@@ -85,6 +85,16 @@ struct ConvSearchArgs {
   unsigned long long *xflags, *tflags, *pflags;  // [S][B], [S][T], [S][T] {epoch, payload} words
   int nmb, T;             // row blocks of 64, tiles (nmb * H / 16)
   unsigned long long *stamps;  // STAMPS instantiation only
+  // collect-step mode (lzm_search_set_step on the handle; lightzero_amd.collect): the seeds of this step from
+  // the device step counter ((base + count * S + k) mod 10^6, seed_sequence_kernel's rule), fresh min-max
+  // bounds, the root outputs (visit counts per legal action, the root value) and the counter advanced by the
+  // last workgroup — the launches around the search folded into it
+  int64_t *step_count;
+  long long step_base;
+  int step_inc, step_fresh;
+  float step_delta;
+  int32_t *out_dist;
+  float *out_values;
   // dynamic LDS plan: float offsets (the two activation buffers come first)
   int off_stat, off_meta, off_val, off_lut, off_legal, off_path, off_pact, off_pbt, off_r, off_hd, off_hid, off_part,
       off_lg, off_seed;
@@ -420,7 +430,12 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   t.pathlen = s_len;
   uint32_t *s_seed = reinterpret_cast<uint32_t *>(smem + p.off_seed);
   uint32_t *s_pow = s_seed + S;
-  for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
+  if (p.step_count) {
+    const long long cnt = *p.step_count;  // (read before the last workgroup's increment)
+    for (int e = tid; e < S; e += kScThreads) s_seed[e] = (uint32_t)((p.step_base + cnt * (long long)S + e) % 1000000ll);
+  } else {
+    for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
+  }
   if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
   for (int k = tid; k < 2 * 3 * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
     const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
@@ -428,7 +443,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     sc_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
   }
   if (tid == 0) {
-    s_mm[0] = p.minmax[b];
+    s_mm[0] = p.step_fresh ? make_float4(kFloatMin, kFloatMax, p.step_delta, 0.0f) : p.minmax[b];
     s_vtp0 = p.vtp_in[b];
     s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -665,15 +680,22 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     st_acc[7] = __builtin_amdgcn_s_memtime() - st_begin;
     for (int n = 0; n < 9; ++n) atomicAdd(p.stamps + 40 + n, st_acc[n]);
   }
+  // collect-step root outputs (root_outputs_kernel's values): visit counts per legal action, the root value
+  if (p.out_dist && tid < A) {
+    const int rl = lm[0].latent;
+    p.out_dist[(size_t)b * A + tid] = (rl >= 0 && tid < llegal[A]) ? ls[1 + A * rl + llegal[tid]].visit : -1;
+  }
+  if (p.out_values && tid == 0) p.out_values[b] = node_value(ls[0]);
   if (tid == 0) {
     p.minmax[b] = s_mm[0];
     p.pathlen[b] = s_len[0];
     // the last workgroup advances the epoch (no release fence: the kernel boundary orders the
-    // write-back for every later reader)
+    // write-back for every later reader) and the collect step's counter (every workgroup has read it)
     const uint32_t done = atomicAdd(p.epoch + 1, 1u);
     if (done == (uint32_t)gridDim.x - 1) {
       p.epoch[1] = 0;
       __hip_atomic_store(p.epoch, (uint32_t)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.step_count && p.step_inc) *p.step_count += 1;
     }
   }
 }
@@ -759,7 +781,12 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   t.pathlen = s_len;
   uint32_t *s_seed = reinterpret_cast<uint32_t *>(smem + p.off_seed);
   uint32_t *s_pow = s_seed + S;
-  for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
+  if (p.step_count) {
+    const long long cnt = *p.step_count;  // (read before the last workgroup's increment)
+    for (int e = tid; e < S; e += kScThreads) s_seed[e] = (uint32_t)((p.step_base + cnt * (long long)S + e) % 1000000ll);
+  } else {
+    for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
+  }
   if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
   auto zero_borders = [&]() {
     for (int k = tid; k < 2 * 3 * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
@@ -770,7 +797,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   };
   if (tid == 0) {
     if (has_root) {
-      s_mm[0] = p.minmax[b];
+      s_mm[0] = p.step_fresh ? make_float4(kFloatMin, kFloatMax, p.step_delta, 0.0f) : p.minmax[b];
       s_vtp0 = p.vtp_in[b];
     }
     s_epoch = (int)__hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1152,17 +1179,23 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     st_acc[9] = __builtin_amdgcn_s_memtime() - st_begin;
     for (int n = 0; n < 14; ++n) atomicAdd(p.stamps + 40 + n, st_acc[n]);
   }
+  if (has_root && p.out_dist && tid < A) {  // collect-step root outputs, as the MuZero kernel
+    const int rl = lm[0].latent;
+    p.out_dist[(size_t)b * A + tid] = (rl >= 0 && tid < t.nlegal[0]) ? ls[1 + A * rl + t.legal[tid]].visit : -1;
+  }
+  if (has_root && p.out_values && tid == 0) p.out_values[b] = node_value(ls[0]);
   if (tid == 0) {
     if (has_root) {
       p.minmax[b] = s_mm[0];
       p.pathlen[b] = s_len[0];
     }
     // the last workgroup advances the epoch (no release fence: the kernel boundary orders the
-    // write-back for every later reader)
+    // write-back for every later reader) and the collect step's counter
     const uint32_t done = atomicAdd(p.epoch + 1, 1u);
     if (done == (uint32_t)gridDim.x - 1) {
       p.epoch[1] = 0;
       __hip_atomic_store(p.epoch, (uint32_t)(epoch + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (p.step_count && p.step_inc) *p.step_count += 1;
     }
   }
 }

@@ -370,9 +370,9 @@ class MuZeroMCTSCtree(object):
                 buf.pool[0].copy_(lat0.reshape((B,) + tuple(shape)))
             # the one-launch searches read device seeds / to_play in place (no staging copies)
             in_place = (fz is not None or cz is not None) and rec is None
-            # the MLP one-launch search runs the collect step's glue in its kernel; the conv one runs
-            # it as two small launches around the search (seed sequence, root outputs)
-            step_in_kernel = step is not None and in_place and fz is not None
+            # the one-launch searches run the collect step's glue in their kernels (lzm_search_set_step:
+            # seeds from the step counter, fresh min-max bounds, root outputs, the counter increment)
+            step_in_kernel = step is not None and in_place
             vt = to_play_batch if in_place and _usable_i32(to_play_batch, B, dev) else None
             if vt is None:
                 buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
@@ -392,9 +392,17 @@ class MuZeroMCTSCtree(object):
             if cz is not None:
                 # the conv network's whole search in one launch (lzm_search_conv)
                 cfg = self._cfg
-                new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
-                t.search_conv(cz, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base), float(cfg.pb_c_init),
-                              float(np.float32(cfg.discount_factor)), self._categorical(), rec=rec)
+                if step_in_kernel:
+                    t.set_step(step["count"], int(step["base"]), step.get("increment", True), step["dist"],
+                               step["values"], True, cfg.value_delta_max)
+                else:
+                    new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
+                try:
+                    t.search_conv(cz, S, buf.mm, sd, vt, buf.pool, int(cfg.pb_c_base), float(cfg.pb_c_init),
+                                  float(np.float32(cfg.discount_factor)), self._categorical(), rec=rec)
+                finally:
+                    if step_in_kernel:
+                        t.set_step()
             elif fz is not None:
                 packed, dims = fz
                 cfg = self._cfg
@@ -642,35 +650,54 @@ class EfficientZeroMCTSCtree(object):
             buf.extra[0][0].copy_(hc0)
             buf.extra[1][0].copy_(hh0)
             buf.vtp_in.copy_(_to_play_tensor(to_play_batch, B, dev))
-            if step is not None:  # seeds (base + count * S + k) mod 10^6 on the device
+            cz = self._fused_conv(model, t, shape, Hl)
+            recording = getattr(self, "record", False)
+            # the one-launch search runs the collect step's glue in its kernel (lzm_search_set_step: seeds
+            # from the step counter, fresh min-max bounds, root outputs, the counter increment)
+            step_in_kernel = step is not None and cz is not None and not recording
+
+            def step_seeds():  # seeds (base + count * S + k) mod 10^6 on the device
                 _lib.call("lzm_seed_sequence", _lib.ptr(step["count"]), int(step["base"]), S, _lib.ptr(buf.seeds),
                           _lib.stream_ptr())
-            else:
+
+            if step is None:
                 buf.seeds.copy_(_seeds(S, dev) if seeds is None else seeds.reshape(S))
-            if getattr(self, "record", False):
+            elif not step_in_kernel:
+                step_seeds()
+            if recording:
                 rec = _Recorder(S, B, t.A, dev)
                 rec.is_reset = torch.zeros((S, B), dtype=torch.int32, device=dev)
                 rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
-            cz = self._fused_conv(model, t, shape, Hl)
             if cz is not None:
                 # the conv network's whole search, reward LSTM included, in one launch (lzm_search_conv_ez);
                 # the launch needs its whole grid co-resident: when the occupancy bound refuses it, nothing
                 # ran and the generic per-simulation path runs instead — eagerly only: inside a stream
                 # capture the refusal is raised (the caller captures a different graph, not a fallback)
                 cfg = self._cfg
-                new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
+                if step_in_kernel:
+                    t.set_step(step["count"], int(step["base"]), step.get("increment", True), step["dist"],
+                               step["values"], True, cfg.value_delta_max)
+                else:
+                    new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
                 try:
-                    t.search_conv_ez(cz, S, buf.mm, buf.seeds, buf.vtp_in, buf.pool, buf.extra[0], buf.extra[1],
-                                     int(cfg.lstm_horizon_len), int(cfg.pb_c_base), float(cfg.pb_c_init),
-                                     float(np.float32(cfg.discount_factor)),
+                    t.search_conv_ez(cz, S, buf.mm, None if step_in_kernel else buf.seeds, buf.vtp_in, buf.pool,
+                                     buf.extra[0], buf.extra[1], int(cfg.lstm_horizon_len), int(cfg.pb_c_base),
+                                     float(cfg.pb_c_init), float(np.float32(cfg.discount_factor)),
                                      bool(cfg.model.get('categorical_distribution', True)), rec=rec)
                     self.last_path = "fused"
                 except _lib.ResidencyError:
                     if torch.cuda.is_current_stream_capturing():
                         raise
+                    if step_in_kernel:  # nothing ran: the glue as launches around the generic path
+                        t.set_step()
+                        step_in_kernel = False
+                        step_seeds()
                     self.residency_fallbacks = getattr(self, "residency_fallbacks", 0) + 1
                     self.last_path = "generic (co-residency refused)"
                     self._loop(t, model, buf, S, row, Hl, rec)
+                finally:
+                    if step_in_kernel:
+                        t.set_step()
             elif graph:
                 self.last_path = "generic"
                 if entry is None:
@@ -680,7 +707,7 @@ class EfficientZeroMCTSCtree(object):
             else:
                 self.last_path = "generic"
                 self._loop(t, model, buf, S, row, Hl, rec)
-            if step is not None:
+            if step is not None and not step_in_kernel:
                 _lib.call("lzm_get_root_outputs", t.h, _lib.ptr(step["dist"]), _lib.ptr(step["values"]),
                           _lib.stream_ptr())
                 if step.get("increment", True):

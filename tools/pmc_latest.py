@@ -3,7 +3,8 @@ FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum / TCC_MISS_sum for each named kernel (the 
 kernels: search_res_kernel for config 2, search_conv_kernel for config 5), with the gfx950 FETCH_SIZE
 correction of MI355X_MICROARCH.md (x2: 128-B streaming reads tallied at 64 B).
 
-    python tools/pmc_latest.py gpurun_out/<dir> search_res_kernel search_conv_kernel > profiles/pmc_latest.json
+    python tools/pmc_latest.py gpurun_out/<dir> search_res_kernel search_conv_kernel search_conv_ez_kernel \
+        az_search_fused_kernel > profiles/pmc_latest.json
 """
 import csv
 import glob
@@ -44,8 +45,18 @@ def summarise(root, pat):
 
 
 def main():
+    import datetime
+    import subprocess
     root = sys.argv[1]
-    print(json.dumps({"kernels": {pat: summarise(root, pat) for pat in sys.argv[2:]}}, indent=1))
+    try:
+        head = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip()
+    except OSError:
+        head = None
+    # where the numbers come from: bench.py copies this into roofline.traffic_source, so the field cannot be
+    # read as measured in the run that prints it
+    source = {"pmc_dir": os.path.normpath(root), "built": datetime.datetime.utcnow().strftime("%Y-%m-%d %H:%M UTC"),
+              "head": head, "passes": "one rocprofv3 --kernel-trace --pmc run per counter group (tools/profile_round.sh)"}
+    print(json.dumps({"source": source, "kernels": {pat: summarise(root, pat) for pat in sys.argv[2:]}}, indent=1))
 
 
 if __name__ == "__main__":
