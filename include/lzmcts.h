@@ -409,6 +409,14 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
 int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const float *r, const float *r_scale, const float *r_shift,
                    const float *hd, const float *w1t, const float *b1, const float *w2t, const float *b2, int Vr,
                    int Vv, int A, float *reward, float *value, float *policy, int32_t *norm_words, void *stream);
+/* lzm_conv_heads' prediction heads (r = NULL form) followed, in the same launch, by lzm_roots_prepare on `h`
+ * (B roots, A <= 256 actions) with the policy logits just computed — the conv policies' initial_inference +
+ * roots.prepare (muzero.py:643-660, efficientzero.py:555-575) without the preparation launch; the same root
+ * records bit for bit (the policy-head workgroups prepare their envs from their LDS copy of the logits). */
+int lzm_conv_heads_prepare(lzm_handle *h, int B, int Khd, int off_policy, const float *hd, const float *w1t,
+                           const float *b1, const float *w2t, const float *b2, int Vr, int Vv, int A, float *value,
+                           float *policy, const int32_t *legal, const int32_t *count, const float *noises,
+                           float noise_weight, const float *rewards, const int32_t *to_play, void *stream);
 
 /* One launch = one whole MuZeroMCTSCtree.search for the conv MuZeroModel (Atari configs; replaces
  * the per-simulation loop of mcts_ctree.py:255-321 around muzero_model.py:241-373's recurrent step:

@@ -77,6 +77,8 @@ SIGNATURES = {
     "lzm_search_conv_ez": [_vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp,
                            _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_conv_heads": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "lzm_conv_heads_prepare": [_vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f,
+                               _vp, _vp, _vp],
     "lzm_set_norm_words": [_vp, _vp],
     "lzm_seed_sequence": [_vp, _i64, _i, _vp, _vp],
     "lzm_get_root_outputs": [_vp, _vp, _vp, _vp],

@@ -90,20 +90,26 @@ class DeviceSearchStep:
                         prepare=dict(roots=self.roots, noise_weight=self.noise_weight, noises=self.noises,
                                      rewards=self.rewards, to_play=self.to_play))
                 else:
-                    if isinstance(self.initial, FoldedConvInitial):  # the latent straight into the root slot
-                        out = self.initial.initial_inference(self.obs, latent_out=self._root_slot())
+                    prepared = False
+                    if isinstance(self.initial, FoldedConvInitial):
+                        # the latent straight into the root slot; the root preparation in the heads' launch
+                        out = self.initial.initial_inference(
+                            self.obs, latent_out=self._root_slot(),
+                            prepare=dict(roots=self.roots, noise_weight=self.noise_weight, noises=self.noises,
+                                         rewards=self.rewards, to_play=self.to_play))
+                        prepared = getattr(out, "prepared", False)
                     else:
                         out = (self.initial or self.model).initial_inference(self.obs)
-                    self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
-                                              self.to_play)
+                    if not prepared:
+                        self.roots.prepare_device(self.noise_weight, self.noises, self.rewards, out.policy_logits,
+                                                  self.to_play)
                 # the seeds (from the step counter), fresh min-max bounds, the root outputs and the
-                # counter increment run inside the search (the one-launch search: in its kernel)
+                # counter increment run inside the search (the one-launch search: in its kernel); an
+                # epilogue (the collector's env step) reads the advanced counter
                 t = self.roots.tree
                 dist = torch.empty((self.B, t.A), dtype=torch.int32, device=self.device)
                 values = torch.empty(self.B, dtype=torch.float32, device=self.device)
-                # (an epilogue reads the counter of this step: it advances after the epilogue)
-                stp = dict(count=self._count, base=self._base, dist=dist, values=values,
-                           increment=self.epilogue is None)
+                stp = dict(count=self._count, base=self._base, dist=dist, values=values, increment=True)
                 if self.ez:  # the roots' LSTM state: the initial inference's reward_hidden_state (zeros)
                     self.mcts.search(self.roots, self.model, out.latent_state, out.reward_hidden_state, self.to_play,
                                      step=stp)
@@ -113,7 +119,6 @@ class DeviceSearchStep:
                            policy_logits=out.policy_logits, value_logits=out.value)
                 if self.epilogue is not None:
                     self.epilogue(res)
-                    self._count.add_(1)
                 return res
             finally:
                 self.mcts_cls.rng_mode = old

@@ -645,9 +645,11 @@ class FoldedConvInitial:
         y = cls._conv_relu(x, w1, b1, 1, fused)
         return cls._conv_add_relu(y, w2, x, b2, fused)
 
-    def initial_inference(self, obs, latent_out=None):
+    def initial_inference(self, obs, latent_out=None, prepare=None):
         """latent_out: optional [B, 64, 8, 8] f32 tensor the native tail writes the latent into (the search's
-        root pool slot: no copy)"""
+        root pool slot: no copy). prepare: optional dict(roots, noise_weight, noises, rewards, to_play) — also
+        Roots.prepare_device with the policy logits, in the heads' launch (lzm_conv_heads_prepare); the caller
+        checks `prepared` on the output (False: the heads ran elsewhere, prepare the roots itself)."""
         self.refresh()
         t = self.t
         x = obs.float()
@@ -687,10 +689,24 @@ class FoldedConvInitial:
                 value = torch.empty((B, hp["Vv"]), dtype=torch.float32, device=x.device)
                 policy = torch.empty((B, hp["A"]), dtype=torch.float32, device=x.device)
                 P = _lib.ptr
-                _lib.call("lzm_conv_heads", B, 0, hp["Khd"], hp["off_policy"], None, None, None, P(h), P(hp["w1t"]),
-                          P(hp["b1"]), P(hp["w2t"]), P(hp["b2"]), hp["Vr"], hp["Vv"], hp["A"], None, P(value),
-                          P(policy), None, _lib.stream_ptr())
-                return self._output(value, policy, latent, B, obs.device)
+                if prepare is not None:
+                    # + the root preparation from the logits, in the same launch
+                    tr, legal, count = prepare["roots"].device_legal(hp["A"], x.device)
+                    f32 = dict(device=x.device, dtype=torch.float32)
+                    noises = prepare.get("noises")
+                    _lib.call("lzm_conv_heads_prepare", tr.h, B, hp["Khd"], hp["off_policy"], P(h), P(hp["w1t"]),
+                              P(hp["b1"]), P(hp["w2t"]), P(hp["b2"]), hp["Vr"], hp["Vv"], hp["A"], P(value), P(policy),
+                              P(legal), P(count), None if noises is None else P(noises.to(**f32).contiguous()),
+                              float(prepare["noise_weight"]), P(prepare["rewards"].to(**f32).contiguous()),
+                              P(prepare["to_play"].to(device=x.device, dtype=torch.int32).contiguous()),
+                              _lib.stream_ptr())
+                else:
+                    _lib.call("lzm_conv_heads", B, 0, hp["Khd"], hp["off_policy"], None, None, None, P(h),
+                              P(hp["w1t"]), P(hp["b1"]), P(hp["w2t"]), P(hp["b2"]), hp["Vr"], hp["Vv"], hp["A"], None,
+                              P(value), P(policy), None, _lib.stream_ptr())
+                out = self._output(value, policy, latent, B, obs.device)
+                out.prepared = prepare is not None
+                return out
         else:
             latent = x
             p = latent

@@ -26,7 +26,7 @@ struct CollectArgs {
   int n, A, T, E, max_steps, deterministic;
   float temperature, noise_alpha;
   uint32_t seed;
-  const int64_t *counter;      // env-step counter (device; advanced by the caller after each step)
+  const int64_t *counter;      // env-step counter (device; the collect step's search advances it before this reads it)
   const int32_t *visits;       // [n][A] root visit counts (legal order)
   const float *root_value;     // [n]
   double *state;               // [n][4]

@@ -23,6 +23,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lzm_tree.h"
+
 namespace lzm {
 
 constexpr int kHdEnvs = 2;     // envs per workgroup
@@ -45,6 +47,10 @@ struct HeadsArgs {
   int32_t *norm_words;                 // optional: ensure_softmax verdict words (see below)
   int norm_nparts;                     // norm_parts(B) word pairs the consumer ANDs
   int head0;                           // first head of the grid's y range (1: prediction heads only)
+  // lzm_conv_heads_prepare: the policy-head workgroups also prepare their envs' roots from the logits they
+  // computed (CRoots::prepare, prepare_root: the root preparation launch folded in); A <= kHdThreads
+  PrepareArgs prep;
+  int prep_on;
 };
 
 __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
@@ -141,6 +147,8 @@ __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
   __syncthreads();
   // ---- output layer: kHdCols columns of this head per thread, 32-deep dot per env
   float *out = head == 0 ? p.reward : (head == 1 ? p.value : p.policy);
+  const bool prep = p.prep_on && head == 2;  // (block-uniform)
+  __shared__ float s_lg[kHdEnvs][kHdThreads];
   float rsum[kHdEnvs];  // this thread's share of each row's sum (verdict words below)
 #pragma unroll
   for (int e = 0; e < kHdEnvs; ++e) rsum[e] = 0.0f;
@@ -159,6 +167,14 @@ __global__ __launch_bounds__(kHdThreads) void conv_heads_kernel(HeadsArgs p) {
     for (int e = 0; e < ne; ++e) out[(size_t)(e0 + e) * wd + jj] = acc[e] + b2[cc];
 #pragma unroll
     for (int e = 0; e < kHdEnvs; ++e) rsum[e] += acc[e] + b2[cc];
+    if (prep && cc == 0) {
+#pragma unroll
+      for (int e = 0; e < kHdEnvs; ++e) s_lg[e][jj] = acc[e] + b2[cc];
+    }
+  }
+  if (prep) {
+    __syncthreads();
+    if (tid < ne) prepare_root(p.prep, e0 + tid, s_lg[tid]);
   }
   // ensure_softmax's verdict (scaling_transform.py:36-62) for the reward and value rows this
   // workgroup wrote, in the word layout normalized_check_kernel uses (lzm_kernels.hip): word pair q,

@@ -2661,8 +2661,52 @@ extern "C" int lzm_conv_heads(int B, int Kr, int Khd, int off_policy, const floa
   p.reward = reward; p.value = value; p.policy = policy;
   p.norm_words = pred_only ? nullptr : norm_words; p.norm_nparts = norm_parts(B);
   p.head0 = pred_only ? 1 : 0;
+  p.prep_on = 0;
   hipLaunchKernelGGL(conv_heads_kernel, dim3((B + kHdEnvs - 1) / kHdEnvs, pred_only ? 2 : 3), dim3(kHdThreads), 0,
                      (hipStream_t)stream, p);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
+// The initial inference's prediction heads (lzm_conv_heads with r == NULL) and, in the same launch, the root
+// preparation from the policy logits (lzm_roots_prepare's arguments and bits): the policy-head workgroups run
+// CRoots::prepare (cnode.cpp:301-358) for their envs from their LDS copy of the logits.
+extern "C" int lzm_conv_heads_prepare(lzm_handle *h, int B, int Khd, int off_policy, const float *hd,
+                                      const float *w1t, const float *b1, const float *w2t, const float *b2, int Vr,
+                                      int Vv, int A, float *value, float *policy, const int32_t *legal,
+                                      const int32_t *count, const float *noises, float noise_weight,
+                                      const float *rewards, const int32_t *to_play, void *stream) {
+  if (!h || h->B != B || h->A != A || A > kHdThreads || !legal || !count || !rewards || !to_play) {
+    set_err("lzm_conv_heads_prepare: the handle must have B roots and A <= 256 actions; legal, count, rewards, "
+            "to_play required");
+    return LZM_ERR_ARG;
+  }
+  if (B <= 0 || Khd <= 0 || Khd > kHdHMax || off_policy <= 0 || off_policy >= Khd || Khd - off_policy > kHdKMax ||
+      off_policy > kHdKMax || Vr <= 0 || Vv <= 0 || Vv > kHdCols * kHdThreads || !hd || !w1t || !b1 || !w2t || !b2 ||
+      !value || !policy || ((uintptr_t)w1t & 15) || (Khd & 3) || (off_policy & 3)) {
+    set_err("lzm_conv_heads_prepare: bad arguments (head planes <= 2048, K per head <= 1024, supports <= 768, "
+            "16-B aligned w1t)");
+    return LZM_ERR_ARG;
+  }
+  HeadsArgs p;
+  memset(&p, 0, sizeof(p));
+  p.B = B; p.Kr = 0; p.Khd = Khd;
+  p.hd = hd;
+  p.src[0] = 0; p.off[0] = 0; p.K[0] = 0;
+  p.src[1] = 1; p.off[1] = 0; p.K[1] = off_policy;
+  p.src[2] = 1; p.off[2] = off_policy; p.K[2] = Khd - off_policy;
+  p.w1t = w1t; p.b1 = b1; p.w2t = w2t; p.b2 = b2;
+  p.Vr = Vr; p.Vv = Vv; p.A = A;
+  p.value = value; p.policy = policy;
+  p.norm_nparts = norm_parts(B);
+  p.head0 = 1;
+  PrepareArgs &q = p.prep;
+  q.stat = h->stat; q.meta = h->meta; q.legal = h->legal; q.nlegal = h->nlegal;
+  q.legal_in = legal; q.count_in = count; q.to_play = to_play; q.noises = noises; q.rewards = rewards;
+  q.logits = policy; q.noise_weight = noise_weight; q.B = h->B; q.A = h->A;
+  p.prep_on = 1;
+  hipLaunchKernelGGL(conv_heads_kernel, dim3((B + kHdEnvs - 1) / kHdEnvs, 2), dim3(kHdThreads), 0, (hipStream_t)stream,
+                     p);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
@@ -2746,6 +2790,10 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_part = (int)o; o += 3 * kHdParts * 32;
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
+  // the walk's precomputed terms (search_conv_kernel TERMS): latent -> node, {total_q, total_v}, child terms
+  p.off_l2n = (int)o; o += round4((size_t)S + 2);
+  p.off_nq = (int)o; o += round4((size_t)2 * (S + 2));
+  p.off_cs = (int)o; o += (size_t)4 * h->cap;
   const size_t lds = o * sizeof(float);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %zu B of LDS needed (tree too large: lower num_simulations)",
@@ -2758,8 +2806,14 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
     LZM_HIP(hipMemset(h->phase, 0, (64 + 1024) * sizeof(unsigned long long)));
   }
   p.stamps = stamps ? h->phase : nullptr;
+  // LZM_CONV_TERMS=1: the walk over precomputed terms (search_res_kernel's selection split; measured slower
+  // here, kept for experiments: profiles/EXPERIMENTS.md round 5)
+  const bool terms = getenv("LZM_CONV_TERMS") && atoi(getenv("LZM_CONV_TERMS")) > 0;
   auto fn = stamps ? (fast ? search_conv_kernel<kBxAhead, true, true> : search_conv_kernel<kBxAhead, false, true>)
                    : (fast ? search_conv_kernel<kBxAhead, true> : search_conv_kernel<kBxAhead, false>);
+  if (terms)
+    fn = stamps ? (fast ? search_conv_kernel<kBxAhead, true, true, true> : search_conv_kernel<kBxAhead, false, true, true>)
+                : (fast ? search_conv_kernel<kBxAhead, true, false, true> : search_conv_kernel<kBxAhead, false, false, true>);
   hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(fn, dim3(h->B), dim3(kScThreads), lds, (hipStream_t)stream, p);

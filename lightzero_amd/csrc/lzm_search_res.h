@@ -465,6 +465,62 @@ __device__ inline void precompute_terms_a2(const TreeView &t, int nlat, const in
   }
 }
 
+// node_terms for small action spaces (A <= AM), written like precompute_terms_a2: every child's records
+// read unconditionally up front (one round of LDS reads, then the node's visit count and its pb_c table
+// row), the per-child branches as selects; the sums run over the children in legal order. Same float
+// operations in the same order as node_terms, so the same bits.
+template <int AM>
+__device__ inline void precompute_terms_small(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
+                                              float4 mm, int players, float disc, const int *rleg, int nleg_root) {
+  for (int L = threadIdx.x; L < nlat; L += kRT) {
+    const int n = lat2node[L];
+    const bool root = L == 0;
+    const int nleg = root ? nleg_root : t.A;
+    const int base = 1 + t.A * L;
+    int c[AM];
+    NodeStat s[AM];
+    float v[AM];
+    int lt[AM];
+#pragma unroll
+    for (int j = 0; j < AM; ++j) {
+      c[j] = base + (j < nleg ? (root ? rleg[j] : j) : 0);
+      s[j] = t.stat[c[j]];
+      v[j] = t.val[c[j]];
+      lt[j] = t.meta[c[j]].latent;
+    }
+    if (n < 0) continue;
+    int N = t.stat[n].visit - 1;
+    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
+    const float2 Lx = t.lut[N];
+    const int row = N * (N + 1) / 2;
+    float total_q = 0.0f;
+    int total_v = 0;
+    float4 term[AM];
+#pragma unroll
+    for (int j = 0; j < AM; ++j) {
+      const bool p = t.pbt && s[j].visit <= N;
+      const float f = p ? t.pbt[row + s[j].visit] : (Lx.y / (float)(s[j].visit + 1));
+      float vv = 0.0f;
+      if (j < nleg && s[j].visit > 0) {
+        total_q += s[j].reward + disc * v[j];
+        ++total_v;
+        float q = (players == 1) ? s[j].reward + disc * v[j] : s[j].reward + disc * (-v[j]);
+        q = mm_normalize(mm, q);
+        if (q < 0) q = 0;
+        if (q > 1) q = 1;
+        vv = q;
+      }
+      float pb = Lx.x;
+      pb *= f;
+      term[j] = make_float4(pb * s[j].prior, vv, __int_as_float(lt[j]), __int_as_float(s[j].visit > 0 ? 1 : 0));
+    }
+#pragma unroll
+    for (int j = 0; j < AM; ++j)
+      if (j < nleg) cs[c[j]] = term[j];
+    nq[L] = make_float2(total_q, __int_as_float(total_v));
+  }
+}
+
 // The walk over the precomputed terms (descend_wave's contract and outputs; wave 0).
 // Where a walk stands at the top of a level (a classification walk stops at a tie with the
 // state of that level, so the resolution resumes there instead of walking from the root).

@@ -727,7 +727,8 @@ struct PrepareArgs {
   int B, A;
 };
 
-__device__ inline void prepare_root(const PrepareArgs &p, int i) {
+// lg: the root's policy logits (null: p.logits row i; lzm_conv_heads_prepare passes its LDS copy)
+__device__ inline void prepare_root(const PrepareArgs &p, int i, const float *lg = nullptr) {
   const int A = p.A;
   int n = p.count_in[i];
   if (n <= 0) {
@@ -737,7 +738,7 @@ __device__ inline void prepare_root(const PrepareArgs &p, int i) {
     for (int j = 0; j < A; ++j) p.legal[(size_t)i * A + j] = j < n ? p.legal_in[(size_t)i * A + j] : -1;
   }
   p.nlegal[i] = n;
-  const float *lg = p.logits + (size_t)i * A;
+  if (!lg) lg = p.logits + (size_t)i * A;
   float pmax = kFloatMin;
   for (int j = 0; j < n; ++j) {
     const float l = lg[p.legal[(size_t)i * A + j]];
