@@ -2794,6 +2794,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_l2n = (int)o; o += round4((size_t)S + 2);
   p.off_nq = (int)o; o += round4((size_t)2 * (S + 2));
   p.off_cs = (int)o; o += (size_t)4 * h->cap;
+  p.off_dec = (int)o; o += round4((size_t)S + 2);
   const size_t lds = o * sizeof(float);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %zu B of LDS needed (tree too large: lower num_simulations)",

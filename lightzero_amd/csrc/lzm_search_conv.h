@@ -98,7 +98,8 @@ struct ConvSearchArgs {
   // dynamic LDS plan: float offsets (the two activation buffers come first)
   int off_stat, off_meta, off_val, off_lut, off_legal, off_path, off_pact, off_pbt, off_r, off_hd, off_hid, off_part,
       off_lg, off_seed;
-  int off_l2n, off_nq, off_cs;  // the MuZero launch's selection tables (TERMS): latent -> node, {total_q, total_v}, terms
+  int off_l2n, off_nq, off_cs, off_dec;  // the MuZero launch's selection tables (TERMS): latent -> node,
+                                         // {total_q, total_v}, child terms, walk-independent decisions
 };
 
 // The MuZero launch's walk over precomputed terms (search_res_kernel's selection split, lzm_search_res.h): the
@@ -108,8 +109,8 @@ struct ConvSearchArgs {
 template <bool CLASSIFY, typename Draw>
 __device__ __forceinline__ Descent sc_walk_terms(const TreeView &t, const float2 *nq, const float4 *cs, float4 mm,
                                                  int vtp, int players, const int *rleg, int nleg, Draw draw,
-                                                 TieInfo *tie) {
-  if (t.A <= 4) return descend_small<4, CLASSIFY>(t, nq, cs, mm, vtp, players, rleg, nleg, draw, tie);
+                                                 TieInfo *tie, const int *dec) {
+  if (t.A <= 4) return descend_small_fast<4, CLASSIFY>(t, nq, cs, mm, vtp, players, rleg, nleg, draw, tie, dec);
   return descend_terms<CLASSIFY>(t, nq, cs, mm, vtp, players, draw, tie);
 }
 
@@ -408,7 +409,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   __shared__ int s_len[1];
   __shared__ float4 s_mm[1];
   __shared__ float s_dec[2];
-  unsigned long long st_prev = 0, st_acc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_prev = 0, st_acc[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long st_w0 = 0;  // (the walk's own cycles, slot 10)
   const unsigned long long st_begin = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
   auto stamp = [&](int n) {
@@ -479,6 +480,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   int *L2N = reinterpret_cast<int *>(smem + p.off_l2n);
   float2 *NQ = reinterpret_cast<float2 *>(smem + p.off_nq);
   float4 *CS = reinterpret_cast<float4 *>(smem + p.off_cs);
+  int *DEC = reinterpret_cast<int *>(smem + p.off_dec);
   int rleg[4];
   const int nleg = llegal[A];
 #pragma unroll
@@ -503,11 +505,25 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     if (STAMPS && tid == 0) st_prev = __builtin_amdgcn_s_memtime();
     if (TERMS) {
       // every expanded node's walk-independent terms (the previous backup and expansion are complete)
-      if (A <= 4)
-        precompute_terms_small<4>(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc, rleg, nleg);
-      else
-        precompute_terms(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc);
-      __syncthreads();
+      if (A <= 4 && k + 1 <= 16) {
+        // a lane quad per node in wave 0, which also walks: no workgroup barrier in between (the wave's own
+        // LDS writes are ordered by its lgkmcnt waits)
+        if (wv == 0) {
+          precompute_terms_quad<64>(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc, rleg, nleg, DEC);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+      } else if (A <= 4) {
+        precompute_terms_quad<kScThreads>(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc, rleg, nleg, DEC);
+        __syncthreads();
+      } else {
+        if (A <= 4)
+          precompute_terms_small<4>(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc, rleg, nleg, DEC);
+        else
+          precompute_terms(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc);
+        __syncthreads();
+      }
       if (STAMPS && tid == 0) st_acc[9] += __builtin_amdgcn_s_memtime() - st_prev;  // (inside selection's stamp)
     }
     if (tid == 0) s_late = 0;
@@ -521,14 +537,18 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)b, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
           return o.x >> 1;
         };
-        d = TERMS ? sc_walk_terms<false>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, draw, nullptr)
+        d = TERMS ? sc_walk_terms<false>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, draw, nullptr, DEC)
                   : descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
       } else {
         TieInfo ti;
         auto nodraw = [](int) -> uint32_t { return 0u; };
-        d = TERMS ? sc_walk_terms<true>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, nodraw, &ti)
+        d = TERMS ? sc_walk_terms<true>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, nodraw, &ti, DEC)
                   : descend_wave<false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
-        if (STAMPS && tid == 0) st_acc[10] += __builtin_amdgcn_s_memtime() - st_w0;
+        if (STAMPS && tid == 0) {
+          st_acc[10] += __builtin_amdgcn_s_memtime() - st_w0;
+          st_acc[11] += d.len;              // levels walked (diagnostics)
+          st_acc[12] += ti.status == 1 ? 1 : 0;  // late-draw ties
+        }
         if (lane == 0 && ti.status != 2)
           __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -536,7 +556,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           // the depth depends on the draws: look back, walk with them, then publish
           const int base = sc_lookback(p, k, b, epoch, lane);
           const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, 0, t.depth_cap, p.err + 1);
-          d = TERMS ? sc_walk_terms<false>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, draw, nullptr)
+          d = TERMS ? sc_walk_terms<false>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, draw, nullptr, DEC)
                     : descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
           if (lane == 0)
             __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
@@ -602,7 +622,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
             const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
             const int base = sc_lookback(p, k, b, epoch, lane);
             if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;
-            const uint32_t rr = glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
+            const uint32_t rr = glibc_draw_wave(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
             unsigned long long m = s_tmask;
             int kk = (int)(rr % (uint32_t)__popcll(m));
             for (; kk > 0; --kk) m &= m - 1;
@@ -720,7 +740,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   }
   if (STAMPS && tid == 0 && p.stamps) {
     st_acc[7] = __builtin_amdgcn_s_memtime() - st_begin;
-    for (int n = 0; n < 11; ++n) atomicAdd(p.stamps + 40 + n, st_acc[n]);
+    for (int n = 0; n < 13; ++n) atomicAdd(p.stamps + 40 + n, st_acc[n]);
   }
   // collect-step root outputs (root_outputs_kernel's values): visit counts per legal action, the root value
   if (p.out_dist && tid < A) {
@@ -992,7 +1012,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
               const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
               const int base = sc_lookback(p, k, b, epoch, lane);
               if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;
-              const uint32_t rr = glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
+              const uint32_t rr = glibc_draw_wave(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
               unsigned long long m = s_tmask;
               int kk = (int)(rr % (uint32_t)__popcll(m));
               for (; kk > 0; --kk) m &= m - 1;

@@ -534,6 +534,26 @@ __device__ inline uint32_t glibc_draw(const uint32_t *coef, int positions, const
   return v >> 1;
 }
 
+// glibc_draw by a whole wave (p wave-uniform): lane j < 31 forms coefficient j's product and the wave adds
+// them (mod 2^32, so in any order: the same value) — one round of loads and a butterfly instead of a
+// 31-term dependent chain. Every lane returns the draw; all 64 lanes must call it.
+__device__ __forceinline__ uint32_t glibc_draw_wave(const uint32_t *coef, int positions, const uint32_t *z0, int p,
+                                                   int32_t *diag) {
+  const int lane = threadIdx.x & 63;
+  if (p >= positions) {
+    if (lane == 0) atomicAdd(diag, 1);
+    return 0u;
+  }
+  uint32_t v = lane < 31 ? coef[(size_t)p * 31 + lane] * z0[lane] : 0u;
+  v += (uint32_t)xor_partner<32>((int)v);
+  v += (uint32_t)xor_partner<16>((int)v);
+  v += (uint32_t)xor_partner<8>((int)v);
+  v += (uint32_t)xor_partner<4>((int)v);
+  v += (uint32_t)xor_partner<2>((int)v);
+  v += (uint32_t)xor_partner<1>((int)v);
+  return v >> 1;
+}
+
 // The draws of one walk's levels lo .. lo + 63, one per lane (lane l: stream position
 // base + lo + l), all coefficient rows in flight at once. cselect_child consumes a rand() at every
 // level (cnode.cpp:587-590), so a walk resolved with draws paid one coefficient-row round trip per

@@ -10,7 +10,7 @@ for rep in 1 2; do
     envs=""
     if [[ "$v" == *:* ]]; then envs=${v#*:}; fi
     tag=$(echo "$v" | tr ':=' '__')
-    env $envs LZM_LIB=lightzero_amd/liblzm_var$lib.so timeout -k 10 200 python bench.py --no-cpu-baseline --secondary none --steps 30 $AB_ARGS > "$out/b_${tag}_$rep.json" 2>&1
+    env $envs LZM_LIB=lightzero_amd/liblzm_var$lib.so timeout -k 10 200 python bench.py --no-cpu-baseline --secondary none --configs none --steps 30 $AB_ARGS > "$out/b_${tag}_$rep.json" 2>&1
     python3 -c "import json,sys;d=json.loads(open('$out/b_${tag}_$rep.json').read().strip().splitlines()[-1]);print('$v', $rep, d['value'], d['roofline']['launch_us'], d['tie_stream_errors'])" >> "$out/summary.txt"
   done
 done

@@ -84,14 +84,15 @@ def main():
         for name, c in zip(WAITS_EZ, per[8:14]):
             print(f"  {name:28s} {c / S:9.0f}")
         return
-    per = np.array(buf[40:51], dtype=np.float64) / (a.searches * B)
+    per = np.array(buf[40:53], dtype=np.float64) / (a.searches * B)
     print(f"one-launch conv search, per workgroup (root) per simulation, cycles (B={B}, S={S}, rng={a.rng}):")
     tot = per[:7].sum()
     for name, c in zip(NAMES, per[:7]):
         print(f"  {name:24s} {c / S:9.0f}  {100 * c / tot:5.1f}%")
     print(f"  sum of phases per sim {tot / S:.0f}; kernel total per root {per[7]:.0f} cycles "
           f"(per sim {per[7] / S:.0f}); late-draw look-back per sim {per[8] / S:.0f}; terms pass per sim "
-          f"{per[9] / S:.0f} (of selection); classification walk per sim {per[10] / S:.0f} (of selection)")
+          f"{per[9] / S:.0f} (of selection); classification walk per sim {per[10] / S:.0f} (of selection), "
+          f"levels per sim {per[11] / S:.2f}, late-draw ties per sim {per[12] / S:.2f}")
 
 
 if __name__ == "__main__":
