@@ -2049,24 +2049,26 @@ __global__ __launch_bounds__(kRT) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     __syncthreads();
     LZM_SUBSTAMP(33);
+    int lrow = 0;  // the late draw's pick: the two-way tie's second candidate when rand() % 2 == 1
     if (NR == 1 && late) {
       const unsigned long long w0_ = p.phase ? __builtin_amdgcn_s_memtime() : 0ull;
       if (G <= kRT) {
-        if (wid == 0) {
-          const int base = lookback_sum_w0(p, k, g, G, epoch);
-          if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
-          const uint32_t rr = glibc_draw_wave(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag);
-          if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, rr, &s_act);
-        }
+        // every wave looks back and draws for itself, so no barrier hands the pick over; wave 0 files it
+        const int base = lookback_sum_w0(p, k, g, G, epoch);
+        if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
+        const uint32_t rr = glibc_draw_wave(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag);
+        lrow = (int)(rr & 1u);  // (resolve_tie: rr % 2 over the mask's two set bits)
+        if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, rr, &s_act);
       } else {
         const int base = lookback_sum(p, k, g, G, epoch, s_part);
         if (p.phase && tid == 0) s_wait += __builtin_amdgcn_s_memtime() - w0_;
         if (tid == 0) resolve_tie(t, A, s_tlevel, s_tmask, glibc_draw(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.diag), &s_act);
+        __syncthreads();
+        lrow = s_act == act_r[1] ? 1 : 0;
       }
-      __syncthreads();
     }
     // the next latent row the rest of the network reads (NR = 1: the late draw's pick)
-    const float *NLb = NL + ((NR == 1 && late && s_act == act_r[1]) ? kRRow : 0);
+    const float *NLb = NL + ((NR == 1 && late && lrow) ? kRRow : 0);
     LZM_SUBSTAMP(34);
     LZM_STAMP(3);
     // The reward chain (fc_dynamics_2 -> reward head) and the prediction chain (prediction
