@@ -2790,11 +2790,6 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_part = (int)o; o += 3 * kHdParts * 32;
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
-  // the walk's precomputed terms (search_conv_kernel TERMS): latent -> node, {total_q, total_v}, child terms
-  p.off_l2n = (int)o; o += round4((size_t)S + 2);
-  p.off_nq = (int)o; o += round4((size_t)2 * (S + 2));
-  p.off_cs = (int)o; o += (size_t)4 * h->cap;
-  p.off_dec = (int)o; o += round4((size_t)S + 2);
   const size_t lds = o * sizeof(float);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %zu B of LDS needed (tree too large: lower num_simulations)",
@@ -2807,14 +2802,8 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
     LZM_HIP(hipMemset(h->phase, 0, (64 + 1024) * sizeof(unsigned long long)));
   }
   p.stamps = stamps ? h->phase : nullptr;
-  // LZM_CONV_TERMS=1: the walk over precomputed terms (search_res_kernel's selection split; measured slower
-  // here, kept for experiments: profiles/EXPERIMENTS.md round 5)
-  const bool terms = getenv("LZM_CONV_TERMS") && atoi(getenv("LZM_CONV_TERMS")) > 0;
   auto fn = stamps ? (fast ? search_conv_kernel<kBxAhead, true, true> : search_conv_kernel<kBxAhead, false, true>)
                    : (fast ? search_conv_kernel<kBxAhead, true> : search_conv_kernel<kBxAhead, false>);
-  if (terms)
-    fn = stamps ? (fast ? search_conv_kernel<kBxAhead, true, true, true> : search_conv_kernel<kBxAhead, false, true, true>)
-                : (fast ? search_conv_kernel<kBxAhead, true, false, true> : search_conv_kernel<kBxAhead, false, false, true>);
   hipError_t e = hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e == hipSuccess) {
     hipLaunchKernelGGL(fn, dim3(h->B), dim3(kScThreads), lds, (hipStream_t)stream, p);

@@ -98,21 +98,7 @@ struct ConvSearchArgs {
   // dynamic LDS plan: float offsets (the two activation buffers come first)
   int off_stat, off_meta, off_val, off_lut, off_legal, off_path, off_pact, off_pbt, off_r, off_hd, off_hid, off_part,
       off_lg, off_seed;
-  int off_l2n, off_nq, off_cs, off_dec;  // the MuZero launch's selection tables (TERMS): latent -> node,
-                                         // {total_q, total_v}, child terms, walk-independent decisions
 };
-
-// The MuZero launch's walk over precomputed terms (search_res_kernel's selection split, lzm_search_res.h): the
-// terms pass gives every expanded node's walk-independent pUCT terms one thread each, then wave 0 walks with a
-// level costing one round of LDS reads (descend_small for A <= 4, else descend_terms: one lane per child).
-// Same float operations and tie rule as descend_wave, so the same bits.
-template <bool CLASSIFY, typename Draw>
-__device__ __forceinline__ Descent sc_walk_terms(const TreeView &t, const float2 *nq, const float4 *cs, float4 mm,
-                                                 int vtp, int players, const int *rleg, int nleg, Draw draw,
-                                                 TieInfo *tie, const int *dec) {
-  if (t.A <= 4) return descend_small_fast<4, CLASSIFY>(t, nq, cs, mm, vtp, players, rleg, nleg, draw, tie, dec);
-  return descend_terms<CLASSIFY>(t, nq, cs, mm, vtp, players, draw, tie);
-}
 
 // Parity-mode draw offset of root b in simulation k: the sum of the depth flags of roots < b (the
 // reference's single rand() stream, cnode.cpp:783-796). Wave-wide, b <= 256 (lzm_search_conv checks
@@ -392,10 +378,9 @@ __device__ __forceinline__ unsigned long long sc_wait_word(const unsigned long l
   return v;
 }
 
-template <int AHEAD, bool FAST, bool STAMPS = false, bool TERMS = false>
+template <int AHEAD, bool FAST, bool STAMPS = false>
 __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void search_conv_kernel(
     ConvSearchArgs p) {
-  static_assert(kScThreads == kRT, "precompute_terms strides by kRT");
   extern __shared__ uint4 sc_lds4[];
   uint16_t *act = reinterpret_cast<uint16_t *>(sc_lds4);
   float *smem = reinterpret_cast<float *>(sc_lds4);
@@ -475,20 +460,6 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   float *lr = smem + p.off_r, *lhd = smem + p.off_hd, *lhid = smem + p.off_hid, *lpart = smem + p.off_part;
   float *llg = smem + p.off_lg;
   const int N2 = p.Vr + p.Vv + A;
-  // TERMS: a search starts from prepared roots (only the root expanded, latent 0; cnode.cpp:301-358) and
-  // simulation k gives its leaf latent k + 1; the root's legal actions in registers (descend_small)
-  int *L2N = reinterpret_cast<int *>(smem + p.off_l2n);
-  float2 *NQ = reinterpret_cast<float2 *>(smem + p.off_nq);
-  float4 *CS = reinterpret_cast<float4 *>(smem + p.off_cs);
-  int *DEC = reinterpret_cast<int *>(smem + p.off_dec);
-  int rleg[4];
-  const int nleg = llegal[A];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) rleg[j] = j < A ? llegal[j] : 0;
-  if (TERMS) {
-    for (int e = tid; e < S + 2; e += kScThreads) L2N[e] = e == 0 ? 0 : -1;  // (ordered by the loop's first barrier)
-  }
-
   // trunk weights: this wave's stream of each 3x3 layer (lzm_conv.h bx layout)
   const ConvTrunkLayout L = conv_trunk_layout_p(p.n_dres, p.n_pres, 1);
   const int n3 = 1 + 2 * p.n_dres + 2 * p.n_pres;
@@ -503,29 +474,6 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     if (!FAST && tid < 31) seed_state_parallel(s_seed[k], s_pow, s_z0);
     __syncthreads();
     if (STAMPS && tid == 0) st_prev = __builtin_amdgcn_s_memtime();
-    if (TERMS) {
-      // every expanded node's walk-independent terms (the previous backup and expansion are complete)
-      if (A <= 4 && k + 1 <= 16) {
-        // a lane quad per node in wave 0, which also walks: no workgroup barrier in between (the wave's own
-        // LDS writes are ordered by its lgkmcnt waits)
-        if (wv == 0) {
-          precompute_terms_quad<64>(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc, rleg, nleg, DEC);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-      } else if (A <= 4) {
-        precompute_terms_quad<kScThreads>(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc, rleg, nleg, DEC);
-        __syncthreads();
-      } else {
-        if (A <= 4)
-          precompute_terms_small<4>(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc, rleg, nleg, DEC);
-        else
-          precompute_terms(t, k + 1, L2N, NQ, CS, s_mm[0], players, p.disc);
-        __syncthreads();
-      }
-      if (STAMPS && tid == 0) st_acc[9] += __builtin_amdgcn_s_memtime() - st_prev;  // (inside selection's stamp)
-    }
     if (tid == 0) s_late = 0;
     if (wv == 0) {
       const float4 mm = s_mm[0];
@@ -537,13 +485,11 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)b, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
           return o.x >> 1;
         };
-        d = TERMS ? sc_walk_terms<false>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, draw, nullptr, DEC)
-                  : descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+        d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
       } else {
         TieInfo ti;
         auto nodraw = [](int) -> uint32_t { return 0u; };
-        d = TERMS ? sc_walk_terms<true>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, nodraw, &ti, DEC)
-                  : descend_wave<false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
+        d = descend_wave<false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
         if (STAMPS && tid == 0) {
           st_acc[10] += __builtin_amdgcn_s_memtime() - st_w0;
           st_acc[11] += d.len;              // levels walked (diagnostics)
@@ -556,8 +502,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           // the depth depends on the draws: look back, walk with them, then publish
           const int base = sc_lookback(p, k, b, epoch, lane);
           const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, 0, t.depth_cap, p.err + 1);
-          d = TERMS ? sc_walk_terms<false>(t, NQ, CS, mm, s_vtp0, players, rleg, nleg, draw, nullptr, DEC)
-                    : descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+          d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
           if (lane == 0)
             __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -715,7 +660,6 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       const int leaf = t.path[s_len[0]];
       const float *plg = llg + p.Vr + p.Vv;
       expand_wave(t, 0, leaf, s_leafvtp, k + 1, r, plg, -1, kExp2fTab, 1);
-      if (TERMS && lane == 0) L2N[k + 1] = leaf;  // the leaf now holds latent k + 1
       backup_wave(t, 0, 0, 1, s_mm, s_leafvtp, v, p.disc);
       if (p.rec_dec) {
         if (lane < 2) p.rec_dec[((size_t)k * B + b) * 2 + lane] = lane ? v : r;

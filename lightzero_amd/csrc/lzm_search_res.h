@@ -465,179 +465,6 @@ __device__ inline void precompute_terms_a2(const TreeView &t, int nlat, const in
   }
 }
 
-// node_terms for small action spaces (A <= AM), written like precompute_terms_a2: every child's records
-// read unconditionally up front (one round of LDS reads, then the node's visit count and its pb_c table
-// row), the per-child branches as selects; the sums run over the children in legal order. Same float
-// operations in the same order as node_terms, so the same bits.
-// dec (nullable): each node's walk-independent decision — the legal position the walk takes when every legal
-// child is visited (no score depends on the walk's mean-q) and the choice is not a tie; AM otherwise.
-// STRIDE: the threads sharing the nodes (kRT: the whole workgroup; 64: wave 0 alone).
-template <int AM, int STRIDE = kRT>
-__device__ inline void precompute_terms_small(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
-                                              float4 mm, int players, float disc, const int *rleg, int nleg_root,
-                                              int *dec = nullptr) {
-  for (int L = threadIdx.x; L < nlat; L += STRIDE) {
-    const int n = lat2node[L];
-    const bool root = L == 0;
-    const int nleg = root ? nleg_root : t.A;
-    const int base = 1 + t.A * L;
-    int c[AM];
-    NodeStat s[AM];
-    float v[AM];
-    int lt[AM];
-#pragma unroll
-    for (int j = 0; j < AM; ++j) {
-      c[j] = base + (j < nleg ? (root ? rleg[j] : j) : 0);
-      s[j] = t.stat[c[j]];
-      v[j] = t.val[c[j]];
-      lt[j] = t.meta[c[j]].latent;
-    }
-    if (n < 0) continue;
-    int N = t.stat[n].visit - 1;
-    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
-    const float2 Lx = t.lut[N];
-    const int row = N * (N + 1) / 2;
-    float total_q = 0.0f;
-    int total_v = 0;
-    float4 term[AM];
-#pragma unroll
-    for (int j = 0; j < AM; ++j) {
-      const bool p = t.pbt && s[j].visit <= N;
-      const float f = p ? t.pbt[row + s[j].visit] : (Lx.y / (float)(s[j].visit + 1));
-      float vv = 0.0f;
-      if (j < nleg && s[j].visit > 0) {
-        total_q += s[j].reward + disc * v[j];
-        ++total_v;
-        float q = (players == 1) ? s[j].reward + disc * v[j] : s[j].reward + disc * (-v[j]);
-        q = mm_normalize(mm, q);
-        if (q < 0) q = 0;
-        if (q > 1) q = 1;
-        vv = q;
-      }
-      float pb = Lx.x;
-      pb *= f;
-      term[j] = make_float4(pb * s[j].prior, vv, __int_as_float(lt[j]), __int_as_float(s[j].visit > 0 ? 1 : 0));
-    }
-#pragma unroll
-    for (int j = 0; j < AM; ++j)
-      if (j < nleg) cs[c[j]] = term[j];
-    nq[L] = make_float2(total_q, __int_as_float(total_v));
-    if (dec) {
-      // every legal child visited: the walk's scores are term.x + term.y, its choice fixed (descend_small's
-      // max / first index / tie list on them)
-      bool all_v = nleg > 0;
-      float sc[AM];
-      float M = -INFINITY;
-#pragma unroll
-      for (int j = 0; j < AM; ++j) {
-        sc[j] = term[j].x + term[j].y;
-        if (j < nleg) {
-          all_v = all_v && s[j].visit > 0;
-          M = fmaxf(M, sc[j]);
-        }
-      }
-      int r = 0;
-#pragma unroll
-      for (int j = AM - 1; j >= 0; --j)
-        if (j < nleg && sc[j] == M) r = j;
-      const float thr = M - 0.000001f;
-      bool tie = false;
-#pragma unroll
-      for (int j = 1; j < AM; ++j)
-        if (j < nleg && j > r && sc[j] >= thr) tie = true;
-      dec[L] = (all_v && !tie) ? r : AM;
-    }
-  }
-}
-
-// precompute_terms_small with one thread per (node, child position): a quad of lanes per node (AM == 4), so
-// a thread's serial work is one child (one division) and the node's sums, tie rule and decision are
-// formed from the quad's values by DPP broadcasts (every lane of the quad the same values, in legal
-// order: the same float operations as node_terms, so the same bits). Threads 0 .. THREADS - 1 call it
-// (THREADS = 64: wave 0 alone); nodes 0 .. nlat - 1, THREADS / 4 per pass.
-template <int THREADS>
-__device__ inline void precompute_terms_quad(const TreeView &t, int nlat, const int *lat2node, float2 *nq, float4 *cs,
-                                             float4 mm, int players, float disc, const int *rleg, int nleg_root,
-                                             int *dec) {
-  constexpr int AM = 4;
-  const int j = threadIdx.x & 3;
-  const float delta = mm.x - mm.y;
-  const bool scale = delta > 0;
-  const float div = (delta < mm.z) ? mm.z : delta;
-  const float lo = mm.y;
-  for (int L0 = 0; L0 < nlat; L0 += THREADS / AM) {
-    const int L = L0 + (threadIdx.x >> 2);
-    const bool live = L < nlat;
-    const int Lc = live ? L : 0;
-    const int n = lat2node[Lc];
-    const bool root = Lc == 0;
-    const int nleg = root ? nleg_root : t.A;
-    const bool valid = live && j < nleg;
-    const int c = 1 + t.A * Lc + (valid ? (root ? rleg[j] : j) : 0);
-    const NodeStat s = t.stat[c];
-    const float v = t.val[c];
-    const int lt = t.meta[c].latent;
-    int N = t.stat[n < 0 ? 0 : n].visit - 1;
-    N = N < 0 ? 0 : (N >= t.lut_n ? t.lut_n - 1 : N);
-    const float2 Lx = t.lut[N];
-    const bool p = t.pbt && s.visit <= N;
-    const float f = p ? t.pbt[N * (N + 1) / 2 + s.visit] : (Lx.y / (float)(s.visit + 1));
-    const bool visited = valid && s.visit > 0;
-    const float qv = s.reward + disc * v;  // compute_mean_q's summand
-    float vv = 0.0f;
-    if (visited) {
-      float q = (players == 1) ? qv : s.reward + disc * (-v);
-      q = scale ? (q - lo) / div : q;  // (mm_normalize)
-      if (q < 0) q = 0;
-      if (q > 1) q = 1;
-      vv = q;
-    }
-    float pb = Lx.x;
-    pb *= f;
-    const float4 term = make_float4(pb * s.prior, vv, __int_as_float(lt), __int_as_float(s.visit > 0 ? 1 : 0));
-    if (valid && n >= 0) cs[c] = term;
-    // the quad's values in legal order (quad_perm broadcasts of lane j)
-    float qq[AM], sc[AM];
-    const float scj = term.x + term.y;  // the walk's score when every child is visited
-    const int vj = visited ? 1 : 0;
-#define LZM_QB(I)                                                                                    \
-  qq[I] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(qv), (I) * 0x55, 0xF, 0xF, false));  \
-  sc[I] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(scj), (I) * 0x55, 0xF, 0xF, false));
-    LZM_QB(0) LZM_QB(1) LZM_QB(2) LZM_QB(3)
-#undef LZM_QB
-    const int vis = (__builtin_amdgcn_mov_dpp(vj, 0x00, 0xF, 0xF, false)) |
-                    (__builtin_amdgcn_mov_dpp(vj, 0x55, 0xF, 0xF, false) << 1) |
-                    (__builtin_amdgcn_mov_dpp(vj, 0xAA, 0xF, 0xF, false) << 2) |
-                    (__builtin_amdgcn_mov_dpp(vj, 0xFF, 0xF, 0xF, false) << 3);
-    if (j == 0 && live && n >= 0) {
-      float total_q = 0.0f;
-      int total_v = 0;
-#pragma unroll
-      for (int i = 0; i < AM; ++i)
-        if ((vis >> i) & 1) {
-          total_q += qq[i];
-          ++total_v;
-        }
-      nq[L] = make_float2(total_q, __int_as_float(total_v));
-      const bool all_v = nleg > 0 && vis == (1 << nleg) - 1;
-      float M = -INFINITY;
-#pragma unroll
-      for (int i = 0; i < AM; ++i)
-        if (i < nleg) M = fmaxf(M, sc[i]);
-      int r = 0;
-#pragma unroll
-      for (int i = AM - 1; i >= 0; --i)
-        if (i < nleg && sc[i] == M) r = i;
-      const float thr = M - 0.000001f;
-      bool tie = false;
-#pragma unroll
-      for (int i = 1; i < AM; ++i)
-        if (i < nleg && i > r && sc[i] >= thr) tie = true;
-      dec[L] = (all_v && !tie) ? r : AM;
-    }
-  }
-}
-
 // The walk over the precomputed terms (descend_wave's contract and outputs; wave 0).
 // Where a walk stands at the top of a level (a classification walk stops at a tie with the
 // state of that level, so the resolution resumes there instead of walking from the root).
@@ -776,139 +603,6 @@ __device__ inline Descent descend_small(const TreeView &t, const float2 *nq, con
     is_root = 0;
     parent_q = mean_q;
     float vu = mm_normalize(mm, mean_q);
-    if (vu < 0) vu = 0;
-    if (vu > 1) vu = 1;
-    float sc[AM];
-    float M = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < AM; ++j) {
-      sc[j] = c[j].x + (__float_as_int(c[j].w) ? c[j].y : vu);
-      if (j < n) M = fmaxf(M, sc[j]);
-    }
-    int r = 0;
-#pragma unroll
-    for (int j = AM - 1; j >= 0; --j)
-      if (j < n && sc[j] == M) r = j;
-    const float thr = M - 0.000001f;
-    unsigned mask = 1u << r;
-#pragma unroll
-    for (int j = 1; j < AM; ++j)
-      if (j < n && j > r && sc[j] >= thr) mask |= 1u << j;
-    const int nl = __popc(mask);
-    if (CLASSIFY && nl > 1) {
-      bool all_leaves = true;
-#pragma unroll
-      for (int j = 0; j < AM; ++j)
-        if (((mask >> j) & 1u) && __float_as_int(c[j].z) >= 0) all_leaves = false;
-      if (players > 1) vtp = (vtp == 1) ? 2 : 1;
-      tie->status = all_leaves ? 1 : 2;
-      tie->level = len;
-      tie->mask = mask;
-      Descent d;
-      d.len = len + 1;
-      d.x = lat;
-      d.action = -1;
-      d.vtp = vtp;
-      d.leaf = -1;
-      return d;
-    }
-    int jsel = r;
-    if (!CLASSIFY) {
-      const uint32_t rr = draw(len);
-      int kk = (int)(rr % (uint32_t)nl);
-      unsigned m_ = mask;
-      for (; kk > 0; --kk) m_ &= m_ - 1;
-      jsel = __ffs(m_) - 1;
-    }
-    int action = act[0], nlat = __float_as_int(c[0].z);
-#pragma unroll
-    for (int j = 1; j < AM; ++j)
-      if (jsel == j) {
-        action = act[j];
-        nlat = __float_as_int(c[j].z);
-      }
-    if (players > 1) vtp = (vtp == 1) ? 2 : 1;
-    node = base + action;
-    last_action = action;
-    if (lane == 0) {
-      t.path_act[len] = action;
-      t.path[len + 1] = node;
-    }
-    ++len;
-    plat = lat;
-    lat = nlat;
-  }
-  Descent d;
-  d.len = len;
-  d.x = plat;
-  d.action = last_action;
-  d.vtp = vtp;
-  d.leaf = node;
-  return d;
-}
-
-// descend_small written for one round of LDS reads per level: every child slot's terms and the node's
-// {total_q, total_v} are read unconditionally (a child slot past the legal count is read and masked: the
-// slots of an expanded node always exist), and the normaliser's divisor is fixed per walk (mm_normalize's
-// branches become one division, as in descend_a2). Same float operations, tie rule and outputs as
-// descend_small, so the same bits.
-// dec (nullable): precompute_terms_small's decisions; a decided level is a pointer chase (its mean-q still
-// computed for the levels below, the same operations).
-template <int AM, bool CLASSIFY, typename Draw>
-__device__ inline Descent descend_small_fast(const TreeView &t, const float2 *nq, const float4 *cs, float4 mm, int vtp,
-                                             int players, const int *rleg, int nleg, Draw draw, TieInfo *tie,
-                                             const int *dec = nullptr) {
-  const int lane = threadIdx.x & 63;
-  const int A = t.A;
-  const float delta = mm.x - mm.y;
-  const bool scale = delta > 0;
-  const float div = (delta < mm.z) ? mm.z : delta;
-  const float lo = mm.y;
-  int node = 0, len = 0, last_action = -1, plat = -1;
-  int lat = t.meta[0].latent;
-  bool is_root = true;
-  float parent_q = 0.0f;
-  if (lane == 0) t.path[0] = 0;
-  if (CLASSIFY) tie->status = 0;
-  const int dmax = t.depth_cap - 1;
-  while (lat >= 0 && len < dmax) {
-    const int base = 1 + A * lat;
-    if (dec) {
-      const int dl = dec[lat];
-      if (dl < AM) {
-        const int action = is_root ? rleg[dl] : dl;
-        const float4 c = cs[base + action];
-        const float2 q = nq[lat];
-        const int total_v = __float_as_int(q.y);
-        parent_q = (is_root && total_v > 0) ? q.x / (float)total_v : (parent_q + q.x) / (float)(total_v + 1);
-        is_root = false;
-        if (players > 1) vtp = (vtp == 1) ? 2 : 1;
-        node = base + action;
-        last_action = action;
-        if (lane == 0) {
-          t.path_act[len] = action;
-          t.path[len + 1] = node;
-        }
-        ++len;
-        plat = lat;
-        lat = __float_as_int(c.z);
-        continue;
-      }
-    }
-    const int n = is_root ? nleg : A;  // (the walk starts at the root and never returns to it)
-    int act[AM];
-    float4 c[AM];
-#pragma unroll
-    for (int j = 0; j < AM; ++j) {
-      act[j] = is_root ? rleg[j] : j;
-      c[j] = cs[base + (j < n ? act[j] : 0)];
-    }
-    const float2 q = nq[lat];
-    const int total_v = __float_as_int(q.y);
-    const float mean_q = (is_root && total_v > 0) ? q.x / (float)total_v : (parent_q + q.x) / (float)(total_v + 1);
-    is_root = false;
-    parent_q = mean_q;
-    float vu = scale ? (mean_q - lo) / div : mean_q;  // (mm_norm_fixed)
     if (vu < 0) vu = 0;
     if (vu > 1) vu = 1;
     float sc[AM];

@@ -90,9 +90,9 @@ def main():
     for name, c in zip(NAMES, per[:7]):
         print(f"  {name:24s} {c / S:9.0f}  {100 * c / tot:5.1f}%")
     print(f"  sum of phases per sim {tot / S:.0f}; kernel total per root {per[7]:.0f} cycles "
-          f"(per sim {per[7] / S:.0f}); late-draw look-back per sim {per[8] / S:.0f}; terms pass per sim "
-          f"{per[9] / S:.0f} (of selection); classification walk per sim {per[10] / S:.0f} (of selection), "
-          f"levels per sim {per[11] / S:.2f}, late-draw ties per sim {per[12] / S:.2f}")
+          f"(per sim {per[7] / S:.0f}); late-draw look-back per sim {per[8] / S:.0f}; classification walk per "
+          f"sim {per[10] / S:.0f} (of selection), levels per sim {per[11] / S:.2f}, late-draw ties per sim "
+          f"{per[12] / S:.2f}")
 
 
 if __name__ == "__main__":
