@@ -949,28 +949,26 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
           if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
           if (i == 0 && late) {
-            // late draw: the look-back and the tie's draw, then the action's map for the epilogue
-            if (wv == 0) {
-              const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
-              const int base = sc_lookback(p, k, b, epoch, lane);
-              if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;
-              const uint32_t rr = glibc_draw_wave(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
-              unsigned long long m = s_tmask;
-              int kk = (int)(rr % (uint32_t)__popcll(m));
-              for (; kk > 0; --kk) m &= m - 1;
-              const int jsel = __ffsll((long long)m) - 1;
-              const int lvl = s_tlevel;
-              const int parent = t.path[lvl];
-              const int action = legal_at(t, 0, parent, jsel);
-              if (lane == 0) {
-                t.path_act[lvl] = action;
-                t.path[lvl + 1] = 1 + A * t.meta[parent].latent + action;
-                s_act = action;
-                if (p.rec_a) p.rec_a[(size_t)k * B + b] = action;
-              }
+            // late draw: the look-back and the tie's draw, then the action's map for the epilogue — by every
+            // wave for itself (no barrier hands the action over); wave 0 files it
+            const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+            const int base = sc_lookback(p, k, b, epoch, lane);
+            if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;
+            const uint32_t rr = glibc_draw_wave(p.coef, p.coef_positions, s_z0, base + s_tlevel, p.err + 1);
+            unsigned long long m = s_tmask;
+            int kk = (int)(rr % (uint32_t)__popcll(m));
+            for (; kk > 0; --kk) m &= m - 1;
+            const int jsel = __ffsll((long long)m) - 1;
+            const int lvl = s_tlevel;
+            const int parent = t.path[lvl];
+            const int action = legal_at(t, 0, parent, jsel);
+            if (tid == 0) {
+              t.path_act[lvl] = action;
+              t.path[lvl + 1] = 1 + A * t.meta[parent].latent + action;
+              s_act = action;
+              if (p.rec_a) p.rec_a[(size_t)k * B + b] = action;
             }
-            __syncthreads();
-            sc_load_amap(am, p.actmap, s_act, c, lane);
+            sc_load_amap(am, p.actmap, action, c, lane);
           }
           bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
           __syncthreads();
