@@ -16,10 +16,14 @@ from collections import defaultdict
 
 def summarise(root, pat):
     acc, disp, kname = defaultdict(float), defaultdict(set), ""
-    for path in sorted(glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv"), recursive=True)):
+    paths = sorted(glob.glob(os.path.join(root, "pmc_*", "**", "*counter_collection.csv"), recursive=True))
+    # the bench line's own launch of the kernel: the largest grid (config 1 also runs search_res_kernel, on 8 roots)
+    grid = max((int(r.get("Grid_Size") or 0) for path in paths for r in csv.DictReader(open(path))
+                if pat in r.get("Kernel_Name", "")), default=0)
+    for path in paths:
         for r in csv.DictReader(open(path)):
             name = r.get("Kernel_Name", "")
-            if pat not in name:
+            if pat not in name or int(r.get("Grid_Size") or 0) != grid:
                 continue
             kname = name
             c = r["Counter_Name"]

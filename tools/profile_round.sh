@@ -8,6 +8,10 @@ mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o fused --output-format csv -- \
   python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $out/bench_traced.log 2>&1
+python3 tools/kstats_grid.py $out/trace/fused_kernel_trace.csv > $out/trace/kernel_stats_by_grid.csv
+# the headline alone (its kernel's stats not merged with config 1's launches of the same kernel)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace_headline -o headline --output-format csv -- \
+  python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --configs none --secondary none > $out/bench_headline_traced.log 2>&1
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
