@@ -2575,15 +2575,15 @@ int64_t lzm_repr_workspace_floats(int B) { return B <= 0 ? -1 : (int64_t)B * (2 
 
 }  // extern "C"
 
-template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
 static int repr_launch(const ReprConvArgs &a, hipStream_t s) {
-  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
-  const size_t lds = 2 * (size_t)G::BUF * sizeof(uint16_t) + (G::KS == 2 ? 8 * 64 * 8 * sizeof(float) : 0);
-  static hipError_t attr = hipFuncSetAttribute((const void *)repr_conv_kernel<CIN, COUT, STRIDE, WOUT, MODE>,
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE, RES> G;
+  const size_t lds = G::LDSB;
+  static hipError_t attr = hipFuncSetAttribute((const void *)repr_conv_kernel<CIN, COUT, STRIDE, WOUT, MODE, RES>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   LZM_HIP(attr);
   const int grid = std::min(a.ntiles, device_cus());
-  hipLaunchKernelGGL((repr_conv_kernel<CIN, COUT, STRIDE, WOUT, MODE>), dim3(grid), dim3(kRpThreads), lds, s, a);
+  hipLaunchKernelGGL((repr_conv_kernel<CIN, COUT, STRIDE, WOUT, MODE, RES>), dim3(grid), dim3(kRpThreads), lds, s, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
@@ -2605,22 +2605,22 @@ int lzm_repr_downsample(int B, int cin, const float *w, const float *obs, float 
   int rc;
   // L1: obs (NCHW 64 x 64) -> A0 [32][32][32] (128-pixel tiles: 8 per image)
   a.ntiles = B * 8; a.in = obs; a.w = w + L.w1; a.bias = w + L.b1; a.res = nullptr; a.out = A0;
-  if ((rc = repr_launch<32, 32, 2, 32, 2>(a, s)) != LZM_OK) return rc;
+  if ((rc = repr_launch<32, 32, 2, 32, 2, false>(a, s)) != LZM_OK) return rc;
   // resblocks1: A0 -> A1 -> A0 (+ A0)
   a.in = A0; a.w = w + L.r1w1; a.bias = w + L.r1b1; a.out = A1;
-  if ((rc = repr_launch<32, 32, 1, 32, 0>(a, s)) != LZM_OK) return rc;
+  if ((rc = repr_launch<32, 32, 1, 32, 0, false>(a, s)) != LZM_OK) return rc;
   a.in = A1; a.w = w + L.r1w2; a.bias = w + L.r1b2; a.res = A0; a.out = A0;
-  if ((rc = repr_launch<32, 32, 1, 32, 0>(a, s)) != LZM_OK) return rc;
+  if ((rc = repr_launch<32, 32, 1, 32, 0, true>(a, s)) != LZM_OK) return rc;
   // the downsample block: A0 -> D0 = relu(conv1 + b1), D1 = conv3 (shortcut); D1 = relu(conv2(D0) + b2 + D1)
   a.ntiles = B * 4; a.in = A0; a.w = w + L.dw; a.bias = w + L.db1; a.res = nullptr; a.out = D0; a.out2 = D1;
-  if ((rc = repr_launch<32, 128, 2, 16, 1>(a, s)) != LZM_OK) return rc;
+  if ((rc = repr_launch<32, 128, 2, 16, 1, false>(a, s)) != LZM_OK) return rc;
   a.in = D0; a.w = w + L.dw2; a.bias = w + L.db2; a.res = D1; a.out = D1; a.out2 = nullptr;
-  if ((rc = repr_launch<64, 64, 1, 16, 0>(a, s)) != LZM_OK) return rc;
+  if ((rc = repr_launch<64, 64, 1, 16, 0, true>(a, s)) != LZM_OK) return rc;
   // resblocks2: D1 -> D0 -> D1 (+ D1)
   a.in = D1; a.w = w + L.r2w1; a.bias = w + L.r2b1; a.res = nullptr; a.out = D0;
-  if ((rc = repr_launch<64, 64, 1, 16, 0>(a, s)) != LZM_OK) return rc;
+  if ((rc = repr_launch<64, 64, 1, 16, 0, false>(a, s)) != LZM_OK) return rc;
   a.in = D0; a.w = w + L.r2w2; a.bias = w + L.r2b2; a.res = D1; a.out = D1;
-  if ((rc = repr_launch<64, 64, 1, 16, 0>(a, s)) != LZM_OK) return rc;
+  if ((rc = repr_launch<64, 64, 1, 16, 0, true>(a, s)) != LZM_OK) return rc;
   // avg pool -> out NCHW [B][64][8][8]
   hipLaunchKernelGGL(repr_avgpool_kernel, dim3(B), dim3(256), 0, s, D1, out, B);
   LZM_CHECK_LAUNCH();

@@ -14,9 +14,16 @@
 // (the MFMA A operand: the folded weights, held in REGISTERS for the whole launch), columns = output pixels
 // (the B operand: read from an LDS image of the input halo), K = 9 taps x in-channels in chunks of 32, on
 // v_mfma_f32_16x16x32_bf16 with every f32 operand split into three bf16 terms (six products per K: f32-level
-// error, the trunk's scheme, lzm_conv.h). A persistent grid (one 4-wave workgroup per CU) walks 64-pixel
-// output tiles; the next tile's halo is loaded into registers before the current tile's MFMAs and written to
-// the other LDS buffer after them.
+// error, the trunk's scheme, lzm_conv.h). A persistent grid (one 8-wave workgroup per CU) walks 64- or 128-pixel
+// output tiles of whole image rows.
+//
+// Staging (the tile loop's memory side, no registers): a tile's input rows, and its residual, are contiguous in
+// HBM (NHWC rows; the first layer: 9 rows of each NCHW plane), so they are copied as they lie into an LDS ring
+// of raw f32 slots by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction), S = 2-3 tiles ahead of the
+// MFMAs. Each tile then runs: counted vmcnt + barrier (the tile's slot has landed) -> split pass (raw f32 slot
+// -> the three bf16 term images, halo borders zeroed) -> barrier -> DMA of tile n + S into the freed slot ->
+// MFMAs -> epilogue (residual from its LDS slot). Only the DMA touches the VM counter inside the loop (the
+// weights are waited for before it, the epilogue only stores), so every wait is an exact count of younger DMAs.
 //
 // LDS image of a halo, per bf16 term: [channel group g = 8 channels][position][8 bf16], a group's plane padded
 // to a multiple of 16 positions. A B-fragment read (lane: pixel l & 15 of a 16-pixel tile, channel group
@@ -39,14 +46,14 @@ struct ReprConvArgs {
   const float *in;         // NHWC [B][HIN][HIN][CIN] (MODE 2: NCHW obs [B][cin_obs][64][64])
   const float *w;          // fragments [out tile][chunk][term][lane][8 bf16] (repr_pack)
   const float *bias;       // [COUT] (MODE 1: [64], the first half's)
-  const float *res;        // nullable: NHWC residual of the output's shape
+  const float *res;        // NHWC residual of the output's shape (RES launches only)
   float *out;              // NHWC [B][HOUT][HOUT][COUT] (MODE 1: the first 64 channels)
   float *out2;             // MODE 1: the shortcut's 64 channels, NHWC
 };
 
 // Geometry of one layer: WOUT-wide output rows, 64-pixel tiles of TR rows; halo HR x HC (bordered), LDS row
 // pitch ROWP (stride 2: even columns, then odd ones), group plane NPP positions (a multiple of 16).
-template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
 struct ReprGeom {
   // output pixels per tile: 128 for the 32-channel layers (two pixel tiles per wave), 64 otherwise
   static constexpr int PX = COUT == 32 ? 128 : 64;
@@ -68,11 +75,31 @@ struct ReprGeom {
   static_assert(OT == 2 || OT == 4 || OT == 8, "out tiles");
   static_assert(NCH % KS == 0, "K split");
   static constexpr int TERM = CG * NPP * 8;                           // bf16 per term image
-  static constexpr int BUF = 3 * TERM;                                // bf16 per halo buffer
+  static constexpr int BUF = 3 * TERM;                                // bf16 of the three term images
   static constexpr int PPW = MODE == 2 ? 64 : 64 / CG;                // positions per wave-instruction
-  // staging items (position, group): 64 per wave-instruction, PPW consecutive positions x CG groups
+  // split items (position, group): 64 per wave-instruction, PPW consecutive positions x CG groups
   static constexpr int ITEMS = MODE == 2 ? PX * 8 : (HR * HC + PPW - 1) / PPW * 64;
   static constexpr int IPT = (ITEMS + kRpThreads - 1) / kRpThreads;  // per thread
+  // raw DMA slot: MODE 2: [c < 7][RR = 2 TR + 1 rows][64] of the NCHW planes; else [HR][HIN][CIN] NHWC rows
+  static constexpr int HIN = MODE == 2 ? 64 : WOUT * STRIDE;
+  static constexpr int RR = 2 * TR + 1;
+  static constexpr int RAW_F4 = MODE == 2 ? 7 * RR * 16 : HR * HIN * CIN / 4;  // float4 (MODE 2: for 7 planes)
+  static constexpr int KRAW = (RAW_F4 + 511) / 512;                   // DMA wave-instructions per wave
+  static constexpr int RAWB = KRAW * 8 * 1024;                        // bytes per raw slot
+  static constexpr int COUT_T = MODE == 1 ? COUT / 2 : COUT;          // channels of one output tensor
+  static constexpr int RES_F4 = RES ? PX * COUT_T / 4 : 0;            // the residual tile, as it lies
+  static constexpr int KRES = (RES_F4 + 511) / 512;
+  static constexpr int RESB = KRES * 8 * 1024;
+  static constexpr int TERMB = BUF * 2;
+  static constexpr int XSB = KS == 2 ? 8 * 64 * 8 * 4 : 0;            // K-split partial sums
+  static constexpr int S = TERMB + 3 * RAWB + 2 * RESB + XSB <= 160 * 1024 ? 3 : 2;  // raw ring depth
+  static constexpr int RAW0 = TERMB, RES0 = RAW0 + S * RAWB, XS0 = RES0 + 2 * RESB;
+  static constexpr int LDSB = XS0 + XSB;
+  static_assert(LDSB <= 160 * 1024, "LDS");
+  // a tile's wait at the top of its iteration: the younger DMAs in flight (RES: the raw copy issued with the
+  // tile's residual; else the S - 1 raw copies after it)
+  static constexpr int NTOP = RES ? KRAW : (S - 1) * KRAW;
+  static_assert(NTOP < 64, "vmcnt");
 };
 
 // the LDS position of halo (row hr, bordered column hc)
@@ -82,7 +109,7 @@ __device__ __forceinline__ int rp_pos(int hr, int hc) {
   else return hr * G::ROWP + hc;
 }
 
-// staging item q of a tile -> (LDS position, channel group); false past the last item
+// split item q of a tile -> (LDS position, channel group); false past the last item
 template <class G, int STRIDE, int MODE>
 __device__ __forceinline__ bool rp_item(int q, int &hr, int &hc, int &g) {
   if (q >= G::ITEMS) return false;
@@ -92,8 +119,7 @@ __device__ __forceinline__ bool rp_item(int q, int &hr, int &hc, int &g) {
     g = q / G::PX;
     return true;
   }
-  // lanes: PPW consecutive halo positions (global: whole NHWC rows, coalesced; LDS: distinct bank slots per
-  // 8-lane write group) x the CG channel groups
+  // lanes: PPW consecutive halo positions (distinct bank slots per 8-lane write group) x the CG channel groups
   const int lin = (q >> 6) * G::PPW + (q & 63) % G::PPW;
   if (lin >= G::HR * G::HC) return false;
   g = (q & 63) / G::PPW;
@@ -102,83 +128,128 @@ __device__ __forceinline__ bool rp_item(int q, int &hr, int &hc, int &g) {
   return true;
 }
 
-// x where ok, else +0 (a bit mask: no select of addresses for the compiler to turn into a scratch array)
-__device__ __forceinline__ float4 rp_keep(bool ok, float4 x) {
-  const uint32_t m = ok ? 0xffffffffu : 0u;
-  return float4{__uint_as_float(__float_as_uint(x.x) & m), __uint_as_float(__float_as_uint(x.y) & m),
-                __uint_as_float(__float_as_uint(x.z) & m), __uint_as_float(__float_as_uint(x.w) & m)};
+// one LDS-DMA wave-instruction: 16 B from each lane's global address to lds_base + 16 lane (lds_base: a
+// wave-uniform LDS byte address). Inline asm, so the compiler inserts no vmcnt waits of its own for it: the
+// kernel counts its DMAs itself (rp_wait_vm)
+__device__ __forceinline__ void rp_dma16(const void *gsrc, uint32_t lds_base) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_base)
+               : "memory");
 }
 
-// load this thread's staging items of tile `tile` into registers (8 f32 per item). Branch-free: every item
-// loads from a clamped in-bounds address and selects zero where it lies outside the image (the halo border),
-// so the registers stay registers (no private-array stores under divergent control flow) and the loads stay
-// in flight until rp_store
-template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
-__device__ __forceinline__ void rp_load(const ReprConvArgs &a, int tile, float4 (&v)[ReprGeom<CIN, COUT, STRIDE, WOUT, MODE>::IPT][2]) {
-  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
-  constexpr int HIN = WOUT * STRIDE;
-  constexpr int TPI = (WOUT / G::TR);  // tiles per image (square output: WOUT rows)
+template <int N>
+__device__ __forceinline__ void rp_wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// every wave's LDS operations retired, then the workgroup barrier (no vmcnt: DMAs stay in flight across it)
+__device__ __forceinline__ void rp_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// DMA of tile `tile`'s raw input rows into the raw slot at LDS byte address `slot` (tiles past the last one:
+// the last tile again, so that every wave issues the same count). Rows outside the image load row 0 / HIN - 1
+// (the split pass zeroes them)
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
+__device__ __forceinline__ void rp_issue_raw(const ReprConvArgs &a, int tile, uint32_t slot, int wv, int lane) {
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE, RES> G;
+  constexpr int TPI = WOUT / G::TR;
+  tile = min(tile, a.ntiles - 1);
   const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
 #pragma unroll
-  for (int i = 0; i < G::IPT; ++i) {
-    int hr = 0, hc = 0, g = 0;
-    const bool item = rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g);
+  for (int i = 0; i < G::KRAW; ++i) {
+    const int f = (i * 8 + wv) * 64 + lane;
+    const float *src;
     if constexpr (MODE == 2) {
-      // im2col: pixel hc of the tile (row r0 + hc / WOUT, column hc % WOUT), K = 8 g .. 8 g + 7 = tap * C + c
-      const int oy = r0 + hc / WOUT, ox = hc % WOUT;
-      float e[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = 8 * g + j, tap = k / a.cin_obs, c = k % a.cin_obs;
-        const int iy = 2 * oy + tap / 3 - 1, ix = 2 * ox + tap % 3 - 1;
-        const bool ok = item && tap < 9 && iy >= 0 && iy < 64 && ix >= 0 && ix < 64;
-        const float x = a.in[ok ? (((int64_t)b * a.cin_obs + c) * 64 + iy) * 64 + ix : 0];
-        e[j] = __uint_as_float(__float_as_uint(x) & (ok ? 0xffffffffu : 0u));
-      }
-      v[i][0] = float4{e[0], e[1], e[2], e[3]};
-      v[i][1] = float4{e[4], e[5], e[6], e[7]};
+      const int C = a.cin_obs, ff = min(f, C * G::RR * 16 - 1);
+      const int c = ff / (G::RR * 16), rem = ff % (G::RR * 16);
+      const int iy = min(max(2 * r0 - 1 + rem / 16, 0), 63);
+      src = a.in + (((int64_t)b * C + c) * 64 + iy) * 64 + (rem % 16) * 4;
     } else {
-      const int iy = r0 * STRIDE - 1 + hr, ix = hc - 1;
-      const bool ok = item && iy >= 0 && iy < HIN && ix >= 0 && ix < HIN;
-      const float4 *src = reinterpret_cast<const float4 *>(
-          a.in + (ok ? (((int64_t)b * HIN + iy) * HIN + ix) * CIN + 8 * g : 0));
-      v[i][0] = rp_keep(ok, src[0]);
-      v[i][1] = rp_keep(ok, src[1]);
+      constexpr int ROWF4 = G::HIN * CIN / 4;
+      const int ff = min(f, G::RAW_F4 - 1), hr = ff / ROWF4;
+      const int iy = min(max(r0 * STRIDE - 1 + hr, 0), G::HIN - 1);
+      src = a.in + ((int64_t)b * G::HIN + iy) * G::HIN * CIN + (ff % ROWF4) * 4;
     }
+    rp_dma16(src, slot + (i * 8 + wv) * 1024);
   }
 }
 
-// split the loaded items into the three bf16 term images of an LDS halo buffer
-template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
-__device__ __forceinline__ void rp_store(uint16_t *buf, const float4 (&v)[ReprGeom<CIN, COUT, STRIDE, WOUT, MODE>::IPT][2]) {
-  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
+// DMA of tile `tile`'s residual (its output rows of a.res, as they lie) into the residual slot at `slot`
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
+__device__ __forceinline__ void rp_issue_res(const ReprConvArgs &a, int tile, uint32_t slot, int wv, int lane) {
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE, RES> G;
+  constexpr int TPI = WOUT / G::TR;
+  tile = min(tile, a.ntiles - 1);
+  const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
+  const float *base = a.res + ((int64_t)b * WOUT + r0) * WOUT * G::COUT_T;
+#pragma unroll
+  for (int i = 0; i < G::KRES; ++i) {
+    const int f = min((i * 8 + wv) * 64 + lane, G::RES_F4 - 1);
+    rp_dma16(base + f * 4, slot + (i * 8 + wv) * 1024);
+  }
+}
+
+// split pass: the tile's raw slot -> the three bf16 term images (halo borders and padding taps zero)
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
+__device__ __forceinline__ void rp_split(const ReprConvArgs &a, const float *raw, uint16_t *buf, int r0) {
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE, RES> G;
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
   typedef float f8 __attribute__((ext_vector_type(8)));
 #pragma unroll
   for (int i = 0; i < G::IPT; ++i) {
     int hr, hc, g;
     if (!rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g)) continue;
-    const int pos = MODE == 2 ? hc : rp_pos<G, STRIDE>(hr, hc);
-    const f8 x = f8{v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w};
+    f8 x;
+    int pos;
+    if constexpr (MODE == 2) {
+      // im2col: pixel hc of the tile (local row hc / WOUT, column hc % WOUT), K = 8 g + j = tap * C + c
+      pos = hc;
+      const int C = a.cin_obs, lr = hc / WOUT, ox = hc % WOUT;
+      int tap = (8 * g) / C, c = 8 * g - tap * C;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rr = 2 * lr + tap / 3, ix = 2 * ox + tap % 3 - 1, iy = 2 * r0 - 1 + rr;
+        const bool ok = tap < 9 && iy >= 0 && iy < 64 && ix >= 0 && ix < 64;
+        const float v = raw[ok ? (c * G::RR + rr) * 64 + ix : 0];
+        x[j] = __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
+        ++c;
+        tap += c == C;
+        c = c == C ? 0 : c;
+      }
+    } else {
+      pos = rp_pos<G, STRIDE>(hr, hc);
+      const int iy = r0 * STRIDE - 1 + hr, ix = hc - 1;
+      const bool ok = iy >= 0 && iy < G::HIN && ix >= 0 && ix < G::HIN;
+      const float4 *src = reinterpret_cast<const float4 *>(raw + (ok ? (hr * G::HIN + ix) * CIN + 8 * g : 0));
+      const uint32_t m = ok ? 0xffffffffu : 0u;
+      const float4 u = src[0], v = src[1];
+      x = f8{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = __uint_as_float(__float_as_uint(x[j]) & m);
+    }
     const b8 h = __builtin_convertvector(x, b8);
     const f8 r1 = x - __builtin_convertvector(h, f8);
-    const b8 m = __builtin_convertvector(r1, b8);
-    const b8 l = __builtin_convertvector(r1 - __builtin_convertvector(m, f8), b8);
+    const b8 md = __builtin_convertvector(r1, b8);
+    const b8 l = __builtin_convertvector(r1 - __builtin_convertvector(md, f8), b8);
     const int o = (g * G::NPP + pos) * 8;
     *reinterpret_cast<b8 *>(buf + o) = h;
-    *reinterpret_cast<b8 *>(buf + G::TERM + o) = m;
+    *reinterpret_cast<b8 *>(buf + G::TERM + o) = md;
     *reinterpret_cast<b8 *>(buf + 2 * G::TERM + o) = l;
   }
 }
 
-template <int CIN, int COUT, int STRIDE, int WOUT, int MODE>
+template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
 __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void repr_conv_kernel(
     ReprConvArgs a) {
-  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE> G;
+  typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE, RES> G;
   extern __shared__ uint4 rp_lds4[];
-  uint16_t *lds = reinterpret_cast<uint16_t *>(rp_lds4);
-  float *xscr = reinterpret_cast<float *>(lds + 2 * G::BUF);  // K-split partial sums
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint8_t *lb = reinterpret_cast<uint8_t *>(rp_lds4);
+  uint16_t *terms = reinterpret_cast<uint16_t *>(lb);
+  float *xscr = reinterpret_cast<float *>(lb + G::XS0);  // K-split partial sums
+  const uint32_t lds0 = (uint32_t)reinterpret_cast<uintptr_t>(lb);  // the LDS byte address of the array
+  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   // this wave's out tile, first pixel tile and K half
   const int ot = G::OT == 2 ? (wv & 1) : (G::OT == 4 ? (wv & 3) : wv);
   const int pt0 = G::OT == 2 ? (wv >> 1) * G::PTW : 0;
@@ -191,36 +262,41 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     for (int q = 0; q < 3; ++q)
       wr[s][q] = reinterpret_cast<const uint4 *>(a.w)[((ot * G::NCH + kh * G::NCW + s) * 3 + q) * 64 + lane];
   // out channels 4 (lane >> 4) .. + 3 of the tile; the dual layer's upper half is the shortcut (no bias)
-  constexpr int COUT_T = MODE == 1 ? COUT / 2 : COUT;  // channels of one output tensor
+  constexpr int COUT_T = G::COUT_T;
   constexpr int HOUT = WOUT, TPI = HOUT / G::TR;
   int ch = 16 * ot + 4 * (lane >> 4);
   const bool sc = MODE == 1 && ch >= COUT_T;
   float *dst = sc ? a.out2 : a.out;
   if (sc) ch -= COUT_T;
   const float4 bias = sc ? float4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4 *>(a.bias + ch);
-  float4 v[G::IPT][2];
+  // the compiler's own loads retired here (a builtin wait it accounts for): inside the loop the VM counter
+  // holds DMAs and stores only
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  const int grid = gridDim.x;
   int tile = blockIdx.x;
-  if (tile < a.ntiles) {
-    rp_load<CIN, COUT, STRIDE, WOUT, MODE>(a, tile, v);
-    rp_store<CIN, COUT, STRIDE, WOUT, MODE>(lds, v);
-  }
-  __syncthreads();
-  for (int it = 0; tile < a.ntiles; ++it, tile += gridDim.x) {
-    const uint16_t *cur = lds + (it & 1) * G::BUF;
-    const int nxt = tile + gridDim.x;
-    if (nxt < a.ntiles) rp_load<CIN, COUT, STRIDE, WOUT, MODE>(a, nxt, v);  // in flight during the MFMAs
-    const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
-    // the epilogue's residual, issued now (its latency hides behind the MFMAs): one float4 per pixel tile this
-    // wave finishes (K split: 2, the tiles 2 kh + j), none for the dual layer
-    constexpr int NRES = MODE == 1 ? 1 : (G::KS == 2 ? 2 : G::PTW);
-    float4 rres[NRES];
+  // prologue: raw copies of tiles 0 .. S - 1 (the residual of tile 0 before the last one: the order the
+  // loop's waits count)
 #pragma unroll
-    for (int j = 0; j < NRES; ++j) {
-      const int p = G::KS == 2 ? 2 * kh + j : j;
-      const int px = 16 * (pt0 + p) + (lane & 15);
-      const int64_t e = (((int64_t)b * HOUT + r0 + px / WOUT) * WOUT + px % WOUT) * COUT_T + ch;
-      rres[j] = (MODE != 1 && a.res) ? *reinterpret_cast<const float4 *>(a.res + e) : float4{0.f, 0.f, 0.f, 0.f};
-    }
+  for (int k = 0; k < G::S - 1; ++k)
+    rp_issue_raw<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile + k * grid, lds0 + G::RAW0 + k * G::RAWB, wv, lane);
+  if constexpr (RES) rp_issue_res<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile, lds0 + G::RES0, wv, lane);
+  rp_issue_raw<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile + (G::S - 1) * grid,
+                                                    lds0 + G::RAW0 + (G::S - 1) * G::RAWB, wv, lane);
+  int slot = 0;  // the raw slot of the current tile (n mod S)
+  for (int it = 0; tile < a.ntiles; ++it, tile += grid) {
+    const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
+    rp_wait_vm<G::NTOP>();  // this wave's copies of the tile landed ...
+    rp_barrier();           // ... and every wave's; every wave is also done with the previous tile's LDS
+    rp_split<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, reinterpret_cast<const float *>(lb + G::RAW0 + slot * G::RAWB),
+                                                 terms, r0);
+    rp_barrier();
+    // refill: the next tile's residual into the other residual slot, tile n + S into the slot just split
+    if constexpr (RES)
+      rp_issue_res<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile + grid, lds0 + G::RES0 + ((it + 1) & 1) * G::RESB,
+                                                        wv, lane);
+    rp_issue_raw<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile + G::S * grid, lds0 + G::RAW0 + slot * G::RAWB, wv,
+                                                      lane);
+    slot = slot + 1 == G::S ? 0 : slot + 1;
     bxf4 acc[G::PTW];
 #pragma unroll
     for (int p = 0; p < G::PTW; ++p) acc[p] = bxf4{0.f, 0.f, 0.f, 0.f};
@@ -238,7 +314,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         else pos = rp_pos<G, STRIDE>((px / WOUT) * STRIDE + dy, (px % WOUT) * STRIDE + dx);
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          x[p][q] = *reinterpret_cast<const uint4 *>(cur + q * G::TERM + (g * G::NPP + pos) * 8);
+          x[p][q] = *reinterpret_cast<const uint4 *>(terms + q * G::TERM + (g * G::NPP + pos) * 8);
       }
     };
     // software pipeline: chunk s + 1's LDS reads issued before chunk s's MFMAs (the scheduling barrier keeps
@@ -272,7 +348,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       const bxf4 g0 = kh ? acc[0] : acc[2], g1 = kh ? acc[1] : acc[3];
       mine[0] = float4{g0[0], g0[1], g0[2], g0[3]};
       mine[1] = float4{g1[0], g1[1], g1[2], g1[3]};
-      __syncthreads();
+      rp_barrier();
       const float4 *theirs = reinterpret_cast<const float4 *>(xscr + ((ot * 2 + kh) * 64 + lane) * 8);
       const float4 q0 = theirs[0], q1 = theirs[1];
 #pragma unroll
@@ -284,6 +360,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       }
     }
     // epilogue: acc[p][r] = out channel ch + r at pixel 16 (pt0 + p) + (lane & 15)
+    const float *rs = reinterpret_cast<const float *>(lb + G::RES0 + (it & 1) * G::RESB);
 #pragma unroll
     for (int p = 0; p < G::PTW; ++p) {
       if (G::KS == 2 && (p >> 1) != kh) continue;  // (the K-split partner's tiles)
@@ -291,17 +368,16 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
       const int64_t e = (((int64_t)b * HOUT + r0 + px / WOUT) * WOUT + px % WOUT) * COUT_T + ch;
       float4 y = float4{acc[p][0] + bias.x, acc[p][1] + bias.y, acc[p][2] + bias.z, acc[p][3] + bias.w};
       if (!sc) {
-        if (a.res) {
-          const float4 rr = rres[MODE == 1 ? 0 : (G::KS == 2 ? (p & 1) : p)];
+        if constexpr (RES) {
+          const float4 rr = *reinterpret_cast<const float4 *>(rs + px * COUT_T + ch);
           y.x += rr.x; y.y += rr.y; y.z += rr.z; y.w += rr.w;
         }
         y.x = fmaxf(y.x, 0.f); y.y = fmaxf(y.y, 0.f); y.z = fmaxf(y.z, 0.f); y.w = fmaxf(y.w, 0.f);
       }
       *reinterpret_cast<float4 *>(dst + e) = y;
     }
-    if (nxt < a.ntiles) rp_store<CIN, COUT, STRIDE, WOUT, MODE>(lds + ((it + 1) & 1) * G::BUF, v);
-    __syncthreads();
   }
+  rp_wait_vm<0>();  // the copies of tiles past the end land before the workgroup's LDS is released
 }
 
 // avg_pool2d(3, 2, padding 1, count_include_pad) of NHWC [B][16][16][64] -> NCHW [B][64][8][8]: one workgroup per

@@ -189,17 +189,25 @@ def test_bench_breakout_workload_line(tmp_path):
     assert line["tie_stream_errors"] == 0 and line["trajectory"]["frame_dtype"] == "uint8"
 
 
-@pytest.mark.parametrize("kind", ["mz", "ez"])
-def test_native_downsample_matches_float64_reference(kind):
+@pytest.mark.parametrize("kind,B,cin", [("mz", 37, 4), ("ez", 37, 4), ("mz", 300, 4), ("mz", 45, 3), ("mz", 29, 7)])
+def test_native_downsample_matches_float64_reference(kind, B, cin):
     """lzm_repr_downsample (the DownSample stages on split-bf16 MFMA, csrc/lzm_repr.h) vs the same BN-folded
     convolutions in float64 on the CPU: conv 3x3/2 -> 32, the 32-channel block, the downsample block with its
-    3x3/2 shortcut, the 64-channel block, avg pool. Tolerance: the split keeps f32-level error — 2e-5 of the
-    layer's magnitude (relative to max |ref|) and rtol 1e-4 elementwise."""
+    3x3/2 shortcut, the 64-channel block, avg pool. B = 37: tiles of several images per workgroup, a ragged last
+    round; B = 300: ~10 tiles per workgroup, every slot of the LDS-DMA ring reused several times; 3 and 7
+    observation planes: the first layer's im2col over other channel counts. Three launches must agree bit for
+    bit (a DMA read before it lands would show as run-to-run differences). Tolerance: the split keeps f32-level
+    error — 2e-5 of the layer's magnitude (relative to max |ref|) and rtol 1e-4 elementwise."""
     import torch.nn.functional as F
     from lightzero_amd.conv_infer import FoldedConvInitial
-    from lightzero_amd.model_conv import atari_efficientzero_model
-    if kind == "mz":
+    from lightzero_amd.model_conv import atari_efficientzero_model, atari_muzero_model
+    if kind == "mz" and cin == 4:
         m = _conv_model(4)
+    elif kind == "mz":
+        torch.manual_seed(cin)
+        m = atari_muzero_model(observation_shape=(cin, 64, 64), last_linear_layer_init_zero=False)
+        bench._random_bn(m, cin + 1)
+        m = m.to(DEV).eval()
     else:
         torch.manual_seed(4)
         m = atari_efficientzero_model(last_linear_layer_init_zero=False)
@@ -207,10 +215,12 @@ def test_native_downsample_matches_float64_reference(kind):
         m = m.to(DEV).eval()
     fi = FoldedConvInitial(m)
     assert fi.repr_native is not None
-    B = 37  # tiles of several images per workgroup, a ragged last round
-    obs = torch.rand(B, 4, 64, 64, device=DEV)
+    obs = torch.rand(B, cin, 64, 64, device=DEV)
     with torch.no_grad():
-        got = fi._downsample_native(obs).cpu().double()
+        runs = [fi._downsample_native(obs).cpu() for _ in range(3)]
+    for r in runs[1:]:
+        assert torch.equal(r, runs[0])
+    got = runs[0].double()
     x = obs.cpu().double()
     ops = [tuple(t.cpu().double() if torch.is_tensor(t) else t for t in op) for op in fi.ops[:fi.tail[0]]]
     for op in ops:
