@@ -14,7 +14,8 @@
 // (the MFMA A operand: the folded weights, held in REGISTERS for the whole launch), columns = output pixels
 // (the B operand: read from an LDS image of the input halo), K = 9 taps x in-channels in chunks of 32, on
 // v_mfma_f32_16x16x32_bf16 with every f32 operand split into three bf16 terms (six products per K: f32-level
-// error, the trunk's scheme, lzm_conv.h). A persistent grid (one 8-wave workgroup per CU) walks 64- or 128-pixel
+// error, the trunk's scheme, lzm_conv.h; the weights rounded to nearest on the host, the activations split
+// exactly by truncation, rp_split8). A persistent grid (one 8-wave workgroup per CU) walks 64- or 128-pixel
 // output tiles of whole image rows.
 //
 // Staging (the tile loop's memory side, no registers): a tile's input rows, and its residual, are contiguous in
@@ -92,12 +93,14 @@ struct ReprGeom {
   static constexpr int RESB = KRES * 8 * 1024;
   static constexpr int TERMB = BUF * 2;
   static constexpr int XSB = KS == 2 ? 8 * 64 * 8 * 4 : 0;            // K-split partial sums
-  static constexpr int S = TERMB + 3 * RAWB + 2 * RESB + XSB <= 160 * 1024 ? 3 : 2;  // raw ring depth
+  static constexpr int FIXB = 2 * RESB + XSB + 32;
+  static constexpr int S = TERMB + 3 * RAWB + FIXB <= 160 * 1024 ? 3 : 2;  // raw ring depth
   static constexpr int RAW0 = TERMB, RES0 = RAW0 + S * RAWB, XS0 = RES0 + 2 * RESB;
-  static constexpr int LDSB = XS0 + XSB;
+  static constexpr int ZB = XS0 + XSB;  // 32 zero bytes: the split pass's source for halo positions off the image
+  static constexpr int LDSB = ZB + 32;
   static_assert(LDSB <= 160 * 1024, "LDS");
-  // a tile's wait at the top of its iteration: the younger DMAs in flight (RES: the raw copy issued with the
-  // tile's residual; else the S - 1 raw copies after it)
+  // a tile's wait at the top of its iteration: the DMAs younger than the newest copy it needs (the tile's raw
+  // copy and residual): the raw copy issued with that residual (RES), or the S - 1 raw copies after it
   static constexpr int NTOP = RES ? KRAW : (S - 1) * KRAW;
   static_assert(NTOP < 64, "vmcnt");
 };
@@ -191,11 +194,35 @@ __device__ __forceinline__ void rp_issue_res(const ReprConvArgs &a, int tile, ui
   }
 }
 
+// x = h + m + l EXACTLY, by truncation: h = x's top 8 significand bits, m = the next 8 of the remainder, l = what
+// is left (at most 8 significant bits: a bf16 as it stands). Every term is an f32 with a zero low half, so pairs
+// pack by v_perm_b32 (the high halves of two lanes' values): 5.5 VALU per value against 9 for round-to-nearest
+// terms (a bf16 rounding plus its conversion back to f32 per term). The dropped products (w_m x_l, w_l x_m,
+// w_l x_l) stay below 2^-24 of |w x|.
+template <class F8>
+__device__ __forceinline__ void rp_split8(const F8 &x, uint4 &h, uint4 &m, uint4 &l) {
+  uint32_t hu[8], mu[8], lu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hu[j] = __float_as_uint(x[j]) & 0xffff0000u;
+    const float r1 = x[j] - __uint_as_float(hu[j]);
+    mu[j] = __float_as_uint(r1) & 0xffff0000u;
+    lu[j] = __float_as_uint(r1 - __uint_as_float(mu[j]));
+  }
+  // pair (2k, 2k + 1) -> bf16 2k in the low half, 2k + 1 in the high half
+  h = uint4{__builtin_amdgcn_perm(hu[1], hu[0], 0x07060302u), __builtin_amdgcn_perm(hu[3], hu[2], 0x07060302u),
+            __builtin_amdgcn_perm(hu[5], hu[4], 0x07060302u), __builtin_amdgcn_perm(hu[7], hu[6], 0x07060302u)};
+  m = uint4{__builtin_amdgcn_perm(mu[1], mu[0], 0x07060302u), __builtin_amdgcn_perm(mu[3], mu[2], 0x07060302u),
+            __builtin_amdgcn_perm(mu[5], mu[4], 0x07060302u), __builtin_amdgcn_perm(mu[7], mu[6], 0x07060302u)};
+  l = uint4{__builtin_amdgcn_perm(lu[1], lu[0], 0x07060302u), __builtin_amdgcn_perm(lu[3], lu[2], 0x07060302u),
+            __builtin_amdgcn_perm(lu[5], lu[4], 0x07060302u), __builtin_amdgcn_perm(lu[7], lu[6], 0x07060302u)};
+}
+
 // split pass: the tile's raw slot -> the three bf16 term images (halo borders and padding taps zero)
 template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
-__device__ __forceinline__ void rp_split(const ReprConvArgs &a, const float *raw, uint16_t *buf, int r0) {
+__device__ __forceinline__ void rp_split(const ReprConvArgs &a, const float *raw, const float *zero, uint16_t *buf,
+                                         int r0) {
   typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE, RES> G;
-  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
   typedef float f8 __attribute__((ext_vector_type(8)));
 #pragma unroll
   for (int i = 0; i < G::IPT; ++i) {
@@ -222,21 +249,16 @@ __device__ __forceinline__ void rp_split(const ReprConvArgs &a, const float *raw
       pos = rp_pos<G, STRIDE>(hr, hc);
       const int iy = r0 * STRIDE - 1 + hr, ix = hc - 1;
       const bool ok = iy >= 0 && iy < G::HIN && ix >= 0 && ix < G::HIN;
-      const float4 *src = reinterpret_cast<const float4 *>(raw + (ok ? (hr * G::HIN + ix) * CIN + 8 * g : 0));
-      const uint32_t m = ok ? 0xffffffffu : 0u;
+      const float4 *src = reinterpret_cast<const float4 *>(ok ? raw + (hr * G::HIN + ix) * CIN + 8 * g : zero);
       const float4 u = src[0], v = src[1];
       x = f8{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = __uint_as_float(__float_as_uint(x[j]) & m);
     }
-    const b8 h = __builtin_convertvector(x, b8);
-    const f8 r1 = x - __builtin_convertvector(h, f8);
-    const b8 md = __builtin_convertvector(r1, b8);
-    const b8 l = __builtin_convertvector(r1 - __builtin_convertvector(md, f8), b8);
+    uint4 h, md, l;
+    rp_split8(x, h, md, l);
     const int o = (g * G::NPP + pos) * 8;
-    *reinterpret_cast<b8 *>(buf + o) = h;
-    *reinterpret_cast<b8 *>(buf + G::TERM + o) = md;
-    *reinterpret_cast<b8 *>(buf + 2 * G::TERM + o) = l;
+    *reinterpret_cast<uint4 *>(buf + o) = h;
+    *reinterpret_cast<uint4 *>(buf + G::TERM + o) = md;
+    *reinterpret_cast<uint4 *>(buf + 2 * G::TERM + o) = l;
   }
 }
 
@@ -272,6 +294,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   // the compiler's own loads retired here (a builtin wait it accounts for): inside the loop the VM counter
   // holds DMAs and stores only
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  if (tid < 8) reinterpret_cast<float *>(lb + G::ZB)[tid] = 0.f;  // (ordered by the first tile's barrier)
   const int grid = gridDim.x;
   int tile = blockIdx.x;
   // prologue: raw copies of tiles 0 .. S - 1 (the residual of tile 0 before the last one: the order the
@@ -282,15 +305,16 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   if constexpr (RES) rp_issue_res<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile, lds0 + G::RES0, wv, lane);
   rp_issue_raw<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile + (G::S - 1) * grid,
                                                     lds0 + G::RAW0 + (G::S - 1) * G::RAWB, wv, lane);
+  const float *zero = reinterpret_cast<const float *>(lb + G::ZB);
   int slot = 0;  // the raw slot of the current tile (n mod S)
   for (int it = 0; tile < a.ntiles; ++it, tile += grid) {
     const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
-    rp_wait_vm<G::NTOP>();  // this wave's copies of the tile landed ...
+    rp_wait_vm<G::NTOP>();  // this wave's copies landed ...
     rp_barrier();           // ... and every wave's; every wave is also done with the previous tile's LDS
     rp_split<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, reinterpret_cast<const float *>(lb + G::RAW0 + slot * G::RAWB),
-                                                 terms, r0);
+                                                 zero, terms, r0);
     rp_barrier();
-    // refill: the next tile's residual into the other residual slot, tile n + S into the slot just split
+    // refill: the next tile's residual into the other residual slot, tile n + S into the slot of tile n
     if constexpr (RES)
       rp_issue_res<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, tile + grid, lds0 + G::RES0 + ((it + 1) & 1) * G::RESB,
                                                         wv, lane);
@@ -338,6 +362,20 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][1]), c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][0]), c, 0, 0, 0);
         acc[p] = c;
+      }
+      // the order within the chunk (left alone, the scheduler sinks chunk s + 1's fragment reads to the end of
+      // chunk s and every chunk then waits out a full LDS latency): two pixel tiles, the reads first, then the
+      // MFMAs; four (64-channel layers, 96 fragment registers), half the reads after the first tile's MFMAs and
+      // half after the third's, within the register file
+      if constexpr (G::PTW == 2) {
+        if (s + 1 < G::NCW) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);                      // MFMAs
+      } else if (s + 1 < G::NCW) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
