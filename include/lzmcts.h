@@ -279,8 +279,9 @@ int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_by
 /* The representation network's DownSample stages (lzero/model/common.py:164-265: conv 3x3/2 -> 32, a 32-channel
  * residual block at 32 x 32, the downsample block (3x3/2 -> 64 with a 3x3/2 shortcut), a 64-channel residual
  * block at 16 x 16, avg_pool 3x3/2) of the conv MuZeroModel / EfficientZeroModel, BatchNorm folded, on the
- * split-bf16 matrix path (csrc/lzm_repr.h): 7 convolution launches with fused bias / residual / ReLU and a pool
- * launch. lzm_repr_prepare packs raw = [conv1 W (32 x cin x 9), b (32) | block1 W1 (32 x 32 x 9), b1, W2, b2 |
+ * split-fp16 matrix path (two fp16 terms per f32 operand, three MFMA products per K; csrc/lzm_repr.h): 7
+ * convolution launches with fused bias / residual / ReLU and a pool launch. lzm_repr_prepare packs raw =
+ * [conv1 W (32 x cin x 9), b (32) | block1 W1 (32 x 32 x 9), b1, W2, b2 |
  * down W1 (64 x 32 x 9), b1 (64), W2 (64 x 64 x 9), b2 (64), W3 (64 x 32 x 9) | block2 W1 (64 x 64 x 9), b1, W2,
  * b2] into lzm_repr_floats() floats. lzm_repr_downsample: obs f32 NCHW [B][cin][64][64] -> out [B][64][8][8]
  * (the input of lzm_conv_resnet8_p's 8 x 8 tail); ws: lzm_repr_workspace_floats(B) floats (NHWC stages). */

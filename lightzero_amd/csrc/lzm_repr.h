@@ -1,5 +1,5 @@
 // lzm_repr.h — the representation network's downsampling stages of the Atari configs (BASELINE.json configs 3
-// and 5) on the split-bf16 matrix path: initial_inference's DownSample (lzero/model/common.py:164-265), with
+// and 5) on the split-fp16 matrix path: initial_inference's DownSample (lzero/model/common.py:164-265), with
 // every eval-mode BatchNorm folded into the convolution in front of it (lightzero_amd/conv_infer.py):
 //
 //   L1  y = relu(conv3x3_s2(obs, W1) + b1)                         obs [C <= 7][64][64] -> [32][32][32]
@@ -13,20 +13,22 @@
 // it stays in the Infinity Cache between layers). Each convolution is an implicit GEMM: rows = out channels
 // (the MFMA A operand: the folded weights, held in REGISTERS for the whole launch), columns = output pixels
 // (the B operand: read from an LDS image of the input halo), K = 9 taps x in-channels in chunks of 32, on
-// v_mfma_f32_16x16x32_bf16 with every f32 operand split into three bf16 terms (six products per K: f32-level
-// error, the trunk's scheme, lzm_conv.h; the weights rounded to nearest on the host, the activations split
-// exactly by truncation, rp_split8). A persistent grid (one 8-wave workgroup per CU) walks 64- or 128-pixel
+// v_mfma_f32_16x16x32_f16 with every f32 operand split into two fp16 terms x = h + l (h = fp16(x), l =
+// fp16(x - h): 22 significand bits, |x - h - l| <= 2^-22 |x|) and three products per K (w_h x_h, w_h x_l,
+// w_l x_h; the dropped w_l x_l is below 2^-22 of |w x|): f32-level error at half the MFMAs of the trunk's
+// three-term bf16 scheme (lzm_conv.h). fp16's range bounds it: |values| < 65504, and below 2^-14 (6.1e-5) the
+// terms are fp16 subnormals, an absolute error of at most 2^-25 per operand. A persistent grid (one 8-wave workgroup per CU) walks 64- or 128-pixel
 // output tiles of whole image rows.
 //
 // Staging (the tile loop's memory side, no registers): a tile's input rows, and its residual, are contiguous in
 // HBM (NHWC rows; the first layer: 9 rows of each NCHW plane), so they are copied as they lie into an LDS ring
 // of raw f32 slots by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction), S = 2-3 tiles ahead of the
 // MFMAs. Each tile then runs: counted vmcnt + barrier (the tile's slot has landed) -> split pass (raw f32 slot
-// -> the three bf16 term images, halo borders zeroed) -> barrier -> DMA of tile n + S into the freed slot ->
+// -> the two fp16 term images, halo borders zeroed) -> barrier -> DMA of tile n + S into the freed slot ->
 // MFMAs -> epilogue (residual from its LDS slot). Only the DMA touches the VM counter inside the loop (the
 // weights are waited for before it, the epilogue only stores), so every wait is an exact count of younger DMAs.
 //
-// LDS image of a halo, per bf16 term: [channel group g = 8 channels][position][8 bf16], a group's plane padded
+// LDS image of a halo, per fp16 term: [channel group g = 8 channels][position][8 fp16], a group's plane padded
 // to a multiple of 16 positions. A B-fragment read (lane: pixel l & 15 of a 16-pixel tile, channel group
 // g0 + (l >> 4)) touches 16 consecutive positions per group, so every ds_read_b128 lane group hits 16
 // distinct 16-B bank slots. Stride-2 convolutions store the halo's even and odd columns apart, which makes
@@ -41,11 +43,15 @@
 namespace lzm {
 
 constexpr int kRpThreads = 512;  // 8 waves: two per SIMD
+constexpr int kRpTerms = 2;      // fp16 terms per f32 operand
+
+typedef _Float16 rpf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ rpf16x8 rp_as(uint4 u) { return __builtin_bit_cast(rpf16x8, u); }
 
 struct ReprConvArgs {
   int B, ntiles, cin_obs;  // cin_obs: first layer's input channels (MODE 2)
   const float *in;         // NHWC [B][HIN][HIN][CIN] (MODE 2: NCHW obs [B][cin_obs][64][64])
-  const float *w;          // fragments [out tile][chunk][term][lane][8 bf16] (repr_pack)
+  const float *w;          // fragments [out tile][chunk][term][lane][8 fp16] (repr_pack)
   const float *bias;       // [COUT] (MODE 1: [64], the first half's)
   const float *res;        // NHWC residual of the output's shape (RES launches only)
   float *out;              // NHWC [B][HOUT][HOUT][COUT] (MODE 1: the first 64 channels)
@@ -75,8 +81,8 @@ struct ReprGeom {
   static constexpr int NCW = NCH / KS;                                // K chunks per wave
   static_assert(OT == 2 || OT == 4 || OT == 8, "out tiles");
   static_assert(NCH % KS == 0, "K split");
-  static constexpr int TERM = CG * NPP * 8;                           // bf16 per term image
-  static constexpr int BUF = 3 * TERM;                                // bf16 of the three term images
+  static constexpr int TERM = CG * NPP * 8;                           // fp16 per term image
+  static constexpr int BUF = kRpTerms * TERM;                         // fp16 of the term images
   static constexpr int PPW = MODE == 2 ? 64 : 64 / CG;                // positions per wave-instruction
   // split items (position, group): 64 per wave-instruction, PPW consecutive positions x CG groups
   static constexpr int ITEMS = MODE == 2 ? PX * 8 : (HR * HC + PPW - 1) / PPW * 64;
@@ -194,31 +200,18 @@ __device__ __forceinline__ void rp_issue_res(const ReprConvArgs &a, int tile, ui
   }
 }
 
-// x = h + m + l EXACTLY, by truncation: h = x's top 8 significand bits, m = the next 8 of the remainder, l = what
-// is left (at most 8 significant bits: a bf16 as it stands). Every term is an f32 with a zero low half, so pairs
-// pack by v_perm_b32 (the high halves of two lanes' values): 5.5 VALU per value against 9 for round-to-nearest
-// terms (a bf16 rounding plus its conversion back to f32 per term). The dropped products (w_m x_l, w_l x_m,
-// w_l x_l) stay below 2^-24 of |w x|.
+// x = h + l: h = fp16(x), l = fp16(x - h) (x - h is exact in f32), both rounded to nearest, pairs packed
 template <class F8>
-__device__ __forceinline__ void rp_split8(const F8 &x, uint4 &h, uint4 &m, uint4 &l) {
-  uint32_t hu[8], mu[8], lu[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    hu[j] = __float_as_uint(x[j]) & 0xffff0000u;
-    const float r1 = x[j] - __uint_as_float(hu[j]);
-    mu[j] = __float_as_uint(r1) & 0xffff0000u;
-    lu[j] = __float_as_uint(r1 - __uint_as_float(mu[j]));
-  }
-  // pair (2k, 2k + 1) -> bf16 2k in the low half, 2k + 1 in the high half
-  h = uint4{__builtin_amdgcn_perm(hu[1], hu[0], 0x07060302u), __builtin_amdgcn_perm(hu[3], hu[2], 0x07060302u),
-            __builtin_amdgcn_perm(hu[5], hu[4], 0x07060302u), __builtin_amdgcn_perm(hu[7], hu[6], 0x07060302u)};
-  m = uint4{__builtin_amdgcn_perm(mu[1], mu[0], 0x07060302u), __builtin_amdgcn_perm(mu[3], mu[2], 0x07060302u),
-            __builtin_amdgcn_perm(mu[5], mu[4], 0x07060302u), __builtin_amdgcn_perm(mu[7], mu[6], 0x07060302u)};
-  l = uint4{__builtin_amdgcn_perm(lu[1], lu[0], 0x07060302u), __builtin_amdgcn_perm(lu[3], lu[2], 0x07060302u),
-            __builtin_amdgcn_perm(lu[5], lu[4], 0x07060302u), __builtin_amdgcn_perm(lu[7], lu[6], 0x07060302u)};
+__device__ __forceinline__ void rp_split8(const F8 &x, uint4 &h, uint4 &l) {
+  typedef float f8 __attribute__((ext_vector_type(8)));
+  const f8 xv = f8{x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]};
+  const rpf16x8 hv = __builtin_convertvector(xv, rpf16x8);
+  const rpf16x8 lv = __builtin_convertvector(xv - __builtin_convertvector(hv, f8), rpf16x8);
+  h = __builtin_bit_cast(uint4, hv);
+  l = __builtin_bit_cast(uint4, lv);
 }
 
-// split pass: the tile's raw slot -> the three bf16 term images (halo borders and padding taps zero)
+// split pass: the tile's raw slot -> the two fp16 term images (halo borders and padding taps zero)
 template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
 __device__ __forceinline__ void rp_split(const ReprConvArgs &a, const float *raw, const float *zero, uint16_t *buf,
                                          int r0) {
@@ -253,12 +246,11 @@ __device__ __forceinline__ void rp_split(const ReprConvArgs &a, const float *raw
       const float4 u = src[0], v = src[1];
       x = f8{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
     }
-    uint4 h, md, l;
-    rp_split8(x, h, md, l);
+    uint4 h, l;
+    rp_split8(x, h, l);
     const int o = (g * G::NPP + pos) * 8;
     *reinterpret_cast<uint4 *>(buf + o) = h;
-    *reinterpret_cast<uint4 *>(buf + G::TERM + o) = md;
-    *reinterpret_cast<uint4 *>(buf + 2 * G::TERM + o) = l;
+    *reinterpret_cast<uint4 *>(buf + G::TERM + o) = l;
   }
 }
 
@@ -276,13 +268,13 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   const int ot = G::OT == 2 ? (wv & 1) : (G::OT == 4 ? (wv & 3) : wv);
   const int pt0 = G::OT == 2 ? (wv >> 1) * G::PTW : 0;
   const int kh = G::KS == 2 ? (wv >> 2) : 0;
-  // the weights of that out tile over its K chunks, three terms: registers for the whole launch
-  uint4 wr[G::NCW][3];
+  // the weights of that out tile over its K chunks, both terms: registers for the whole launch
+  uint4 wr[G::NCW][kRpTerms];
 #pragma unroll
   for (int s = 0; s < G::NCW; ++s)
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-      wr[s][q] = reinterpret_cast<const uint4 *>(a.w)[((ot * G::NCH + kh * G::NCW + s) * 3 + q) * 64 + lane];
+    for (int q = 0; q < kRpTerms; ++q)
+      wr[s][q] = reinterpret_cast<const uint4 *>(a.w)[((ot * G::NCH + kh * G::NCW + s) * kRpTerms + q) * 64 + lane];
   // out channels 4 (lane >> 4) .. + 3 of the tile; the dual layer's upper half is the shortcut (no bias)
   constexpr int COUT_T = G::COUT_T;
   constexpr int HOUT = WOUT, TPI = HOUT / G::TR;
@@ -326,7 +318,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     for (int p = 0; p < G::PTW; ++p) acc[p] = bxf4{0.f, 0.f, 0.f, 0.f};
     // B fragments of chunk s for the wave's pixel tiles (lane: pixel 16 (pt0 + p) + (lane & 15) of the tile,
     // output row px / WOUT, column px % WOUT; channel group 4 j + (lane >> 4))
-    auto load_x = [&](int s, uint4 (&x)[G::PTW][3]) {
+    auto load_x = [&](int s, uint4 (&x)[G::PTW][kRpTerms]) {
       const int sg = kh * G::NCW + s;  // chunk within the layer's K
       const int tap = MODE == 2 ? 0 : sg / (CIN / 32), j = MODE == 2 ? sg : sg % (CIN / 32);
       const int dy = tap / 3, dx = tap % 3, g = 4 * j + (lane >> 4);
@@ -337,45 +329,42 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         if constexpr (MODE == 2) pos = px;
         else pos = rp_pos<G, STRIDE>((px / WOUT) * STRIDE + dy, (px % WOUT) * STRIDE + dx);
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < kRpTerms; ++q)
           x[p][q] = *reinterpret_cast<const uint4 *>(terms + q * G::TERM + (g * G::NPP + pos) * 8);
       }
     };
     // software pipeline: chunk s + 1's LDS reads issued before chunk s's MFMAs (the scheduling barrier keeps
     // the compiler from hoisting every chunk's reads to the top, which would need 9 x the fragment registers)
-    uint4 xa[G::PTW][3], xb[G::PTW][3];
+    uint4 xa[G::PTW][kRpTerms], xb[G::PTW][kRpTerms];
     load_x(0, xa);
 #pragma unroll
     for (int s = 0; s < G::NCW; ++s) {
-      uint4(&xc)[G::PTW][3] = (s & 1) ? xb : xa;
-      uint4(&xn)[G::PTW][3] = (s & 1) ? xa : xb;
+      uint4(&xc)[G::PTW][kRpTerms] = (s & 1) ? xb : xa;
+      uint4(&xn)[G::PTW][kRpTerms] = (s & 1) ? xa : xb;
       if (s + 1 < G::NCW) load_x(s + 1, xn);
-      const uint4(&w)[3] = wr[s];
+      const uint4(&w)[kRpTerms] = wr[s];
 #pragma unroll
       for (int p = 0; p < G::PTW; ++p) {
-        // small terms first: w_l x_h, w_h x_l, w_m x_m, w_m x_h, w_h x_m, w_h x_h
+        // small terms first: w_l x_h, w_h x_l, w_h x_h
         bxf4 c = acc[p];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[2]), bx_as(xc[p][0]), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][2]), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(xc[p][1]), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[1]), bx_as(xc[p][0]), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][1]), c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(w[0]), bx_as(xc[p][0]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(rp_as(w[1]), rp_as(xc[p][0]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(rp_as(w[0]), rp_as(xc[p][1]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(rp_as(w[0]), rp_as(xc[p][0]), c, 0, 0, 0);
         acc[p] = c;
       }
       // the order within the chunk (left alone, the scheduler sinks chunk s + 1's fragment reads to the end of
       // chunk s and every chunk then waits out a full LDS latency): two pixel tiles, the reads first, then the
-      // MFMAs; four (64-channel layers, 96 fragment registers), half the reads after the first tile's MFMAs and
+      // MFMAs; four (64-channel layers, 64 fragment registers), half the reads after the first tile's MFMAs and
       // half after the third's, within the register file
       if constexpr (G::PTW == 2) {
-        if (s + 1 < G::NCW) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);  // DS reads
-        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);                      // MFMAs
+        if (s + 1 < G::NCW) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);                       // MFMAs
       } else if (s + 1 < G::NCW) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -451,7 +440,7 @@ __global__ __launch_bounds__(256) void repr_avgpool_kernel(const float *__restri
 }
 
 // ---- host side: packing
-// A-operand fragments of one convolution: W [cout][cin][3][3] (folded) -> [out tile][chunk][term][lane][8 bf16],
+// A-operand fragments of one convolution: W [cout][cin][3][3] (folded) -> [out tile][chunk][term][lane][8 fp16],
 // lane -> out channel 16 tile + (lane & 15), K = 8 (lane >> 4) + e within the chunk; chunk s = tap * (cin / 32)
 // + j with K -> in channel 32 j + ..., or (first layer, cin <= 7) chunk s with K = 32 s + ... = tap * cin + c.
 // Two weights stacked (the dual layer: W [64] then W3 [64]) give cout = 128.
@@ -471,9 +460,9 @@ inline void repr_pack(const float *W, int cout, int cin, bool im2col, float *out
             const int tap = s / (cin / 32), c = 32 * (s % (cin / 32)) + k;
             wv = W[(co * cin + c) * 9 + tap];
           }
-          uint16_t t[3];
-          bx_split(wv, t[0], t[1], t[2]);
-          for (int q = 0; q < 3; ++q) out[(((ot * nch + s) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+          const _Float16 h = (_Float16)wv, l = (_Float16)(wv - (float)h);  // the kernel's split, rp_split8
+          const uint16_t t[kRpTerms] = {__builtin_bit_cast(uint16_t, h), __builtin_bit_cast(uint16_t, l)};
+          for (int q = 0; q < kRpTerms; ++q) out[(((ot * nch + s) * kRpTerms + q) * 64 + lane) * 8 + e] = t[q];
         }
 }
 
@@ -481,7 +470,7 @@ inline void repr_pack(const float *W, int cout, int cin, bool im2col, float *out
 struct ReprLayout {
   int w1, b1, r1w1, r1b1, r1w2, r1b2, dw, db1, dw2, db2, r2w1, r2b1, r2w2, r2b2, total;
 };
-inline int repr_frag_floats(int cout, int nch) { return cout / 16 * nch * 3 * 64 * 4; }
+inline int repr_frag_floats(int cout, int nch) { return cout / 16 * nch * kRpTerms * 64 * 4; }
 inline ReprLayout repr_layout() {
   ReprLayout L;
   int o = 0;

@@ -196,8 +196,9 @@ def test_native_downsample_matches_float64_reference(kind, B, cin):
     3x3/2 shortcut, the 64-channel block, avg pool. B = 37: tiles of several images per workgroup, a ragged last
     round; B = 300: ~10 tiles per workgroup, every slot of the LDS-DMA ring reused several times; 3 and 7
     observation planes: the first layer's im2col over other channel counts. Three launches must agree bit for
-    bit (a DMA read before it lands would show as run-to-run differences). Tolerance: the split keeps f32-level
-    error — 2e-5 of the layer's magnitude (relative to max |ref|) and rtol 1e-4 elementwise."""
+    bit (a DMA read before it lands would show as run-to-run differences). Tolerance: the two-term fp16 split
+    keeps f32-level error — 2e-5 of the layer's magnitude (relative to max |ref|); the achieved ratio is
+    printed."""
     import torch.nn.functional as F
     from lightzero_amd.conv_infer import FoldedConvInitial
     from lightzero_amd.model_conv import atari_efficientzero_model, atari_muzero_model
@@ -236,5 +237,6 @@ def test_native_downsample_matches_float64_reference(kind, B, cin):
             x = F.avg_pool2d(x, 3, 2, 1)
     assert got.shape == x.shape == (B, 64, 8, 8)
     err = (got - x).abs()
+    print(f"downsample {kind} B={B} C={cin}: max |err| / max |ref| = {float(err.max() / x.abs().max()):.3e}")
     assert float(err.max()) <= 2e-5 * float(x.abs().max()), float(err.max() / x.abs().max())
     torch.testing.assert_close(got, x, rtol=1e-4, atol=2e-5 * float(x.abs().max()))

@@ -3,5 +3,5 @@
 set -e
 out=$1; shift
 mkdir -p $out
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_config5.py -k "downsample or folded_initial or conv_collect_step" > $out/t.log 2>&1
+timeout -k 10 400 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_gpu_config5.py -k "downsample or folded_initial or conv_collect_step" > $out/t.log 2>&1
 bash tools/repr_ab.sh $out/ab "$@"
