@@ -382,7 +382,7 @@ def mlp_flops_per_sim(H, A, F, V, res=True):
 
 def conv_flops_per_sim(model, B, device):
     """(all, matrix-pipe) FLOPs of one recurrent_inference row of the conv MuZeroModel / EfficientZeroModel
-    (torch FlopCounterMode at batch B: the convolutions are the trunk on the split-bf16 MFMA path, the
+    (torch FlopCounterMode at batch B: the convolutions are the trunk on the split-fp16 MFMA path, the
     Linears the head MLPs on the VALU). EfficientZero's reward LSTM, which the counter does not see inside
     nn.LSTM, is counted by hand as its gate GEMM, 2 x 4H x (K + H) per row (K = reward planes, H = 512),
     on the matrix pipe too (lzm_ez_lstm_step)."""
@@ -752,19 +752,25 @@ def check_step(step, S, fused):
 
 def conv_roofline(step, model, B, S, device):
     """configs 5 / 3: the dominant kernel, search_conv_kernel / search_conv_ez_kernel (one launch = B x S
-    simulations): the trunk's convolutions (and EZ's LSTM gate GEMM) run on the bf16 matrix pipe as
-    split-bf16 (three bf16 terms per f32 operand, six products per f32 product), so the
-    bound is the dense BF16 MFMA peak against 6x the algorithmic matrix FLOPs; the f32-equivalent rate
-    and the head MLPs (VALU) ride beside."""
+    simulations): the trunk's convolutions run on the fp16 matrix pipe as split-fp16 (two fp16 terms per f32
+    operand, three products per f32 product), EZ's LSTM gate GEMM on the bf16 pipe as
+    split-bf16 (three terms, six products), so the bound is the dense FP16/BF16 MFMA peak (the same 2.5 PF)
+    against 3x the convolutions' and 6x the gate GEMM's algorithmic FLOPs; the f32-equivalent rate and the
+    head MLPs (VALU) ride beside."""
     ms, dbar = kernel_timing(step)
     ez = "search_conv_ez" in ms
     key, kname = ("search_conv_ez", "search_conv_ez_kernel") if ez else ("search_conv", "search_conv_kernel")
     sec = ms[key] * 1e-3
     flops, conv = conv_flops_per_sim(model, B, device)
-    mfma = 6.0 * conv * B * S / sec / 1e12
+    gate = 0.0
+    if ez:
+        lstm = model.dynamics_network.lstm
+        gate = 2.0 * 4 * lstm.hidden_size * (lstm.input_size + lstm.hidden_size)
+    mfma = (3.0 * (conv - gate) + 6.0 * gate) * B * S / sec / 1e12
     f32 = flops * B * S / sec / 1e12
-    return {"bound": "mfma", "compute": "split-bf16 MFMA (v_mfma_f32_16x16x32_bf16, 6 products per f32 product) "
-                                        "for the conv trunk" + (" and the LSTM gate GEMM" if ez else "") +
+    return {"bound": "mfma", "compute": "split-fp16 MFMA (v_mfma_f32_16x16x32_f16, 3 products per f32 product) "
+                                        "for the conv trunk" + (", split-bf16 (v_mfma_f32_16x16x32_bf16, 6 products) "
+                                                                "for the LSTM gate GEMM" if ez else "") +
                                         "; head MLPs on the fp32 VALU",
             "kernel": kname, "achieved": round(mfma, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(mfma / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(kname),
@@ -969,7 +975,7 @@ def config3(args, device, cpu):
                        f"EfficientZeroModel (4x64x64 frames, latent 64x8x8, LSTM 512, support 101, 6 actions)",
            "step": "collect-time search (initial inference + prepare + search + root outputs)",
            "value": round(B * S * steps / el, 1), "unit": "sims/s", "ms_per_step": round(el / steps * 1e3, 4),
-           "steps": steps, "n_gpus": 1, "dtype": "f32 (convolutions as split-bf16 MFMA)",
+           "steps": steps, "n_gpus": 1, "dtype": "f32 (convolutions as split-fp16 MFMA)",
            "search_path": step.mcts.last_path, "tie_stream_errors": tie, "search_diag": sdiag,
            "data": "synthetic (random-init conv EfficientZeroModel, synthetic frames)",
            "roofline": conv_roofline(step, model, B, S, device)}

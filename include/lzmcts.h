@@ -360,11 +360,13 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
  * actmap float[A][64][64] (action planes' conv + dynamics bias), action int32[B];
  * outputs out_latent float[B][4096], out_r float[B][r_ch*64], out_h float[B][h_ch*64].
  * The unsuffixed entry points run the exact-f32 matrix path (LZM_CONV_F32); the _p forms take the
- * precision: LZM_CONV_F32 (v_mfma_f32_32x32x2_f32) or LZM_CONV_BF16X3 (each f32 operand split into
- * three bf16 terms, six products per K on v_mfma_f32_16x16x32_bf16: f32-level error at 2.7x fewer
- * matrix cycles). A blob packed for one precision must be run with the same precision. */
+ * precision: LZM_CONV_F32 (v_mfma_f32_32x32x2_f32) or LZM_CONV_SPLIT (each f32 operand split into two
+ * fp16 terms, three products per K on v_mfma_f32_16x16x32_f16: f32-level error, 2^-22 per operand, for
+ * values inside fp16's range; the EfficientZero LSTM gate GEMM keeps three bf16 terms). A blob packed for
+ * one precision must be run with the same precision. LZM_CONV_BF16X3 is the split precision's former name. */
 #define LZM_CONV_F32 0
-#define LZM_CONV_BF16X3 1
+#define LZM_CONV_SPLIT 1
+#define LZM_CONV_BF16X3 LZM_CONV_SPLIT
 int64_t lzm_conv_trunk_floats(int n_dres, int n_pres);
 int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const float *raw, float *out_host);
 int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights, const float *actmap,

@@ -26,8 +26,8 @@ counters), so captured HIP graphs keep valid pointers.
 
 On the GPU the convolutional trunk (dynamics conv, residual blocks, reward 1x1, prediction blocks,
 head 1x1) is ONE hand-written HIP launch per simulation, one workgroup per env with the
-activations in LDS and split-bf16 MFMA convolutions (csrc/lzm_conv.h, lzm_conv_trunk_p; each f32
-operand as three bf16 terms, six products per K — f32-level error on the bf16 matrix path; the
+activations in LDS and split-fp16 MFMA convolutions (csrc/lzm_conv.h, lzm_conv_trunk_p; each f32
+operand as two fp16 terms, three products per K — f32-level error on the fp16 matrix path; the
 exact-f32 MFMA kernel stays selectable, precision='f32'): it reads the leaf
 latent straight from the search's latent pool and writes the next latent straight into the next
 pool slot (`step_from_pool`), so the gather and the pool filing kernels disappear too. The head
@@ -156,13 +156,15 @@ def pack_heads(t, hv):
 class FoldedConvNet:
     """recurrent_inference of a conv MuZeroModel / EfficientZeroModel with every BN folded."""
 
-    PRECISIONS = {"f32": 0, "bf16x3": 1}  # LZM_CONV_F32 / LZM_CONV_BF16X3 (include/lzmcts.h)
+    PRECISIONS = {"f32": 0, "split": 1}  # LZM_CONV_F32 / LZM_CONV_SPLIT (include/lzmcts.h)
 
     def __init__(self, model, precision=None):
-        """precision of the native trunk: 'bf16x3' (default: f32 operands split into three bf16
-        terms, six products per K on the bf16 matrix path, f32-level error) or 'f32' (the exact
-        f32 matrix path); LZM_CONV_PRECISION overrides the default."""
-        precision = precision or os.environ.get("LZM_CONV_PRECISION", "bf16x3")
+        """precision of the native trunk: 'split' (default: f32 operands split into two fp16 terms,
+        three products per K on the fp16 matrix path, f32-level error; the EZ LSTM gate GEMM in three
+        bf16 terms) or 'f32' (the exact f32 matrix path); 'bf16x3' is the split precision's former
+        name; LZM_CONV_PRECISION overrides the default."""
+        precision = precision or os.environ.get("LZM_CONV_PRECISION", "split")
+        precision = "split" if precision == "bf16x3" else precision
         if precision not in self.PRECISIONS:
             raise ValueError(f"conv trunk precision {precision!r}: expected one of {sorted(self.PRECISIONS)}")
         self.precision = precision
@@ -179,7 +181,7 @@ class FoldedConvNet:
         self._lstm_ws = {}
         # EZ: the gate GEMM + cell as one split-bf16 launch (the f32 precision keeps rocBLAS + the cell
         # pass; LZM_LSTM_FUSED=0 too)
-        self.lstm_fused = precision == "bf16x3" and os.environ.get("LZM_LSTM_FUSED", "1") != "0"
+        self.lstm_fused = precision == "split" and os.environ.get("LZM_LSTM_FUSED", "1") != "0"
         self.refresh()
 
     def _version(self):
@@ -494,7 +496,7 @@ class FoldedConvInitial:
 
     def _tail_start(self):
         """index of the first op after the representation's last average pool when every op from there
-        on is a 64-channel residual block at 8 x 8 (the split-bf16 trunk's shape), else None"""
+        on is a 64-channel residual block at 8 x 8 (the split trunk's shape), else None"""
         pools = [i for i, op in enumerate(self.ops) if op[0] == "avgpool"]
         if not pools or tuple(self.model.latent_hw) != (8, 8):
             return None
@@ -507,7 +509,7 @@ class FoldedConvInitial:
 
     def _pack_native(self):
         """the 8 x 8 tail (representation blocks, prediction blocks, head 1x1) as one lzm_conv_resnet8_p
-        launch on the split-bf16 trunk kernel (LZM_CONV_INIT_NATIVE=0: the MIOpen convolutions)"""
+        launch on the split-fp16 trunk kernel (LZM_CONV_INIT_NATIVE=0: the MIOpen convolutions)"""
         t = self.t
         dev = t["head_w"].device
         i0 = self._tail_start()
@@ -550,7 +552,7 @@ class FoldedConvInitial:
 
     def _pack_repr(self, L, dev, i0):
         """the DownSample stages in front of the tail (conv 3x3/2 -> 32, a 32-channel block, the downsample block,
-        a 64-channel block, avg pool: common.py:164-265 at 64 x 64 frames) as lzm_repr_downsample's split-bf16
+        a 64-channel block, avg pool: common.py:164-265 at 64 x 64 frames) as lzm_repr_downsample's split-fp16
         launches (csrc/lzm_repr.h); LZM_REPR_NATIVE=0: MIOpen convolutions"""
         ops = self.ops[:i0]
         kinds = [op[0] for op in ops]
@@ -659,7 +661,7 @@ class FoldedConvInitial:
         native = self.native is not None and x.is_cuda
         pre = self.ops[:self.tail[0]] if native else self.ops
         if native and self.repr_native is not None and tuple(x.shape[1:]) == (self.repr_cin, 64, 64):
-            x = self._downsample_native(x)  # the DownSample stages in front of the tail, split-bf16 launches
+            x = self._downsample_native(x)  # the DownSample stages in front of the tail, split-fp16 launches
             pre = []
         for op in pre:
             kind = op[0]

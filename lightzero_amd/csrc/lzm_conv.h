@@ -216,33 +216,37 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Split-bf16 trunk (precision 1, the default): the same network on v_mfma_f32_16x16x32_bf16.
+// Split trunk (precision 1, the default): the same network on v_mfma_f32_16x16x32_f16.
 //
-// Every f32 operand x is held as three bf16 terms x = h + m + l (h = bf16(x), m = bf16(x - h),
-// l = bf16(x - h - m); each subtraction is exact, so h + m carries 16 significant bits and h + m + l
-// the full 24 in all but carry cases). A product is summed from the six terms whose magnitude is
-// >= 2^-16 of h_a h_b: l_a h_b, h_a l_b, m_a m_b, m_a h_b, h_a m_b, h_a h_b (the dropped m l, l m, l l
-// terms are <= 2^-24 relative: f32 round-off). The bf16 matrix rate is 16x the f32 one
-// (MI355X_MICROARCH.md constants: 16x16x32 bf16 16 cycles vs 32x32x2 f32 64 cycles, 16x the K), so
-// six products per K are 2.7x fewer matrix cycles than the exact-f32 kernel above.
+// Every f32 operand x is held as two fp16 terms x = h + l (h = fp16(x), l = fp16(x - h); the subtraction
+// is exact, so h + l carries 22 significant bits: |x - h - l| <= 2^-22 |x|). A product is summed from
+// the three terms l_a h_b, h_a l_b, h_a h_b (the dropped l l term is <= 2^-22 relative): f32-level
+// error for values inside fp16's range (|x| < 65504; below 2^-14 the terms are fp16 subnormals, an
+// absolute error of at most 2^-25). The fp16 matrix rate is 16x the f32 one (MI355X_MICROARCH.md
+// constants: 16x16x32 16 cycles vs 32x32x2 f32 64 cycles, 16x the K), so three products per K are
+// 5.3x fewer matrix cycles than the exact-f32 kernel above, and half those of the three-term bf16 split
+// (six products: l h, h l, m m, m h, h m, h h) this trunk ran through round 5, which the EfficientZero
+// LSTM gate GEMM (lzm_lstm.h) keeps: bx_split / bx_split_d below.
 //
 // Layout. Wave w owns out-channels 16w..16w+15 for all 64 pixels (four 16-pixel M tiles), so the four
 // waves stream disjoint weights (221 KB per 3x3 layer per workgroup, vs 295 KB when two waves of
 // the f32 tiling share a half). K = tap-major (9 taps) x 64 in-channels, in 18 chunks of 32.
-// Activations live in LDS as the three bf16 planes of each buffer, [100 bordered positions][64 ch],
+// Activations live in LDS as the two fp16 planes of each buffer, [100 bordered positions][64 ch],
 // 16-B chunk c of position ps stored at chunk c ^ ((ps % 10) & 7): the A-fragment reads (lane:
 // pixel l&15 of the tile, channels 8(l>>4)..+7 of the chunk, one ds_read_b128) are then
 // conflict-free for every tap (checked over the four lane groups of ds_read_b128).
-// B fragments come from the host-packed [wave][chunk][term][lane][8 bf16] layout, one 1 KiB
+// B fragments come from the host-packed [wave][chunk][term][lane][8 fp16] layout, one 1 KiB
 // dwordx4 wave-load per term, a ring of kBxRing chunks issued kBxAhead ahead.
-constexpr int kBxComp = 100 * 64;                  // bf16 per term plane
-constexpr int kBxBuf = 3 * kBxComp;                // bf16 per activation buffer (h, m, l); two buffers
-constexpr int kBx3Frag = 4 * 18 * 3 * 64 * 4;      // floats: [wave][chunk][term][lane][8 bf16]
-constexpr int kBx1Frag = 2 * 2 * 3 * 64 * 4;       // 1x1 64->32: [wave 0..1][chunk][term][lane][8 bf16]
+constexpr int kBxTerms = 2;                        // fp16 terms per f32 operand (h, l)
+constexpr int kBxComp = 100 * 64;                  // 16-bit elements per term plane
+constexpr int kBxBuf = kBxTerms * kBxComp;         // per activation buffer (h, l planes); two buffers
+constexpr int kBx3Frag = 4 * 18 * kBxTerms * 64 * 4;  // floats: [wave][chunk][term][lane][8 fp16]
+constexpr int kBx1Frag = 2 * 2 * kBxTerms * 64 * 4;   // 1x1 64->32: [wave 0..1][chunk][term][lane][8 fp16]
 constexpr int kBxBlock = 2 * kBx3Frag + 2 * kCvCh;
 constexpr int kBxAhead = 3;  // default weight read-ahead (chunks)
 
 typedef __bf16 bxv8 __attribute__((ext_vector_type(8)));
+typedef _Float16 bxh8 __attribute__((ext_vector_type(8)));
 typedef float bxf4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ inline uint16_t bx_rn(float x) {  // f32 -> bf16, round to nearest even (finite x)
@@ -264,7 +268,15 @@ __host__ __device__ inline void bx_split(float x, uint16_t &h, uint16_t &m, uint
   l = bx_rn(r - bx_f(m));
 }
 
-// the same split on the device with the hardware conversion (v_cvt_pk_bf16_f32, round to nearest even)
+// the trunk's split: x = h + l, h = fp16(x), l = fp16(x - h) (x - h exact in f32), round to nearest even
+__host__ __device__ inline void bx_split2(float x, uint16_t &h, uint16_t &l) {
+  const _Float16 hh = (_Float16)x;
+  const _Float16 ll = (_Float16)(x - (float)hh);
+  h = __builtin_bit_cast(uint16_t, hh);
+  l = __builtin_bit_cast(uint16_t, ll);
+}
+
+// the three-term bf16 split on the device with the hardware conversion (v_cvt_pk_bf16_f32, round to nearest even)
 __device__ __forceinline__ void bx_split_d(float x, uint16_t &h, uint16_t &m, uint16_t &l) {
   const __bf16 hb = (__bf16)x;
   const float r = x - (float)hb;
@@ -290,36 +302,36 @@ __host__ __device__ inline ConvTrunkLayout conv_trunk_layout_p(int n_dres, int n
   return L;
 }
 
-// element offset (bf16) of (bordered position ps, channel c) inside one term plane
+// element offset (16-bit elements) of (bordered position ps, channel c) inside one term plane
 __device__ __forceinline__ int bx_at(int ps, int c) { return ps * 64 + ((((c >> 3) ^ (ps % 10)) & 7) << 3) + (c & 7); }
 
 __device__ __forceinline__ float bx_load(const uint16_t *buf, int ps, int c) {
   const int o = bx_at(ps, c);
-  return (bx_f(buf[o]) + bx_f(buf[kBxComp + o])) + bx_f(buf[2 * kBxComp + o]);
+  return (float)__builtin_bit_cast(_Float16, buf[o]) + (float)__builtin_bit_cast(_Float16, buf[kBxComp + o]);
 }
 
 __device__ __forceinline__ void bx_store(uint16_t *buf, int ps, int c, float v) {
-  uint16_t h, m, l;
-  bx_split_d(v, h, m, l);
+  uint16_t h, l;
+  bx_split2(v, h, l);
   const int o = bx_at(ps, c);
   buf[o] = h;
-  buf[kBxComp + o] = m;
-  buf[2 * kBxComp + o] = l;
+  buf[kBxComp + o] = l;
 }
 
 __device__ __forceinline__ bxv8 bx_as(uint4 u) { return __builtin_bit_cast(bxv8, u); }
+__device__ __forceinline__ bxh8 bx_ash(uint4 u) { return __builtin_bit_cast(bxh8, u); }
 
-// Weight ring of one wave: RING chunks x 3 terms (one uint4 per lane each).
+// Weight ring of one wave: RING chunks x the terms (one uint4 per lane each).
 template <int AHEAD>
 struct BxRing {
-  uint4 w[AHEAD + 1][3];
+  uint4 w[AHEAD + 1][kBxTerms];
 };
 
 template <int AHEAD, int DIAG>
 __device__ __forceinline__ void bx_load_w(BxRing<AHEAD> &r, const uint4 *__restrict__ wf, int s, int lane) {
 #pragma unroll
-  for (int q = 0; q < 3; ++q)
-    r.w[s % (AHEAD + 1)][q] = DIAG == 1 ? uint4{(uint32_t)(lane + s), 1u, 2u, 3u} : wf[(s * 3 + q) * 64 + lane];
+  for (int q = 0; q < kBxTerms; ++q)
+    r.w[s % (AHEAD + 1)][q] = DIAG == 1 ? uint4{(uint32_t)(lane + s), 1u, 2u, 3u} : wf[(s * kBxTerms + q) * 64 + lane];
 }
 
 // a conv's first chunks of weights; issued early (before the previous layer's epilogue and barrier)
@@ -339,7 +351,7 @@ __device__ __forceinline__ void bx_prefetch(BxRing<AHEAD> &r, const uint4 *__res
 template <int NCH, int AHEAD, int DIAG, int S0 = 0>
 __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restrict__ wf, BxRing<AHEAD> &r, int lane,
                                         bxf4 (&acc)[4]) {
-  uint4 a[2][4][3];
+  uint4 a[2][4][kBxTerms];
   const int px = lane & 7, g = lane >> 4;
   // lane's pixel in tile t: p = 16t + (lane & 15), plane row py = 2t + ((lane >> 3) & 1), column px; tap
   // (dy, dx) reads bordered position (py + dy) * 10 + px + dx
@@ -352,7 +364,7 @@ __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restr
     for (int t = 0; t < 4; ++t) {
       const int ps = lbase + (2 * t + dy) * 10 + dx;
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < kBxTerms; ++q)
         a[s & 1][t][q] = *reinterpret_cast<const uint4 *>(in + q * kBxComp + ps * 64 + chunk * 8);
     }
   };
@@ -365,23 +377,17 @@ __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restr
     if (s + AHEAD < NCH) bx_load_w<AHEAD, DIAG>(r, wf, s + AHEAD, lane);
     if (s + 1 < NCH) load_a(s + 1);
     const uint4 *w = r.w[s % (AHEAD + 1)];
-    const uint4(&x)[4][3] = a[s & 1];
-    // small terms first: l_a h_b, h_a l_b, m_a m_b, m_a h_b, h_a m_b, h_a h_b
+    const uint4(&x)[4][kBxTerms] = a[s & 1];
+    // small terms first: l_a h_b, h_a l_b, h_a h_b
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(x[t][1]), bx_ash(w[0]), acc[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][0]), bx_as(w[2]), acc[t], 0, 0, 0);
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(x[t][0]), bx_ash(w[1]), acc[t], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][1]), bx_as(w[1]), acc[t], 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][1]), bx_as(w[0]), acc[t], 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][0]), bx_as(w[1]), acc[t], 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(x[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
+    for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(x[t][0]), bx_ash(w[0]), acc[t], 0, 0, 0);
     // issue the next chunks' loads in the MFMA gaps (an MFMA holds the vector issue for half its
     // cycles): weights first (they have the longest way), then one activation read per MFMA
-    const int nw = (s + AHEAD < NCH && DIAG != 1) ? 3 : 0, na = s + 1 < NCH ? 12 : 0;
+    const int nw = (s + AHEAD < NCH && DIAG != 1) ? kBxTerms : 0, na = s + 1 < NCH ? 4 * kBxTerms : 0;
 #pragma unroll
     for (int k = 0; k < nw; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
@@ -393,7 +399,7 @@ __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restr
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
     }
 #pragma unroll
-    for (int k = 0; k < 24 - nw - na; ++k) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    for (int k = 0; k < 12 - nw - na; ++k) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -414,7 +420,7 @@ __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out
                                              const float4 (&am)[NT], float (&xres)[4 * NT], bool add_res, bool keep,
                                              int lane, int c) {
   typedef float bxf2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 bxb2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 bxb2 __attribute__((ext_vector_type(2)));
   const int cb = c >> 3, odd = lane & 1;
 #pragma unroll
   for (int t = T0; t < T0 + NT; ++t) {
@@ -437,16 +443,13 @@ __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out
           float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
       const bxf2 pr = odd ? bxf2{recv, v[2 * k + 1]} : bxf2{v[2 * k], recv};  // (channel c & ~1, channel c | 1)
       const bxb2 h = __builtin_convertvector(pr, bxb2);
-      const bxf2 r1 = pr - __builtin_convertvector(h, bxf2);
-      const bxb2 m = __builtin_convertvector(r1, bxb2);
-      const bxb2 l = __builtin_convertvector(r1 - __builtin_convertvector(m, bxf2), bxb2);
+      const bxb2 l = __builtin_convertvector(pr - __builtin_convertvector(h, bxf2), bxb2);
       const int r = 2 * k + odd;
       const int ps = bx_ep_pos(lane, t, r);
       // swizzle key (ps % 10) & 7 = column + 1; the pair's dword at channel c & ~1
       const int o = ps * 64 + (((cb ^ (4 * ((lane >> 4) & 1) + r + 1)) & 7) << 3) + (c & 6);
       *reinterpret_cast<bxb2 *>(out + o) = h;
-      *reinterpret_cast<bxb2 *>(out + kBxComp + o) = m;
-      *reinterpret_cast<bxb2 *>(out + 2 * kBxComp + o) = l;
+      *reinterpret_cast<bxb2 *>(out + kBxComp + o) = l;
     }
   }
 }
@@ -458,7 +461,7 @@ __device__ __forceinline__ void bx_conv1_layer(const uint16_t *in, const float *
                                                const float *__restrict__ bias, int nch, float *dst, int lane,
                                                int wv) {
   BxRing<2> r1;
-  const uint4 *wf = reinterpret_cast<const uint4 *>(wl) + wv * 2 * 3 * 64;
+  const uint4 *wf = reinterpret_cast<const uint4 *>(wl) + wv * 2 * kBxTerms * 64;
   bx_prefetch<2, 2, DIAG>(r1, wf, lane);
   const int c = 16 * wv + (lane & 15);
   const float bc = c < nch ? bias[c] : 0.f;
@@ -503,7 +506,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const ConvTrunkLayout L = conv_trunk_layout_p(a.n_dres, a.n_pres, 1);
   const int n3 = 1 + 2 * a.n_dres + 2 * a.n_pres;
   auto layer_w = [&](int i) { return a.w + bx_layer_off(L, a.n_dres, i); };
-  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * 3 * 64; };
+  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   const int i0 = a.skip_dyn ? 1 : 0;  // the first layer run (skip_dyn: the first residual block's)
   BxRing<AHEAD> ring;
   bx_prefetch<18, AHEAD, DIAG>(ring, wave_stream(layer_w(i0)), lane);
@@ -525,7 +528,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     const float4 no_am[4] = {};
     bx_epilogue3<0, 4, false>(in4, buf(i0 & 1), 0.f, false, no_am, xres, false, false, lane, c);
   }
-  for (int k = tid; k < 2 * 3 * 36 * 8; k += kCvThreads) {  // [buffer][term][border position][16-B chunk]
+  for (int k = tid; k < 2 * kBxTerms * 36 * 8; k += kCvThreads) {  // [buffer][term][border position][16-B chunk]
     const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
     const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
     bx_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
@@ -584,7 +587,7 @@ __global__ __launch_bounds__(kBx2Threads) __attribute__((amdgpu_waves_per_eu(2, 
   const int n3 = 1 + 2 * a.n_dres + 2 * a.n_pres;
   auto layer_w = [&](int i) { return a.w + bx_layer_off(L, a.n_dres, i); };
   // this wave's chunk stream: group grp, chunks 9 kh ..
-  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + (grp * 18 + 9 * kh) * 3 * 64; };
+  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + (grp * 18 + 9 * kh) * kBxTerms * 64; };
   BxRing<AHEAD> ring;
   bx_prefetch<9, AHEAD, 0>(ring, wave_stream(a.w + L.dyn), lane);
   const float *src = a.pool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
@@ -657,9 +660,9 @@ inline void bx_pack3(const float *W, float *outf) {
       for (int lane = 0; lane < 64; ++lane)
         for (int e = 0; e < 8; ++e) {
           const int tap = s >> 1, j = s & 1, cin = 32 * j + 8 * (lane >> 4) + e, cout = 16 * w + (lane & 15);
-          uint16_t t[3];
-          bx_split(W[(cout * 64 + cin) * 9 + tap], t[0], t[1], t[2]);
-          for (int q = 0; q < 3; ++q) out[(((w * 18 + s) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+          uint16_t t[kBxTerms];
+          bx_split2(W[(cout * 64 + cin) * 9 + tap], t[0], t[1]);
+          for (int q = 0; q < kBxTerms; ++q) out[(((w * 18 + s) * kBxTerms + q) * 64 + lane) * 8 + e] = t[q];
         }
 }
 
@@ -671,9 +674,9 @@ inline void bx_pack1(const float *W, int n, float *outf) {
       for (int lane = 0; lane < 64; ++lane)
         for (int e = 0; e < 8; ++e) {
           const int cin = 32 * j + 8 * (lane >> 4) + e, cout = 16 * w + (lane & 15);
-          uint16_t t[3] = {0, 0, 0};
-          if (cout < n) bx_split(W[cout * 64 + cin], t[0], t[1], t[2]);
-          for (int q = 0; q < 3; ++q) out[(((w * 2 + j) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+          uint16_t t[kBxTerms] = {0, 0};
+          if (cout < n) bx_split2(W[cout * 64 + cin], t[0], t[1]);
+          for (int q = 0; q < kBxTerms; ++q) out[(((w * 2 + j) * kBxTerms + q) * 64 + lane) * 8 + e] = t[q];
         }
 }
 

@@ -2410,7 +2410,7 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
 
 
 int64_t lzm_conv_trunk_floats_p(int n_dres, int n_pres, int precision) {
-  if (n_dres < 0 || n_pres < 0 || n_dres > 8 || n_pres > 8 || (precision != LZM_CONV_F32 && precision != LZM_CONV_BF16X3))
+  if (n_dres < 0 || n_pres < 0 || n_dres > 8 || n_pres > 8 || (precision != LZM_CONV_F32 && precision != LZM_CONV_SPLIT))
     return -1;
   return conv_trunk_layout_p(n_dres, n_pres, precision).total;
 }
@@ -2424,7 +2424,7 @@ int lzm_conv_trunk_prepare_p(int precision, int n_dres, int n_pres, int r_ch, in
             "buffers");
     return LZM_ERR_ARG;
   }
-  const bool bx = precision == LZM_CONV_BF16X3;
+  const bool bx = precision == LZM_CONV_SPLIT;
   const ConvTrunkLayout L = conv_trunk_layout_p(n_dres, n_pres, precision);
   const int frag3 = bx ? kBx3Frag : kCv3Frag, block = bx ? kBxBlock : kCvBlock;
   auto pack3 = [&](const float *W, float *o) { bx ? bx_pack3(W, o) : conv_pack3(W, o); };
@@ -2470,8 +2470,8 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
     return LZM_ERR_ARG;
   }
   float *out_r = xin;
-  const bool bx = precision == LZM_CONV_BF16X3;
-  // split-bf16 variants: weight read-ahead depth (LZM_CONV_AHEAD) and timing-only ablations
+  const bool bx = precision == LZM_CONV_SPLIT;
+  // split trunk variants: weight read-ahead depth (LZM_CONV_AHEAD) and timing-only ablations
   // (LZM_CONV_DIAG=1: no weight loads; results invalid)
   typedef void (*bx_fn)(ConvTrunkArgs);
   static const int ahead = getenv("LZM_CONV_AHEAD") ? atoi(getenv("LZM_CONV_AHEAD")) : kBxAhead;
@@ -2523,7 +2523,7 @@ int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int
 
 int lzm_conv_resnet8_p(int B, int n_blocks, int n_pres, int h_ch, const float *weights, const float *in,
                        float *out_latent, float *out_h, void *stream) {
-  if (B <= 0 || n_blocks < 1 || lzm_conv_trunk_floats_p(n_blocks, n_pres, LZM_CONV_BF16X3) < 0 || h_ch < 1 ||
+  if (B <= 0 || n_blocks < 1 || lzm_conv_trunk_floats_p(n_blocks, n_pres, LZM_CONV_SPLIT) < 0 || h_ch < 1 ||
       h_ch > 32 || !weights || !in || !out_latent || !out_h || (((uintptr_t)weights | (uintptr_t)in) & 15)) {
     set_err("lzm_conv_resnet8_p: bad arguments (1..8 blocks, 1..32 head channels, 16-byte aligned weights / input)");
     return LZM_ERR_ARG;
@@ -2773,7 +2773,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.rec_x = rec_x; p.rec_a = rec_a; p.rec_len = rec_len; p.rec_dec = rec_decoded; p.rec_logits = rec_logits;
   p.step_count = h->step_count; p.step_base = h->step_base; p.step_inc = h->step_inc; p.step_fresh = h->step_fresh;
   p.step_delta = h->step_delta; p.out_dist = h->step_dist; p.out_values = h->step_vals;
-  // dynamic LDS plan (float offsets, 16-B aligned): the two split-bf16 activation buffers first
+  // dynamic LDS plan (float offsets, 16-B aligned): the two split-fp16 activation buffers first
   size_t o = (size_t)2 * kBxBuf / 2;
   p.off_stat = (int)o; o += (size_t)h->cap * 4;
   p.off_meta = (int)o; o += (size_t)h->cap * 4;

@@ -10,7 +10,7 @@
 //      the walk first runs draw-free, publishes the depth in a {epoch, depth} flag and, only when a
 //      draw value is needed, looks back over its predecessors' flags (lzm_traverse_lb.h's scheme,
 //      inside the persistent kernel);
-//   2. the four waves run the split-bf16 MFMA trunk (lzm_conv.h: dynamics conv + action map,
+//   2. the four waves run the split-fp16 MFMA trunk (lzm_conv.h: dynamics conv + action map,
 //      residual blocks, reward 1x1, prediction blocks, value/policy 1x1) from the leaf's parent
 //      latent pool[x][b] (HBM: every expanded node's latent is 16 KB, written by this workgroup in an
 //      earlier simulation, so it is an L2 hit on this XCD) and file the next latent in pool[k+1][b];
@@ -55,7 +55,7 @@ struct ConvSearchArgs {
   const int32_t *vtp_in;  // [B]
   float4 *minmax;         // [B]
   float *pool;            // [S+1][B][4096]
-  // trunk (split-bf16 layout, lzm_conv_trunk_prepare_p) and heads (lzm_heads.h layouts)
+  // trunk (split-fp16 layout, lzm_conv_trunk_prepare_p) and heads (lzm_heads.h layouts)
   const float *w, *actmap;
   int n_dres, n_pres, r_ch, h_ch;
   const float *w1t, *b1, *w2q, *b2;  // w2q: the output layer as [8][N2][4] (k4-major float4s, 16-B aligned)
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
   }
   if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
-  for (int k = tid; k < 2 * 3 * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
+  for (int k = tid; k < 2 * kBxTerms * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
     const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
     const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
     sc_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
@@ -464,7 +464,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const ConvTrunkLayout L = conv_trunk_layout_p(p.n_dres, p.n_pres, 1);
   const int n3 = 1 + 2 * p.n_dres + 2 * p.n_pres;
   auto layer_w = [&](int i) { return p.w + bx_layer_off(L, p.n_dres, i); };
-  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * 3 * 64; };
+  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   BxRing<AHEAD> ring;
 
   for (int k = 0; k < S; ++k) {
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   }
   if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
   auto zero_borders = [&]() {
-    for (int k = tid; k < 2 * 3 * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
+    for (int k = tid; k < 2 * kBxTerms * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
       const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
       const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
       sc_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
@@ -846,7 +846,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const ConvTrunkLayout L = conv_trunk_layout_p(p.n_dres, p.n_pres, 1);
   const int n3 = 1 + 2 * p.n_dres + 2 * p.n_pres;
   auto layer_w = [&](int i) { return p.w + bx_layer_off(L, p.n_dres, i); };
-  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * 3 * 64; };
+  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   BxRing<AHEAD> ring;
 
   for (int k = 0; k < S; ++k) {

@@ -276,7 +276,7 @@ class MuZeroMCTSCtree(object):
         return packed, dims
 
     def _fused_conv(self, model, t, shape):
-        """The native split-bf16 FoldedConvNet when the whole search can run as one lzm_search_conv
+        """The native split-precision FoldedConvNet when the whole search can run as one lzm_search_conv
         launch (conv MuZeroModel, 64 x 8 x 8 latent, packed heads with K multiples of 128, one root
         per CU); None otherwise (the generic per-simulation path). cfg.fused_search (default on) and
         LZM_FUSED_CONV=0 turn it off."""
@@ -286,7 +286,7 @@ class MuZeroMCTSCtree(object):
             return None
         net = _step_net(self, model)
         hp = getattr(net, "heads", None)
-        if getattr(net, "native", None) is None or hp is None or getattr(net, "precision", None) != "bf16x3" \
+        if getattr(net, "native", None) is None or hp is None or getattr(net, "precision", None) != "split" \
                 or getattr(net, "ez", True):
             return None
         if hp["Kr"] % 128 or hp["Khd"] % 128 or hp["off_policy"] % 128 or hp["A"] != t.A:
@@ -536,7 +536,7 @@ class EfficientZeroMCTSCtree(object):
         return ez_tree.Roots(active_collect_env_num, legal_actions, fast_rng=(cls.rng_mode == 'philox'))
 
     def _fused_conv(self, model, t, shape, Hl):
-        """The native split-bf16 FoldedConvNet (with the fused LSTM step packed) when the whole search
+        """The native split-precision FoldedConvNet (with the fused LSTM step packed) when the whole search
         can run as one lzm_search_conv_ez launch: conv EfficientZeroModel, 64 x 8 x 8 latent, head K
         multiples of 128, LSTM width a multiple of 128, max(B, 2 T) workgroups co-resident (T = ceil(B / 64)
         * H / 16 LSTM tiles); None otherwise (the generic per-simulation path). cfg.fused_search (default
@@ -550,7 +550,7 @@ class EfficientZeroMCTSCtree(object):
             return None
         net = _step_net(self, model)
         hp = getattr(net, "heads", None)
-        if getattr(net, "native", None) is None or hp is None or getattr(net, "precision", None) != "bf16x3" \
+        if getattr(net, "native", None) is None or hp is None or getattr(net, "precision", None) != "split" \
                 or not getattr(net, "ez", False) or getattr(net, "lstm_frag", None) is None:
             return None
         if hp["Khd"] % 128 or hp["off_policy"] % 128 or hp["A"] != t.A or hp["Kr"] != Hl \

@@ -202,7 +202,7 @@ class DeviceTree:
     def search_conv(self, net, S, minmax, seeds, vtp_in, pool, pb_c_base=19652, pb_c_init=1.25, discount=0.997,
                     categorical=True, rec=None, stream=None):
         """One launch for the whole search of a conv MuZeroModel (lzm_search_conv; net: a native
-        split-bf16 conv_infer.FoldedConvNet); rec: optional _Recorder-like object."""
+        split-precision conv_infer.FoldedConvNet); rec: optional _Recorder-like object."""
         r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n)))
         hp = net.heads
         self._unchecked = True
@@ -215,7 +215,7 @@ class DeviceTree:
     def search_conv_ez(self, net, S, minmax, seeds, vtp_in, pool, hpool, cpool, horizon, pb_c_base=19652,
                        pb_c_init=1.25, discount=0.997, categorical=True, rec=None, stream=None):
         """One launch for the whole search of a conv EfficientZeroModel (lzm_search_conv_ez; net: a native
-        split-bf16 conv_infer.FoldedConvNet with the fused LSTM step packed); hpool / cpool: the LSTM
+        split-precision conv_infer.FoldedConvNet with the fused LSTM step packed); hpool / cpool: the LSTM
         state pools [S + 1, B, H] with slot 0 = the roots' state; rec: optional _Recorder-like object
         (with is_reset)."""
         r = (lambda n: None) if rec is None else (lambda n: ptr(getattr(rec, n, None)))

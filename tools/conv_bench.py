@@ -53,8 +53,8 @@ def main():
     ap.add_argument("--searches", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--graph", type=int, default=1)
-    ap.add_argument("--precision", choices=["bf16x3", "f32"], default=None,
-                    help="native conv trunk precision (default: LZM_CONV_PRECISION or bf16x3)")
+    ap.add_argument("--precision", choices=["split", "f32"], default=None,
+                    help="native conv trunk precision (default: LZM_CONV_PRECISION or split)")
     ap.add_argument("--fused", type=int, default=1,
                     help="the one-launch search (lzm_search_conv / lzm_search_conv_ez) when it applies; 0: the generic path")
     ap.add_argument("--rng", choices=["glibc", "philox"], default="glibc",
@@ -64,7 +64,8 @@ def main():
     a = ap.parse_args()
     if a.precision:
         os.environ["LZM_CONV_PRECISION"] = a.precision
-    precision = os.environ.get("LZM_CONV_PRECISION", "bf16x3")
+    precision = os.environ.get("LZM_CONV_PRECISION", "split")
+    precision = "split" if precision == "bf16x3" else precision
     dev = torch.device("cuda", 0)
     B, S = a.envs, a.sims
     torch.manual_seed(0)
@@ -111,8 +112,13 @@ def main():
              mcts._fused_conv(model, roots.tree, (64, 8, 8), model.lstm_hidden_size)) is not None
     flops, matrix = recurrent_flops(model, a.kind, B, dev)
     net_tflops = flops * B * S / dt / 1e12
-    split = precision == "bf16x3"
-    mfma = (6.0 if split else 1.0) * matrix * B * S / dt / 1e12
+    split = precision == "split"
+    # split: the trunk's convolutions at 3 fp16 products per f32 product, EZ's LSTM gate GEMM at 6 bf16 ones
+    gate = 0.0
+    if a.kind == "ez":
+        lstm = model.dynamics_network.lstm
+        gate = 2.0 * 4 * lstm.hidden_size * (lstm.input_size + lstm.hidden_size)
+    mfma = ((3.0 * (matrix - gate) + 6.0 * gate) if split else matrix) * B * S / dt / 1e12
     peak = BF16_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS
     cpu = None
     if a.cpu_baseline_secs > 0:
