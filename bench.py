@@ -752,25 +752,19 @@ def check_step(step, S, fused):
 
 def conv_roofline(step, model, B, S, device):
     """configs 5 / 3: the dominant kernel, search_conv_kernel / search_conv_ez_kernel (one launch = B x S
-    simulations): the trunk's convolutions run on the fp16 matrix pipe as split-fp16 (two fp16 terms per f32
-    operand, three products per f32 product), EZ's LSTM gate GEMM on the bf16 pipe as
-    split-bf16 (three terms, six products), so the bound is the dense FP16/BF16 MFMA peak (the same 2.5 PF)
-    against 3x the convolutions' and 6x the gate GEMM's algorithmic FLOPs; the f32-equivalent rate and the
+    simulations): the trunk's convolutions and EZ's LSTM gate GEMM run on the fp16 matrix pipe as split-fp16
+    (two fp16 terms per f32 operand, three products per f32 product), so the bound is the dense
+    FP16 MFMA peak (2.5 PF, as BF16) against 3x the algorithmic matrix FLOPs; the f32-equivalent rate and the
     head MLPs (VALU) ride beside."""
     ms, dbar = kernel_timing(step)
     ez = "search_conv_ez" in ms
     key, kname = ("search_conv_ez", "search_conv_ez_kernel") if ez else ("search_conv", "search_conv_kernel")
     sec = ms[key] * 1e-3
     flops, conv = conv_flops_per_sim(model, B, device)
-    gate = 0.0
-    if ez:
-        lstm = model.dynamics_network.lstm
-        gate = 2.0 * 4 * lstm.hidden_size * (lstm.input_size + lstm.hidden_size)
-    mfma = (3.0 * (conv - gate) + 6.0 * gate) * B * S / sec / 1e12
+    mfma = 3.0 * conv * B * S / sec / 1e12
     f32 = flops * B * S / sec / 1e12
     return {"bound": "mfma", "compute": "split-fp16 MFMA (v_mfma_f32_16x16x32_f16, 3 products per f32 product) "
-                                        "for the conv trunk" + (", split-bf16 (v_mfma_f32_16x16x32_bf16, 6 products) "
-                                                                "for the LSTM gate GEMM" if ez else "") +
+                                        "for the conv trunk" + (" and the LSTM gate GEMM" if ez else "") +
                                         "; head MLPs on the fp32 VALU",
             "kernel": kname, "achieved": round(mfma, 2), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(mfma / BF16_PEAK_TFLOPS, 4), "traffic": pmc_traffic(kname),

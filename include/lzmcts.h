@@ -362,8 +362,8 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
  * The unsuffixed entry points run the exact-f32 matrix path (LZM_CONV_F32); the _p forms take the
  * precision: LZM_CONV_F32 (v_mfma_f32_32x32x2_f32) or LZM_CONV_SPLIT (each f32 operand split into two
  * fp16 terms, three products per K on v_mfma_f32_16x16x32_f16: f32-level error, 2^-22 per operand, for
- * values inside fp16's range; the EfficientZero LSTM gate GEMM keeps three bf16 terms). A blob packed for
- * one precision must be run with the same precision. LZM_CONV_BF16X3 is the split precision's former name. */
+ * values inside fp16's range; the EfficientZero LSTM gate GEMM on the same split). A blob packed for one
+ * precision must be run with the same precision. LZM_CONV_BF16X3 is the split precision's former name. */
 #define LZM_CONV_F32 0
 #define LZM_CONV_SPLIT 1
 #define LZM_CONV_BF16X3 LZM_CONV_SPLIT

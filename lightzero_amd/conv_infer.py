@@ -33,7 +33,7 @@ latent straight from the search's latent pool and writes the next latent straigh
 pool slot (`step_from_pool`), so the gather and the pool filing kernels disappear too. The head
 MLPs (reward, value, policy; both layers, ReLUs, the EZ value-prefix BatchNorm) are ONE more
 launch (csrc/lzm_heads.h, lzm_conv_heads); the EfficientZero reward LSTM (gate GEMM + cell) one
-split-bf16 launch (csrc/lzm_lstm.h, lzm_ez_lstm_step). The one-launch searches (lzm_search_conv,
+split-fp16 launch (csrc/lzm_lstm.h, lzm_ez_lstm_step). The one-launch searches (lzm_search_conv,
 lzm_search_conv_ez) run all of it inside the search kernel.
 """
 import os
@@ -160,8 +160,8 @@ class FoldedConvNet:
 
     def __init__(self, model, precision=None):
         """precision of the native trunk: 'split' (default: f32 operands split into two fp16 terms,
-        three products per K on the fp16 matrix path, f32-level error; the EZ LSTM gate GEMM in three
-        bf16 terms) or 'f32' (the exact f32 matrix path); 'bf16x3' is the split precision's former
+        three products per K on the fp16 matrix path, f32-level error; the EZ LSTM gate GEMM too) or
+        'f32' (the exact f32 matrix path); 'bf16x3' is the split precision's former
         name; LZM_CONV_PRECISION overrides the default."""
         precision = precision or os.environ.get("LZM_CONV_PRECISION", "split")
         precision = "split" if precision == "bf16x3" else precision
@@ -179,7 +179,7 @@ class FoldedConvNet:
         self.native = None  # device weight blob of lzm_conv_trunk (GPU models with a 64x8x8 latent)
         self.lstm_frag = None  # EZ: the gate-weight fragments of lzm_ez_lstm_step and lzm_search_conv_ez
         self._lstm_ws = {}
-        # EZ: the gate GEMM + cell as one split-bf16 launch (the f32 precision keeps rocBLAS + the cell
+        # EZ: the gate GEMM + cell as one split-fp16 launch (the f32 precision keeps rocBLAS + the cell
         # pass; LZM_LSTM_FUSED=0 too)
         self.lstm_fused = precision == "split" and os.environ.get("LZM_LSTM_FUSED", "1") != "0"
         self.refresh()
@@ -241,7 +241,7 @@ class FoldedConvNet:
                         self.heads[k].copy_(v)
 
     def _pack_lstm(self, L):
-        """lzm_ez_lstm_step's split-bf16 fragments of the LSTM gate weights [4H, K] (EZ), or None
+        """lzm_ez_lstm_step's split-fp16 fragments of the LSTM gate weights [4H, K] (EZ), or None
         (MuZero, or a shape the fused gate GEMM + cell kernel does not take)."""
         if not self.ez or "lstm_w" not in self.t:
             return None
@@ -312,7 +312,7 @@ class FoldedConvNet:
         h1 = torch.empty((B, H), dtype=torch.float32, device=r.device)
         c1 = torch.empty_like(h1)
         if self.lstm_frag is not None and self.lstm_fused:
-            # the gate GEMM and the cell in one launch (split-bf16 MFMA, csrc/lzm_lstm.h)
+            # the gate GEMM and the cell in one launch (split-fp16 MFMA, csrc/lzm_lstm.h)
             ws, werr = self._lstm_workspace(B, H, xin.device)
             _lib.call("lzm_ez_lstm_step", B, Kr + H, H, P(xin), P(self.lstm_frag), P(t["lstm_b"]), P(cpool), P(x),
                       P(search_len), int(horizon), P(h1), P(c1), P(hpool[k + 1]), P(cpool[k + 1]), P(ws),

@@ -225,8 +225,8 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 // absolute error of at most 2^-25). The fp16 matrix rate is 16x the f32 one (MI355X_MICROARCH.md
 // constants: 16x16x32 16 cycles vs 32x32x2 f32 64 cycles, 16x the K), so three products per K are
 // 5.3x fewer matrix cycles than the exact-f32 kernel above, and half those of the three-term bf16 split
-// (six products: l h, h l, m m, m h, h m, h h) this trunk ran through round 5, which the EfficientZero
-// LSTM gate GEMM (lzm_lstm.h) keeps: bx_split / bx_split_d below.
+// (six products: l h, h l, m m, m h, h m, h h) this trunk ran through round 5 (bx_split / bx_split_d
+// below, kept for tests and comparisons).
 //
 // Layout. Wave w owns out-channels 16w..16w+15 for all 64 pixels (four 16-pixel M tiles), so the four
 // waves stream disjoint weights (221 KB per 3x3 layer per workgroup, vs 295 KB when two waves of

@@ -2994,7 +2994,7 @@ extern "C" int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *c
 
 extern "C" int64_t lzm_ez_lstm_frag_floats(int K, int H) {
   if (K <= 0 || H <= 0 || K % kLsKc || H % kLsUnits) return -1;
-  return (int64_t)K * 4 * H * 3 / 2;
+  return (int64_t)K * 4 * H * kLsTerms / 2;
 }
 
 extern "C" int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out) {

@@ -69,14 +69,14 @@ __global__ __launch_bounds__(256) void ez_lstm_cell_kernel(int B, int H, const f
   }
 }
 
-// ---- the gate GEMM and the cell in one launch, on split-bf16 MFMA (lzm_conv.h's bf16x3 scheme)
+// ---- the gate GEMM and the cell in one launch, on split-fp16 MFMA (lzm_conv.h's split scheme)
 //
 // gates = xin W^T + b is M = B rows x N = 4H columns x K; rocBLAS ran it in f32 (16 us at Pong's
 // 256 x 2048 x 1536) and the cell was a second pass over the gates in HBM. Here a tile is 64 rows
 // (envs) x 16 hidden units, i.e. the 64 gate columns {i, f, g, o} x 16 units, so the cell runs in the
-// GEMM's epilogue from registers. Operands: each f32 value is held as h + m + l (three bf16 terms,
-// exact splits) and every product is summed from the six terms >= 2^-16 of h.h
-// (v_mfma_f32_16x16x32_bf16), as in the conv trunk.
+// GEMM's epilogue from registers. Operands: each f32 value is held as h + l (two fp16 terms, an exact
+// split: 22 significand bits) and every product is summed from the three terms l.h, h.l, h.h
+// (v_mfma_f32_16x16x32_f16), as in the conv trunk.
 //   * 512 threads, two waves per SIMD: wave w owns column tile w & 3 (units 4 (w & 3) .. + 3, column
 //     4 u + gate) and row half w >> 2 (two 16-row tiles). The four gates of a (row, unit) then sit in
 //     the four lanes of a quad, and one DPP broadcast per gate hands them to the lane that writes it.
@@ -85,9 +85,9 @@ __global__ __launch_bounds__(256) void ez_lstm_cell_kernel(int B, int H, const f
 //     raises a flag, the lower half adds them (lower + upper) and runs the cell. 256 workgroups at
 //     B = 256 (every CU), 126 MB of L2 reads instead of 201 MB for 64 x 32 tiles without the split.
 //   * Per 64-K stage both operands go through LDS, double-buffered, one barrier per stage: xin rows
-//     are loaded as f32 and split on the fly ([term][row][64 K] bf16, 16-B chunk c of row r at
+//     are loaded as f32 and split on the fly ([term][row][64 K] fp16, 16-B chunk c of row r at
 //     c ^ (r & 7)); W comes pre-split from the host in MFMA fragment order
-//     ([n-block][column tile][32-K chunk][term][lane][8 bf16], copied as is). Global loads run two
+//     ([n-block][column tile][32-K chunk][term][lane][8 fp16], copied as is). Global loads run two
 //     stages ahead.
 //   * Tiles are mapped XCD by XCD (block id % 8 = XCD), whole n-blocks per XCD, so an XCD's L2 holds
 //     its slice of W and every row of xin.
@@ -99,10 +99,11 @@ constexpr int kLsRows = 64;                      // rows (envs) per tile
 constexpr int kLsUnits = 16;                     // hidden units per tile (64 gate columns)
 constexpr int kLsKc = 64;                        // K per LDS stage
 constexpr int kLsThreads = 512;
-constexpr int kLsPlane = kLsRows * kLsKc;        // bf16 per A term plane
-constexpr int kLsABuf = 3 * kLsPlane;            // bf16: A stage (three planes)
-constexpr int kLsBBuf = 2 * 4 * 3 * 64 * 8;      // bf16: B stage [chunk 2][col tile 4][term 3][lane][8]
-constexpr int kLsStage = kLsABuf + kLsBBuf;      // bf16 per stage buffer
+constexpr int kLsTerms = 2;                      // fp16 terms per f32 operand
+constexpr int kLsPlane = kLsRows * kLsKc;        // 16-bit elements per A term plane
+constexpr int kLsABuf = kLsTerms * kLsPlane;     // A stage (the term planes)
+constexpr int kLsBBuf = 2 * 4 * kLsTerms * 64 * 8;  // B stage [chunk 2][col tile 4][term][lane][8]
+constexpr int kLsStage = kLsABuf + kLsBBuf;      // 16-bit elements per stage buffer
 constexpr int kLsLdsBytes = 2 * kLsStage * 2;    // two stage buffers
 constexpr int kLsPartFloats = kLsThreads * 8;    // one tile's partial sums (8 per thread)
 
@@ -132,9 +133,10 @@ inline void ls_pack(const float *W, int K, int H, float *outf) {
           for (int e = 0; e < 8; ++e) {
             const int n = lane & 15, unit = kLsUnits * nb + 4 * w + (n >> 2), gate = n & 3;
             const int k = 32 * j + 8 * (lane >> 4) + e;
-            uint16_t t[3];
-            bx_split(W[((size_t)gate * H + unit) * K + k], t[0], t[1], t[2]);
-            for (int q = 0; q < 3; ++q) out[((((size_t)(nb * 4 + w) * nch + j) * 3 + q) * 64 + lane) * 8 + e] = t[q];
+            uint16_t t[kLsTerms];
+            bx_split2(W[((size_t)gate * H + unit) * K + k], t[0], t[1]);
+            for (int q = 0; q < kLsTerms; ++q)
+              out[((((size_t)(nb * 4 + w) * nch + j) * kLsTerms + q) * 64 + lane) * 8 + e] = t[q];
           }
 }
 
@@ -169,52 +171,50 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
   const int sr = tid >> 3, sseg = tid & 7;
   const bool srow = row0 + sr < B;
   const float4 *asrc = reinterpret_cast<const float4 *>(p.xin + (size_t)(srow ? row0 + sr : 0) * K + k0) + 2 * sseg;
-  const uint4 *bsrc = p.wf + (size_t)nb * 4 * nch * 3 * 64;  // [col tile][chunk][term][lane]
+  const uint4 *bsrc = p.wf + (size_t)nb * 4 * nch * kLsTerms * 64;  // [col tile][chunk][term][lane]
   // staging registers of two stages (native vector types: HIP's uint4 / float4 structs kept these
   // arrays in scratch)
   typedef unsigned ls_u4 __attribute__((ext_vector_type(4)));
   typedef float ls_f4 __attribute__((ext_vector_type(4)));
   ls_f4 va0[2], va1[2];
-  ls_u4 vb0[3], vb1[3];
+  ls_u4 vb0[kLsTerms], vb1[kLsTerms];
   const ls_u4 *bsrc4 = reinterpret_cast<const ls_u4 *>(bsrc);
   const ls_f4 *asrc4 = reinterpret_cast<const ls_f4 *>(asrc);
-  auto load_stage = [&](int s, ls_f4(&VA)[2], ls_u4(&VB)[3]) __attribute__((always_inline)) {
+  // B stage = [chunk c][col tile][term][lane]: element e = tid + 512 u of 2 x 4 x kLsTerms x 64 uint4s
+  constexpr int kBc = 4 * kLsTerms * 64, kBt = kLsTerms * 64;  // uint4s per chunk, per column tile
+  static_assert(2 * kBc == kLsTerms * kLsThreads, "B stage: kLsTerms uint4s per thread");
+  auto load_stage = [&](int s, ls_f4(&VA)[2], ls_u4(&VB)[kLsTerms]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) VA[u] = srow ? asrc4[s * (kLsKc / 4) + u] : ls_f4{0.f, 0.f, 0.f, 0.f};
-    // B stage = [chunk c][col tile][term][lane]: element e = tid + 512 u of 1536 uint4s
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int e = tid + kLsThreads * u, c = e / 768, r = e - c * 768, tl = r / 192, rest = r - tl * 192;
+    for (int u = 0; u < kLsTerms; ++u) {
+      const int e = tid + kLsThreads * u, c = e / kBc, r = e - c * kBc, tl = r / kBt, rest = r - tl * kBt;
       const int j = (k0 / 32) + 2 * s + c;
-      VB[u] = bsrc4[((size_t)tl * nch + j) * 192 + rest];
+      VB[u] = bsrc4[((size_t)tl * nch + j) * kBt + rest];
     }
   };
-  auto store_stage = [&](int bsel, const ls_f4(&VA)[2], const ls_u4(&VB)[3]) __attribute__((always_inline)) {
+  auto store_stage = [&](int bsel, const ls_f4(&VA)[2], const ls_u4(&VB)[kLsTerms]) __attribute__((always_inline)) {
     typedef float f2 __attribute__((ext_vector_type(2)));
-    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-    uint32_t h[4], m[4], l[4];
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    uint32_t h[4], l[4];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const f2 pr[2] = {f2{VA[u][0], VA[u][1]}, f2{VA[u][2], VA[u][3]}};
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
-        const b2 hh = __builtin_convertvector(pr[v], b2);
-        const f2 r1 = pr[v] - __builtin_convertvector(hh, f2);
-        const b2 mm = __builtin_convertvector(r1, b2);
-        const b2 ll = __builtin_convertvector(r1 - __builtin_convertvector(mm, f2), b2);
+        const h2 hh = __builtin_convertvector(pr[v], h2);
+        const h2 ll = __builtin_convertvector(pr[v] - __builtin_convertvector(hh, f2), h2);
         h[2 * u + v] = __builtin_bit_cast(uint32_t, hh);
-        m[2 * u + v] = __builtin_bit_cast(uint32_t, mm);
         l[2 * u + v] = __builtin_bit_cast(uint32_t, ll);
       }
     }
     uint16_t *abuf = lds + bsel * kLsStage;
     uint16_t *base = abuf + sr * kLsKc + ((sseg ^ (sr & 7)) & 7) * 8;
     *reinterpret_cast<uint4 *>(base) = uint4{h[0], h[1], h[2], h[3]};
-    *reinterpret_cast<uint4 *>(base + kLsPlane) = uint4{m[0], m[1], m[2], m[3]};
-    *reinterpret_cast<uint4 *>(base + 2 * kLsPlane) = uint4{l[0], l[1], l[2], l[3]};
+    *reinterpret_cast<uint4 *>(base + kLsPlane) = uint4{l[0], l[1], l[2], l[3]};
     ls_u4 *bbuf = reinterpret_cast<ls_u4 *>(abuf + kLsABuf);
 #pragma unroll
-    for (int u = 0; u < 3; ++u) bbuf[tid + kLsThreads * u] = VB[u];
+    for (int u = 0; u < kLsTerms; ++u) bbuf[tid + kLsThreads * u] = VB[u];
   };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -239,39 +239,32 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
     const uint4 *bbuf = reinterpret_cast<const uint4 *>(abuf + kLsABuf);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      uint4 a[2][3], w[3];
+      uint4 a[2][kLsTerms], w[kLsTerms];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int r = 32 * mh + 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
 #pragma unroll
-        for (int tm = 0; tm < 3; ++tm)
+        for (int tm = 0; tm < kLsTerms; ++tm)
           a[t][tm] = LZM_LS_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)s, (uint32_t)t, (uint32_t)tm}
                                       : *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
       }
 #pragma unroll
-      for (int tm = 0; tm < 3; ++tm)
+      for (int tm = 0; tm < kLsTerms; ++tm)
         w[tm] = LZM_LS_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)c, 1u, (uint32_t)tm}
-                                 : bbuf[((c * 4 + ct) * 3 + tm) * 64 + lane];
+                                 : bbuf[((c * 4 + ct) * kLsTerms + tm) * 64 + lane];
       if (LZM_LS_DIAG == 2) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
-          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y),
-                         __builtin_bit_cast(float, a[t][2].z ^ w[2].z), 0.f};
+          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y), 0.f, 0.f};
         continue;
       }
-      // small terms first: l.h, h.l, m.m, m.h, h.m, h.h (the conv trunk's order)
+      // small terms first: l.h, h.l, h.h (the conv trunk's order)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][1]), bx_ash(w[0]), acc[t], 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[2]), acc[t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][0]), bx_ash(w[1]), acc[t], 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[1]), acc[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[0]), acc[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[1]), acc[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
+      for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][0]), bx_ash(w[0]), acc[t], 0, 0, 0);
     }
     if (s + 1 < nst && LZM_LS_DIAG != 5) {
       if constexpr (PAR == 0)
@@ -390,7 +383,7 @@ struct LpTile {
 // the GEMM part: acc[t] = the tile's K-half partial sums (row tile t = rows 16 t .. + 15 of the tile,
 // this wave's 16 gate columns), accumulated from zero exactly as the 512-thread kernel does.
 // lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4); wfrag:
-// ls_pack's split-bf16 fragments (lzm_ez_lstm_prepare, the ones ez_lstm_gemm_cell_kernel reads). A
+// ls_pack's split-fp16 fragments (lzm_ez_lstm_prepare, the ones ez_lstm_gemm_cell_kernel reads). A
 // is read as f32 and split on the fly (a thread stages 4 values of 4 rows through LDS); a wave loads
 // the B fragments its own MFMAs consume (chunk 0 and 1, column tile = the wave, its lane, 3 terms)
 // straight into registers: B never touches LDS. (Measured: B read as f32 in the same order and split
@@ -413,54 +406,53 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
     arow[u] = tl.row0 + rr < B;
     avo[u] = ((tl.row0 + (arow[u] ? rr : 0)) * K + k0 + 4 * a4) * 4;
   }
-  // B: ls_pack's layout [nb][column tile][chunk][term][lane][8 bf16]: wave-instruction (chunk, term)
+  // B: ls_pack's layout [nb][column tile][chunk][term][lane][8 fp16]: wave-instruction (chunk, term)
   // reads 1 KiB contiguous
   const __amdgpu_buffer_rsrc_t wq = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t *>(wfrag + (size_t)tl.nb * 4 * nch * 3 * 64 * 8), 0, 4 * nch * 3 * 64 * 16, 0x00020000);
-  const int bqo = ((ct * nch * 3) * 64 + lane) * 16;  // (column tile, chunk 0, term 0, lane), bytes
+      const_cast<uint16_t *>(wfrag + (size_t)tl.nb * 4 * nch * kLsTerms * 64 * 8), 0, 4 * nch * kLsTerms * 64 * 16,
+      0x00020000);
+  const int bqo = ((ct * nch * kLsTerms) * 64 + lane) * 16;  // (column tile, chunk 0, term 0, lane), bytes
+  constexpr int NVB = 2 * kLsTerms;                          // B loads per stage: (chunk, term)
   lp_f4 va[LZM_LP_DEPTH][4];
-  uint4 vb[LZM_LP_DEPTH][6];  // global loads LZM_LP_DEPTH - 1 stages ahead
-  uint4 wreg[2][3];  // the next stage's B fragments (chunk, term) of this wave's column tile
-  auto load_stage = [&](int s, lp_f4(&VA)[4], uint4(&VB)[6]) __attribute__((always_inline)) {
+  uint4 vb[LZM_LP_DEPTH][NVB];  // global loads LZM_LP_DEPTH - 1 stages ahead
+  uint4 wreg[2][kLsTerms];  // the next stage's B fragments (chunk, term) of this wave's column tile
+  auto load_stage = [&](int s, lp_f4(&VA)[4], uint4(&VB)[NVB]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       VA[u] = arow[u] ? __builtin_bit_cast(lp_f4, __builtin_amdgcn_raw_buffer_load_b128(xr, avo[u], s * kLsKc * 4, 16))
                       : lp_f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int u = 0; u < 6; ++u) {  // chunk u / 3 of the stage, term u % 3
-      const int j = (k0 / 32) + 2 * s + u / 3;
-      VB[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wq, bqo, (3 * j + u % 3) * 64 * 16, 0));
+    for (int u = 0; u < NVB; ++u) {  // chunk u / kLsTerms of the stage, term u % kLsTerms
+      const int j = (k0 / 32) + 2 * s + u / kLsTerms;
+      VB[u] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(wq, bqo, (kLsTerms * j + u % kLsTerms) * 64 * 16, 0));
     }
   };
-  auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const uint4(&VB)[6]) __attribute__((always_inline)) {
+  auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const uint4(&VB)[NVB]) __attribute__((always_inline)) {
     typedef float f2 __attribute__((ext_vector_type(2)));
-    typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     uint16_t *abuf = lds + bsel * kLsStage;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // row 16 ct + 4 u + lane / 16: 4 values, half (a4 & 1) of chunk a4 / 2
       const int rr = 16 * ct + 4 * u + (lane >> 4);
-      uint32_t hh[2], mm[2], ll[2];
+      uint32_t hh[2], ll[2];
       const f2 pr[2] = {f2{VA[u][0], VA[u][1]}, f2{VA[u][2], VA[u][3]}};
 #pragma unroll
       for (int v = 0; v < 2; ++v) {
-        const b2 th = __builtin_convertvector(pr[v], b2);
-        const f2 r1 = pr[v] - __builtin_convertvector(th, f2);
-        const b2 tm = __builtin_convertvector(r1, b2);
-        const b2 tq = __builtin_convertvector(r1 - __builtin_convertvector(tm, f2), b2);
+        const h2 th = __builtin_convertvector(pr[v], h2);
+        const h2 tq = __builtin_convertvector(pr[v] - __builtin_convertvector(th, f2), h2);
         hh[v] = __builtin_bit_cast(uint32_t, th);
-        mm[v] = __builtin_bit_cast(uint32_t, tm);
         ll[v] = __builtin_bit_cast(uint32_t, tq);
       }
       uint16_t *base = abuf + rr * kLsKc + (((a4 >> 1) ^ (rr & 7)) & 7) * 8 + 4 * (a4 & 1);
       *reinterpret_cast<uint2 *>(base) = uint2{hh[0], hh[1]};
-      *reinterpret_cast<uint2 *>(base + kLsPlane) = uint2{mm[0], mm[1]};
-      *reinterpret_cast<uint2 *>(base + 2 * kLsPlane) = uint2{ll[0], ll[1]};
+      *reinterpret_cast<uint2 *>(base + kLsPlane) = uint2{ll[0], ll[1]};
     }
     // B: a wave loads exactly the fragments its own MFMAs consume, so they stay in registers
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) wreg[c][q] = VB[3 * c + q];
+      for (int q = 0; q < kLsTerms; ++q) wreg[c][q] = VB[kLsTerms * c + q];
   };
 #pragma unroll
   for (int s0 = 0; s0 < LZM_LP_DEPTH - 1; ++s0)
@@ -478,37 +470,30 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
     const uint16_t *abuf = lds + (s & 1) * kLsStage;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      uint4 a[4][3], w[3];
+      uint4 a[4][kLsTerms], w[kLsTerms];
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int r = 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
 #pragma unroll
-        for (int tm = 0; tm < 3; ++tm)
+        for (int tm = 0; tm < kLsTerms; ++tm)
           a[t][tm] = LZM_LP_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)s, (uint32_t)t, (uint32_t)tm}
                                       : *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
       }
 #pragma unroll
-      for (int tm = 0; tm < 3; ++tm) w[tm] = wreg[c][tm];
+      for (int tm = 0; tm < kLsTerms; ++tm) w[tm] = wreg[c][tm];
       if (LZM_LP_DIAG == 2) {
 #pragma unroll
         for (int t = 0; t < 4; ++t)
-          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y),
-                         __builtin_bit_cast(float, a[t][2].z ^ w[2].z), 0.f};
+          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y), 0.f, 0.f};
         continue;
       }
-      // small terms first: l.h, h.l, m.m, m.h, h.m, h.h (ez_lstm_gemm_cell_kernel's order)
+      // small terms first: l.h, h.l, h.h (ez_lstm_gemm_cell_kernel's order)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][2]), bx_as(w[0]), acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][1]), bx_ash(w[0]), acc[t], 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[2]), acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][0]), bx_ash(w[1]), acc[t], 0, 0, 0);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[1]), acc[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][1]), bx_as(w[0]), acc[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[1]), acc[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bx_as(a[t][0]), bx_as(w[0]), acc[t], 0, 0, 0);
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][0]), bx_ash(w[0]), acc[t], 0, 0, 0);
     }
     // (measured: splitting / storing stage s + 1 BEFORE this stage's MFMAs instead, into the other LDS
     // buffer, made the GEMM slower, 33 K -> 40 K cycles per simulation)

@@ -77,7 +77,7 @@ struct ConvSearchArgs {
   float *xin;             // [B][Kx] LSTM input rows [reward planes | leaf hidden state] (sc1 hand-off)
   int Kx, H, horizon;     // Kx = r_ch * 64 + H; lstm_horizon_len
   float *hpool, *cpool;   // [S + 1][B][H] state pools (slot 0 = the roots' state)
-  const uint16_t *lwfrag; // gate weights, split-bf16 fragments (lzm_ez_lstm_prepare)
+  const uint16_t *lwfrag; // gate weights, split-fp16 fragments (lzm_ez_lstm_prepare)
   const float *lbias;     // [4H] b_ih + b_hh
   const float *vp_s, *vp_t;  // value-prefix BatchNorm as an affine map (relu(h1 * s + t) feeds the head)
   float *h1g;             // [B][H] unmasked LSTM outputs (sc1 hand-off, tile -> root)
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 //     and publishes {epoch, x, search_len} in xflags[k][b] (every storing wave's vmcnt(0), a barrier,
 //     one agent-scope flag store: MI355X_MICROARCH.md's first hand-off row);
 //   - the value / policy heads run while the other roots finish their trunks;
-//   - the tile waits for its 64 rows' flags, runs the split-bf16 gate GEMM over its K half
+//   - the tile waits for its 64 rows' flags, runs the split-fp16 gate GEMM over its K half
 //     (lp_tile_gemm, ez_lstm_gemm_cell_kernel's arithmetic), the upper half hands its partial sums to
 //     the lower (pflags), which adds them, runs the cell with c0 = cpool[x][b] and files the masked c
 //     state (its own slots: the tile map is fixed, so only this workgroup ever reads them), and hands

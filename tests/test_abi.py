@@ -98,29 +98,30 @@ def test_split_trunk_packing_recovers_f32_weights():
 
 
 def test_lstm_gate_fragments_recover_f32_weights():
-    """lzm_ez_lstm_prepare (host code, no GPU): the [n-block][wave][chunk][term][lane][8] split-bf16
-    fragments of the LSTM gate weights W [4H][K] give back W (h + m + l within 2^-24 relative) at the
+    """lzm_ez_lstm_prepare (host code, no GPU): the [n-block][wave][chunk][term][lane][8] split-fp16
+    fragments of the LSTM gate weights W [4H][K] give back W (h + l within 2^-22 relative, 2^-25 absolute
+    below fp16's normal range) at the
     place the fused gate-GEMM + cell kernel reads it: lane l of wave w in n-block nb is column l % 16 =
     4 u + gate of unit 16 nb + 4 w + u (torch row gate * H + unit), k = 32 chunk + 8 (l / 16) + e"""
     import ctypes
     import numpy as np
     L = _lib.load()
     K, H = 128, 32
-    assert L.lzm_ez_lstm_frag_floats(K, H) == K * 4 * H * 3 // 2
+    assert L.lzm_ez_lstm_frag_floats(K, H) == K * 4 * H * 2 // 2
     assert L.lzm_ez_lstm_frag_floats(100, H) < 0 and L.lzm_ez_lstm_frag_floats(K, 24) < 0
     rng = np.random.default_rng(1)
     W = (rng.standard_normal((4 * H, K)) * 0.05).astype(np.float32)
     out = np.zeros(L.lzm_ez_lstm_frag_floats(K, H), np.float32)
     assert L.lzm_ez_lstm_prepare(K, H, ctypes.c_void_p(W.ctypes.data), ctypes.c_void_p(out.ctypes.data)) == 0
     nb_n, nch = H // 16, K // 32
-    u = out.view(np.uint16).reshape(nb_n, 4, nch, 3, 64, 8)
-    rec = ((u.astype(np.uint32) << 16).view(np.float32).astype(np.float64)).sum(axis=3)  # [nb][w][j][lane][e]
+    u = out.view(np.uint16).reshape(nb_n, 4, nch, 2, 64, 8)
+    rec = u.view(np.float16).astype(np.float64).sum(axis=3)  # [nb][w][j][lane][e]
     nb_, w_, j_, l_, e_ = np.meshgrid(np.arange(nb_n), np.arange(4), np.arange(nch), np.arange(64), np.arange(8),
                                       indexing="ij")
     n = l_ & 15
     unit = 16 * nb_ + 4 * w_ + (n >> 2)
     want = W.astype(np.float64)[(n & 3) * H + unit, 32 * j_ + 8 * (l_ >> 4) + e_]
-    np.testing.assert_allclose(rec, want, rtol=2.0 ** -23, atol=0)
+    assert np.all(np.abs(rec - want) <= np.abs(want) * 2.0 ** -22 + 2.0 ** -25)
 
 
 def test_representation_entry_points_validate_arguments_on_the_host():

@@ -113,12 +113,8 @@ def main():
     flops, matrix = recurrent_flops(model, a.kind, B, dev)
     net_tflops = flops * B * S / dt / 1e12
     split = precision == "split"
-    # split: the trunk's convolutions at 3 fp16 products per f32 product, EZ's LSTM gate GEMM at 6 bf16 ones
-    gate = 0.0
-    if a.kind == "ez":
-        lstm = model.dynamics_network.lstm
-        gate = 2.0 * 4 * lstm.hidden_size * (lstm.input_size + lstm.hidden_size)
-    mfma = ((3.0 * (matrix - gate) + 6.0 * gate) if split else matrix) * B * S / dt / 1e12
+    # split: the trunk's convolutions and EZ's LSTM gate GEMM at 3 fp16 products per f32 product
+    mfma = (3.0 if split else 1.0) * matrix * B * S / dt / 1e12
     peak = BF16_PEAK_TFLOPS if split else FP32_MFMA_PEAK_TFLOPS
     cpu = None
     if a.cpu_baseline_secs > 0:
