@@ -701,7 +701,7 @@ def cpu_baseline(B, S, zero_heads, secs, device):
             "variants": var, "host": host_cpu_info(), "calibration": load_calibration()}
 
 
-BF16_PEAK_TFLOPS = 2500.0  # MI355X dense BF16 MFMA (MI355X_MICROARCH.md; not the 2:1-sparse figure)
+BF16_PEAK_TFLOPS = 2500.0  # MI355X dense BF16 = FP16 MFMA (MI355X_MICROARCH.md: the F16 forms take the same cycles; not the 2:1-sparse figure)
 
 
 def make_step(args, workload, model, device, rank):
