@@ -244,6 +244,9 @@ constexpr int kBx3Frag = 4 * 18 * kBxTerms * 64 * 4;  // floats: [wave][chunk][t
 constexpr int kBx1Frag = 2 * 2 * kBxTerms * 64 * 4;   // 1x1 64->32: [wave 0..1][chunk][term][lane][8 fp16]
 constexpr int kBxBlock = 2 * kBx3Frag + 2 * kCvCh;
 constexpr int kBxAhead = 3;  // default weight read-ahead (chunks)
+// the EZ search's read-ahead: with fp16 terms (two uint4s per chunk) 5 chunks fit its registers and measured
+// 2.49 -> 2.46 ms per Pong search; the Breakout search even at 2, 3, 4, 5 (profiles/r05/ab/ab_ahead.txt)
+constexpr int kBxAheadEz = 5;
 
 typedef __bf16 bxv8 __attribute__((ext_vector_type(8)));
 typedef _Float16 bxh8 __attribute__((ext_vector_type(8)));

@@ -2937,8 +2937,8 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
     LZM_HIP(hipMemset(h->phase, 0, (64 + 1024) * sizeof(unsigned long long)));
   }
   p.stamps = stamps ? h->phase : nullptr;
-  auto fn = stamps ? (fast ? search_conv_ez_kernel<kBxAhead, true, true> : search_conv_ez_kernel<kBxAhead, false, true>)
-                   : (fast ? search_conv_ez_kernel<kBxAhead, true> : search_conv_ez_kernel<kBxAhead, false>);
+  auto fn = stamps ? (fast ? search_conv_ez_kernel<kBxAheadEz, true, true> : search_conv_ez_kernel<kBxAheadEz, false, true>)
+                   : (fast ? search_conv_ez_kernel<kBxAheadEz, true> : search_conv_ez_kernel<kBxAheadEz, false>);
   LZM_HIP(hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   // The roots wait on LSTM tiles and the tiles on roots inside the launch, so every workgroup must be
   // resident at once. The check is static: resident workgroups per CU at this LDS / register use (the
