@@ -194,7 +194,7 @@ WORKLOADS = {
     # name: (actions, observation shape, device env of the collect step, support_scale)
     "cartpole": (2, (4,), "cartpole", 300),
     "breakout": (4, (4, 64, 64), "breakout", 300),
-    "pong": (6, (4, 64, 64), None, 50),
+    "pong": (6, (4, 64, 64), "pong", 50),
 }
 
 
@@ -242,8 +242,9 @@ class CollectStep:
         self.dst = dst  # trajectory return: gather to rank dst (None: all-gather)
         env = WORKLOADS[workload][2]
         # CartPole episodes are short (tens of steps): many slots per env; Breakout stand-in episodes
-        # last >= ~17 steps, 400-step limit
-        slots, T = (64, 200) if env == "cartpole" else (8, 400)
+        # last >= ~17 steps, 400-step limit; Pong stand-in episodes (21 points, hundreds of steps) truncated
+        # at 100 steps, so that episodes finish inside a 100-step timed region
+        slots, T = {"cartpole": (64, 200), "pong": (8, 100)}.get(env, (8, 400))
         self.col = DeviceCollector(model, B, S, device=device, seed=seed, rng_mode=rng_mode, graph=True,
                                    episode_slots=slots, max_episode_steps=T, env=env)
         self.step = self.col.search
@@ -956,22 +957,27 @@ def config1(args, device, cpu):
 
 
 def config3(args, device, cpu):
-    """BASELINE.json config 3: Pong EfficientZero, 256 envs x 50 sims on one GPU, as the collect-time step
-    (efficientzero.py:538-656): BN-folded conv initial inference (the representation network included),
-    root preparation, the one-launch EZ search with the reward LSTM, root outputs — one HIP graph"""
+    """BASELINE.json config 3: Pong EfficientZero, 256 envs x 50 sims on one GPU, as the device collect step
+    (efficientzero.py:538-656 inside muzero_collector.py:399-705): BN-folded conv initial inference (the
+    representation network included), root preparation, the one-launch EZ search with the reward LSTM, root
+    outputs, the Pong stand-in env's step and recording — one HIP graph per env step — and the timed region
+    ends with the trajectory return (device packing + the process group's gather, config 5's path)"""
     B, S = args.envs, args.sims
     model = build_ez_model(device, seed=0, zero_heads=args.zero_heads)
-    step = GraphStep(B, S, model, device, args.rng, seed=shard_seed(0), workload="pong")
-    steps = max(args.steps, 20)
-    el, _ = timed_run(step, steps, args.warmup, 1, device)
+    step = CollectStep(B, S, model, device, args.rng, seed=shard_seed(0), workload="pong",
+                       dst=0 if args.traj == "gather" else None)
+    steps = max(args.steps, 100)
+    world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    el, traj = timed_run(step, steps, args.warmup, world, device)
     tie, sdiag = check_step(step, S, True)
     out = {"workload": f"Atari Pong EfficientZero (BASELINE.json config 3), {B} envs x {S} sims, conv "
                        f"EfficientZeroModel (4x64x64 frames, latent 64x8x8, LSTM 512, support 101, 6 actions)",
-           "step": "collect-time search (initial inference + prepare + search + root outputs)",
-           "value": round(B * S * steps / el, 1), "unit": "sims/s", "ms_per_step": round(el / steps * 1e3, 4),
-           "steps": steps, "n_gpus": 1, "dtype": "f32 (convolutions as split-fp16 MFMA)",
+           "step": "collect", "value": round(B * S * steps / el, 1), "unit": "sims/s",
+           "ms_per_step": round(el / steps * 1e3, 4), "steps": steps, "n_gpus": 1,
+           "env_steps_per_s": round(B * steps / el, 1), "trajectory": traj,
+           "dtype": "f32 (convolutions as split-fp16 MFMA)",
            "search_path": step.mcts.last_path, "tie_stream_errors": tie, "search_diag": sdiag,
-           "data": "synthetic (random-init conv EfficientZeroModel, synthetic frames)",
+           "data": "synthetic (random-init conv EfficientZeroModel; Pong stand-in env, ALE absent)",
            "roofline": conv_roofline(step, model, B, S, device)}
     if cpu:
         out["cpu_baseline"] = cpu_baseline_conv("ez", B, S, model, 0.5 * args.cpu_baseline_secs, device)

@@ -35,7 +35,9 @@ enum lzm_status {
   LZM_ERR_HIP = -2,      /* a HIP runtime call failed */
   LZM_ERR_CAPACITY = -3, /* latent index beyond the reserved simulations: call lzm_reserve */
   LZM_ERR_STATE = -4,    /* call order violated (e.g. backprop before traverse) */
-  LZM_ERR_RESIDENCY = -5 /* a launch that needs its whole grid co-resident was refused; nothing ran */
+  LZM_ERR_RESIDENCY = -5, /* a launch that needs its whole grid co-resident was refused; nothing ran */
+  LZM_ERR_RANGE = -6      /* split-fp16 network values left their range (non-finite, or beyond ~2^114): the
+                             outputs are not f32-exact; rerun the network with LZM_CONV_F32 */
 };
 
 enum lzm_flags {
@@ -182,10 +184,12 @@ int lzm_debug_root_wait_cycles(lzm_handle *h, uint64_t *out_host, int n, int res
 
 /* Post-search integrity check (host-synchronous on `stream`): the sticky error counters of every
  * search path on the handle — {look-back spin timeouts, draw positions beyond the coefficient
- * table, serial-traverse fixed-point failures, fused-search errors} into out_host[4] (nullable).
- * Returns LZM_ERR_STATE when any is non-zero (the parity-mode tie-break stream then differs from
- * the reference's); clear != 0 resets them. No reference counterpart: the reference's draws are
- * serial on one host thread (cnode.cpp:770, :590) and cannot fail this way. */
+ * table, serial-traverse fixed-point failures, fused-search errors, split-fp16 range errors, 0, 0, 0}
+ * into out_host[8] (nullable). Returns LZM_ERR_RANGE when word 4 is non-zero (a split-fp16 network
+ * value was non-finite or out of range: rerun with LZM_CONV_F32), else LZM_ERR_STATE when any is
+ * non-zero (the parity-mode tie-break stream then differs from the reference's); clear != 0 resets
+ * them. No reference counterpart: the reference's draws are serial on one host thread
+ * (cnode.cpp:770, :590) and cannot fail this way. */
 int lzm_check_errors(lzm_handle *h, int32_t *out_host, int clear, void *stream);
 
 /* Diagnostics: traverse passes used by the last parity-mode traverse (device int32[1]). */
@@ -224,7 +228,9 @@ int lzm_debug_xor(const float *in, float *out, void *stream);
  * store_search_stats does), step the env (gymnasium CartPole equations in float64, truncation at
  * max_steps), auto-reset finished episodes (ep_len[n][E], ep_count[n]) and write the next root's
  * obs and Dirichlet(noise_alpha) noises float[n][A]. `counter` (int64, device) keys this step's
- * Philox streams; the caller advances it. pred_value / rec_pred: both or neither. ep_return float[n][E]
+ * Philox streams and is only read: in the collect loop the search advances it (lzm_search_set_step with
+ * increment) before this epilogue runs, so step n's streams use key n + 1; a caller driving the env without
+ * such a search advances it itself after each step. pred_value / rec_pred: both or neither. ep_return float[n][E]
  * (nullable): each finished episode's return, the env's eval_episode_return (the reward sum, 1 per step;
  * muzero_collector.py:596-603 logs it). */
 int lzm_cartpole_reset(int n, double *state, int32_t *steps, float *obs, uint32_t seed, void *stream);
@@ -244,9 +250,12 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
  * auto-reset finished episodes (their final frame goes to slot row L; ep_len / ep_count advance) and
  * draw the next root's Dirichlet(noise_alpha) noise. The game is a stand-in with Breakout's action set
  * and frame format (ALE is not installed; csrc/lzm_atari.h). state int32 [n][16], cur u8 [n][4096]
- * (the newest frame), counter: the device env-step counter. ep_return float[n][E] (nullable): each finished
- * episode's UNCLIPPED score (eval_episode_return, muzero_collector.py:596-603; the recorded rewards are
- * clipped). */
+ * (the newest frame), counter: the device env-step counter, read as lzm_cartpole_collect_step reads it (the
+ * collect-step search has already advanced it). ep_return float[n][E] (nullable): each finished episode's
+ * UNCLIPPED score (eval_episode_return, muzero_collector.py:596-603; the recorded rewards are clipped).
+ * lzm_pong_reset / lzm_pong_collect_step: the same step for config 3's Pong EfficientZero with a Pong stand-in
+ * (6 actions {NOOP, FIRE, RIGHT = up, LEFT = down, RIGHTFIRE, LEFTFIRE}, the agent's paddle on the right, a
+ * scripted opponent, +1 / -1 per point, 21 points end the episode; ep_return: the point difference). */
 int lzm_atari_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream);
 int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
                            const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
@@ -254,6 +263,13 @@ int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, co
                            int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
                            float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
                            uint32_t seed, const int64_t *counter, void *stream);
+int lzm_pong_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream);
+int lzm_pong_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
+                          const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
+                          float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
+                          int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
+                          float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
+                          uint32_t seed, const int64_t *counter, void *stream);
 
 /* Device packing of a collector's finished episodes for the trajectory return (SURVEY.md §8(e);
  * replaces the host loop over envs that builds GameSegments' arrays, muzero_collector.py:612-632, and
@@ -283,8 +299,10 @@ int lzm_episodes_pack(int n, int E, int T, int A, int has_pred, int64_t frame_by
  * convolution launches with fused bias / residual / ReLU and a pool launch. lzm_repr_prepare packs raw =
  * [conv1 W (32 x cin x 9), b (32) | block1 W1 (32 x 32 x 9), b1, W2, b2 |
  * down W1 (64 x 32 x 9), b1 (64), W2 (64 x 64 x 9), b2 (64), W3 (64 x 32 x 9) | block2 W1 (64 x 64 x 9), b1, W2,
- * b2] into lzm_repr_floats() floats. lzm_repr_downsample: obs f32 NCHW [B][cin][64][64] -> out [B][64][8][8]
- * (the input of lzm_conv_resnet8_p's 8 x 8 tail); ws: lzm_repr_workspace_floats(B) floats (NHWC stages). */
+ * b2] into lzm_repr_floats() floats (every weight row scaled by a power of two, its inverse kept for the
+ * epilogue; each tile's input split after scaling by a power of two from its exact max: lzm_conv.h's range
+ * rule). lzm_repr_downsample: obs f32 NCHW [B][cin][64][64] -> out [B][64][8][8] (the input of
+ * lzm_conv_resnet8_p's 8 x 8 tail); ws: lzm_repr_workspace_floats(B) floats (NHWC stages). */
 int64_t lzm_repr_floats(void);
 int lzm_repr_prepare(int cin, const float *raw, float *out);
 int64_t lzm_repr_workspace_floats(int B);
@@ -355,15 +373,20 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
  * lzm_conv_trunk_prepare packs, on the host, raw = dyn W[64][64][9] (latent input channels);
  *   n_dres x { W1[64][64][9], b1[64], W2[64][64][9], b2[64] };  reward W[r_ch][64], b[r_ch];
  *   n_pres x { same };  head W[h_ch][64], b[h_ch]
- * into lzm_conv_trunk_floats() floats (copy to the device, 16-byte aligned).
+ * into lzm_conv_trunk_floats() floats (copy to the device, 16-byte aligned). The split layout also holds each
+ * layer's weight-row scales and the bounds its activation scales are derived from (lzm_conv.h, "Range");
+ * the dynamics conv's bias bound is max |actmap|: set it with lzm_conv_trunk_actmap_bound before the copy.
  * lzm_conv_trunk: input latent of env b = pool[(x[b] * B + b) * 4096 ..] (x nullable: pool[b * 4096]);
  * actmap float[A][64][64] (action planes' conv + dynamics bias), action int32[B];
  * outputs out_latent float[B][4096], out_r float[B][r_ch*64], out_h float[B][h_ch*64].
  * The unsuffixed entry points run the exact-f32 matrix path (LZM_CONV_F32); the _p forms take the
  * precision: LZM_CONV_F32 (v_mfma_f32_32x32x2_f32) or LZM_CONV_SPLIT (each f32 operand split into two
- * fp16 terms, three products per K on v_mfma_f32_16x16x32_f16: f32-level error, 2^-22 per operand, for
- * values inside fp16's range; the EfficientZero LSTM gate GEMM on the same split). A blob packed for one
- * precision must be run with the same precision. LZM_CONV_BF16X3 is the split precision's former name. */
+ * fp16 terms, three products per K on v_mfma_f32_16x16x32_f16, every weight row and activation tensor scaled
+ * by a power of two so both terms stay normal fp16: f32-level error, 2^-22 per operand; the EfficientZero
+ * LSTM gate GEMM on the same split). err (nullable, device int32): counts envs whose split activations were
+ * non-finite or beyond the scales' range (lzm_error_word(h, 4) reports them through lzm_check_errors). A blob
+ * packed for one precision must be run with the same precision. LZM_CONV_BF16X3 is the split precision's
+ * former name. */
 #define LZM_CONV_F32 0
 #define LZM_CONV_SPLIT 1
 #define LZM_CONV_BF16X3 LZM_CONV_SPLIT
@@ -375,9 +398,10 @@ int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const floa
 int64_t lzm_conv_trunk_floats_p(int n_dres, int n_pres, int precision);
 int lzm_conv_trunk_prepare_p(int precision, int n_dres, int n_pres, int r_ch, int h_ch, const float *raw,
                              float *out_host);
+int lzm_conv_trunk_actmap_bound(int n_dres, int n_pres, float actmap_absmax, float *packed_host);
 int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
                      const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
-                     float *out_latent, float *out_r, float *out_h, void *stream);
+                     float *out_latent, float *out_r, float *out_h, int32_t *err, void *stream);
 /* The conv representation network's 8 x 8 tail on the same split-bf16 trunk kernel (no dynamics conv,
  * no reward 1x1): in [B][64][8][8] (the DownSample's output after its last average pool) through
  * n_blocks residual blocks -> out_latent [B][64 * 64] (the initial latent), then n_pres prediction
@@ -386,16 +410,18 @@ int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int
  * prediction trunk). Weights: lzm_conv_trunk_prepare_p(LZM_CONV_BF16X3, n_blocks, n_pres, 1, h_ch, raw)
  * with a zero dynamics conv and a zero 1-channel reward 1x1 in raw. */
 int lzm_conv_resnet8_p(int B, int n_blocks, int n_pres, int h_ch, const float *weights, const float *in,
-                       float *out_latent, float *out_h, void *stream);
+                       float *out_latent, float *out_h, int32_t *err, void *stream);
 /* lzm_conv_trunk_p writing the EfficientZero LSTM input row directly (mcts_ctree.py:776-790 +
  * efficientzero_model.py:551-556: nn.LSTM over [reward planes | leaf hidden state]): row b of xin
  * (xin_stride floats, >= r_ch*64 + H) gets the reward planes at [0, r_ch*64) and, when hpool
  * (float[.][B][H], H % 4 == 0) is given, the leaf's hidden state hpool[x[b]][b] at [r_ch*64, +H)
- * — the gather + concat that lzm_ez_lstm_input would do as a separate launch. */
+ * — the gather + concat that lzm_ez_lstm_input would do as a separate launch — and (split precision) xscale[b]
+ * (int32 [B], required with hpool) the row's split scale exponent 14 - floor(log2 max(max reward plane, 1)) that
+ * lzm_ez_lstm_step reads. */
 int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
                          const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
-                         float *out_latent, float *xin, int xin_stride, const float *hpool, int H, float *out_h,
-                         void *stream);
+                         float *out_latent, float *xin, int xin_stride, const float *hpool, int H, int32_t *xscale,
+                         float *out_h, int32_t *err, void *stream);
 
 /* The MLP heads of the conv recurrent step in one launch (lzm_heads.h): reward hidden from
  * r [B][Kr] (optionally relu(r * r_scale + r_shift), the EfficientZero value-prefix BatchNorm),
@@ -545,7 +571,9 @@ int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *cpool, const
  * rocBLAS GEMM + lzm_ez_lstm_cell pair did in two launches. xin [B][K] (K = Kr + H, % 64 == 0),
  * wfrag = lzm_ez_lstm_prepare(W [4H][K], nn.LSTM gate order i, f, g, o), bias [4H], c0 =
  * cpool[x[b]][b]; writes h1 / c1 [B][H] and the next state slot hslot / cslot (zeroed where
- * search_len[b] % horizon == 0). H % 16 == 0. Within f32 tolerance of the f32 GEMM (rtol 1e-4). */
+ * search_len[b] % horizon == 0). H % 16 == 0. Within f32 tolerance of the f32 GEMM (rtol 1e-4): each gate
+ * column's weights packed scaled by a power of two (the inverse scales follow the fragments), each row's
+ * 64-K stage split after scaling by a power of two from its exact max. */
 int64_t lzm_ez_lstm_frag_floats(int K, int H);
 int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out);
 /* workspace (optional, zero-filled once): lzm_ez_lstm_workspace_bytes(B, H) bytes; with it the K range
@@ -554,12 +582,17 @@ int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out);
 int64_t lzm_ez_lstm_workspace_bytes(int B, int H);
 /* diagnostics: lzm_ez_lstm_step launches record shader-clock stamps into buf [blocks][8] (nullptr: off) */
 int lzm_debug_lstm_stamps(void *buf);
-/* Device address of the handle's sticky error word i (0..3) for kernels launched outside the handle
- * (word 3: lzm_ez_lstm_step's hand-off timeouts); lzm_check_errors reports it. */
+/* Device address of the handle's sticky error word i (0..7) for kernels launched outside the handle
+ * (word 3: lzm_ez_lstm_step's hand-off timeouts, word 4: split-fp16 range errors); lzm_check_errors
+ * reports them. */
 int32_t *lzm_error_word(lzm_handle *h, int i);
-int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const float *wfrag, const float *bias, const float *cpool,
-                     const int32_t *x, const int32_t *search_len, int horizon, float *h1, float *c1, float *hslot,
-                     float *cslot, void *workspace, int32_t *err, void *stream);
+/* xscale [B]: each row's split scale exponent (lzm_conv_trunk_xin_p writes it; any s with |x 2^s| < 2^15 over the
+ * row is correct, 14 - floor(log2 max |row|) keeps the most bits); range_err (nullable): counts split values
+ * out of fp16's range (lzm_error_word(h, 4)). */
+int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const int32_t *xscale, const float *wfrag,
+                     const float *bias, const float *cpool, const int32_t *x, const int32_t *search_len, int horizon,
+                     float *h1, float *c1, float *hslot, float *cslot, void *workspace, int32_t *err,
+                     int32_t *range_err, void *stream);
 
 #ifdef __cplusplus
 }

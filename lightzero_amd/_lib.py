@@ -22,6 +22,8 @@ LZM_ERR_HIP = -2
 LZM_ERR_CAPACITY = -3
 LZM_ERR_STATE = -4
 LZM_ERR_RESIDENCY = -5
+LZM_ERR_RANGE = -6
+LZM_ERR_WORDS = 8  # sticky error words per tree handle (lzm_check_errors)
 LZM_TREE_EZ = 1
 LZM_RNG_FAST = 2
 
@@ -71,7 +73,7 @@ SIGNATURES = {
     "lzm_ez_lstm_workspace_bytes": [_i, _i],
     "lzm_error_word": [_vp, _i],
     "lzm_debug_lstm_stamps": [_vp],
-    "lzm_ez_lstm_step": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_ez_lstm_step": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_conv": [_vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i,
                         _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_conv_ez": [_vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp,
@@ -100,9 +102,12 @@ SIGNATURES = {
     "lzm_atari_reset": [_i, _vp, _vp, _vp, _vp, _u32, _vp],
     "lzm_atari_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp,
                                _vp, _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
+    "lzm_pong_reset": [_i, _vp, _vp, _vp, _vp, _u32, _vp],
+    "lzm_pong_collect_step": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _vp, _vp,
+                              _vp, _vp, _vp, _vp, _vp, _i, _u32, _vp, _vp],
     "lzm_episodes_scan": [_i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_bias_add_relu": [_vp, _vp, _vp, _i, _i, _i, _i, _vp],
-    "lzm_conv_resnet8_p": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp],
+    "lzm_conv_resnet8_p": [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_repr_floats": [],
     "lzm_repr_prepare": [_i, _vp, _vp],
     "lzm_repr_workspace_floats": [_i],
@@ -125,8 +130,10 @@ SIGNATURES = {
     "lzm_conv_trunk": [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_conv_trunk_floats_p": [_i, _i, _i],
     "lzm_conv_trunk_prepare_p": [_i, _i, _i, _i, _i, _vp, _vp],
-    "lzm_conv_trunk_p": [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "lzm_conv_trunk_xin_p": [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp, _vp],
+    "lzm_conv_trunk_actmap_bound": [_i, _i, _f, _vp],
+    "lzm_conv_trunk_p": [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "lzm_conv_trunk_xin_p": [_i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp, _vp, _vp,
+                             _vp],
 }
 _RESTYPE = {"lzm_last_error": ctypes.c_char_p, "lzm_mlp_packed_floats": ctypes.c_int64,
             "lzm_mlp_kernel_floats": ctypes.c_int64, "lzm_az_net_floats": ctypes.c_int64,
@@ -144,6 +151,12 @@ class LzmError(RuntimeError):
 
 class ResidencyError(LzmError):
     """A launch that needs its whole grid co-resident was refused (LZM_ERR_RESIDENCY); nothing ran."""
+
+
+class SplitRangeError(LzmError):
+    """Split-fp16 network values were non-finite or beyond the power-of-two scales' range (LZM_ERR_RANGE): the
+    search's network outputs are not f32-exact. Run the conv network with precision='f32'
+    (LZM_CONV_PRECISION=f32)."""
 
 
 # objects owning device memory allocated by the library (tree handles, ...): closed by the exit hook
@@ -203,6 +216,8 @@ def check(rc, what):
         raise ValueError(f"{what}: {msg}")
     if rc == LZM_ERR_RESIDENCY:
         raise ResidencyError(f"{what}: {msg}")
+    if rc == LZM_ERR_RANGE:
+        raise SplitRangeError(f"{what}: {msg}")
     raise LzmError(f"{what} failed ({rc}): {msg}")
 
 

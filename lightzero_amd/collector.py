@@ -1,8 +1,10 @@
 """Device-resident collector — the collector's fast mode.
 
 Mirrors what MuZeroCollector.collect (lzero/worker/muzero_collector.py:399-705) does per env step
-for a MuZero policy — stack the observation, run the collect-time search
-(MuZeroPolicy._forward_collect, policy/muzero.py:617-690), select an action from the root visit
+for a MuZero or EfficientZero policy — stack the observation, run the collect-time search
+(MuZeroPolicy._forward_collect, policy/muzero.py:617-690; EfficientZeroPolicy._forward_collect,
+policy/efficientzero.py:538-656, whose roots carry the value prefix and the LSTM state: the model picks
+the search, DeviceSearchStep), select an action from the root visit
 counts (select_action, policy/utils.py:515-539), step the env, append to the GameSegment
 (game_segment.py:129-218) — with everything on the device: one HIP graph per env step holds
 initial_inference, root preparation with Dirichlet noise, the search and the env's collect kernel
@@ -15,7 +17,9 @@ Two device envs (DEVICE_ENVS):
 - "breakout": the Atari image path of config 5 (conv MuZeroModel, 4 x 64 x 64 stacked grey frames, 4
   actions; one workgroup per env, lzm_atari.h) — a stand-in game with Breakout's action set and frame
   format, since ALE is not installed (env parity unpinned; the frames, recording and trajectory sizes
-  have the real shape).
+  have the real shape);
+- "pong": config 3's image path (conv EfficientZeroModel: the one-launch EfficientZero search with the
+  reward LSTM in the same captured step; 6 actions) with a Pong stand-in game on the same kernel.
 
 Each env records its episodes into device slots: one frame per step (the env's observation for
 CartPole, the newest u8 grey frame for Atari — GameSegment stores one frame per step and stacks
@@ -100,14 +104,37 @@ class BreakoutDevice:
              stream_ptr())
 
 
-DEVICE_ENVS = {"cartpole": CartPoleDevice, "breakout": BreakoutDevice}
+class PongDevice(BreakoutDevice):
+    """Config 3's Atari image env on the device (lzm_pong_*, the same collect kernel as Breakout's with the Pong
+    stand-in game, csrc/lzm_atari.h): Pong's minimal action set {NOOP, FIRE, RIGHT (up), LEFT (down), RIGHTFIRE,
+    LEFTFIRE}, the agent's paddle on the right against a scripted opponent, +1 / -1 per point, 21 points end the
+    episode, grey 64 x 64 frames, frame_stack_num 4. A stand-in game (ALE absent); EfficientZero's value support
+    (scale 50: atari_efficientzero_config.py)."""
+    name = "Pong (stand-in, ALE absent)"
+    A = 6
+    support_scale = 50
+
+    def reset(self, obs, seed):
+        call("lzm_pong_reset", self.n, ptr(self.state), ptr(self.steps), ptr(self.cur), ptr(obs), seed, stream_ptr())
+
+    def collect_step(self, c, out, pred):
+        call("lzm_pong_collect_step", c.n, self.A, c.T, c.E, ptr(out["distributions"]), ptr(out["values"]),
+             ptr(pred), ptr(self.state), ptr(self.steps), ptr(self.cur), ptr(c.search.obs), ptr(c.search.noises),
+             float(c.noise_alpha), float(c.temperature), int(c.deterministic), ptr(c.rec_frames),
+             ptr(c.rec_action), ptr(c.rec_reward), ptr(c.rec_visits), ptr(c.rec_value), ptr(c.rec_pred),
+             ptr(c.ep_len), ptr(c.ep_count), ptr(c.ep_return), int(c.T), c.seed, ptr(c.search.step_counter),
+             stream_ptr())
+
+
+DEVICE_ENVS = {"cartpole": CartPoleDevice, "breakout": BreakoutDevice, "pong": PongDevice}
 
 
 class DeviceCollector:
     def __init__(self, model, env_num, num_simulations, device="cuda", max_episode_steps=200, episode_slots=8,
                  temperature=1.0, deterministic=False, noise_alpha=0.3, noise_weight=0.25, seed=0,
                  rng_mode="glibc", graph=True, poll_every=8, record_pred=False, support_scale=None,
-                 categorical_distribution=True, env="cartpole"):
+                 categorical_distribution=True, env="cartpole", search_cfg=None):
+        """search_cfg: the search's config keys (discount_factor, lstm_horizon_len, ...: the policy's)"""
         _lib.require_gpu()
         self.n, self.S = int(env_num), int(num_simulations)
         self.dev = torch.device(device)
@@ -150,9 +177,11 @@ class DeviceCollector:
         def epilogue(out):
             me()._env_step(out)
 
+        sc = dict(search_cfg or {})
         self.search = DeviceSearchStep(model, n, self.S, [list(range(A))] * n, self.env.obs_shape, dev,
                                        noise_weight=noise_weight, seed=seed, rng_mode=rng_mode, graph=graph,
-                                       epilogue=epilogue, support_scale=support_scale)
+                                       epilogue=epilogue, support_scale=support_scale,
+                                       discount_factor=sc.pop("discount_factor", 0.997), cfg_extra=sc)
         self.search.build_graph()
         self.reset()
 

@@ -223,6 +223,9 @@ class FoldedConvNet:
         self.r_ch, self.h_ch = int(t["rw_w"].shape[0]), int(t["head_w"].shape[0])
         _lib.check(L.lzm_conv_trunk_prepare_p(prec, self.n_dres, self.n_pres, self.r_ch, self.h_ch,
                                               raw.ctypes.data, host.ctypes.data), "lzm_conv_trunk_prepare_p")
+        if prec == self.PRECISIONS["split"]:  # the dynamics conv's bias bound: max |actmap| (lzm_conv.h, "Range")
+            _lib.check(L.lzm_conv_trunk_actmap_bound(self.n_dres, self.n_pres, float(t["dyn_actmap"].abs().max()),
+                                                     host.ctypes.data), "lzm_conv_trunk_actmap_bound")
         blob = torch.from_numpy(host).to(dev)
         heads = self._pack_heads()
         lstm = self._pack_lstm(L)
@@ -258,8 +261,10 @@ class FoldedConvNet:
     def _pack_heads(self):
         return pack_heads(self.t, self.hv)
 
-    def _trunk(self, pool, x, action, out_latent):
-        """lzm_conv_trunk: (reward planes [B, r_ch*64], head planes [B, h_ch*64]); next latent -> out_latent"""
+    def _trunk(self, pool, x, action, out_latent, err=None):
+        """lzm_conv_trunk: (reward planes [B, r_ch*64], head planes [B, h_ch*64]); next latent -> out_latent.
+        err: nullable device int32 word counting envs whose split activations left their range (a tree's
+        lzm_error_word(4), reported by its check_errors)"""
         B = out_latent.shape[0]
         act = action if action.dtype == torch.int32 else action.to(torch.int32)
         r = torch.empty((B, self.r_ch * 64), dtype=torch.float32, device=out_latent.device)
@@ -267,13 +272,13 @@ class FoldedConvNet:
         _lib.call("lzm_conv_trunk_p", self.PRECISIONS[self.precision], B, self.n_dres, self.n_pres, self.r_ch,
                   self.h_ch, _lib.ptr(self.native),
                   _lib.ptr(self.actmap), _lib.ptr(pool), _lib.ptr(x), _lib.ptr(act.contiguous()), _lib.ptr(out_latent),
-                  _lib.ptr(r), _lib.ptr(h), _lib.stream_ptr())
+                  _lib.ptr(r), _lib.ptr(h), err, _lib.stream_ptr())
         return r, h
 
-    def step_from_pool(self, pool, x, action, out_latent, hidden=None):
+    def step_from_pool(self, pool, x, action, out_latent, hidden=None, range_err=None):
         """The recurrent step for leaf latents pool[x[b]][b] (pool [S+1, B, 64, 8, 8]); the next latent
         is written to out_latent ([B, 64, 8, 8], e.g. the next pool slot). Native trunk only."""
-        r, h = self._trunk(pool, x, action, out_latent)
+        r, h = self._trunk(pool, x, action, out_latent, range_err)
         return self._heads(r, h, out_latent, hidden)
 
     def _lstm_workspace(self, B, H, dev):
@@ -291,32 +296,35 @@ class FoldedConvNet:
         """hand-off timeouts counted by lzm_ez_lstm_step calls made without a tree's error word"""
         return sum(int(e.item()) for _, e in self._lstm_ws.values())
 
-    def step_from_pool_lstm(self, pool, x, action, out_latent, hpool, cpool, k, search_len, horizon, err=None):
+    def step_from_pool_lstm(self, pool, x, action, out_latent, hpool, cpool, k, search_len, horizon, err=None,
+                            range_err=None):
         """EfficientZero step on the pools: leaf latent pool[x[b]][b] and LSTM state (hpool, cpool)[x[b]][b]
         ([S+1, B, H] each). The next latent goes to out_latent, the next LSTM state — zeroed where
         search_len % horizon == 0 (mcts_ctree.py:810-813) — to hpool[k + 1] / cpool[k + 1]
         (csrc/lzm_lstm.h around the rocBLAS gate GEMM; the trunk kernel writes the LSTM input rows,
         lzm_conv_trunk_xin_p). Native trunk only. err: device int32 word counting the fused LSTM
-        step's hand-off timeouts (a tree's lzm_error_word, reported by its check_errors)."""
+        step's hand-off timeouts (a tree's lzm_error_word(3), reported by its check_errors); range_err: the trunk's
+        split-range word (lzm_error_word(4))."""
         t, P = self.t, _lib.ptr
         B, H = out_latent.shape[0], hpool.shape[2]
         Kr = self.r_ch * 64
         # the trunk writes the [reward planes | leaf hidden state] LSTM input rows itself
         xin = torch.empty((B, Kr + H), dtype=torch.float32, device=out_latent.device)
+        xscale = torch.empty(B, dtype=torch.int32, device=out_latent.device)  # the rows' split scales
         hd = torch.empty((B, self.h_ch * 64), dtype=torch.float32, device=out_latent.device)
         act = action if action.dtype == torch.int32 else action.to(torch.int32)
         _lib.call("lzm_conv_trunk_xin_p", self.PRECISIONS[self.precision], B, self.n_dres, self.n_pres, self.r_ch,
                   self.h_ch, P(self.native), P(self.actmap), P(pool), P(x), P(act.contiguous()), P(out_latent),
-                  P(xin), Kr + H, P(hpool), H, P(hd), _lib.stream_ptr())
+                  P(xin), Kr + H, P(hpool), H, P(xscale), P(hd), range_err, _lib.stream_ptr())
         r = xin[:, :Kr]
         h1 = torch.empty((B, H), dtype=torch.float32, device=r.device)
         c1 = torch.empty_like(h1)
         if self.lstm_frag is not None and self.lstm_fused:
             # the gate GEMM and the cell in one launch (split-fp16 MFMA, csrc/lzm_lstm.h)
             ws, werr = self._lstm_workspace(B, H, xin.device)
-            _lib.call("lzm_ez_lstm_step", B, Kr + H, H, P(xin), P(self.lstm_frag), P(t["lstm_b"]), P(cpool), P(x),
-                      P(search_len), int(horizon), P(h1), P(c1), P(hpool[k + 1]), P(cpool[k + 1]), P(ws),
-                      err if err is not None else P(werr), _lib.stream_ptr())
+            _lib.call("lzm_ez_lstm_step", B, Kr + H, H, P(xin), P(xscale), P(self.lstm_frag), P(t["lstm_b"]), P(cpool),
+                      P(x), P(search_len), int(horizon), P(h1), P(c1), P(hpool[k + 1]), P(cpool[k + 1]), P(ws),
+                      err if err is not None else P(werr), range_err, _lib.stream_ptr())
         else:
             gates = torch.addmm(t["lstm_b"], xin, t["lstm_w"].t())
             _lib.call("lzm_ez_lstm_cell", B, H, P(gates), P(cpool), P(x), P(search_len), int(horizon), P(h1), P(c1),
@@ -683,8 +691,9 @@ class FoldedConvInitial:
             latent = latent_out if latent_out is not None and tuple(latent_out.shape) == tuple(x.shape) \
                 and latent_out.is_contiguous() else torch.empty_like(x)
             h = torch.empty((B, h_ch * 64), dtype=torch.float32, device=x.device)
+            # (no error word: a non-finite value here reaches the root latent, whose range the search checks)
             _lib.call("lzm_conv_resnet8_p", B, nb, n_pres, h_ch, _lib.ptr(self.native), _lib.ptr(x),
-                      _lib.ptr(latent), _lib.ptr(h), _lib.stream_ptr())
+                      _lib.ptr(latent), _lib.ptr(h), None, _lib.stream_ptr())
             hp = getattr(self, "heads", None)
             if hp is not None and h.shape[1] == hp["Khd"]:
                 # the value / policy MLPs in one launch (lzm_conv_heads, prediction heads only)

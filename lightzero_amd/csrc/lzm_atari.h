@@ -20,6 +20,14 @@
 // at max_episode_steps. Env parity is unpinned; the data path — frame format,
 // per-step recording, trajectory sizes — has the real shape. Random streams are Philox per
 // (seed, env, step, purpose) as in lzm_collect.h.
+//
+// The second game (GAME = 1, config 3's Pong EfficientZero) is a stand-in with Pong's interface: the minimal
+// action set {NOOP, FIRE, RIGHT, LEFT, RIGHTFIRE, LEFTFIRE} (RIGHT moves the agent's paddle up, LEFT down, as
+// ALE's Pong), the agent's paddle on the right, a scripted opponent on the left that tracks the ball at a
+// lower speed, a point (+1 / -1) when the ball passes a paddle, the serve after FIRE or kPgAutoServe idle
+// steps, the episode over at 21 points for either side (or at max_episode_steps), rewards clipped to their
+// sign (already -1 / 0 / +1), the score (eval_episode_return) the point difference. The collect kernel
+// is the same for both games; the game functions are chosen by the template parameter.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -184,24 +192,127 @@ __device__ inline void at_store_obs16(float *obs_env, int k, int tid, const uint
     dst[q] = make_float4(px[4 * q] * sc, px[4 * q + 1] * sc, px[4 * q + 2] * sc, px[4 * q + 3] * sc);
 }
 
+// ---- the Pong stand-in (GAME = 1)
+constexpr int kPgPaddleH = 8, kPgSpeed = 3, kPgOppSpeed = 2, kPgMeX = 56, kPgOppX = 6, kPgAutoServe = 8, kPgWin = 21;
+// state words (PG_SCORE at AT_SCORE's index: the collect kernel accumulates it)
+enum { PG_PADDLE = 0, PG_BX, PG_BY, PG_VX, PG_VY, PG_IN_PLAY, PG_OPP, PG_ME_PTS, PG_OPP_PTS, PG_UNUSED, PG_IDLE,
+       PG_SCORE };
+static_assert(PG_SCORE == AT_SCORE, "score word");
+
+__device__ inline void pg_reset(int32_t *s, PhiloxStream &rs) {
+  const uint4 r = rs.next();
+  for (int k = 0; k < kAtStateWords; ++k) s[k] = 0;
+  const int span = kAtHW - 2 * kAtWall - kPgPaddleH + 1;
+  s[PG_PADDLE] = kAtWall + (int)(r.x % (uint32_t)span);
+  s[PG_OPP] = kAtWall + (int)(r.y % (uint32_t)span);
+}
+
+__device__ inline int pg_clamp_paddle(int y) {
+  return y < kAtWall ? kAtWall : (y > kAtHW - kAtWall - kPgPaddleH ? kAtHW - kAtWall - kPgPaddleH : y);
+}
+
+// the ball's vertical speed after a paddle hit at offset off of the ball's centre from the paddle's
+__device__ inline int pg_bounce_vy(int off) { return off < -2 ? -2 : (off < 0 ? -1 : (off < 2 ? 1 : 2)); }
+
+// One env step of the Pong stand-in: returns the points (+1 agent, -1 opponent); *terminated at 21 points.
+__device__ inline float pg_step(int32_t *s, int action, PhiloxStream &rs, bool *terminated) {
+  *terminated = false;
+  const bool up = action == 2 || action == 4, down = action == 3 || action == 5;
+  const bool fire = action == 1 || action == 4 || action == 5;
+  const int py = pg_clamp_paddle(s[PG_PADDLE] + (up ? -kPgSpeed : 0) + (down ? kPgSpeed : 0));
+  s[PG_PADDLE] = py;
+  if (!s[PG_IN_PLAY]) {
+    s[PG_IDLE] += 1;
+    if (!fire && s[PG_IDLE] < kPgAutoServe) return 0.0f;
+    s[PG_IDLE] = 0;
+    const uint4 r = rs.next();
+    s[PG_IN_PLAY] = 1;
+    s[PG_BX] = kAtHW / 2 - 1;
+    s[PG_BY] = kAtHW / 2 - 1;
+    s[PG_VX] = (r.x & 1) ? 1 : -1;
+    s[PG_VY] = (r.x & 2) ? 1 : -1;
+    return 0.0f;
+  }
+  float pts = 0.0f;
+  int x = s[PG_BX], y = s[PG_BY], vx = s[PG_VX], vy = s[PG_VY], oy = s[PG_OPP];
+  for (int sub = 0; sub < kAtSub; ++sub) {
+    // the opponent tracks the ball's centre
+    const int oc = oy + kPgPaddleH / 2, bc = y + 1;
+    oy = pg_clamp_paddle(oy + (bc > oc + 1 ? kPgOppSpeed : (bc < oc - 1 ? -kPgOppSpeed : 0)));
+    int nx = x + vx, ny = y + vy;
+    if (ny < kAtWall) { ny = kAtWall; vy = -vy; }
+    if (ny > kAtHW - kAtWall - 2) { ny = kAtHW - kAtWall - 2; vy = -vy; }
+    if (vx > 0 && nx + 1 >= kPgMeX && nx <= kPgMeX + 1 && ny + 1 >= py && ny <= py + kPgPaddleH - 1) {
+      vy = pg_bounce_vy((ny + 1) - (py + kPgPaddleH / 2));
+      vx = -vx;
+      nx = kPgMeX - 2;
+    } else if (vx < 0 && nx <= kPgOppX + 1 && nx + 1 >= kPgOppX && ny + 1 >= oy && ny <= oy + kPgPaddleH - 1) {
+      vy = pg_bounce_vy((ny + 1) - (oy + kPgPaddleH / 2));
+      vx = -vx;
+      nx = kPgOppX + 2;
+    }
+    x = nx;
+    y = ny;
+    if (x < 0 || x > kAtHW - 2) {  // a point: the ball passed a paddle
+      const bool mine = x < 0;
+      pts = mine ? 1.0f : -1.0f;
+      s[mine ? PG_ME_PTS : PG_OPP_PTS] += 1;
+      s[PG_IN_PLAY] = 0;
+      *terminated = s[PG_ME_PTS] >= kPgWin || s[PG_OPP_PTS] >= kPgWin;
+      break;
+    }
+  }
+  s[PG_BX] = x; s[PG_BY] = y; s[PG_VX] = vx; s[PG_VY] = vy; s[PG_OPP] = oy;
+  return pts;
+}
+
+__device__ inline void pg_render16(const int32_t *s, int tid, uint8_t px[16]) {
+  const int y = tid >> 2, x0 = (tid & 3) * 16;
+  const int py = s[PG_PADDLE], oy = s[PG_OPP], bx = s[PG_BX], by = s[PG_BY], inp = s[PG_IN_PLAY];
+  for (int j = 0; j < 16; ++j) {
+    const int x = x0 + j;
+    uint8_t v = 87;  // court
+    if (y < kAtWall || y >= kAtHW - kAtWall) v = 236;
+    if (x >= kPgMeX && x < kPgMeX + 2 && y >= py && y < py + kPgPaddleH) v = 147;
+    if (x >= kPgOppX && x < kPgOppX + 2 && y >= oy && y < oy + kPgPaddleH) v = 130;
+    if (inp && x >= bx && x < bx + 2 && y >= by && y < by + 2) v = 236;
+    px[j] = v;
+  }
+}
+
+template <int GAME>
+__device__ inline void game_reset(int32_t *s, PhiloxStream &rs) {
+  if constexpr (GAME == 1) pg_reset(s, rs); else at_reset(s, rs);
+}
+template <int GAME>
+__device__ inline float game_step(int32_t *s, int action, PhiloxStream &rs, bool *terminated) {
+  if constexpr (GAME == 1) return pg_step(s, action, rs, terminated); else return at_step(s, action, rs, terminated);
+}
+template <int GAME>
+__device__ inline void game_render16(const int32_t *s, int tid, uint8_t px[16]) {
+  if constexpr (GAME == 1) pg_render16(s, tid, px); else at_render16(s, tid, px);
+}
+
+template <int GAME>
 __global__ void __launch_bounds__(kAtThreads) atari_reset_kernel(int n, int32_t *state, int32_t *steps, uint8_t *cur,
                                                                  float *obs, uint32_t seed) {
   const int i = blockIdx.x, tid = threadIdx.x;
   __shared__ int32_t s[kAtStateWords];
   if (tid == 0) {
     PhiloxStream rs{seed, (uint32_t)i, 0xffffffffu, 0xffffffffu, 5u, 0u};
-    at_reset(s, rs);
+    game_reset<GAME>(s, rs);
     for (int k = 0; k < kAtStateWords; ++k) state[(size_t)i * kAtStateWords + k] = s[k];
     steps[i] = 0;
   }
   __syncthreads();
   uint8_t px[16];
-  at_render16(s, tid, px);
+  game_render16<GAME>(s, tid, px);
   reinterpret_cast<uint4 *>(cur + (size_t)i * kAtPix)[tid] = at_pack16(px);
   float *ob = obs + (size_t)i * kAtStack * kAtPix;
   for (int k = 0; k < kAtStack; ++k) at_store_obs16(ob, k, tid, px);  // the reset window: 4 x the first frame
 }
 
+template <int GAME>
 __global__ void __launch_bounds__(kAtThreads) atari_collect_kernel(AtariArgs p) {
   const int i = blockIdx.x, tid = threadIdx.x;
   __shared__ int32_t s1[kAtStateWords], s0[kAtStateWords];
@@ -248,9 +359,9 @@ __global__ void __launch_bounds__(kAtThreads) atari_collect_kernel(AtariArgs p) 
     bool terminated = false;
     // ClipRewardWrapper (the collector env's clip_rewards=True, atari_lightzero_env.py:57): sign(points);
     // the unclipped points add up to the episode's return, the env's eval_episode_return
-    const float points = at_step(s1, action, rg, &terminated);
+    const float points = game_step<GAME>(s1, action, rg, &terminated);
     s1[AT_SCORE] += (int32_t)points;
-    const float reward = points > 0.0f ? 1.0f : 0.0f;
+    const float reward = points > 0.0f ? 1.0f : (points < 0.0f ? -1.0f : 0.0f);
     const int nt = t + 1;
     const bool done = terminated || nt >= p.max_steps;
     if (t < p.T) p.rec_reward[slot * p.T + t] = reward;
@@ -259,7 +370,7 @@ __global__ void __launch_bounds__(kAtThreads) atari_collect_kernel(AtariArgs p) 
       if (p.ep_return) p.ep_return[slot] = (float)s1[AT_SCORE];
       p.ep_count[i] += 1;
       PhiloxStream rr{p.seed, (uint32_t)i, (uint32_t)step, (uint32_t)(step >> 32), 3u, 0u};
-      at_reset(s0, rr);
+      game_reset<GAME>(s0, rr);
       p.steps[i] = 0;
       for (int k = 0; k < kAtStateWords; ++k) p.state[(size_t)i * kAtStateWords + k] = s0[k];
     } else {
@@ -287,7 +398,7 @@ __global__ void __launch_bounds__(kAtThreads) atari_collect_kernel(AtariArgs p) 
   // the frame the search saw (o_t) into the episode slot
   if (t < p.T) rec[(size_t)t * (kAtPix / 16) + tid] = cur[tid];
   uint8_t px[16];
-  at_render16(s1, tid, px);  // o_{t+1}
+  game_render16<GAME>(s1, tid, px);  // o_{t+1}
   float *ob = p.obs + (size_t)i * kAtStack * kAtPix;
   if (!sh_done) {
     cur[tid] = at_pack16(px);
@@ -299,7 +410,7 @@ __global__ void __launch_bounds__(kAtThreads) atari_collect_kernel(AtariArgs p) 
     at_store_obs16(ob, kAtStack - 1, tid, px);
   } else {
     if (nt <= p.T) rec[(size_t)nt * (kAtPix / 16) + tid] = at_pack16(px);  // the episode's final frame
-    at_render16(s0, tid, px);  // the next episode's first frame
+    game_render16<GAME>(s0, tid, px);  // the next episode's first frame
     cur[tid] = at_pack16(px);
     for (int k = 0; k < kAtStack; ++k) at_store_obs16(ob, k, tid, px);
   }

@@ -24,6 +24,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include "lzm_tree.h"
 
 namespace lzm {
 
@@ -39,7 +42,7 @@ constexpr int kCvBlock = 2 * kCv3Frag + 2 * kCvCh;  // basic block: W1 frag, b1,
 typedef float cvf16 __attribute__((ext_vector_type(16)));
 
 struct ConvTrunkLayout {
-  int dyn, dres, rw, rb, pres, hw, hb, total;
+  int dyn, dres, rw, rb, pres, hw, hb, sc, bd, total;  // sc, bd: the split layout's scales and bounds (below)
 };
 
 __host__ __device__ inline ConvTrunkLayout conv_trunk_layout(int n_dres, int n_pres) {
@@ -52,6 +55,7 @@ __host__ __device__ inline ConvTrunkLayout conv_trunk_layout(int n_dres, int n_p
   L.pres = o; o += n_pres * kCvBlock;
   L.hw = o; o += kCv1Frag;
   L.hb = o; o += 32;
+  L.sc = L.bd = -1;
   L.total = o;
   return L;
 }
@@ -71,6 +75,8 @@ struct ConvTrunkArgs {
   int H;                 // is copied to out_r[b][r_ch * 64 ..] (the [r | h] LSTM input row, no gather launch)
   int skip_dyn;          // 1: no dynamics conv — the input runs straight into the residual blocks, and no
                          // reward 1x1 (lzm_conv_resnet8_p: the representation network's 8 x 8 tail)
+  int32_t *err;          // nullable: counts envs whose split activations left the fp16 range (split trunk)
+  int32_t *xscale;       // with hpool: [B] the LSTM input row's scale exponent (lzm_lstm.h, ls_row_exp)
 };
 
 // [r | h] LSTM input row: the leaf's hidden state after the reward planes (every thread calls it)
@@ -219,24 +225,35 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 // Split trunk (precision 1, the default): the same network on v_mfma_f32_16x16x32_f16.
 //
 // Every f32 operand x is held as two fp16 terms x = h + l (h = fp16(x), l = fp16(x - h); the subtraction
-// is exact, so h + l carries 22 significant bits: |x - h - l| <= 2^-22 |x|). A product is summed from
-// the three terms l_a h_b, h_a l_b, h_a h_b (the dropped l l term is <= 2^-22 relative): f32-level
-// error for values inside fp16's range (|x| < 65504; below 2^-14 the terms are fp16 subnormals, an
-// absolute error of at most 2^-25). The fp16 matrix rate is 16x the f32 one (MI355X_MICROARCH.md
-// constants: 16x16x32 16 cycles vs 32x32x2 f32 64 cycles, 16x the K), so three products per K are
-// 5.3x fewer matrix cycles than the exact-f32 kernel above, and half those of the three-term bf16 split
-// (six products: l h, h l, m m, m h, h m, h h) this trunk ran through round 5 (bx_split / bx_split_d
-// below, kept for tests and comparisons).
+// is exact). A product is summed from the three terms l_a h_b, h_a l_b, h_a h_b (the dropped l l term is
+// <= 2^-22 relative). The fp16 matrix rate is 16x the f32 one (MI355X_MICROARCH.md constants: 16x16x32 16
+// cycles vs 32x32x2 f32 64 cycles, 16x the K), so three products per K are 5.3x fewer matrix cycles than the
+// exact-f32 kernel above.
+//
+// Range. fp16 holds |x| < 65504, and h + l keeps 22 significant bits only while l is a normal fp16 (|x| >=
+// 2^-3); below that the split's error is an absolute 2^-25. So no operand is split as it is:
+//   * weights: out channel c's row is packed as W_c 2^e_c, e_c = 14 - floor(log2 max_k |W_c,k|) (the row's
+//     largest |w| in [2^14, 2^15)), clamped to +-kBxWExp; the epilogue multiplies by 2^-e_c, exactly;
+//   * activations: each stored activation tensor (one env's 64 planes of one layer) as x 2^s, s = 14 -
+//     floor(log2 bound), clamped to +-kBxAExp, with bound >= max |x| from what is known before the epilogue
+//     stores it: the exact max of the layer's input M_in (each wave's max of its outputs meets the others'
+//     in LDS at the barrier that follows every epilogue), the layer's packed bounds Wb = max_c sum_k |W_c,k|
+//     and Bb = max_c |b_c| (the dynamics conv: max |actmap|), and the residual's exact max: bound = Wb M_in
+//     + Bb (+ M_res). The input latent is scaled from its own exact max (one more barrier per step).
+// A power of two commutes with fp16 and f32 rounding, so where the unscaled split was in range every term,
+// product and sum is the same; elsewhere the split keeps its 22 bits down to 2^-17 below the tensor's
+// bound. Every stored tensor's exact max is checked against its scale (max 2^s < 65504, and finite; only
+// a non-finite value or one beyond ~2^114 can fail it) and a failure counts in the caller's error word
+// (lzm_check_errors: LZM_ERR_RANGE). ReLUs propagate NaN (x < 0 ? 0 : x), as torch's do.
 //
 // Layout. Wave w owns out-channels 16w..16w+15 for all 64 pixels (four 16-pixel M tiles), so the four
-// waves stream disjoint weights (221 KB per 3x3 layer per workgroup, vs 295 KB when two waves of
-// the f32 tiling share a half). K = tap-major (9 taps) x 64 in-channels, in 18 chunks of 32.
-// Activations live in LDS as the two fp16 planes of each buffer, [100 bordered positions][64 ch],
-// 16-B chunk c of position ps stored at chunk c ^ ((ps % 10) & 7): the A-fragment reads (lane:
-// pixel l&15 of the tile, channels 8(l>>4)..+7 of the chunk, one ds_read_b128) are then
-// conflict-free for every tap (checked over the four lane groups of ds_read_b128).
+// waves stream disjoint weights (221 KB per 3x3 layer per workgroup). K = tap-major (9 taps) x 64
+// in-channels, in 18 chunks of 32. Activations live in LDS as the two fp16 planes of each buffer,
+// [100 bordered positions][64 ch], 16-B chunk c of position ps stored at chunk c ^ ((ps % 10) & 7): the
+// A-fragment reads (lane: pixel l&15 of the tile, channels 8(l>>4)..+7 of the chunk, one ds_read_b128)
+// are then conflict-free for every tap (checked over the four lane groups of ds_read_b128).
 // B fragments come from the host-packed [wave][chunk][term][lane][8 fp16] layout, one 1 KiB
-// dwordx4 wave-load per term, a ring of kBxRing chunks issued kBxAhead ahead.
+// dwordx4 wave-load per term, a ring of AHEAD + 1 chunks issued AHEAD ahead.
 constexpr int kBxTerms = 2;                        // fp16 terms per f32 operand (h, l)
 constexpr int kBxComp = 100 * 64;                  // 16-bit elements per term plane
 constexpr int kBxBuf = kBxTerms * kBxComp;         // per activation buffer (h, l planes); two buffers
@@ -247,28 +264,35 @@ constexpr int kBxAhead = 3;  // default weight read-ahead (chunks)
 // the EZ search's read-ahead: with fp16 terms (two uint4s per chunk) 5 chunks fit its registers and measured
 // 2.49 -> 2.46 ms per Pong search; the Breakout search even at 2, 3, 4, 5 (profiles/r05/ab/ab_ahead.txt)
 constexpr int kBxAheadEz = 5;
+constexpr int kBxWExp = 24;   // weight-row scale exponents within +-24
+constexpr int kBxAExp = 100;  // activation scale exponents within +-100: 2^-(e + s) stays a normal f32
 
-typedef __bf16 bxv8 __attribute__((ext_vector_type(8)));
 typedef _Float16 bxh8 __attribute__((ext_vector_type(8)));
 typedef float bxf4 __attribute__((ext_vector_type(4)));
 
-__host__ __device__ inline uint16_t bx_rn(float x) {  // f32 -> bf16, round to nearest even (finite x)
-  uint32_t u;
-  memcpy(&u, &x, 4);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-__host__ __device__ inline float bx_f(uint16_t h) {
-  const uint32_t u = (uint32_t)h << 16;
+// 2^n for |n| <= 126
+__host__ __device__ inline float bx_pow2(int n) {
+  const uint32_t u = (uint32_t)(127 + n) << 23;
   float x;
   memcpy(&x, &u, 4);
   return x;
 }
-__host__ __device__ inline void bx_split(float x, uint16_t &h, uint16_t &m, uint16_t &l) {
-  h = bx_rn(x);
-  const float r = x - bx_f(h);
-  m = bx_rn(r);
-  l = bx_rn(r - bx_f(m));
+// floor(log2 |x|) from the exponent field (0 and subnormals -> -127, inf / NaN -> 128)
+__host__ __device__ inline int bx_ilog2(float x) {
+  uint32_t u;
+  memcpy(&u, &x, 4);
+  return (int)((u >> 23) & 0xffu) - 127;
+}
+// the scale exponent that puts `bound` in [2^14, 2^15), clamped to +-lim
+__host__ __device__ inline int bx_scale_exp(float bound, int lim) {
+  const int s = 14 - bx_ilog2(bound);
+  return s < -lim ? -lim : (s > lim ? lim : s);
+}
+
+// the scale exponent of an EfficientZero LSTM input row [reward planes | h] from the exact max of its reward
+// planes (|h| < 1: the bound is max(M_r, 1); lzm_lstm.h)
+__host__ __device__ inline int ls_row_exp(float reward_max) {
+  return bx_scale_exp(reward_max > 1.f || reward_max != reward_max ? reward_max : 1.f, kBxAExp);
 }
 
 // the trunk's split: x = h + l, h = fp16(x), l = fp16(x - h) (x - h exact in f32), round to nearest even
@@ -277,17 +301,6 @@ __host__ __device__ inline void bx_split2(float x, uint16_t &h, uint16_t &l) {
   const _Float16 ll = (_Float16)(x - (float)hh);
   h = __builtin_bit_cast(uint16_t, hh);
   l = __builtin_bit_cast(uint16_t, ll);
-}
-
-// the three-term bf16 split on the device with the hardware conversion (v_cvt_pk_bf16_f32, round to nearest even)
-__device__ __forceinline__ void bx_split_d(float x, uint16_t &h, uint16_t &m, uint16_t &l) {
-  const __bf16 hb = (__bf16)x;
-  const float r = x - (float)hb;
-  const __bf16 mb = (__bf16)r;
-  const __bf16 lb = (__bf16)(r - (float)mb);
-  h = __builtin_bit_cast(uint16_t, hb);
-  m = __builtin_bit_cast(uint16_t, mb);
-  l = __builtin_bit_cast(uint16_t, lb);
 }
 
 __host__ __device__ inline ConvTrunkLayout conv_trunk_layout_p(int n_dres, int n_pres, int precision) {
@@ -301,27 +314,13 @@ __host__ __device__ inline ConvTrunkLayout conv_trunk_layout_p(int n_dres, int n
   L.pres = o; o += n_pres * kBxBlock;
   L.hw = o; o += kBx1Frag;
   L.hb = o; o += 32;
+  const int n3 = 1 + 2 * (n_dres + n_pres);
+  L.sc = o; o += (n3 + 2) * 64;  // 2^-e_c per layer: the 3x3 layers in order, the reward 1x1, the head 1x1
+  L.bd = o; o += (n3 + 2) * 4;   // {Wb, Bb, 0, 0} per layer, same order
   L.total = o;
   return L;
 }
 
-// element offset (16-bit elements) of (bordered position ps, channel c) inside one term plane
-__device__ __forceinline__ int bx_at(int ps, int c) { return ps * 64 + ((((c >> 3) ^ (ps % 10)) & 7) << 3) + (c & 7); }
-
-__device__ __forceinline__ float bx_load(const uint16_t *buf, int ps, int c) {
-  const int o = bx_at(ps, c);
-  return (float)__builtin_bit_cast(_Float16, buf[o]) + (float)__builtin_bit_cast(_Float16, buf[kBxComp + o]);
-}
-
-__device__ __forceinline__ void bx_store(uint16_t *buf, int ps, int c, float v) {
-  uint16_t h, l;
-  bx_split2(v, h, l);
-  const int o = bx_at(ps, c);
-  buf[o] = h;
-  buf[kBxComp + o] = l;
-}
-
-__device__ __forceinline__ bxv8 bx_as(uint4 u) { return __builtin_bit_cast(bxv8, u); }
 __device__ __forceinline__ bxh8 bx_ash(uint4 u) { return __builtin_bit_cast(bxh8, u); }
 
 // Weight ring of one wave: RING chunks x the terms (one uint4 per lane each).
@@ -344,23 +343,26 @@ __device__ __forceinline__ void bx_prefetch(BxRing<AHEAD> &r, const uint4 *__res
   for (int s = 0; s < (NCH < AHEAD ? NCH : AHEAD); ++s) bx_load_w<AHEAD, DIAG>(r, wf, s, lane);
 }
 
+struct BxNoHook {
+  __device__ void operator()() const {}
+};
+
 // one convolution for this wave's 16 out-channels x 64 pixels: NCH = 18 chunks (3x3) or 2 (1x1), its
 // first AHEAD chunks already in the ring (bx_prefetch). DIAG = 1: no weight loads (timing
 // experiments only, results invalid). Software pipeline, in issue order (the scheduling barriers keep
 // the compiler from sinking loads next to their first use): weights of chunk s + AHEAD, activations
-// of chunk s + 1, then chunk s's 24 MFMAs.
-// S0: index of the first chunk within the 18 of a 3x3 layer (the two-waves-per-SIMD kernel splits K;
-// wf then points at chunk S0's weights)
-template <int NCH, int AHEAD, int DIAG, int S0 = 0>
+// of chunk s + 1, then chunk s's 12 MFMAs. hook(): VALU work run in chunk 1's MFMA shadow (the range
+// bookkeeping's wave reduction).
+template <int NCH, int AHEAD, int DIAG, class Hook = BxNoHook>
 __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restrict__ wf, BxRing<AHEAD> &r, int lane,
-                                        bxf4 (&acc)[4]) {
+                                        bxf4 (&acc)[4], const Hook &hook = Hook()) {
   uint4 a[2][4][kBxTerms];
   const int px = lane & 7, g = lane >> 4;
   // lane's pixel in tile t: p = 16t + (lane & 15), plane row py = 2t + ((lane >> 3) & 1), column px; tap
   // (dy, dx) reads bordered position (py + dy) * 10 + px + dx
   const int lbase = ((lane >> 3) & 1) * 10 + px;
   auto load_a = [&](int s) {
-    const int tap = NCH == 2 ? 4 : (S0 + s) >> 1, j = NCH == 2 ? s : (S0 + s) & 1;
+    const int tap = NCH == 2 ? 4 : s >> 1, j = NCH == 2 ? s : s & 1;
     const int dy = tap / 3, dx = tap % 3;
     const int chunk = ((4 * j + g) ^ (px + dx)) & 7;
 #pragma unroll
@@ -388,6 +390,7 @@ __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restr
     for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(x[t][0]), bx_ash(w[1]), acc[t], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(x[t][0]), bx_ash(w[0]), acc[t], 0, 0, 0);
+    if (s == (NCH > 1 ? 1 : 0)) hook();
     // issue the next chunks' loads in the MFMA gaps (an MFMA holds the vector issue for half its
     // cycles): weights first (they have the longest way), then one activation read per MFMA
     const int nw = (s + AHEAD < NCH && DIAG != 1) ? kBxTerms : 0, na = s + 1 < NCH ? 4 * kBxTerms : 0;
@@ -415,28 +418,32 @@ __device__ __forceinline__ int bx_ep_pos(int lane, int t, int r) {
   return (2 * t + (lane >> 5) + 1) * 10 + 4 * ((lane >> 4) & 1) + r + 1;
 }
 
-// 3x3 epilogue: v = relu(acc + bias [+ amap] [+ xres]) -> split LDS planes of `out`; KEEP: xres = v
-// tiles T0 .. T0 + NT - 1 (xres / am hold those tiles only)
-// RELU = false: store acc as is (the input latent's staging)
-template <int T0 = 0, int NT = 4, bool RELU = true>
-__device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out, float bc, bool use_am,
-                                             const float4 (&am)[NT], float (&xres)[4 * NT], bool add_res, bool keep,
-                                             int lane, int c) {
+// 3x3 epilogue: v = relu(acc f + bias [+ amap] [+ xres]) (f = 2^-(e_c + s_in): the weight row's and the input's
+// scales undone) -> the split planes of `out` as v 2^s_out (so = 2^s_out); KEEP: xres = v. Returns the max of
+// this lane's |v| as bits (NaN above every finite value) for the output's range bookkeeping.
+// RELU = false: store acc as is (the input latent's staging; f = 1, bias 0)
+template <bool RELU = true>
+__device__ __forceinline__ uint32_t bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out, float f, float bc, bool use_am,
+                                                 const float4 (&am)[4], float (&xres)[16], bool add_res, bool keep,
+                                                 float so, int lane, int c) {
   typedef float bxf2 __attribute__((ext_vector_type(2)));
   typedef _Float16 bxb2 __attribute__((ext_vector_type(2)));
   const int cb = c >> 3, odd = lane & 1;
+  uint32_t mx = 0;
 #pragma unroll
-  for (int t = T0; t < T0 + NT; ++t) {
+  for (int t = 0; t < 4; ++t) {
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float x = acc[t][r] + bc;
-      if (use_am) x += r == 0 ? am[t - T0].x : r == 1 ? am[t - T0].y : r == 2 ? am[t - T0].z : am[t - T0].w;
-      if (add_res) x += xres[4 * (t - T0) + r];
-      if (RELU) x = x > 0.f ? x : 0.f;
-      if (keep) xres[4 * (t - T0) + r] = x;
+      float x = RELU ? __fmaf_rn(acc[t][r], f, bc) : acc[t][r];
+      if (use_am) x += r == 0 ? am[t].x : r == 1 ? am[t].y : r == 2 ? am[t].z : am[t].w;
+      if (add_res) x += xres[4 * t + r];
+      if (RELU) x = x < 0.f ? 0.f : x;  // (NaN stays NaN)
+      if (keep) xres[4 * t + r] = x;
       v[r] = x;
     }
+    mx = max(mx, max(max(__float_as_uint(v[0]) & 0x7fffffffu, __float_as_uint(v[1]) & 0x7fffffffu),
+                     max(__float_as_uint(v[2]) & 0x7fffffffu, __float_as_uint(v[3]) & 0x7fffffffu)));
     // lanes 2j, 2j + 1 hold channels c, c + 1 (one dword of a plane row): per pixel pair (2k, 2k + 1)
     // the even lane writes pixel 2k's dword and the odd lane pixel 2k + 1's, after one DPP swap
 #pragma unroll
@@ -444,7 +451,7 @@ __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out
       const float send = odd ? v[2 * k] : v[2 * k + 1];
       const float recv = __builtin_bit_cast(
           float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-      const bxf2 pr = odd ? bxf2{recv, v[2 * k + 1]} : bxf2{v[2 * k], recv};  // (channel c & ~1, channel c | 1)
+      const bxf2 pr = (odd ? bxf2{recv, v[2 * k + 1]} : bxf2{v[2 * k], recv}) * so;  // (channel c & ~1, c | 1)
       const bxb2 h = __builtin_convertvector(pr, bxb2);
       const bxb2 l = __builtin_convertvector(pr - __builtin_convertvector(h, bxf2), bxb2);
       const int r = 2 * k + odd;
@@ -455,29 +462,98 @@ __device__ __forceinline__ void bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out
       *reinterpret_cast<bxb2 *>(out + kBxComp + o) = l;
     }
   }
+  return mx;
 }
 
-// 1x1 layer (<= 32 out channels, waves 0 and 1): relu(conv + b) -> global [c][p]
-// (SC1: 16-B sc1 buffer stores, for planes another CU reads in the same launch)
+// the layers' bounds {Wb, Bb, 0, 0} into LDS once per launch (read per layer without a scalar load in the way of
+// the LDS counter); nl = n3 + 2 <= kBxMaxLayers
+constexpr int kBxMaxLayers = 1 + 2 * 16 + 2;
+__device__ __forceinline__ void bx_stage_bounds(float4 *s_bd, const float *w, const ConvTrunkLayout &L, int nl, int tid,
+                                                int nthreads) {
+  for (int i = tid; i < nl; i += nthreads) s_bd[i] = reinterpret_cast<const float4 *>(w + L.bd)[i];
+}
+
+// Range bookkeeping of one workgroup's trunk (every wave holds the same copy): the exact max |x| of the
+// current layer input and of the current block input, the input buffer's scale exponent, a sticky failure.
+// Per layer: the epilogue writes each lane's max (bits) to LDS, unreduced; after the barrier every wave reads
+// four of the 256 and reduces them inside the next convolution's MFMA stream (bx_conv's hook): the max of a
+// layer's output is first needed for the NEXT layer's output scale.
+struct BxRange {
+  float m_in, m_blk;
+  int s_in, bad;
+  uint4 lm;  // this lane's four of the previous epilogue's 256 lane maxima (read after the barrier)
+};
+
+// this wave's max (lane maxima as bits) into its LDS slot; read back after the next barrier (bx_read_max)
+__device__ __forceinline__ void bx_post_max(uint32_t *slot, uint32_t mx, int wv, int lane) {
+  mx = (uint32_t)xor_max((int)mx);  // (bits of |x| <= 0x7fffffff: the signed max is the unsigned one)
+  if (lane == 0) slot[wv] = mx;
+}
+__device__ __forceinline__ float bx_read_max(const uint32_t *slot) {
+  const uint4 v = *reinterpret_cast<const uint4 *>(slot);
+  return __uint_as_float(max(max(v.x, v.y), max(v.z, v.w)));
+}
+// the max |x| of a latent of this lane's 16 values; one barrier (every thread)
+__device__ __forceinline__ float bx_latent_max(const float (&xres)[16], uint32_t *slot, int wv, int lane) {
+  uint32_t mx = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) mx = max(mx, __float_as_uint(xres[j]) & 0x7fffffffu);
+  bx_post_max(slot, mx, wv, lane);
+  __syncthreads();
+  return bx_read_max(slot);
+}
+// the input latent of exact max m: its scale
+__device__ __forceinline__ BxRange bx_range_input(float m) {
+  BxRange rg;
+  rg.m_in = rg.m_blk = m;
+  rg.s_in = bx_scale_exp(m, kBxAExp);
+  rg.bad = !(m * bx_pow2(rg.s_in) < 65504.f);
+  rg.lm = uint4{0u, 0u, 0u, 0u};
+  return rg;
+}
+// the output scale of a 3x3 layer from its packed bounds bd = {Wb, Bb}; res: + the block input (the dynamics
+// conv: + the latent). A block's first conv makes its input the block input.
+__device__ __forceinline__ int bx_layer_scale(const float4 bd, bool res, BxRange &rg) {
+  if (!res) rg.m_blk = rg.m_in;
+  float bound = bd.x * rg.m_in + bd.y;
+  if (res) bound += rg.m_blk;
+  return bx_scale_exp(bound, kBxAExp);
+}
+// after the barrier that follows an epilogue storing at scale s_out: this lane's four lane maxima (slots[256])
+__device__ __forceinline__ void bx_range_fetch(BxRange &rg, const uint32_t *slots, int s_out, int lane) {
+  rg.lm = reinterpret_cast<const uint4 *>(slots)[lane];
+  rg.s_in = s_out;
+}
+// ... reduced (bx_conv's hook, or directly): the layer input's exact max, checked against its scale
+__device__ __forceinline__ void bx_range_reduce(BxRange &rg) {
+  const uint32_t m = (uint32_t)xor_max((int)max(max(rg.lm.x, rg.lm.y), max(rg.lm.z, rg.lm.w)));
+  const float M = __uint_as_float(m);
+  rg.bad |= !(M * bx_pow2(rg.s_in) < 65504.f);
+  rg.m_in = M;
+}
+
+// 1x1 layer (<= 32 out channels, waves 0 and 1): relu(conv x inv[c] 2^-s_in + b) -> global [c][p]
+// (SC1: 16-B sc1 buffer stores, for planes another CU reads in the same launch); returns the lane's max |v| (bits)
 template <int DIAG, bool SC1 = false>
-__device__ __forceinline__ void bx_conv1_layer(const uint16_t *in, const float *__restrict__ wl,
-                                               const float *__restrict__ bias, int nch, float *dst, int lane,
-                                               int wv) {
+__device__ __forceinline__ uint32_t bx_conv1_layer(const uint16_t *in, const float *__restrict__ wl,
+                                               const float *__restrict__ bias, const float *__restrict__ inv,
+                                               float sinv, int nch, float *dst, int lane, int wv) {
   BxRing<2> r1;
   const uint4 *wf = reinterpret_cast<const uint4 *>(wl) + wv * 2 * kBxTerms * 64;
   bx_prefetch<2, 2, DIAG>(r1, wf, lane);
   const int c = 16 * wv + (lane & 15);
-  const float bc = c < nch ? bias[c] : 0.f;
+  const float bc = c < nch ? bias[c] : 0.f, f = c < nch ? inv[c] * sinv : 0.f;
   bxf4 acc[4];
   bx_conv<2, 2, DIAG>(in, wf, r1, lane, acc);
-  if (c >= nch) return;
+  if (c >= nch) return 0u;
+  auto relu = [&](float x) { x = __fmaf_rn(x, f, bc); return x < 0.f ? 0.f : x; };
+  uint32_t mx = 0;
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    float4 v;
-    v.x = fmaxf(acc[t][0] + bc, 0.f);
-    v.y = fmaxf(acc[t][1] + bc, 0.f);
-    v.z = fmaxf(acc[t][2] + bc, 0.f);
-    v.w = fmaxf(acc[t][3] + bc, 0.f);
+    const float4 v = float4{relu(acc[t][0]), relu(acc[t][1]), relu(acc[t][2]), relu(acc[t][3])};
+    mx = max(max(mx, __float_as_uint(v.x) & 0x7fffffffu),
+             max(__float_as_uint(v.y) & 0x7fffffffu, max(__float_as_uint(v.z) & 0x7fffffffu,
+                                                         __float_as_uint(v.w) & 0x7fffffffu)));
     if constexpr (SC1) {
       typedef unsigned u4v __attribute__((ext_vector_type(4)));
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, nch * kCvPix * 4, 0x00020000);
@@ -487,6 +563,7 @@ __device__ __forceinline__ void bx_conv1_layer(const uint16_t *in, const float *
       *reinterpret_cast<float4 *>(dst + c * kCvPix + 16 * t + 4 * (lane >> 4)) = v;
     }
   }
+  return mx;
 }
 
 // The 3x3 layers in order: 0 = dynamics conv, then two per residual block (dynamics blocks, then
@@ -498,21 +575,35 @@ __device__ __forceinline__ int bx_layer_off(const ConvTrunkLayout &L, int n_dres
   return base + (k >> 1) * kBxBlock + (k & 1) * (kBx3Frag + kCvCh);
 }
 
-template <int AHEAD, int DIAG>
+// zero the 36 border positions of both buffers' term planes ([buffer][term][border position][16-B chunk])
+__device__ __forceinline__ void bx_zero_borders(uint4 *lds4, int tid, int nthreads) {
+  for (int k = tid; k < 2 * kBxTerms * 36 * 8; k += nthreads) {
+    const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
+    const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
+    lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
+  }
+}
+
+template <int AHEAD>
 __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_trunk_bx_kernel(
     ConvTrunkArgs a) {
   extern __shared__ uint4 bx_lds4[];
+  __shared__ uint32_t s_mx[4], s_rmx[2], s_lm[2][kCvThreads];
+  __shared__ float4 s_bd[kBxMaxLayers];
   uint16_t *lds = reinterpret_cast<uint16_t *>(bx_lds4);
   auto buf = [&](int i) { return lds + i * kBxBuf; };
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int c = 16 * wv + (lane & 15);
   const ConvTrunkLayout L = conv_trunk_layout_p(a.n_dres, a.n_pres, 1);
   const int n3 = 1 + 2 * a.n_dres + 2 * a.n_pres;
+  const float *inv = a.w + L.sc;
+  const float4 *bd = s_bd;
+  bx_stage_bounds(s_bd, a.w, L, n3 + 2, tid, kCvThreads);  // (ordered by the first barrier)
   auto layer_w = [&](int i) { return a.w + bx_layer_off(L, a.n_dres, i); };
   auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   const int i0 = a.skip_dyn ? 1 : 0;  // the first layer run (skip_dyn: the first residual block's)
   BxRing<AHEAD> ring;
-  bx_prefetch<18, AHEAD, DIAG>(ring, wave_stream(layer_w(i0)), lane);
+  bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i0)), lane);
   // the input latent: this lane's 16 values in registers (the dynamics residual, exact f32) ...
   const float *src = a.pool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
   float xres[16];
@@ -522,6 +613,7 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     xres[4 * t] = v.x; xres[4 * t + 1] = v.y; xres[4 * t + 2] = v.z; xres[4 * t + 3] = v.w;
   }
   trunk_copy_hidden(a, b);
+  BxRange rg = bx_range_input(bx_latent_max(xres, s_mx, wv, lane));
   // ... split into buffer 0 from those registers by the epilogue's store path (interior), while the
   // 36 border positions of both buffers are zeroed (disjoint addresses: one barrier)
   {
@@ -529,19 +621,17 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
 #pragma unroll
     for (int t = 0; t < 4; ++t) in4[t] = bxf4{xres[4 * t], xres[4 * t + 1], xres[4 * t + 2], xres[4 * t + 3]};
     const float4 no_am[4] = {};
-    bx_epilogue3<0, 4, false>(in4, buf(i0 & 1), 0.f, false, no_am, xres, false, false, lane, c);
+    bx_epilogue3<false>(in4, buf(i0 & 1), 1.f, 0.f, false, no_am, xres, false, false, bx_pow2(rg.s_in), lane, c);
   }
-  for (int k = tid; k < 2 * kBxTerms * 36 * 8; k += kCvThreads) {  // [buffer][term][border position][16-B chunk]
-    const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
-    const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
-    bx_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
-  }
+  bx_zero_borders(bx_lds4, tid, kCvThreads);
   __syncthreads();
   for (int i = i0; i < n3; ++i) {
     const float *w = layer_w(i);
     const bool second = i > 0 && ((i - 1) & 1);  // a block's second conv: + residual, new block input
     // epilogue operands first (vmcnt counts in order: they must not queue behind the next prefetch)
     const float bc = i ? w[kBx3Frag + c] : 0.f;
+    const float4 bdi = bd[i];
+    const float wsc = inv[i * 64 + c];
     float4 am[4] = {};
     if (i == 0) {
       const float4 *amap = reinterpret_cast<const float4 *>(a.actmap + ((int64_t)a.action[b] * kCvCh + c) * kCvPix);
@@ -549,138 +639,106 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       for (int t = 0; t < 4; ++t) am[t] = amap[4 * t + (lane >> 4)];
     }
     bxf4 acc[4];
-    bx_conv<18, AHEAD, DIAG>(buf(i & 1), wave_stream(w), ring, lane, acc);
-    if (i + 1 < n3) bx_prefetch<18, AHEAD, DIAG>(ring, wave_stream(layer_w(i + 1)), lane);
-    bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
+    const bool gather = i > i0;  // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow
+    bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&]() {
+      if (gather) bx_range_reduce(rg);
+    });
+    if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
+    const int s_out = bx_layer_scale(bdi, i == 0 || second, rg);
+    s_lm[i & 1][tid] = bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
+                                    i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c);
     __syncthreads();
+    bx_range_fetch(rg, s_lm[i & 1], s_out, lane);
     if (i == 2 * a.n_dres) {  // the next latent (registers, exact) and the reward planes
       float *dst = a.out_latent + (int64_t)b * kCvCh * kCvPix + c * kCvPix + 4 * (lane >> 4);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         *reinterpret_cast<float4 *>(dst + 16 * t) = float4{xres[4 * t], xres[4 * t + 1], xres[4 * t + 2], xres[4 * t + 3]};
-      if (!a.skip_dyn && wv < 2)
-        bx_conv1_layer<DIAG>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_stride,
-                             lane, wv);
+      if (!a.skip_dyn && wv < 2) {
+        const uint32_t rm = bx_conv1_layer<0>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, inv + n3 * 64,
+                                              bx_pow2(-rg.s_in), a.r_ch, a.out_r + (int64_t)b * a.r_stride, lane, wv);
+        bx_post_max(s_rmx, rm, wv, lane);
+      }
     }
   }
   if (wv < 2)
-    bx_conv1_layer<DIAG>(buf(n3 & 1), a.w + L.hw, a.w + L.hb, a.h_ch, a.out_h + (int64_t)b * a.h_ch * kCvPix, lane, wv);
+    bx_conv1_layer<0>(buf(n3 & 1), a.w + L.hw, a.w + L.hb, inv + (n3 + 1) * 64, bx_pow2(-rg.s_in), a.h_ch,
+                      a.out_h + (int64_t)b * a.h_ch * kCvPix, lane, wv);
+  bx_range_reduce(rg);  // the last layer's output, checked
+  if (a.xscale) {  // the LSTM input row's scale (every wave reaches this barrier)
+    __syncthreads();
+    if (tid == 0) a.xscale[b] = ls_row_exp(__uint_as_float(max(s_rmx[0], s_rmx[1])));
+  }
+  if (rg.bad && tid == 0 && a.err) atomicAdd(a.err, 1);
 }
 
-// Two waves per SIMD (512 threads): wave w owns out-channel group w & 3 and HALF of K — chunks
-// 9 (w >> 2) .. +8 of every 3x3 layer — so one wave's waits (barriers, vmcnt / lgkmcnt) and
-// epilogue overlap the other's MFMAs (the 4-wave form keeps the matrix pipe busy ≈ 51%). At a layer
-// end the two halves swap partial sums of two tiles each through LDS; the K-half-0 wave finishes
-// tiles 0-1 (epilogue, residual in registers), the K-half-1 wave tiles 2-3. The 1x1 convolutions
-// stay whole on waves 0-1.
-constexpr int kBx2Threads = 512;
-constexpr int kBx2Scratch = 4 * 2 * 64 * 8;  // floats: [group][tile pair][lane][8]
-
-template <int AHEAD>
-__global__ __launch_bounds__(kBx2Threads) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_trunk_bx2_kernel(
-    ConvTrunkArgs a) {
-  extern __shared__ uint4 bx_lds4[];
-  uint16_t *lds = reinterpret_cast<uint16_t *>(bx_lds4);
-  float *scr = reinterpret_cast<float *>(lds + 2 * kBxBuf);
-  auto buf = [&](int i) { return lds + i * kBxBuf; };
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int grp = wv & 3, kh = wv >> 2, t0 = 2 * kh;  // epilogue tiles t0, t0 + 1
-  const int c = 16 * grp + (lane & 15);
-  const ConvTrunkLayout L = conv_trunk_layout_p(a.n_dres, a.n_pres, 1);
-  const int n3 = 1 + 2 * a.n_dres + 2 * a.n_pres;
-  auto layer_w = [&](int i) { return a.w + bx_layer_off(L, a.n_dres, i); };
-  // this wave's chunk stream: group grp, chunks 9 kh ..
-  auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + (grp * 18 + 9 * kh) * kBxTerms * 64; };
-  BxRing<AHEAD> ring;
-  bx_prefetch<9, AHEAD, 0>(ring, wave_stream(a.w + L.dyn), lane);
-  const float *src = a.pool + ((a.x ? (int64_t)max(a.x[b], 0) * a.B : 0) + b) * (int64_t)(kCvCh * kCvPix);
-  float xres[8];  // tiles t0, t0 + 1 of the block input (exact f32)
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * (t0 + u) + 4 * (lane >> 4));
-    xres[4 * u] = v.x; xres[4 * u + 1] = v.y; xres[4 * u + 2] = v.z; xres[4 * u + 3] = v.w;
+// host packing for the split trunk (every weight row scaled, the layer's bounds). 3x3: W[64 out][64 in][9] ->
+// [wave][chunk s][term][lane][8]: chunk s = 2 * tap + j, lane -> (out 16 * wave + (lane & 15), in 32 j + 8 (lane >>
+// 4) + e); inv[64] = 2^-e_c; bd[0] = Wb
+inline int bx_row_exp(const float *row, int n, double *l1) {
+  float m = 0.f;
+  double s = 0.0;
+  for (int k = 0; k < n; ++k) {
+    const float v = fabsf(row[k]);
+    m = v > m ? v : m;
+    s += v;
   }
-  trunk_copy_hidden(a, b);
-  for (int i = tid; i < 2 * kBxBuf / 8; i += kBx2Threads) bx_lds4[i] = uint4{0u, 0u, 0u, 0u};
-  __syncthreads();
-  for (int i = tid; i < kCvCh * kCvPix; i += kBx2Threads) bx_store(buf(0), cv_plane(i & 63), i >> 6, src[i]);
-  __syncthreads();
-  for (int i = 0; i < n3; ++i) {
-    const float *w = layer_w(i);
-    const bool second = i > 0 && ((i - 1) & 1);
-    const float bc = i ? w[kBx3Frag + c] : 0.f;
-    float4 am[2] = {};
-    if (i == 0) {
-      const float4 *amap = reinterpret_cast<const float4 *>(a.actmap + ((int64_t)a.action[b] * kCvCh + c) * kCvPix);
-#pragma unroll
-      for (int u = 0; u < 2; ++u) am[u] = amap[4 * (t0 + u) + (lane >> 4)];
-    }
-    bxf4 acc[4];
-    if (kh == 0)
-      bx_conv<9, AHEAD, 0, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
-    else
-      bx_conv<9, AHEAD, 0, 9>(buf(i & 1), wave_stream(w), ring, lane, acc);
-    if (i + 1 < n3) bx_prefetch<9, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
-    // swap partial sums: K-half 0 hands tiles 2-3 over, K-half 1 tiles 0-1
-    {
-      float4 *mine = reinterpret_cast<float4 *>(scr + ((grp * 2 + (1 - kh)) * 64 + lane) * 8);
-      const int o = 2 * (1 - kh);
-      mine[0] = float4{acc[o][0], acc[o][1], acc[o][2], acc[o][3]};
-      mine[1] = float4{acc[o + 1][0], acc[o + 1][1], acc[o + 1][2], acc[o + 1][3]};
-    }
-    __syncthreads();
-    {
-      const float4 *theirs = reinterpret_cast<const float4 *>(scr + ((grp * 2 + kh) * 64 + lane) * 8);
-      const float4 p0 = theirs[0], p1 = theirs[1];
-      acc[t0][0] += p0.x; acc[t0][1] += p0.y; acc[t0][2] += p0.z; acc[t0][3] += p0.w;
-      acc[t0 + 1][0] += p1.x; acc[t0 + 1][1] += p1.y; acc[t0 + 1][2] += p1.z; acc[t0 + 1][3] += p1.w;
-    }
-    if (kh == 0)
-      bx_epilogue3<0, 2>(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
-    else
-      bx_epilogue3<2, 2>(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
-    __syncthreads();
-    if (i == 2 * a.n_dres) {
-      float *dst = a.out_latent + (int64_t)b * kCvCh * kCvPix + c * kCvPix + 4 * (lane >> 4);
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        *reinterpret_cast<float4 *>(dst + 16 * (t0 + u)) =
-            float4{xres[4 * u], xres[4 * u + 1], xres[4 * u + 2], xres[4 * u + 3]};
-      if (wv < 2)
-        bx_conv1_layer<0>(buf((i + 1) & 1), a.w + L.rw, a.w + L.rb, a.r_ch, a.out_r + (int64_t)b * a.r_stride, lane, wv);
-    }
-  }
-  if (wv < 2)
-    bx_conv1_layer<0>(buf(n3 & 1), a.w + L.hw, a.w + L.hb, a.h_ch, a.out_h + (int64_t)b * a.h_ch * kCvPix, lane, wv);
+  *l1 = s;
+  return m > 0.f ? bx_scale_exp(m, kBxWExp) : 0;
 }
+// a float >= the double x (the bounds are upper bounds)
+inline float bx_round_up(double x) { return (float)(x * (1.0 + 1e-6)); }
 
-// host packing for the split trunk. 3x3: W[64 out][64 in][9] -> [wave][chunk s][term][lane][8]:
-// chunk s = 2 * tap + j, lane -> (out 16 * wave + (lane & 15), in 32 j + 8 (lane >> 4) + e)
-inline void bx_pack3(const float *W, float *outf) {
+inline void bx_pack3(const float *W, float *outf, float *inv, float *bd) {
   uint16_t *out = reinterpret_cast<uint16_t *>(outf);
+  int e[64];
+  double wb = 0.0;
+  for (int co = 0; co < 64; ++co) {
+    double l1;
+    e[co] = bx_row_exp(W + co * 64 * 9, 64 * 9, &l1);
+    inv[co] = bx_pow2(-e[co]);
+    wb = l1 > wb ? l1 : wb;
+  }
+  bd[0] = bx_round_up(wb);
   for (int w = 0; w < 4; ++w)
     for (int s = 0; s < 18; ++s)
       for (int lane = 0; lane < 64; ++lane)
-        for (int e = 0; e < 8; ++e) {
-          const int tap = s >> 1, j = s & 1, cin = 32 * j + 8 * (lane >> 4) + e, cout = 16 * w + (lane & 15);
+        for (int el = 0; el < 8; ++el) {
+          const int tap = s >> 1, j = s & 1, cin = 32 * j + 8 * (lane >> 4) + el, cout = 16 * w + (lane & 15);
           uint16_t t[kBxTerms];
-          bx_split2(W[(cout * 64 + cin) * 9 + tap], t[0], t[1]);
-          for (int q = 0; q < kBxTerms; ++q) out[(((w * 18 + s) * kBxTerms + q) * 64 + lane) * 8 + e] = t[q];
+          bx_split2(ldexpf(W[(cout * 64 + cin) * 9 + tap], e[cout]), t[0], t[1]);
+          for (int q = 0; q < kBxTerms; ++q) out[(((w * 18 + s) * kBxTerms + q) * 64 + lane) * 8 + el] = t[q];
         }
 }
 
 // 1x1: W[n <= 32 out][64 in] -> [wave 0..1][chunk j][term][lane][8], zero columns past n
-inline void bx_pack1(const float *W, int n, float *outf) {
+inline void bx_pack1(const float *W, int n, float *outf, float *inv, float *bd) {
   uint16_t *out = reinterpret_cast<uint16_t *>(outf);
+  int e[32];
+  double wb = 0.0;
+  for (int co = 0; co < 32; ++co) {
+    double l1 = 0.0;
+    e[co] = co < n ? bx_row_exp(W + co * 64, 64, &l1) : 0;
+    inv[co] = bx_pow2(-e[co]);
+    wb = l1 > wb ? l1 : wb;
+  }
+  bd[0] = bx_round_up(wb);
   for (int w = 0; w < 2; ++w)
     for (int j = 0; j < 2; ++j)
       for (int lane = 0; lane < 64; ++lane)
-        for (int e = 0; e < 8; ++e) {
-          const int cin = 32 * j + 8 * (lane >> 4) + e, cout = 16 * w + (lane & 15);
+        for (int el = 0; el < 8; ++el) {
+          const int cin = 32 * j + 8 * (lane >> 4) + el, cout = 16 * w + (lane & 15);
           uint16_t t[kBxTerms] = {0, 0};
-          if (cout < n) bx_split2(W[cout * 64 + cin], t[0], t[1]);
-          for (int q = 0; q < kBxTerms; ++q) out[(((w * 2 + j) * kBxTerms + q) * 64 + lane) * 8 + e] = t[q];
+          if (cout < n) bx_split2(ldexpf(W[cout * 64 + cin], e[cout]), t[0], t[1]);
+          for (int q = 0; q < kBxTerms; ++q) out[(((w * 2 + j) * kBxTerms + q) * 64 + lane) * 8 + el] = t[q];
         }
+}
+
+// max |b| over n biases (rounded up)
+inline float bx_bias_bound(const float *b, int n) {
+  double m = 0.0;
+  for (int k = 0; k < n; ++k) m = fabs((double)b[k]) > m ? fabs((double)b[k]) : m;
+  return bx_round_up(m);
 }
 
 // host packing: natural layouts -> fragment layouts

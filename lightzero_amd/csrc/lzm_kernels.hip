@@ -699,6 +699,7 @@ __global__ __launch_bounds__(kTlbThreads) void decode_traverse_kernel(DecodeArgs
 using namespace lzm;
 
 static thread_local char g_err[512];
+constexpr int kErrWords = 8;  // sticky error words per handle (lzm_check_errors)
 static void set_err(const char *msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
 #define LZM_HIP(call)                                                                              \
   do {                                                                                             \
@@ -904,8 +905,8 @@ int lzm_create(int B, int A, int max_sims, int flags, lzm_handle **out) {
   TRY(hipMalloc(&h->pathlen, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->off, sizeof(int32_t) * B) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->diag, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
-  TRY(hipMalloc(&h->err, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
-  TRY(hipMemset(h->err, 0, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMalloc(&h->err, sizeof(int32_t) * kErrWords) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
+  TRY(hipMemset(h->err, 0, sizeof(int32_t) * kErrWords) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->hint, sizeof(int32_t) * 2) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMalloc(&h->norm_flag, sizeof(int32_t) * 2 * norm_parts(B)) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
   TRY(hipMemset(h->diag, 0, sizeof(int32_t) * 4) == hipSuccess ? LZM_OK : LZM_ERR_HIP);
@@ -1928,25 +1929,33 @@ int lzm_search_diagnostics(lzm_handle *h, int32_t *out, void *stream) {
 
 // Sticky error counters of every search path on this handle (a look-back spin that
 // times out, or a draw position beyond the coefficient table, would otherwise leave a silently
-// wrong tie-break stream). Synchronises `stream`; out_host (nullable) gets {look-back timeouts,
-// draw-table overflows, traverse fixed-point failures, fused-search errors}.
-int32_t *lzm_error_word(lzm_handle *h, int i) { return (h && i >= 0 && i < 4) ? h->err + i : nullptr; }
+// wrong tie-break stream; round 6: split-fp16 activations out of range). Synchronises `stream`;
+// out_host (nullable) gets the kErrWords words {look-back timeouts, draw-table overflows, traverse
+// fixed-point failures, fused-search errors, split-range errors, 0, 0, 0}.
+int32_t *lzm_error_word(lzm_handle *h, int i) { return (h && i >= 0 && i < kErrWords) ? h->err + i : nullptr; }
 
 int lzm_check_errors(lzm_handle *h, int32_t *out_host, int clear, void *stream) {
   if (!h) return LZM_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  int32_t w[4] = {0, 0, 0, 0};
+  int32_t w[kErrWords] = {};
   int32_t sd = 0;
-  LZM_HIP(hipMemcpyAsync(w, h->err, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  LZM_HIP(hipMemcpyAsync(w, h->err, kErrWords * sizeof(int32_t), hipMemcpyDeviceToHost, s));
   if (h->search_diag) LZM_HIP(hipMemcpyAsync(&sd, h->search_diag, sizeof(int32_t), hipMemcpyDeviceToHost, s));
   LZM_HIP(hipStreamSynchronize(s));
   w[3] += sd;  // err[3]: the EZ LSTM step's split-K hand-off timeouts (lzm_error_word(h, 3))
   if (out_host) memcpy(out_host, w, sizeof(w));
-  const bool bad = w[0] || w[1] || w[2] || w[3];
+  const bool bad = w[0] || w[1] || w[2] || w[3] || w[4];
   if (bad && clear) {
-    LZM_HIP(hipMemsetAsync(h->err, 0, 4 * sizeof(int32_t), s));
+    LZM_HIP(hipMemsetAsync(h->err, 0, kErrWords * sizeof(int32_t), s));
     if (h->search_diag) LZM_HIP(hipMemsetAsync(h->search_diag, 0, sizeof(int32_t), s));
     LZM_HIP(hipStreamSynchronize(s));
+  }
+  if (w[4]) {
+    snprintf(g_err, sizeof(g_err),
+             "split-fp16 network values out of range in %d workgroup-searches (non-finite, or beyond ~2^114): the "
+             "search's network outputs are not f32-exact; run the conv network with precision='f32' "
+             "(LZM_CONV_PRECISION=f32)", w[4]);
+    return LZM_ERR_RANGE;
   }
   if (bad) {
     snprintf(g_err, sizeof(g_err),
@@ -1993,28 +2002,30 @@ int lzm_cartpole_collect_step(int n, int A, int T, int E, const int32_t *visits,
   return LZM_OK;
 }
 
-int lzm_atari_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream) {
+static int atari_reset_g(int game, const char *name, int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
+                         uint32_t seed, void *stream) {
   if (n <= 0 || !state || !steps || !cur || !obs || (((uintptr_t)cur | (uintptr_t)obs) & 15)) {
-    set_err("lzm_atari_reset: bad arguments (16-B aligned frame buffers)");
+    snprintf(g_err, sizeof(g_err), "%s: bad arguments (16-B aligned frame buffers)", name);
     return LZM_ERR_ARG;
   }
-  hipLaunchKernelGGL(atari_reset_kernel, dim3(n), dim3(kAtThreads), 0, (hipStream_t)stream, n, state, steps, cur, obs,
-                     seed);
+  hipLaunchKernelGGL(game ? atari_reset_kernel<1> : atari_reset_kernel<0>, dim3(n), dim3(kAtThreads), 0,
+                     (hipStream_t)stream, n, state, steps, cur, obs, seed);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
 
-int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
-                           const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
-                           float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
-                           int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
-                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
-                           uint32_t seed, const int64_t *counter, void *stream) {
+static int atari_collect_step_g(int game, const char *name, int n, int A, int T, int E, const int32_t *visits,
+                                const float *root_value, const float *pred_value, int32_t *state, int32_t *steps,
+                                uint8_t *cur, float *obs, float *noises, float noise_alpha, float temperature,
+                                int deterministic, uint8_t *rec_frames, int32_t *rec_action, float *rec_reward,
+                                int32_t *rec_visits, float *rec_value, float *rec_pred, int32_t *ep_len,
+                                int32_t *ep_count, float *ep_return, int max_steps, uint32_t seed,
+                                const int64_t *counter, void *stream) {
   if (n <= 0 || A <= 0 || A > 64 || T <= 0 || E <= 0 || max_steps <= 0 || !visits || !root_value || !state || !steps ||
       !cur || !obs || !noises || !rec_frames || !rec_action || !rec_reward || !rec_visits || !rec_value || !ep_len ||
       !ep_count || !counter || !(temperature > 0.0f) || !(noise_alpha > 0.0f) || (!pred_value) != (!rec_pred) ||
       (((uintptr_t)cur | (uintptr_t)obs | (uintptr_t)rec_frames) & 15)) {
-    set_err("lzm_atari_collect_step: bad arguments");
+    snprintf(g_err, sizeof(g_err), "%s: bad arguments", name);
     return LZM_ERR_ARG;
   }
   AtariArgs a;
@@ -2024,9 +2035,42 @@ int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, co
   a.noises = noises; a.rec_frames = rec_frames; a.rec_action = rec_action; a.rec_reward = rec_reward;
   a.rec_visits = rec_visits; a.rec_value = rec_value; a.pred_value = pred_value; a.rec_pred = rec_pred;
   a.ep_len = ep_len; a.ep_count = ep_count; a.ep_return = ep_return;
-  hipLaunchKernelGGL(atari_collect_kernel, dim3(n), dim3(kAtThreads), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(game ? atari_collect_kernel<1> : atari_collect_kernel<0>, dim3(n), dim3(kAtThreads), 0,
+                     (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
+}
+
+int lzm_atari_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream) {
+  return atari_reset_g(0, "lzm_atari_reset", n, state, steps, cur, obs, seed, stream);
+}
+
+int lzm_atari_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
+                           const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
+                           float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
+                           int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
+                           float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
+                           uint32_t seed, const int64_t *counter, void *stream) {
+  return atari_collect_step_g(0, "lzm_atari_collect_step", n, A, T, E, visits, root_value, pred_value, state, steps,
+                              cur, obs, noises, noise_alpha, temperature, deterministic, rec_frames, rec_action,
+                              rec_reward, rec_visits, rec_value, rec_pred, ep_len, ep_count, ep_return, max_steps, seed,
+                              counter, stream);
+}
+
+int lzm_pong_reset(int n, int32_t *state, int32_t *steps, uint8_t *cur, float *obs, uint32_t seed, void *stream) {
+  return atari_reset_g(1, "lzm_pong_reset", n, state, steps, cur, obs, seed, stream);
+}
+
+int lzm_pong_collect_step(int n, int A, int T, int E, const int32_t *visits, const float *root_value,
+                          const float *pred_value, int32_t *state, int32_t *steps, uint8_t *cur, float *obs,
+                          float *noises, float noise_alpha, float temperature, int deterministic, uint8_t *rec_frames,
+                          int32_t *rec_action, float *rec_reward, int32_t *rec_visits, float *rec_value,
+                          float *rec_pred, int32_t *ep_len, int32_t *ep_count, float *ep_return, int max_steps,
+                          uint32_t seed, const int64_t *counter, void *stream) {
+  return atari_collect_step_g(1, "lzm_pong_collect_step", n, A, T, E, visits, root_value, pred_value, state, steps,
+                              cur, obs, noises, noise_alpha, temperature, deterministic, rec_frames, rec_action,
+                              rec_reward, rec_visits, rec_value, rec_pred, ep_len, ep_count, ep_return, max_steps, seed,
+                              counter, stream);
 }
 
 int lzm_episodes_scan(int n, int E, const int32_t *ep_count, const int32_t *consumed, const int32_t *ep_len,
@@ -2427,27 +2471,47 @@ int lzm_conv_trunk_prepare_p(int precision, int n_dres, int n_pres, int r_ch, in
   const bool bx = precision == LZM_CONV_SPLIT;
   const ConvTrunkLayout L = conv_trunk_layout_p(n_dres, n_pres, precision);
   const int frag3 = bx ? kBx3Frag : kCv3Frag, block = bx ? kBxBlock : kCvBlock;
-  auto pack3 = [&](const float *W, float *o) { bx ? bx_pack3(W, o) : conv_pack3(W, o); };
-  auto pack1 = [&](const float *W, int n, float *o) { bx ? bx_pack1(W, n, o) : conv_pack1(W, n, o); };
+  const int n3 = 1 + 2 * (n_dres + n_pres);
+  // split: layer li's row scales at sc + 64 li, its bounds {Wb, Bb} at bd + 4 li (3x3 layers in order, then the
+  // reward and head 1x1s); the dynamics conv's Bb (max |actmap|) is set by lzm_conv_trunk_actmap_bound
+  auto pack3 = [&](const float *W, float *o, int li, const float *bias) {
+    if (!bx) return conv_pack3(W, o);
+    bx_pack3(W, o, out + L.sc + 64 * li, out + L.bd + 4 * li);
+    out[L.bd + 4 * li + 1] = bias ? bx_bias_bound(bias, 64) : 0.f;
+  };
+  auto pack1 = [&](const float *W, int n, float *o, int li, const float *bias) {
+    if (!bx) return conv_pack1(W, n, o);
+    bx_pack1(W, n, o, out + L.sc + 64 * li, out + L.bd + 4 * li);
+    out[L.bd + 4 * li + 1] = bx_bias_bound(bias, n);
+  };
   memset(out, 0, sizeof(float) * (size_t)L.total);
   const float *r = raw;
   const int W3 = 64 * 64 * 9;
-  pack3(r, out + L.dyn); r += W3;
-  auto blocks = [&](int n, int base) {
+  pack3(r, out + L.dyn, 0, nullptr); r += W3;
+  auto blocks = [&](int n, int base, int li0) {
     for (int k = 0; k < n; ++k) {
       float *o = out + base + k * block;
-      pack3(r, o); r += W3;
+      pack3(r, o, li0 + 2 * k, r + W3); r += W3;
       memcpy(o + frag3, r, 64 * sizeof(float)); r += 64;
-      pack3(r, o + frag3 + 64); r += W3;
+      pack3(r, o + frag3 + 64, li0 + 2 * k + 1, r + W3); r += W3;
       memcpy(o + 2 * frag3 + 64, r, 64 * sizeof(float)); r += 64;
     }
   };
-  blocks(n_dres, L.dres);
-  pack1(r, r_ch, out + L.rw); r += r_ch * 64;
+  blocks(n_dres, L.dres, 1);
+  pack1(r, r_ch, out + L.rw, n3, r + r_ch * 64); r += r_ch * 64;
   memcpy(out + L.rb, r, r_ch * sizeof(float)); r += r_ch;
-  blocks(n_pres, L.pres);
-  pack1(r, h_ch, out + L.hw); r += h_ch * 64;
+  blocks(n_pres, L.pres, 1 + 2 * n_dres);
+  pack1(r, h_ch, out + L.hw, n3 + 1, r + h_ch * 64); r += h_ch * 64;
   memcpy(out + L.hb, r, h_ch * sizeof(float));
+  return LZM_OK;
+}
+
+int lzm_conv_trunk_actmap_bound(int n_dres, int n_pres, float actmap_absmax, float *packed) {
+  if (lzm_conv_trunk_floats_p(n_dres, n_pres, LZM_CONV_SPLIT) < 0 || !packed || !(actmap_absmax >= 0.f)) {
+    set_err("lzm_conv_trunk_actmap_bound: a split-layout blob and a finite max |actmap| >= 0");
+    return LZM_ERR_ARG;
+  }
+  packed[conv_trunk_layout_p(n_dres, n_pres, LZM_CONV_SPLIT).bd + 1] = bx_round_up(actmap_absmax);
   return LZM_OK;
 }
 
@@ -2457,8 +2521,8 @@ int lzm_conv_trunk_prepare(int n_dres, int n_pres, int r_ch, int h_ch, const flo
 
 int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
                          const float *actmap, const float *pool, const int32_t *x, const int32_t *action,
-                         float *out_latent, float *xin, int xin_stride, const float *hpool, int H, float *out_h,
-                         void *stream) {
+                         float *out_latent, float *xin, int xin_stride, const float *hpool, int H, int32_t *xscale,
+                         float *out_h, int32_t *err, void *stream) {
   if (B <= 0 || lzm_conv_trunk_floats_p(n_dres, n_pres, precision) < 0 || r_ch < 1 || r_ch > 32 || h_ch < 1 ||
       h_ch > 32 || !weights || !actmap || !pool || !action || !out_latent || !xin || !out_h ||
       xin_stride < r_ch * 64 + (hpool ? H : 0) || (hpool && (H <= 0 || H % 4)) || xin_stride % 4) {
@@ -2471,43 +2535,24 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
   }
   float *out_r = xin;
   const bool bx = precision == LZM_CONV_SPLIT;
-  // split trunk variants: weight read-ahead depth (LZM_CONV_AHEAD) and timing-only ablations
-  // (LZM_CONV_DIAG=1: no weight loads; results invalid)
-  typedef void (*bx_fn)(ConvTrunkArgs);
-  static const int ahead = getenv("LZM_CONV_AHEAD") ? atoi(getenv("LZM_CONV_AHEAD")) : kBxAhead;
-  static const int diag = getenv("LZM_CONV_DIAG") ? atoi(getenv("LZM_CONV_DIAG")) : 0;
-  const bx_fn bx_kernel = diag == 1   ? conv_trunk_bx_kernel<kBxAhead, 1>
-                          : ahead == 8 ? conv_trunk_bx_kernel<8, 0>
-                          : ahead == 5 ? conv_trunk_bx_kernel<5, 0>
-                                       : conv_trunk_bx_kernel<kBxAhead, 0>;
-  // LZM_CONV_WAVES (experiments): 8 = two waves per SIMD splitting K (conv_trunk_bx2_kernel; measured
-  // 43 vs 34 us per launch at Breakout), 4 (default) = one
-  static const int cwaves = getenv("LZM_CONV_WAVES") ? atoi(getenv("LZM_CONV_WAVES")) : 4;
   static std::once_flag once;
   static hipError_t attr_err = hipSuccess;
   const size_t lds_f32 = 3 * kCvBuf * sizeof(float), lds_bx = 2 * kBxBuf * sizeof(uint16_t);
-  const size_t lds_bx2 = lds_bx + kBx2Scratch * sizeof(float);
   std::call_once(once, [&] {
     attr_err = hipFuncSetAttribute((const void *)conv_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)lds_f32);
-    const bx_fn all[] = {conv_trunk_bx_kernel<kBxAhead, 0>, conv_trunk_bx_kernel<kBxAhead, 1>,
-                         conv_trunk_bx_kernel<8, 0>, conv_trunk_bx_kernel<5, 0>};
-    for (bx_fn f : all)
-      if (attr_err == hipSuccess)
-        attr_err = hipFuncSetAttribute((const void *)f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bx);
     if (attr_err == hipSuccess)
-      attr_err = hipFuncSetAttribute((const void *)conv_trunk_bx2_kernel<kBxAhead>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bx2);
+      attr_err = hipFuncSetAttribute((const void *)conv_trunk_bx_kernel<kBxAhead>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bx);
   });
   LZM_HIP(attr_err);
   ConvTrunkArgs a;
   a.B = B; a.n_dres = n_dres; a.n_pres = n_pres; a.r_ch = r_ch; a.h_ch = h_ch; a.w = weights; a.actmap = actmap;
   a.pool = pool; a.x = x; a.action = action; a.out_latent = out_latent; a.out_r = out_r; a.out_h = out_h;
-  a.r_stride = xin_stride; a.hpool = hpool; a.H = hpool ? H : 0; a.skip_dyn = 0;
-  if (bx && cwaves == 8 && diag == 0 && ahead == kBxAhead)
-    hipLaunchKernelGGL(conv_trunk_bx2_kernel<kBxAhead>, dim3(B), dim3(kBx2Threads), lds_bx2, (hipStream_t)stream, a);
-  else if (bx)
-    hipLaunchKernelGGL(bx_kernel, dim3(B), dim3(kCvThreads), lds_bx, (hipStream_t)stream, a);
+  a.r_stride = xin_stride; a.hpool = hpool; a.H = hpool ? H : 0; a.skip_dyn = 0; a.err = err;
+  a.xscale = precision == LZM_CONV_SPLIT ? xscale : nullptr;
+  if (bx)
+    hipLaunchKernelGGL(conv_trunk_bx_kernel<kBxAhead>, dim3(B), dim3(kCvThreads), lds_bx, (hipStream_t)stream, a);
   else
     hipLaunchKernelGGL(conv_trunk_kernel, dim3(B), dim3(kCvThreads), lds_f32, (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
@@ -2516,27 +2561,27 @@ int lzm_conv_trunk_xin_p(int precision, int B, int n_dres, int n_pres, int r_ch,
 
 int lzm_conv_trunk_p(int precision, int B, int n_dres, int n_pres, int r_ch, int h_ch, const float *weights,
                      const float *actmap, const float *pool, const int32_t *x, const int32_t *action, float *out_latent,
-                     float *out_r, float *out_h, void *stream) {
+                     float *out_r, float *out_h, int32_t *err, void *stream) {
   return lzm_conv_trunk_xin_p(precision, B, n_dres, n_pres, r_ch, h_ch, weights, actmap, pool, x, action, out_latent,
-                              out_r, r_ch * 64, nullptr, 0, out_h, stream);
+                              out_r, r_ch * 64, nullptr, 0, nullptr, out_h, err, stream);
 }
 
 int lzm_conv_resnet8_p(int B, int n_blocks, int n_pres, int h_ch, const float *weights, const float *in,
-                       float *out_latent, float *out_h, void *stream) {
+                       float *out_latent, float *out_h, int32_t *err, void *stream) {
   if (B <= 0 || n_blocks < 1 || lzm_conv_trunk_floats_p(n_blocks, n_pres, LZM_CONV_SPLIT) < 0 || h_ch < 1 ||
       h_ch > 32 || !weights || !in || !out_latent || !out_h || (((uintptr_t)weights | (uintptr_t)in) & 15)) {
     set_err("lzm_conv_resnet8_p: bad arguments (1..8 blocks, 1..32 head channels, 16-byte aligned weights / input)");
     return LZM_ERR_ARG;
   }
-  static hipError_t attr_err = hipFuncSetAttribute((const void *)conv_trunk_bx_kernel<kBxAhead, 0>,
+  static hipError_t attr_err = hipFuncSetAttribute((const void *)conv_trunk_bx_kernel<kBxAhead>,
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    (int)(2 * kBxBuf * sizeof(uint16_t)));
   LZM_HIP(attr_err);
   ConvTrunkArgs a;
   memset(&a, 0, sizeof(a));
   a.B = B; a.n_dres = n_blocks; a.n_pres = n_pres; a.r_ch = 0; a.h_ch = h_ch; a.w = weights;
-  a.pool = in; a.out_latent = out_latent; a.out_h = out_h; a.skip_dyn = 1;
-  hipLaunchKernelGGL((conv_trunk_bx_kernel<kBxAhead, 0>), dim3(B), dim3(kCvThreads), 2 * kBxBuf * sizeof(uint16_t),
+  a.pool = in; a.out_latent = out_latent; a.out_h = out_h; a.skip_dyn = 1; a.err = err;
+  hipLaunchKernelGGL((conv_trunk_bx_kernel<kBxAhead>), dim3(B), dim3(kCvThreads), 2 * kBxBuf * sizeof(uint16_t),
                      (hipStream_t)stream, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
@@ -2554,9 +2599,9 @@ int lzm_repr_prepare(int cin, const float *raw, float *out) {
   memset(out, 0, sizeof(float) * (size_t)L.total);
   const float *r = raw;
   auto bias = [&](int off, int n) { memcpy(out + off, r, n * sizeof(float)); r += n; };
-  repr_pack(r, 32, cin, true, out + L.w1); r += 32 * cin * 9; bias(L.b1, 32);
-  repr_pack(r, 32, 32, false, out + L.r1w1); r += 32 * 32 * 9; bias(L.r1b1, 32);
-  repr_pack(r, 32, 32, false, out + L.r1w2); r += 32 * 32 * 9; bias(L.r1b2, 32);
+  repr_pack(r, 32, cin, true, out + L.w1, out + L.s1); r += 32 * cin * 9; bias(L.b1, 32);
+  repr_pack(r, 32, 32, false, out + L.r1w1, out + L.r1s1); r += 32 * 32 * 9; bias(L.r1b1, 32);
+  repr_pack(r, 32, 32, false, out + L.r1w2, out + L.r1s2); r += 32 * 32 * 9; bias(L.r1b2, 32);
   // the downsample block: conv1 (64) and the shortcut conv3 (64) stacked as one 128-channel layer
   std::vector<float> dual((size_t)128 * 32 * 9);
   memcpy(dual.data(), r, sizeof(float) * 64 * 32 * 9); r += 64 * 32 * 9;
@@ -2564,10 +2609,10 @@ int lzm_repr_prepare(int cin, const float *raw, float *out) {
   const float *w2 = r; r += 64 * 64 * 9;
   bias(L.db2, 64);
   memcpy(dual.data() + 64 * 32 * 9, r, sizeof(float) * 64 * 32 * 9); r += 64 * 32 * 9;
-  repr_pack(dual.data(), 128, 32, false, out + L.dw);
-  repr_pack(w2, 64, 64, false, out + L.dw2);
-  repr_pack(r, 64, 64, false, out + L.r2w1); r += 64 * 64 * 9; bias(L.r2b1, 64);
-  repr_pack(r, 64, 64, false, out + L.r2w2); r += 64 * 64 * 9; bias(L.r2b2, 64);
+  repr_pack(dual.data(), 128, 32, false, out + L.dw, out + L.ds);
+  repr_pack(w2, 64, 64, false, out + L.dw2, out + L.ds2);
+  repr_pack(r, 64, 64, false, out + L.r2w1, out + L.r2s1); r += 64 * 64 * 9; bias(L.r2b1, 64);
+  repr_pack(r, 64, 64, false, out + L.r2w2, out + L.r2s2); r += 64 * 64 * 9; bias(L.r2b2, 64);
   return LZM_OK;
 }
 
@@ -2604,22 +2649,23 @@ int lzm_repr_downsample(int B, int cin, const float *w, const float *obs, float 
   a.B = B; a.cin_obs = cin;
   int rc;
   // L1: obs (NCHW 64 x 64) -> A0 [32][32][32] (128-pixel tiles: 8 per image)
-  a.ntiles = B * 8; a.in = obs; a.w = w + L.w1; a.bias = w + L.b1; a.res = nullptr; a.out = A0;
+  a.ntiles = B * 8; a.in = obs; a.w = w + L.w1; a.winv = w + L.s1; a.bias = w + L.b1; a.res = nullptr; a.out = A0;
   if ((rc = repr_launch<32, 32, 2, 32, 2, false>(a, s)) != LZM_OK) return rc;
   // resblocks1: A0 -> A1 -> A0 (+ A0)
-  a.in = A0; a.w = w + L.r1w1; a.bias = w + L.r1b1; a.out = A1;
+  a.in = A0; a.w = w + L.r1w1; a.winv = w + L.r1s1; a.bias = w + L.r1b1; a.out = A1;
   if ((rc = repr_launch<32, 32, 1, 32, 0, false>(a, s)) != LZM_OK) return rc;
-  a.in = A1; a.w = w + L.r1w2; a.bias = w + L.r1b2; a.res = A0; a.out = A0;
+  a.in = A1; a.w = w + L.r1w2; a.winv = w + L.r1s2; a.bias = w + L.r1b2; a.res = A0; a.out = A0;
   if ((rc = repr_launch<32, 32, 1, 32, 0, true>(a, s)) != LZM_OK) return rc;
   // the downsample block: A0 -> D0 = relu(conv1 + b1), D1 = conv3 (shortcut); D1 = relu(conv2(D0) + b2 + D1)
-  a.ntiles = B * 4; a.in = A0; a.w = w + L.dw; a.bias = w + L.db1; a.res = nullptr; a.out = D0; a.out2 = D1;
+  a.ntiles = B * 4; a.in = A0; a.w = w + L.dw; a.winv = w + L.ds; a.bias = w + L.db1; a.res = nullptr; a.out = D0;
+  a.out2 = D1;
   if ((rc = repr_launch<32, 128, 2, 16, 1, false>(a, s)) != LZM_OK) return rc;
-  a.in = D0; a.w = w + L.dw2; a.bias = w + L.db2; a.res = D1; a.out = D1; a.out2 = nullptr;
+  a.in = D0; a.w = w + L.dw2; a.winv = w + L.ds2; a.bias = w + L.db2; a.res = D1; a.out = D1; a.out2 = nullptr;
   if ((rc = repr_launch<64, 64, 1, 16, 0, true>(a, s)) != LZM_OK) return rc;
   // resblocks2: D1 -> D0 -> D1 (+ D1)
-  a.in = D1; a.w = w + L.r2w1; a.bias = w + L.r2b1; a.res = nullptr; a.out = D0;
+  a.in = D1; a.w = w + L.r2w1; a.winv = w + L.r2s1; a.bias = w + L.r2b1; a.res = nullptr; a.out = D0;
   if ((rc = repr_launch<64, 64, 1, 16, 0, false>(a, s)) != LZM_OK) return rc;
-  a.in = D0; a.w = w + L.r2w2; a.bias = w + L.r2b2; a.res = D1; a.out = D1;
+  a.in = D0; a.w = w + L.r2w2; a.winv = w + L.r2s2; a.bias = w + L.r2b2; a.res = D1; a.out = D1;
   if ((rc = repr_launch<64, 64, 1, 16, 0, true>(a, s)) != LZM_OK) return rc;
   // avg pool -> out NCHW [B][64][8][8]
   hipLaunchKernelGGL(repr_avgpool_kernel, dim3(B), dim3(256), 0, s, D1, out, B);
@@ -2631,7 +2677,7 @@ int lzm_conv_trunk(int B, int n_dres, int n_pres, int r_ch, int h_ch, const floa
                    const float *pool, const int32_t *x, const int32_t *action, float *out_latent, float *out_r,
                    float *out_h, void *stream) {
   return lzm_conv_trunk_p(LZM_CONV_F32, B, n_dres, n_pres, r_ch, h_ch, weights, actmap, pool, x, action, out_latent,
-                          out_r, out_h, stream);
+                          out_r, out_h, nullptr, stream);
 }
 
 }  // extern "C"
@@ -2790,6 +2836,7 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_part = (int)o; o += 3 * kHdParts * 32;
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
+  p.off_lmax = (int)o; o += round4((size_t)S + 1);
   const size_t lds = o * sizeof(float);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %zu B of LDS needed (tree too large: lower num_simulations)",
@@ -2842,12 +2889,12 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
       off_policy <= 0 || off_policy >= Khd || off_policy > kHdKMax || Khd - off_policy > kHdKMax || (off_policy % 128) ||
       (Khd % 128) || H <= 0 || H % kLsUnits || H % 128 || H > kHdKMax || H / kLsUnits > 64 || Kx % (2 * kLsKc) ||
       horizon <= 0 || Vr <= 0 || Vv <= 0 || Vr > 1024 || Vv > 1024 || (!categorical && (Vr != 1 || Vv != 1)) ||
-      S + 1 > 0xffff ||
+      S > 4094 ||
       (((uintptr_t)trunk_w | (uintptr_t)actmap | (uintptr_t)w1t | (uintptr_t)w2q | (uintptr_t)latent_pool |
         (uintptr_t)hpool | (uintptr_t)cpool | (uintptr_t)lstm_frag | (uintptr_t)vp_s | (uintptr_t)vp_t) & 15)) {
     set_err("lzm_search_conv_ez: unsupported network shape (64x8x8 latent, <= 32 reward / head planes, K per head a "
             "multiple of 128 and <= 1024, LSTM width a multiple of 128, (r_ch * 64 + H) % 128 == 0, horizon > 0, "
-            "16-B aligned weights and pools)");
+            "16-B aligned weights and pools) or more than 4094 simulations");
     return LZM_ERR_ARG;
   }
   if (S > h->sims_cap) {
@@ -2906,7 +2953,8 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
   p.xin = wsf; p.h1g = wsf + f_xin; p.kpart = wsf + f_xin + f_h1;
   p.xflags = wsl; p.tflags = wsl + (size_t)S * B; p.pflags = wsl + (size_t)S * B + (size_t)S * T;
   p.Kx = Kx; p.H = H; p.horizon = horizon; p.hpool = hpool; p.cpool = cpool;
-  p.lwfrag = reinterpret_cast<const uint16_t *>(lstm_frag); p.lbias = lstm_bias; p.vp_s = vp_s; p.vp_t = vp_t;
+  p.lwfrag = reinterpret_cast<const uint16_t *>(lstm_frag); p.lwinv = lstm_frag + ls_frag_floats(Kx, H);
+  p.lbias = lstm_bias; p.vp_s = vp_s; p.vp_t = vp_t;
   p.nmb = nmb; p.T = T;
   // dynamic LDS plan (float offsets, 16-B aligned): the activation buffers / LSTM stage buffers first
   size_t o = std::max((size_t)2 * kBxBuf / 2, (size_t)kLsLdsBytes / 4);
@@ -2925,6 +2973,7 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
   p.off_part = (int)o; o += 3 * kHdParts * 32;
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
+  p.off_lmax = (int)o; o += round4((size_t)S + 1);
   const size_t lds = o * sizeof(float);
   if (lds > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_conv_ez: %zu B of LDS needed (tree too large: lower num_simulations)",
@@ -2994,7 +3043,7 @@ extern "C" int lzm_ez_lstm_cell(int B, int H, const float *gates, const float *c
 
 extern "C" int64_t lzm_ez_lstm_frag_floats(int K, int H) {
   if (K <= 0 || H <= 0 || K % kLsKc || H % kLsUnits) return -1;
-  return (int64_t)K * 4 * H * kLsTerms / 2;
+  return ls_frag_floats(K, H) + 4 * (int64_t)H;  // the fragments, then the 4H column scales
 }
 
 extern "C" int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out) {
@@ -3018,10 +3067,11 @@ extern "C" int64_t lzm_ez_lstm_workspace_bytes(int B, int H) {
   return tiles * kLsPartFloats * 4 + tiles * 4;
 }
 
-extern "C" int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const float *wfrag, const float *bias,
-                                const float *cpool, const int32_t *x, const int32_t *search_len, int horizon, float *h1,
-                                float *c1, float *hslot, float *cslot, void *workspace, int32_t *err, void *stream) {
-  if (B <= 0 || lzm_ez_lstm_frag_floats(K, H) < 0 || !xin || !wfrag || !bias || !cpool || !x || !search_len || !h1 ||
+extern "C" int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const int32_t *xscale, const float *wfrag,
+                                const float *bias, const float *cpool, const int32_t *x, const int32_t *search_len,
+                                int horizon, float *h1, float *c1, float *hslot, float *cslot, void *workspace,
+                                int32_t *err, int32_t *range_err, void *stream) {
+  if (B <= 0 || lzm_ez_lstm_frag_floats(K, H) < 0 || !xin || !xscale || !wfrag || !bias || !cpool || !x || !search_len || !h1 ||
       !c1 || !hslot || !cslot || (((uintptr_t)xin | (uintptr_t)wfrag | (uintptr_t)workspace) & 15) ||
       (workspace && !err)) {
     set_err("lzm_ez_lstm_step: bad arguments (K % 64 == 0, H % 16 == 0, 16-B aligned xin / fragments / workspace, "
@@ -3030,7 +3080,9 @@ extern "C" int lzm_ez_lstm_step(int B, int K, int H, const float *xin, const flo
   }
   LstmArgs a;
   a.B = B; a.K = K; a.H = H; a.nmb = (B + kLsRows - 1) / kLsRows;
-  a.xin = xin; a.wf = reinterpret_cast<const uint4 *>(wfrag); a.bias = bias; a.cpool = cpool; a.x = x;
+  a.xin = xin; a.xscale = xscale; a.range_err = range_err;
+  a.wf = reinterpret_cast<const uint4 *>(wfrag); a.winv = wfrag + ls_frag_floats(K, H);
+  a.bias = bias; a.cpool = cpool; a.x = x;
   a.search_len = search_len; a.horizon = horizon; a.h1 = h1; a.c1 = c1; a.hslot = hslot; a.cslot = cslot;
   const int tiles = a.nmb * (H / kLsUnits);
   // split K in two when a workspace is given and every workgroup is resident at once (the lower K

@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <vector>
 
 #include "lzm_conv.h"
 
@@ -77,6 +78,11 @@ __global__ __launch_bounds__(256) void ez_lstm_cell_kernel(int B, int H, const f
 // GEMM's epilogue from registers. Operands: each f32 value is held as h + l (two fp16 terms, an exact
 // split: 22 significand bits) and every product is summed from the three terms l.h, h.l, h.h
 // (v_mfma_f32_16x16x32_f16), as in the conv trunk.
+// Range (lzm_conv.h): W's row (gate column) j is packed as W_j 2^e_j (its largest |w| in [2^14, 2^15)) and
+// xin row b is split as x 2^s_b with s_b = 14 - floor(log2 max(M_r, 1)), M_r the exact max of the row's reward
+// planes (|h| < 1): the trunk that writes the row computes it (xscale[b], or the EZ search's hand-off flag);
+// the epilogue multiplies by 2^-(e_j + s_b), exactly. Every split value is checked (|x 2^s| < 65504, finite)
+// into the range error word.
 //   * 512 threads, two waves per SIMD: wave w owns column tile w & 3 (units 4 (w & 3) .. + 3, column
 //     4 u + gate) and row half w >> 2 (two 16-row tiles). The four gates of a (row, unit) then sit in
 //     the four lanes of a quad, and one DPP broadcast per gate hands them to the lane that writes it.
@@ -86,15 +92,11 @@ __global__ __launch_bounds__(256) void ez_lstm_cell_kernel(int B, int H, const f
 //     B = 256 (every CU), 126 MB of L2 reads instead of 201 MB for 64 x 32 tiles without the split.
 //   * Per 64-K stage both operands go through LDS, double-buffered, one barrier per stage: xin rows
 //     are loaded as f32 and split on the fly ([term][row][64 K] fp16, 16-B chunk c of row r at
-//     c ^ (r & 7)); W comes pre-split from the host in MFMA fragment order
+//     c ^ (r & 7), then 64 row scales); W comes pre-split from the host in MFMA fragment order
 //     ([n-block][column tile][32-K chunk][term][lane][8 fp16], copied as is). Global loads run two
 //     stages ahead.
 //   * Tiles are mapped XCD by XCD (block id % 8 = XCD), whole n-blocks per XCD, so an XCD's L2 holds
 //     its slice of W and every row of xin.
-#ifndef LZM_LS_DIAG
-#define LZM_LS_DIAG 0  // timing experiments only (results invalid): 1 = no global loads after the first
-                       // stages, 2 = no MFMAs, 3 = no LDS fragment reads
-#endif
 constexpr int kLsRows = 64;                      // rows (envs) per tile
 constexpr int kLsUnits = 16;                     // hidden units per tile (64 gate columns)
 constexpr int kLsKc = 64;                        // K per LDS stage
@@ -110,7 +112,10 @@ constexpr int kLsPartFloats = kLsThreads * 8;    // one tile's partial sums (8 p
 struct LstmArgs {
   int B, K, H, nmb, splitk;  // nmb = ceil(B / 64); splitk 1 or 2
   const float *xin;          // [B][K]
+  const int32_t *xscale;     // [B] the rows' scale exponents s_b (lzm_conv_trunk_xin_p)
+  int32_t *range_err;        // nullable: split values out of range (sticky)
   const uint4 *wf;           // fragments (lzm_ez_lstm_prepare)
+  const float *winv;         // [4H] 2^-e_j of gate column j (lzm_ez_lstm_prepare, after the fragments)
   const float *bias;         // [4H] (b_ih + b_hh), nn.LSTM gate order
   const float *cpool;        // [slots][B][H]
   const int32_t *x, *search_len;
@@ -122,21 +127,32 @@ struct LstmArgs {
   unsigned long long *stamps;      // diagnostics (nullptr in production): [block][8] 100 MHz real-time stamps
 };
 
-// fragment element (nb, column tile, chunk, term, lane, e) <- W[(gate H + unit) K + k]
+inline int64_t ls_frag_floats(int K, int H) { return (int64_t)K * 4 * H * kLsTerms / 2; }
+
+// fragment element (nb, column tile, chunk, term, lane, e) <- W[(gate H + unit) K + k] 2^e_(gate H + unit);
+// then the 4H inverse column scales
 inline void ls_pack(const float *W, int K, int H, float *outf) {
   uint16_t *out = reinterpret_cast<uint16_t *>(outf);
+  float *winv = outf + ls_frag_floats(K, H);
   const int nch = K / 32, NB = H / kLsUnits;
+  std::vector<int> e((size_t)4 * H);
+  for (int j = 0; j < 4 * H; ++j) {
+    double l1;
+    e[j] = bx_row_exp(W + (size_t)j * K, K, &l1);
+    winv[j] = bx_pow2(-e[j]);
+  }
   for (int nb = 0; nb < NB; ++nb)
     for (int w = 0; w < 4; ++w)
       for (int j = 0; j < nch; ++j)
         for (int lane = 0; lane < 64; ++lane)
-          for (int e = 0; e < 8; ++e) {
+          for (int el = 0; el < 8; ++el) {
             const int n = lane & 15, unit = kLsUnits * nb + 4 * w + (n >> 2), gate = n & 3;
-            const int k = 32 * j + 8 * (lane >> 4) + e;
+            const int k = 32 * j + 8 * (lane >> 4) + el;
+            const size_t row = (size_t)gate * H + unit;
             uint16_t t[kLsTerms];
-            bx_split2(W[((size_t)gate * H + unit) * K + k], t[0], t[1]);
+            bx_split2(ldexpf(W[row * K + k], e[row]), t[0], t[1]);
             for (int q = 0; q < kLsTerms; ++q)
-              out[((((size_t)(nb * 4 + w) * nch + j) * kLsTerms + q) * 64 + lane) * 8 + e] = t[q];
+              out[((((size_t)(nb * 4 + w) * nch + j) * kLsTerms + q) * 64 + lane) * 8 + el] = t[q];
           }
 }
 
@@ -149,16 +165,33 @@ __device__ __forceinline__ float ls_quad_bcast(float v, int g) {
   return __builtin_bit_cast(float, r);
 }
 
+// The split pass of N stage values of one row scaled by sc = 2^s_b: the two term vectors (pairs packed). (A row
+// whose scale is clamped, s_b = -kBxAExp — reward planes beyond ~2^114 or not finite — counts as a range error
+// where the scales are read: ls_row_bad.)
+typedef float ls_f2 __attribute__((ext_vector_type(2)));
+typedef _Float16 ls_h2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int ls_row_bad(int s) { return s <= -kBxAExp; }
+template <int N>
+__device__ __forceinline__ void ls_split_row(const float (&v)[N], float sc, uint32_t (&hh)[N / 2], uint32_t (&ll)[N / 2]) {
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) {
+    const ls_f2 pr = ls_f2{v[2 * j], v[2 * j + 1]} * sc;
+    const ls_h2 th = __builtin_convertvector(pr, ls_h2);
+    const ls_h2 tq = __builtin_convertvector(pr - __builtin_convertvector(th, ls_f2), ls_h2);
+    hh[j] = __builtin_bit_cast(uint32_t, th);
+    ll[j] = __builtin_bit_cast(uint32_t, tq);
+  }
+}
+
 __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs p) {
   extern __shared__ uint4 ls_lds4[];
   uint16_t *lds = reinterpret_cast<uint16_t *>(ls_lds4);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ct = wv & 3, mh = wv >> 2;
-  const int NB = p.H / kLsUnits, T = NB * p.nmb, G = T * p.splitk;
+  const int NB = p.H / kLsUnits, T = NB * p.nmb;
   // block -> (K half, tile): the upper K half takes the lower block ids; tiles XCD-major
   const int kh = p.splitk == 2 && (int)blockIdx.x < T ? 1 : 0;
   int q = (int)blockIdx.x - (p.splitk == 2 && kh == 0 ? T : 0);
   if ((T & 7) == 0) q = (q & 7) * (T >> 3) + (q >> 3);
-  (void)G;
   const int nb = q / p.nmb, mb = q - nb * p.nmb;
   const int row0 = kLsRows * mb, B = p.B, K = p.K, H = p.H;
   const int nch = K / 32, kspan = K / p.splitk, nst = kspan / kLsKc, k0 = kh * kspan;
@@ -167,9 +200,12 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
     if (p.stamps && tid == 0) p.stamps[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  // ---- staging: thread -> A (row tid / 8, 8 K values at 8 (tid % 8)) and 3 B uint4s per stage
+  // ---- staging: thread -> A (row tid / 8, 8 K values at 8 (tid % 8)) and 2 B uint4s per stage
   const int sr = tid >> 3, sseg = tid & 7;
   const bool srow = row0 + sr < B;
+  const int sexp = srow ? p.xscale[row0 + sr] : 0;
+  const float ssc = bx_pow2(sexp);  // the staged row's scale
+  const int bad = sseg == 0 && ls_row_bad(sexp);
   const float4 *asrc = reinterpret_cast<const float4 *>(p.xin + (size_t)(srow ? row0 + sr : 0) * K + k0) + 2 * sseg;
   const uint4 *bsrc = p.wf + (size_t)nb * 4 * nch * kLsTerms * 64;  // [col tile][chunk][term][lane]
   // staging registers of two stages (native vector types: HIP's uint4 / float4 structs kept these
@@ -194,20 +230,9 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
     }
   };
   auto store_stage = [&](int bsel, const ls_f4(&VA)[2], const ls_u4(&VB)[kLsTerms]) __attribute__((always_inline)) {
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const float v[8] = {VA[0][0], VA[0][1], VA[0][2], VA[0][3], VA[1][0], VA[1][1], VA[1][2], VA[1][3]};
     uint32_t h[4], l[4];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const f2 pr[2] = {f2{VA[u][0], VA[u][1]}, f2{VA[u][2], VA[u][3]}};
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const h2 hh = __builtin_convertvector(pr[v], h2);
-        const h2 ll = __builtin_convertvector(pr[v] - __builtin_convertvector(hh, f2), h2);
-        h[2 * u + v] = __builtin_bit_cast(uint32_t, hh);
-        l[2 * u + v] = __builtin_bit_cast(uint32_t, ll);
-      }
-    }
+    ls_split_row<8>(v, ssc, h, l);
     uint16_t *abuf = lds + bsel * kLsStage;
     uint16_t *base = abuf + sr * kLsKc + ((sseg ^ (sr & 7)) & 7) * 8;
     *reinterpret_cast<uint4 *>(base) = uint4{h[0], h[1], h[2], h[3]};
@@ -229,7 +254,7 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
   auto stage = [&](int s, auto par) __attribute__((always_inline)) {
     constexpr int PAR = decltype(par)::value;
     __syncthreads();
-    if (s + 2 < nst && LZM_LS_DIAG != 1) {
+    if (s + 2 < nst) {
       if constexpr (PAR == 0)
         load_stage(s + 2, va0, vb0);
       else
@@ -244,20 +269,10 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
       for (int t = 0; t < 2; ++t) {
         const int r = 32 * mh + 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
 #pragma unroll
-        for (int tm = 0; tm < kLsTerms; ++tm)
-          a[t][tm] = LZM_LS_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)s, (uint32_t)t, (uint32_t)tm}
-                                      : *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
+        for (int tm = 0; tm < kLsTerms; ++tm) a[t][tm] = *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
       }
 #pragma unroll
-      for (int tm = 0; tm < kLsTerms; ++tm)
-        w[tm] = LZM_LS_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)c, 1u, (uint32_t)tm}
-                                 : bbuf[((c * 4 + ct) * kLsTerms + tm) * 64 + lane];
-      if (LZM_LS_DIAG == 2) {
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y), 0.f, 0.f};
-        continue;
-      }
+      for (int tm = 0; tm < kLsTerms; ++tm) w[tm] = bbuf[((c * 4 + ct) * kLsTerms + tm) * 64 + lane];
       // small terms first: l.h, h.l, h.h (the conv trunk's order)
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][1]), bx_ash(w[0]), acc[t], 0, 0, 0);
@@ -266,12 +281,11 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
 #pragma unroll
       for (int t = 0; t < 2; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][0]), bx_ash(w[0]), acc[t], 0, 0, 0);
     }
-    if (s + 1 < nst && LZM_LS_DIAG != 5) {
+    if (s + 1 < nst) {
       if constexpr (PAR == 0)
         store_stage(1, va1, vb1);
       else
         store_stage(0, va0, vb0);
-  stamp(1);
     }
   };
   for (int s = 0; s < nst; s += 2) {
@@ -279,19 +293,26 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
     if (s + 1 < nst) stage(s + 1, I1());
   }
   stamp(2);
+  if (bad && p.range_err) atomicAdd(p.range_err, 1);
   // the cell's inputs for this lane's rows (lower K half only): issued after the GEMM's loads (vmcnt
   // counts in order: issued first, the dependent x -> cpool gather would hold up the first stage),
   // in flight during the hand-off
-  float c0[2] = {0.f, 0.f}, bias_l = 0.f;
+  float c0[2] = {0.f, 0.f}, bias_l = 0.f, wsc = 0.f, rsc[2][4] = {};
   int rst[2] = {0, 0};
   if (kh == 0) {
     bias_l = p.bias[(size_t)gate * H + unit];
+    wsc = p.winv[(size_t)gate * H + unit];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int b = row0 + 32 * mh + 16 * t + 4 * (lane >> 4) + gate;
       if (b < B) {
         c0[t] = p.cpool[((size_t)max(p.x[b], 0) * B + b) * H + unit];
         rst[t] = p.horizon > 0 && (p.search_len[b] % p.horizon) == 0;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // accumulator row 32 mh + 16 t + 4 (lane >> 4) + r: 2^-(e_j + s_row)
+        const int br = row0 + 32 * mh + 16 * t + 4 * (lane >> 4) + r;
+        rsc[t][r] = wsc * (br < B ? bx_pow2(-p.xscale[br]) : 1.f);
       }
     }
   }
@@ -300,8 +321,7 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
   // stores with the sc1 policy; the flag by an agent-scope relaxed atomic), every storing wave's
   // vmcnt(0) and a workgroup barrier before the one flag store; the consumer's one lane polls the flag
   // sc1, a barrier, then sc1 payload loads.
-  if (p.splitk == 2 && LZM_LS_DIAG == 4 && kh == 1) return;
-  if (p.splitk == 2 && LZM_LS_DIAG != 4) {
+  if (p.splitk == 2) {
     // payload: 16-B buffer stores / loads with the sc1 cache policy (aux = 16)
     typedef unsigned ls_u4v __attribute__((ext_vector_type(4)));
     const __amdgpu_buffer_rsrc_t rs =
@@ -333,14 +353,14 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
     for (int t = 0; t < 2; ++t)
       acc[t] += __builtin_bit_cast(bxf4, __builtin_amdgcn_raw_buffer_load_b128(rs, (tid * 8 + 4 * t) * 4, 0, 16));
   }
-  // ---- epilogue: + bias, the four gates of (row, unit) from the quad, the cell by lane gate = r
-  // (ez_lstm_cell_kernel's operations in its order)
+  // ---- epilogue: the column's weight scale undone, + bias, the four gates of (row, unit) from the quad, the
+  // cell by lane gate = r (ez_lstm_cell_kernel's operations in its order)
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     float gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float v = acc[t][r] + bias_l;
+      const float v = __fmaf_rn(acc[t][r], rsc[t][r], bias_l);
       const float vi = ls_quad_bcast(v, 0), vf = ls_quad_bcast(v, 1), vg = ls_quad_bcast(v, 2), vo = ls_quad_bcast(v, 3);
       if (gate == r) { gi = vi; gf = vf; gg = vg; go = vo; }
     }
@@ -360,10 +380,10 @@ __global__ __launch_bounds__(kLsThreads) void ez_lstm_gemm_cell_kernel(LstmArgs 
 
 // ---- one gate-GEMM + cell tile inside a persistent launch (the EfficientZero one-launch search,
 // lzm_search_conv.h): 256 threads, same tile (64 rows x 16 hidden units, K split in two halves over
-// two workgroups), same operand layouts, stage pipeline and MFMA order as ez_lstm_gemm_cell_kernel,
+// two workgroups), same operand layouts, stage pipeline, scales and MFMA order as ez_lstm_gemm_cell_kernel,
 // so every output bit is the same. Wave w owns column tile w and all four 16-row tiles (the 512-thread
 // kernel gives each wave two); the staging thread map changes with the thread count (thread -> row
-// tid / 4, two 16-B K chunks), the LDS layout does not. The xin rows are read with sc1 loads (they were
+// 16 w + 4 u + lane / 16, 4 values), the LDS layout does not. The xin rows are read with sc1 loads (they were
 // handed over by other workgroups, MI355X_MICROARCH.md's first hand-off row).
 typedef unsigned lp_u4 __attribute__((ext_vector_type(4)));
 typedef float lp_f4 __attribute__((ext_vector_type(4)));
@@ -371,28 +391,26 @@ constexpr int kLpThreads = 256;
 #ifndef LZM_LP_DEPTH
 #define LZM_LP_DEPTH 2  // register sets of staged loads: global loads run LZM_LP_DEPTH - 1 stages ahead (2..4)
 #endif
-#ifndef LZM_LP_DIAG
-#define LZM_LP_DIAG 0  // timing experiments only (results invalid): 1 = no global loads after the first two
-                       // stages, 2 = no MFMAs, 3 = no LDS A reads, 4 = no split / LDS stores after the first
-#endif
 
 struct LpTile {
   int row0, nb, kh;  // tile rows [row0, row0 + 64), hidden units [16 nb, 16 nb + 16), K half
 };
 
 // the GEMM part: acc[t] = the tile's K-half partial sums (row tile t = rows 16 t .. + 15 of the tile,
-// this wave's 16 gate columns), accumulated from zero exactly as the 512-thread kernel does.
-// lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4); wfrag:
-// ls_pack's split-fp16 fragments (lzm_ez_lstm_prepare, the ones ez_lstm_gemm_cell_kernel reads). A
+// this wave's 16 gate columns; still scaled by 2^(e_j + s_row)), accumulated exactly as the 512-thread
+// kernel does. rexp: the tile's 64 row scale exponents (LDS); bad: |= a split value out of range.
+// lds: kLsLdsBytes of staging; xr: buffer resource over xin [B][K] (num_records = B * K * 4);
+// wfrag: ls_pack's split-fp16 fragments (lzm_ez_lstm_prepare, the ones ez_lstm_gemm_cell_kernel reads). A
 // is read as f32 and split on the fly (a thread stages 4 values of 4 rows through LDS); a wave loads
-// the B fragments its own MFMAs consume (chunk 0 and 1, column tile = the wave, its lane, 3 terms)
+// the B fragments its own MFMAs consume (chunk 0 and 1, column tile = the wave, its lane, both terms)
 // straight into registers: B never touches LDS. (Measured: B read as f32 in the same order and split
 // on the device — two thirds of the bytes — made the GEMM slower, 29 K -> 33 K cycles per
 // simulation: the split's VALU work sits on the stage's critical path, the bytes do not.)
 // Loads go through buffer resources (one 32-bit per-thread offset each, the stage in the scalar
 // offset): no 64-bit address per load for the compiler to hoist out of the simulation loop and spill.
 __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, const __amdgpu_buffer_rsrc_t xr,
-                                             const uint16_t *wfrag, uint16_t *lds, bxf4 (&acc)[4]) {
+                                             const uint16_t *wfrag, const int *rexp, uint16_t *lds, bxf4 (&acc)[4],
+                                             int &bad) {
   const int tid = threadIdx.x, lane = tid & 63, ct = tid >> 6;
   const int nch = K / 32, kspan = K / 2, nst = kspan / kLsKc, k0 = tl.kh * kspan;
   // A: wave-instruction u of wave w reads 4 whole 256-B row segments of the stage (rows 16 w + 4 u +
@@ -400,11 +418,14 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
   const int a4 = lane & 15;
   int avo[4];
   bool arow[4];
+  float asc[4];  // the staged rows' scales 2^s_row
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int rr = 16 * ct + 4 * u + (lane >> 4);
     arow[u] = tl.row0 + rr < B;
     avo[u] = ((tl.row0 + (arow[u] ? rr : 0)) * K + k0 + 4 * a4) * 4;
+    asc[u] = bx_pow2(rexp[rr]);
+    bad |= a4 == 0 && arow[u] && ls_row_bad(rexp[rr]);
   }
   // B: ls_pack's layout [nb][column tile][chunk][term][lane][8 fp16]: wave-instruction (chunk, term)
   // reads 1 KiB contiguous
@@ -429,21 +450,13 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
     }
   };
   auto store_stage = [&](int bsel, const lp_f4(&VA)[4], const uint4(&VB)[NVB]) __attribute__((always_inline)) {
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     uint16_t *abuf = lds + bsel * kLsStage;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {  // row 16 ct + 4 u + lane / 16: 4 values, half (a4 & 1) of chunk a4 / 2
       const int rr = 16 * ct + 4 * u + (lane >> 4);
+      const float v[4] = {VA[u][0], VA[u][1], VA[u][2], VA[u][3]};
       uint32_t hh[2], ll[2];
-      const f2 pr[2] = {f2{VA[u][0], VA[u][1]}, f2{VA[u][2], VA[u][3]}};
-#pragma unroll
-      for (int v = 0; v < 2; ++v) {
-        const h2 th = __builtin_convertvector(pr[v], h2);
-        const h2 tq = __builtin_convertvector(pr[v] - __builtin_convertvector(th, f2), h2);
-        hh[v] = __builtin_bit_cast(uint32_t, th);
-        ll[v] = __builtin_bit_cast(uint32_t, tq);
-      }
+      ls_split_row<4>(v, asc[u], hh, ll);
       uint16_t *base = abuf + rr * kLsKc + (((a4 >> 1) ^ (rr & 7)) & 7) * 8 + 4 * (a4 & 1);
       *reinterpret_cast<uint2 *>(base) = uint2{hh[0], hh[1]};
       *reinterpret_cast<uint2 *>(base + kLsPlane) = uint2{ll[0], ll[1]};
@@ -466,7 +479,7 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
   auto stage = [&](int s, auto par) __attribute__((always_inline)) {
     constexpr int P = decltype(par)::value, D = LZM_LP_DEPTH;
     __syncthreads();
-    if (s + D - 1 < nst && LZM_LP_DIAG != 1) load_stage(s + D - 1, va[(P + D - 1) % D], vb[(P + D - 1) % D]);
+    if (s + D - 1 < nst) load_stage(s + D - 1, va[(P + D - 1) % D], vb[(P + D - 1) % D]);
     const uint16_t *abuf = lds + (s & 1) * kLsStage;
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
@@ -475,18 +488,10 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
       for (int t = 0; t < 4; ++t) {
         const int r = 16 * t + ar, o = r * kLsKc + (((4 * c + ag) ^ (r & 7)) & 7) * 8;
 #pragma unroll
-        for (int tm = 0; tm < kLsTerms; ++tm)
-          a[t][tm] = LZM_LP_DIAG == 3 ? uint4{(uint32_t)lane, (uint32_t)s, (uint32_t)t, (uint32_t)tm}
-                                      : *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
+        for (int tm = 0; tm < kLsTerms; ++tm) a[t][tm] = *reinterpret_cast<const uint4 *>(abuf + tm * kLsPlane + o);
       }
 #pragma unroll
       for (int tm = 0; tm < kLsTerms; ++tm) w[tm] = wreg[c][tm];
-      if (LZM_LP_DIAG == 2) {
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          acc[t] += bxf4{__builtin_bit_cast(float, a[t][0].x ^ w[0].x), __builtin_bit_cast(float, a[t][1].y ^ w[1].y), 0.f, 0.f};
-        continue;
-      }
       // small terms first: l.h, h.l, h.h (ez_lstm_gemm_cell_kernel's order)
 #pragma unroll
       for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(a[t][1]), bx_ash(w[0]), acc[t], 0, 0, 0);
@@ -497,7 +502,7 @@ __device__ __forceinline__ void lp_tile_gemm(const LpTile &tl, int B, int K, con
     }
     // (measured: splitting / storing stage s + 1 BEFORE this stage's MFMAs instead, into the other LDS
     // buffer, made the GEMM slower, 33 K -> 40 K cycles per simulation)
-    if (s + 1 < nst && LZM_LP_DIAG != 4) store_stage((s + 1) & 1, va[(P + 1) % D], vb[(P + 1) % D]);
+    if (s + 1 < nst) store_stage((s + 1) & 1, va[(P + 1) % D], vb[(P + 1) % D]);
   };
   for (int s = 0; s < nst; s += LZM_LP_DEPTH) {
     stage(s, std::integral_constant<int, 0>());

@@ -15,10 +15,12 @@
 // (the B operand: read from an LDS image of the input halo), K = 9 taps x in-channels in chunks of 32, on
 // v_mfma_f32_16x16x32_f16 with every f32 operand split into two fp16 terms x = h + l (h = fp16(x), l =
 // fp16(x - h): 22 significand bits, |x - h - l| <= 2^-22 |x|) and three products per K (w_h x_h, w_h x_l,
-// w_l x_h; the dropped w_l x_l is below 2^-22 of |w x|): f32-level error at half the MFMAs of the trunk's
-// three-term bf16 scheme (lzm_conv.h). fp16's range bounds it: |values| < 65504, and below 2^-14 (6.1e-5) the
-// terms are fp16 subnormals, an absolute error of at most 2^-25 per operand. A persistent grid (one 8-wave workgroup per CU) walks 64- or 128-pixel
-// output tiles of whole image rows.
+// w_l x_h; the dropped w_l x_l is below 2^-22 of |w x|): f32-level error at half the MFMAs of a three-term
+// bf16 scheme. Range (lzm_conv.h's rule): out channel c's weight row is packed as W_c 2^e_c (its largest |w|
+// in [2^14, 2^15)); a tile's input halo is split as x 2^s with s from the tile's exact max |x| (each wave's
+// max of the values it splits meets the others' in LDS at one more barrier of the split pass); the epilogue
+// multiplies by 2^-(e_c + s), exactly. ReLUs propagate NaN. A persistent grid (one 8-wave workgroup per CU)
+// walks 64- or 128-pixel output tiles of whole image rows.
 //
 // Staging (the tile loop's memory side, no registers): a tile's input rows, and its residual, are contiguous in
 // HBM (NHWC rows; the first layer: 9 rows of each NCHW plane), so they are copied as they lie into an LDS ring
@@ -38,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "lzm_conv.h"
 
 namespace lzm {
@@ -52,6 +56,7 @@ struct ReprConvArgs {
   int B, ntiles, cin_obs;  // cin_obs: first layer's input channels (MODE 2)
   const float *in;         // NHWC [B][HIN][HIN][CIN] (MODE 2: NCHW obs [B][cin_obs][64][64])
   const float *w;          // fragments [out tile][chunk][term][lane][8 fp16] (repr_pack)
+  const float *winv;       // [COUT] 2^-e_c of the packed rows (MODE 1: 128, conv1's then the shortcut's)
   const float *bias;       // [COUT] (MODE 1: [64], the first half's)
   const float *res;        // NHWC residual of the output's shape (RES launches only)
   float *out;              // NHWC [B][HOUT][HOUT][COUT] (MODE 1: the first 64 channels)
@@ -103,7 +108,8 @@ struct ReprGeom {
   static constexpr int S = TERMB + 3 * RAWB + FIXB <= 160 * 1024 ? 3 : 2;  // raw ring depth
   static constexpr int RAW0 = TERMB, RES0 = RAW0 + S * RAWB, XS0 = RES0 + 2 * RESB;
   static constexpr int ZB = XS0 + XSB;  // 32 zero bytes: the split pass's source for halo positions off the image
-  static constexpr int LDSB = ZB + 32;
+  static constexpr int MX = ZB + 32;    // 8 words: the waves' maxima of a tile's halo (the split pass)
+  static constexpr int LDSB = MX + 32;
   static_assert(LDSB <= 160 * 1024, "LDS");
   // a tile's wait at the top of its iteration: the DMAs younger than the newest copy it needs (the tile's raw
   // copy and residual): the raw copy issued with that residual (RES), or the S - 1 raw copies after it
@@ -211,47 +217,69 @@ __device__ __forceinline__ void rp_split8(const F8 &x, uint4 &h, uint4 &l) {
   l = __builtin_bit_cast(uint4, lv);
 }
 
-// split pass: the tile's raw slot -> the two fp16 term images (halo borders and padding taps zero)
+// split pass: the tile's raw slot -> the two fp16 term images (halo borders and padding taps zero), scaled by
+// 2^s from the halo's exact max (a barrier inside: every thread calls it); returns 2^-s
 template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
-__device__ __forceinline__ void rp_split(const ReprConvArgs &a, const float *raw, const float *zero, uint16_t *buf,
-                                         int r0) {
+__device__ __forceinline__ float rp_split(const ReprConvArgs &a, const float *raw, const float *zero, uint16_t *buf,
+                                          uint32_t *mslot, int r0, int wv, int lane) {
   typedef ReprGeom<CIN, COUT, STRIDE, WOUT, MODE, RES> G;
   typedef float f8 __attribute__((ext_vector_type(8)));
+  f8 xs[G::IPT];
+  int pos[G::IPT], grp[G::IPT];
+  bool on[G::IPT];
+  uint32_t m = 0;
 #pragma unroll
   for (int i = 0; i < G::IPT; ++i) {
     int hr, hc, g;
-    if (!rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g)) continue;
-    f8 x;
-    int pos;
-    if constexpr (MODE == 2) {
-      // im2col: pixel hc of the tile (local row hc / WOUT, column hc % WOUT), K = 8 g + j = tap * C + c
-      pos = hc;
-      const int C = a.cin_obs, lr = hc / WOUT, ox = hc % WOUT;
-      int tap = (8 * g) / C, c = 8 * g - tap * C;
+    on[i] = rp_item<G, STRIDE, MODE>(threadIdx.x + i * kRpThreads, hr, hc, g);
+    grp[i] = g;
+    f8 x = f8{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (on[i]) {
+      if constexpr (MODE == 2) {
+        // im2col: pixel hc of the tile (local row hc / WOUT, column hc % WOUT), K = 8 g + j = tap * C + c
+        pos[i] = hc;
+        const int C = a.cin_obs, lr = hc / WOUT, ox = hc % WOUT;
+        int tap = (8 * g) / C, c = 8 * g - tap * C;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int rr = 2 * lr + tap / 3, ix = 2 * ox + tap % 3 - 1, iy = 2 * r0 - 1 + rr;
-        const bool ok = tap < 9 && iy >= 0 && iy < 64 && ix >= 0 && ix < 64;
-        const float v = raw[ok ? (c * G::RR + rr) * 64 + ix : 0];
-        x[j] = __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
-        ++c;
-        tap += c == C;
-        c = c == C ? 0 : c;
+        for (int j = 0; j < 8; ++j) {
+          const int rr = 2 * lr + tap / 3, ix = 2 * ox + tap % 3 - 1, iy = 2 * r0 - 1 + rr;
+          const bool ok = tap < 9 && iy >= 0 && iy < 64 && ix >= 0 && ix < 64;
+          const float v = raw[ok ? (c * G::RR + rr) * 64 + ix : 0];
+          x[j] = __uint_as_float(__float_as_uint(v) & (ok ? 0xffffffffu : 0u));
+          ++c;
+          tap += c == C;
+          c = c == C ? 0 : c;
+        }
+      } else {
+        pos[i] = rp_pos<G, STRIDE>(hr, hc);
+        const int iy = r0 * STRIDE - 1 + hr, ix = hc - 1;
+        const bool ok = iy >= 0 && iy < G::HIN && ix >= 0 && ix < G::HIN;
+        const float4 *src = reinterpret_cast<const float4 *>(ok ? raw + (hr * G::HIN + ix) * CIN + 8 * g : zero);
+        const float4 u = src[0], v = src[1];
+        x = f8{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
       }
-    } else {
-      pos = rp_pos<G, STRIDE>(hr, hc);
-      const int iy = r0 * STRIDE - 1 + hr, ix = hc - 1;
-      const bool ok = iy >= 0 && iy < G::HIN && ix >= 0 && ix < G::HIN;
-      const float4 *src = reinterpret_cast<const float4 *>(ok ? raw + (hr * G::HIN + ix) * CIN + 8 * g : zero);
-      const float4 u = src[0], v = src[1];
-      x = f8{u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
     }
+    xs[i] = x;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = max(m, __float_as_uint(x[j]) & 0x7fffffffu);
+  }
+  m = (uint32_t)xor_max((int)m);
+  if (lane == 0) mslot[wv] = m;
+  rp_barrier();
+  const uint4 m0 = reinterpret_cast<const uint4 *>(mslot)[0], m1 = reinterpret_cast<const uint4 *>(mslot)[1];
+  const uint32_t mm = max(max(max(m0.x, m0.y), max(m0.z, m0.w)), max(max(m1.x, m1.y), max(m1.z, m1.w)));
+  const int s = bx_scale_exp(__uint_as_float(mm), kBxAExp);
+  const float sc = bx_pow2(s);
+#pragma unroll
+  for (int i = 0; i < G::IPT; ++i) {
+    if (!on[i]) continue;
     uint4 h, l;
-    rp_split8(x, h, l);
-    const int o = (g * G::NPP + pos) * 8;
+    rp_split8(xs[i] * sc, h, l);
+    const int o = (grp[i] * G::NPP + pos[i]) * 8;
     *reinterpret_cast<uint4 *>(buf + o) = h;
     *reinterpret_cast<uint4 *>(buf + G::TERM + o) = l;
   }
+  return bx_pow2(-s);
 }
 
 template <int CIN, int COUT, int STRIDE, int WOUT, int MODE, bool RES>
@@ -283,6 +311,7 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
   float *dst = sc ? a.out2 : a.out;
   if (sc) ch -= COUT_T;
   const float4 bias = sc ? float4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4 *>(a.bias + ch);
+  const float4 wsc = *reinterpret_cast<const float4 *>(a.winv + 16 * ot + 4 * (lane >> 4));  // the packed rows' 2^-e
   // the compiler's own loads retired here (a builtin wait it accounts for): inside the loop the VM counter
   // holds DMAs and stores only
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
@@ -303,8 +332,9 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
     const int b = tile / TPI, r0 = (tile % TPI) * G::TR;
     rp_wait_vm<G::NTOP>();  // this wave's copies landed ...
     rp_barrier();           // ... and every wave's; every wave is also done with the previous tile's LDS
-    rp_split<CIN, COUT, STRIDE, WOUT, MODE, RES>(a, reinterpret_cast<const float *>(lb + G::RAW0 + slot * G::RAWB),
-                                                 zero, terms, r0);
+    const float rinv = rp_split<CIN, COUT, STRIDE, WOUT, MODE, RES>(
+        a, reinterpret_cast<const float *>(lb + G::RAW0 + slot * G::RAWB), zero, terms,
+        reinterpret_cast<uint32_t *>(lb + G::MX), r0, wv, lane);
     rp_barrier();
     // refill: the next tile's residual into the other residual slot, tile n + S into the slot of tile n
     if constexpr (RES)
@@ -386,20 +416,23 @@ __global__ __launch_bounds__(kRpThreads) __attribute__((amdgpu_waves_per_eu(2, 2
         }
       }
     }
-    // epilogue: acc[p][r] = out channel ch + r at pixel 16 (pt0 + p) + (lane & 15)
+    // epilogue: acc[p][r] = out channel ch + r at pixel 16 (pt0 + p) + (lane & 15), scaled by 2^(e + s)
     const float *rs = reinterpret_cast<const float *>(lb + G::RES0 + (it & 1) * G::RESB);
+    const float4 f = float4{wsc.x * rinv, wsc.y * rinv, wsc.z * rinv, wsc.w * rinv};
 #pragma unroll
     for (int p = 0; p < G::PTW; ++p) {
       if (G::KS == 2 && (p >> 1) != kh) continue;  // (the K-split partner's tiles)
       const int px = 16 * (pt0 + p) + (lane & 15);
       const int64_t e = (((int64_t)b * HOUT + r0 + px / WOUT) * WOUT + px % WOUT) * COUT_T + ch;
-      float4 y = float4{acc[p][0] + bias.x, acc[p][1] + bias.y, acc[p][2] + bias.z, acc[p][3] + bias.w};
+      float4 y = float4{__fmaf_rn(acc[p][0], f.x, bias.x), __fmaf_rn(acc[p][1], f.y, bias.y),
+                        __fmaf_rn(acc[p][2], f.z, bias.z), __fmaf_rn(acc[p][3], f.w, bias.w)};
       if (!sc) {
         if constexpr (RES) {
           const float4 rr = *reinterpret_cast<const float4 *>(rs + px * COUT_T + ch);
           y.x += rr.x; y.y += rr.y; y.z += rr.z; y.w += rr.w;
         }
-        y.x = fmaxf(y.x, 0.f); y.y = fmaxf(y.y, 0.f); y.z = fmaxf(y.z, 0.f); y.w = fmaxf(y.w, 0.f);
+        // relu, NaN kept (torch's)
+        y.x = y.x < 0.f ? 0.f : y.x; y.y = y.y < 0.f ? 0.f : y.y; y.z = y.z < 0.f ? 0.f : y.z; y.w = y.w < 0.f ? 0.f : y.w;
       }
       *reinterpret_cast<float4 *>(dst + e) = y;
     }
@@ -440,13 +473,20 @@ __global__ __launch_bounds__(256) void repr_avgpool_kernel(const float *__restri
 }
 
 // ---- host side: packing
-// A-operand fragments of one convolution: W [cout][cin][3][3] (folded) -> [out tile][chunk][term][lane][8 fp16],
-// lane -> out channel 16 tile + (lane & 15), K = 8 (lane >> 4) + e within the chunk; chunk s = tap * (cin / 32)
-// + j with K -> in channel 32 j + ..., or (first layer, cin <= 7) chunk s with K = 32 s + ... = tap * cin + c.
-// Two weights stacked (the dual layer: W [64] then W3 [64]) give cout = 128.
-inline void repr_pack(const float *W, int cout, int cin, bool im2col, float *outf) {
+// A-operand fragments of one convolution: W [cout][cin][3][3] (folded), each row c scaled by 2^e_c (inv[c] =
+// 2^-e_c) -> [out tile][chunk][term][lane][8 fp16], lane -> out channel 16 tile + (lane & 15), K = 8 (lane >> 4)
+// + e within the chunk; chunk s = tap * (cin / 32) + j with K -> in channel 32 j + ..., or (first layer, cin <= 7)
+// chunk s with K = 32 s + ... = tap * cin + c. Two weights stacked (the dual layer: W [64] then W3 [64]) give
+// cout = 128.
+inline void repr_pack(const float *W, int cout, int cin, bool im2col, float *outf, float *inv) {
   uint16_t *out = reinterpret_cast<uint16_t *>(outf);
   const int nch = im2col ? 2 : 9 * (cin / 32);
+  std::vector<int> er(cout);
+  for (int co = 0; co < cout; ++co) {
+    double l1;
+    er[co] = bx_row_exp(W + (size_t)co * cin * 9, cin * 9, &l1);
+    inv[co] = bx_pow2(-er[co]);
+  }
   for (int ot = 0; ot < cout / 16; ++ot)
     for (int s = 0; s < nch; ++s)
       for (int lane = 0; lane < 64; ++lane)
@@ -460,6 +500,7 @@ inline void repr_pack(const float *W, int cout, int cin, bool im2col, float *out
             const int tap = s / (cin / 32), c = 32 * (s % (cin / 32)) + k;
             wv = W[(co * cin + c) * 9 + tap];
           }
+          wv = ldexpf(wv, er[co]);
           const _Float16 h = (_Float16)wv, l = (_Float16)(wv - (float)h);  // the kernel's split, rp_split8
           const uint16_t t[kRpTerms] = {__builtin_bit_cast(uint16_t, h), __builtin_bit_cast(uint16_t, l)};
           for (int q = 0; q < kRpTerms; ++q) out[(((ot * nch + s) * kRpTerms + q) * 64 + lane) * 8 + e] = t[q];
@@ -468,7 +509,9 @@ inline void repr_pack(const float *W, int cout, int cin, bool im2col, float *out
 
 // packed blob layout (floats): one entry per layer, fragments then the bias
 struct ReprLayout {
-  int w1, b1, r1w1, r1b1, r1w2, r1b2, dw, db1, dw2, db2, r2w1, r2b1, r2w2, r2b2, total;
+  int w1, b1, r1w1, r1b1, r1w2, r1b2, dw, db1, dw2, db2, r2w1, r2b1, r2w2, r2b2;
+  int s1, r1s1, r1s2, ds, ds2, r2s1, r2s2;  // the layers' row scales 2^-e_c (ds: 128, the dual layer's)
+  int total;
 };
 inline int repr_frag_floats(int cout, int nch) { return cout / 16 * nch * kRpTerms * 64 * 4; }
 inline ReprLayout repr_layout() {
@@ -482,6 +525,8 @@ inline ReprLayout repr_layout() {
   L.dw2 = take(repr_frag_floats(64, 18)); L.db2 = take(64);
   L.r2w1 = take(repr_frag_floats(64, 18)); L.r2b1 = take(64);
   L.r2w2 = take(repr_frag_floats(64, 18)); L.r2b2 = take(64);
+  L.s1 = take(32); L.r1s1 = take(32); L.r1s2 = take(32); L.ds = take(128); L.ds2 = take(64); L.r2s1 = take(64);
+  L.r2s2 = take(64);
   L.total = o;
   return L;
 }

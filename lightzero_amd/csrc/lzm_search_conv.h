@@ -78,6 +78,7 @@ struct ConvSearchArgs {
   int Kx, H, horizon;     // Kx = r_ch * 64 + H; lstm_horizon_len
   float *hpool, *cpool;   // [S + 1][B][H] state pools (slot 0 = the roots' state)
   const uint16_t *lwfrag; // gate weights, split-fp16 fragments (lzm_ez_lstm_prepare)
+  const float *lwinv;     // [4H] their column scales 2^-e_j (after the fragments)
   const float *lbias;     // [4H] b_ih + b_hh
   const float *vp_s, *vp_t;  // value-prefix BatchNorm as an affine map (relu(h1 * s + t) feeds the head)
   float *h1g;             // [B][H] unmasked LSTM outputs (sc1 hand-off, tile -> root)
@@ -97,7 +98,7 @@ struct ConvSearchArgs {
   float *out_values;
   // dynamic LDS plan: float offsets (the two activation buffers come first)
   int off_stat, off_meta, off_val, off_lut, off_legal, off_path, off_pact, off_pbt, off_r, off_hd, off_hid, off_part,
-      off_lg, off_seed;
+      off_lg, off_seed, off_lmax;
 };
 
 // Parity-mode draw offset of root b in simulation k: the sum of the depth flags of roots < b (the
@@ -438,11 +439,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
   }
   if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
-  for (int k = tid; k < 2 * kBxTerms * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
-    const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
-    const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
-    sc_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
-  }
+  bx_zero_borders(sc_lds4, tid, kScThreads);
   if (tid == 0) {
     s_mm[0] = p.step_fresh ? make_float4(kFloatMin, kFloatMax, p.step_delta, 0.0f) : p.minmax[b];
     s_vtp0 = p.vtp_in[b];
@@ -460,12 +457,30 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   float *lr = smem + p.off_r, *lhd = smem + p.off_hd, *lhid = smem + p.off_hid, *lpart = smem + p.off_part;
   float *llg = smem + p.off_lg;
   const int N2 = p.Vr + p.Vv + A;
-  // trunk weights: this wave's stream of each 3x3 layer (lzm_conv.h bx layout)
+  // trunk weights: this wave's stream of each 3x3 layer (lzm_conv.h bx layout), row scales and bounds
   const ConvTrunkLayout L = conv_trunk_layout_p(p.n_dres, p.n_pres, 1);
   const int n3 = 1 + 2 * p.n_dres + 2 * p.n_pres;
+  const float *winv = p.w + L.sc;
+  __shared__ float4 s_bd[kBxMaxLayers];  // the layers' bounds (staged below, before the first simulation's barrier)
+  const float4 *wbd = s_bd;
+  bx_stage_bounds(s_bd, p.w, L, n3 + 2, tid, kScThreads);
   auto layer_w = [&](int i) { return p.w + bx_layer_off(L, p.n_dres, i); };
   auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   BxRing<AHEAD> ring;
+  __shared__ uint32_t s_mx[4], s_lm[2][kScThreads];
+  int range_bad = 0;
+  float *lmax = smem + p.off_lmax;  // the exact max |x| of this root's pool latents, by slot (lzm_conv.h "Range")
+  {  // slot 0: the root's latent
+    float x0[16];
+    const float *src = p.pool + (size_t)b * (kCvCh * kCvPix);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * q + 4 * (lane >> 4));
+      x0[4 * q] = v.x; x0[4 * q + 1] = v.y; x0[4 * q + 2] = v.z; x0[4 * q + 3] = v.w;
+    }
+    const float m0 = bx_latent_max(x0, s_mx, wv, lane);
+    if (tid == 0) lmax[0] = m0;  // (read after the first simulation's barriers)
+  }
 
   for (int k = 0; k < S; ++k) {
     // ---- selection (wave 0; parity mode: draw-free walk, depth flag, look-back only for a value)
@@ -545,12 +560,13 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         xres[4 * q] = v.x; xres[4 * q + 1] = v.y; xres[4 * q + 2] = v.z; xres[4 * q + 3] = v.w;
       }
       if (!late) sc_load_amap(am, p.actmap, s_act, c, lane);
+      BxRange rg = bx_range_input(lmax[max(s_x, 0)]);
       {
         bxf4 in4[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) in4[q] = bxf4{xres[4 * q], xres[4 * q + 1], xres[4 * q + 2], xres[4 * q + 3]};
         const float4 no_am[4] = {};
-        bx_epilogue3<0, 4, false>(in4, buf(0), 0.f, false, no_am, xres, false, false, lane, c);
+        bx_epilogue3<false>(in4, buf(0), 1.f, 0.f, false, no_am, xres, false, false, bx_pow2(rg.s_in), lane, c);
       }
       __syncthreads();
       stamp(1);
@@ -558,8 +574,16 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         const float *w = layer_w(i);
         const bool second = i > 0 && ((i - 1) & 1);  // a block's second conv: + residual, new block input
         const float bc = i ? w[kBx3Frag + c] : 0.f;
+        const float4 bdi = wbd[i];
+        const float wsc = winv[i * 64 + c];
         bxf4 acc[4];
-        bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
+        // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow (the latent's: filed)
+        bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&]() {
+          if (i > 0) {
+            bx_range_reduce(rg);
+            if (i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
+          }
+        });
         if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
         if (i == 0 && late) {
           // late draw: the look-back and the tie's draw, then the action's map for the epilogue — by every
@@ -583,18 +607,28 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           }
           sc_load_amap(am, p.actmap, action, c, lane);
         }
-        bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
+        const int s_out = bx_layer_scale(bdi, i == 0 || second, rg);
+        s_lm[i & 1][tid] = bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
+                                        i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c);
         __syncthreads();
+        bx_range_fetch(rg, s_lm[i & 1], s_out, lane);
         if (i == 2 * p.n_dres) {  // the next latent (registers, exact) and the reward planes
           float *dst = p.pool + ((size_t)(k + 1) * B + b) * (kCvCh * kCvPix) + c * kCvPix + 4 * (lane >> 4);
 #pragma unroll
           for (int q = 0; q < 4; ++q)
             *reinterpret_cast<float4 *>(dst + 16 * q) = float4{xres[4 * q], xres[4 * q + 1], xres[4 * q + 2], xres[4 * q + 3]};
-          if (wv < 2) bx_conv1_layer<0>(buf((i + 1) & 1), p.w + L.rw, p.w + L.rb, p.r_ch, lr, lane, wv);
+          if (wv < 2)
+            bx_conv1_layer<0>(buf((i + 1) & 1), p.w + L.rw, p.w + L.rb, winv + n3 * 64, bx_pow2(-rg.s_in), p.r_ch, lr,
+                              lane, wv);
         }
       }
+      if (wv < 2)
+        bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, winv + (n3 + 1) * 64, bx_pow2(-rg.s_in), p.h_ch, lhd,
+                          lane, wv);
+      bx_range_reduce(rg);  // the last layer's output, checked (and filed when it is the latent)
+      if (n3 - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
+      range_bad |= rg.bad;
     }
-    if (wv < 2) bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, p.h_ch, lhd, lane, wv);
     __syncthreads();
     stamp(2);
     // ---- head MLPs: the three hidden layers
@@ -691,6 +725,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   }
   if (p.out_values && tid == 0) p.out_values[b] = node_value(ls[0]);
   if (tid == 0) {
+    if (range_bad) atomicAdd(p.err + 4, 1);  // split activations out of the fp16 range (lzm_conv.h)
     p.minmax[b] = s_mm[0];
     p.pathlen[b] = s_len[0];
     // the last workgroup advances the epoch (no release fence: the kernel boundary orders the
@@ -792,13 +827,6 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     for (int e = tid; e < S; e += kScThreads) s_seed[e] = p.seeds[e];
   }
   if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
-  auto zero_borders = [&]() {
-    for (int k = tid; k < 2 * kBxTerms * 36 * 8; k += kScThreads) {  // [buffer][term][border position][16-B chunk]
-      const int ch = k & 7, bp = (k >> 3) % 36, plane = k / (36 * 8);
-      const int ps = bp < 10 ? bp : bp < 20 ? 80 + bp : (1 + ((bp - 20) >> 1)) * 10 + ((bp - 20) & 1) * 9;
-      sc_lds4[(plane * kBxComp + ps * 64) / 8 + ch] = uint4{0u, 0u, 0u, 0u};
-    }
-  };
   if (tid == 0) {
     if (has_root) {
       s_mm[0] = p.step_fresh ? make_float4(kFloatMin, kFloatMax, p.step_delta, 0.0f) : p.minmax[b];
@@ -820,7 +848,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const int N2 = p.Vr + p.Vv + A;
 
   // EfficientZero: this workgroup's LSTM tile (fixed for the launch)
-  __shared__ int s_rx[64], s_rlen[64];
+  __shared__ int s_rx[64], s_rlen[64], s_rexp[64];
   const int T = p.T, NB = p.H / kLsUnits;
   const bool has_tile = b < 2 * T;
   int q = 0;
@@ -842,12 +870,30 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   const int Kx = p.Kx, H = p.H;
   typedef unsigned sc_u4 __attribute__((ext_vector_type(4)));
 
-  // trunk weights: this wave's stream of each 3x3 layer (lzm_conv.h bx layout)
+  // trunk weights: this wave's stream of each 3x3 layer (lzm_conv.h bx layout), row scales and bounds
   const ConvTrunkLayout L = conv_trunk_layout_p(p.n_dres, p.n_pres, 1);
   const int n3 = 1 + 2 * p.n_dres + 2 * p.n_pres;
+  const float *winv = p.w + L.sc;
+  __shared__ float4 s_bd[kBxMaxLayers];  // the layers' bounds (staged below, before the first simulation's barrier)
+  const float4 *wbd = s_bd;
+  bx_stage_bounds(s_bd, p.w, L, n3 + 2, tid, kScThreads);
   auto layer_w = [&](int i) { return p.w + bx_layer_off(L, p.n_dres, i); };
   auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   BxRing<AHEAD> ring;
+  __shared__ uint32_t s_mx[4], s_rmx[2], s_lm[2][kScThreads];
+  int range_bad = 0;
+  float *lmax = smem + p.off_lmax;  // the exact max |x| of this root's pool latents, by slot (lzm_conv.h "Range")
+  if (has_root) {  // slot 0: the root's latent
+    float x0[16];
+    const float *src = p.pool + (size_t)b * (kCvCh * kCvPix);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4 *>(src + c * kCvPix + 16 * q + 4 * (lane >> 4));
+      x0[4 * q] = v.x; x0[4 * q + 1] = v.y; x0[4 * q + 2] = v.z; x0[4 * q + 3] = v.w;
+    }
+    const float m0 = bx_latent_max(x0, s_mx, wv, lane);
+    if (tid == 0) lmax[0] = m0;  // (read after the first simulation's barriers)
+  }
 
   for (int k = 0; k < S; ++k) {
     if (has_root) {
@@ -855,7 +901,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       // the dynamics conv's first weight chunks, in flight during the walk
       bx_prefetch<18, AHEAD, 0>(ring, wave_stream(p.w + L.dyn), lane);
       if (!FAST && tid < 31) seed_state_parallel(s_seed[k], s_pow, s_z0);
-      zero_borders();  // (every simulation: the LSTM stages reuse the activation buffers)
+      bx_zero_borders(sc_lds4, tid, kScThreads);  // (every simulation: the LSTM stages reuse the buffers)
       __syncthreads();
       if (STAMPS && tid == 0) st_prev = __builtin_amdgcn_s_memtime();
       if (tid == 0) s_late = 0;
@@ -932,12 +978,13 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(sc_u4, v), rs, (Kx - H + 4 * tid) * 4, 0, 16);
           }
         }
+        BxRange rg = bx_range_input(lmax[max(s_x, 0)]);
         {
           bxf4 in4[4];
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) in4[q4] = bxf4{xres[4 * q4], xres[4 * q4 + 1], xres[4 * q4 + 2], xres[4 * q4 + 3]};
           const float4 no_am[4] = {};
-          bx_epilogue3<0, 4, false>(in4, buf(0), 0.f, false, no_am, xres, false, false, lane, c);
+          bx_epilogue3<false>(in4, buf(0), 1.f, 0.f, false, no_am, xres, false, false, bx_pow2(rg.s_in), lane, c);
         }
         __syncthreads();
         stamp(1);
@@ -945,8 +992,16 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           const float *w = layer_w(i);
           const bool second = i > 0 && ((i - 1) & 1);  // a block's second conv: + residual, new block input
           const float bc = i ? w[kBx3Frag + c] : 0.f;
+          const float4 bdi = wbd[i];
+          const float wsc = winv[i * 64 + c];
           bxf4 acc[4];
-          bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
+          // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow (the latent's: filed)
+          bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&]() {
+            if (i > 0) {
+              bx_range_reduce(rg);
+              if (i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
+            }
+          });
           if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
           if (i == 0 && late) {
             // late draw: the look-back and the tie's draw, then the action's map for the epilogue — by every
@@ -970,8 +1025,11 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
             }
             sc_load_amap(am, p.actmap, action, c, lane);
           }
-          bx_epilogue3(acc, buf((i + 1) & 1), bc, i == 0, am, xres, i == 0 || second, i == 0 || second, lane, c);
+          const int s_out = bx_layer_scale(bdi, i == 0 || second, rg);
+          s_lm[i & 1][tid] = bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
+                                          i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c);
           __syncthreads();
+          bx_range_fetch(rg, s_lm[i & 1], s_out, lane);
           if (i == 2 * p.n_dres) {  // the next latent (registers, exact) and the reward planes
             // the latent by sc1 (write-through) stores, which do not keep the line in this XCD's L2: 16 KB
             // per root and simulation that would otherwise push the LSTM weights and the trunk's out of
@@ -983,19 +1041,30 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
               __builtin_amdgcn_raw_buffer_store_b128(
                   __builtin_bit_cast(sc_u4, float4{xres[4 * q4], xres[4 * q4 + 1], xres[4 * q4 + 2], xres[4 * q4 + 3]}),
                   lr4, (c * kCvPix + 4 * (lane >> 4) + 16 * q4) * 4, 0, LZM_EZ_POOL_AUX);
-            if (wv < 2)  // the reward planes: the LSTM input row's first part, sc1
-              bx_conv1_layer<0, true>(buf((i + 1) & 1), p.w + L.rw, p.w + L.rb, p.r_ch, p.xin + (size_t)b * Kx, lane, wv);
+            if (wv < 2) {  // the reward planes: the LSTM input row's first part, sc1; their max for its scale
+              const uint32_t rm = bx_conv1_layer<0, true>(buf((i + 1) & 1), p.w + L.rw, p.w + L.rb, winv + n3 * 64,
+                                                          bx_pow2(-rg.s_in), p.r_ch, p.xin + (size_t)b * Kx, lane, wv);
+              bx_post_max(s_rmx, rm, wv, lane);
+            }
           }
         }
+        if (wv < 2)
+          bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, winv + (n3 + 1) * 64, bx_pow2(-rg.s_in), p.h_ch, lhd,
+                            lane, wv);
+        bx_range_reduce(rg);  // the last layer's output, checked (and filed when it is the latent)
+        if (n3 - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
+        range_bad |= rg.bad;
       }
-      if (wv < 2) bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, p.h_ch, lhd, lane, wv);
       // publish the LSTM input row: every storing wave drained, one barrier, one flag store
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (tid == 0)
+      if (tid == 0) {  // {epoch | row scale exponent + 128 : 8 | x : 12 | search_len : 12} (S <= 4094)
+        const unsigned se = (unsigned)(ls_row_exp(__uint_as_float(max(s_rmx[0], s_rmx[1]))) + 128) & 0xffu;
         __hip_atomic_store(&p.xflags[(size_t)k * B + b],
-                           (epoch << 32) | ((unsigned long long)(max(s_x, 0) & 0xffff) << 16) | (unsigned)(s_len[0] & 0xffff),
+                           (epoch << 32) | ((unsigned long long)se << 24) |
+                               ((unsigned long long)(max(s_x, 0) & 0xfff) << 12) | (unsigned)(s_len[0] & 0xfff),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       stamp(2);
       // ---- head MLPs: value and policy now (while the other roots finish their trunks), the value
       // prefix after the LSTM
@@ -1022,15 +1091,18 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           const int row = tile.row0 + lane;
           unsigned long long v = 0;
           if (row < B) v = sc_wait_word(&p.xflags[(size_t)k * B + row], epoch, p.err);
-          s_rx[lane] = (int)((v >> 16) & 0xffff);
-          s_rlen[lane] = (int)(v & 0xffff);
+          s_rx[lane] = (int)((v >> 12) & 0xfff);
+          s_rlen[lane] = (int)(v & 0xfff);
+          s_rexp[lane] = row < B ? (int)((v >> 24) & 0xff) - 128 : 0;
         }
         __syncthreads();
         const unsigned long long w1 = st_now();
         if (STAMPS && tid == 0) st_acc[10] += w1 - w0;
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(p.xin, 0, B * Kx * 4, 0x00020000);
         bxf4 acc[4];
-        lp_tile_gemm(tile, B, Kx, xr, p.lwfrag, act, acc);
+        int lbad = 0;
+        lp_tile_gemm(tile, B, Kx, xr, p.lwfrag, s_rexp, act, acc, lbad);
+        range_bad |= lbad;
         if (STAMPS && tid == 0) st_acc[13] += st_now() - w1;
         const __amdgpu_buffer_rsrc_t pr =
             __builtin_amdgcn_make_buffer_rsrc(p.kpart + (size_t)q * (kLpThreads * 16), 0, kLpThreads * 16 * 4, 0x00020000);
@@ -1048,8 +1120,8 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           const int gate = lane & 3, ct = wv;
           const int unit = kLsUnits * tile.nb + 4 * ct + ((lane & 15) >> 2);
           // the cell's inputs (c0 from this workgroup's own state slots, or the roots' state)
-          const float bias_l = p.lbias[(size_t)gate * H + unit];
-          float c0[4];
+          const float bias_l = p.lbias[(size_t)gate * H + unit], wsc = p.lwinv[(size_t)gate * H + unit];
+          float c0[4], rsc[4][4];
           int rst[4];
 #pragma unroll
           for (int tt = 0; tt < 4; ++tt) {
@@ -1060,6 +1132,9 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
               c0[tt] = p.cpool[((size_t)s_rx[rl] * B + row) * H + unit];
               rst[tt] = p.horizon > 0 && (s_rlen[rl] % p.horizon) == 0;
             }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)  // accumulator row 16 tt + 4 (lane >> 4) + r: 2^-(e_j + s_row)
+              rsc[tt][r] = wsc * bx_pow2(-s_rexp[16 * tt + 4 * (lane >> 4) + r]);
           }
           const unsigned long long w2 = st_now();
           if (tid == 0) (void)sc_wait_word(&p.pflags[(size_t)k * T + q], epoch, p.err);
@@ -1076,7 +1151,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
             float gi = 0.f, gf = 0.f, gg = 0.f, go = 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float v = acc[tt][r] + bias_l;
+              const float v = __fmaf_rn(acc[tt][r], rsc[tt][r], bias_l);
               const float vi = ls_quad_bcast(v, 0), vf = ls_quad_bcast(v, 1), vg = ls_quad_bcast(v, 2), vo = ls_quad_bcast(v, 3);
               if (gate == r) { gi = vi; gf = vf; gg = vg; go = vo; }
             }
@@ -1187,6 +1262,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   }
   if (has_root && p.out_values && tid == 0) p.out_values[b] = node_value(ls[0]);
   if (tid == 0) {
+    if (range_bad) atomicAdd(p.err + 4, 1);  // split activations out of the fp16 range (lzm_conv.h, lzm_lstm.h)
     if (has_root) {
       p.minmax[b] = s_mm[0];
       p.pathlen[b] = s_len[0];

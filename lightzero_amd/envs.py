@@ -183,3 +183,11 @@ class DeviceBreakoutEnvManager(DeviceEnvManager):
 
     def __init__(self, env_num, seed=0, max_episode_steps=400):
         super().__init__(env_num, seed, max_episode_steps)
+
+
+class DevicePongEnvManager(DeviceBreakoutEnvManager):
+    """The Atari image env of config 3 (Pong EfficientZero) on the device (lzm_pong_* kernels): Pong's action set
+    {NOOP, FIRE, RIGHT, LEFT, RIGHTFIRE, LEFTFIRE} and frame format — 4 x 64 x 64 stacked grey frames, one
+    recorded per step — as a stand-in game (ALE is not installed)."""
+    env_kind = "pong"
+    actions = 6

@@ -316,7 +316,7 @@ class MuZeroMCTSCtree(object):
             if infer is not None:
                 infer[k] = (t.x >= 0).sum()
             if native:  # leaf latents read from the pool and the next latents filed by the trunk kernel
-                out = model.step_from_pool(buf.pool, t.x, t.action, buf.pool[k + 1])
+                out = model.step_from_pool(buf.pool, t.x, t.action, buf.pool[k + 1], range_err=t.error_word(4))
             else:
                 t.gather(buf.pool, row, buf.net_in)
                 out = model.recurrent_inference(buf.net_in, t.action64)
@@ -584,7 +584,8 @@ class EfficientZeroMCTSCtree(object):
             if native:
                 # the LSTM state is gathered from / filed (reset-masked) into the state pools on the device
                 out = model.step_from_pool_lstm(buf.pool, t.x, t.action, buf.pool[k + 1], buf.extra[0], buf.extra[1],
-                                                k, t.search_len, horizon, err=t.error_word(3))
+                                                k, t.search_len, horizon, err=t.error_word(3),
+                                                range_err=t.error_word(4))
             else:
                 t.gather(buf.extra[0], Hl, buf.extra_in[0])
                 t.gather(buf.extra[1], Hl, buf.extra_in[1])

@@ -95,7 +95,7 @@ class DeviceTree:
 
     def reset_errors(self, stream=None):
         """zero the sticky error words without raising (a recycled handle starts clean); synchronises"""
-        out = (ctypes.c_int32 * 4)()
+        out = (ctypes.c_int32 * _lib.LZM_ERR_WORDS)()
         _lib.load().lzm_check_errors(self.h, out, 1, stream_ptr(stream))
         self._unchecked = False
 
@@ -245,9 +245,10 @@ class DeviceTree:
     def check_errors(self, clear=True, stream=None):
         """Post-search integrity check (synchronises the stream): raises LzmError when a look-back
         spin timed out or a draw fell outside the coefficient table on any search path of this
-        handle, i.e. when the parity-mode tie-break stream may differ from the reference's.
-        Returns the four counters otherwise (all zero)."""
-        out = (ctypes.c_int32 * 4)()
+        handle, i.e. when the parity-mode tie-break stream may differ from the reference's, and
+        SplitRangeError when a split-fp16 network value was non-finite or out of range (word 4).
+        Returns the counters otherwise (all zero)."""
+        out = (ctypes.c_int32 * _lib.LZM_ERR_WORDS)()
         if clear:
             self._unchecked = False
         call("lzm_check_errors", self.h, out, int(bool(clear)), stream_ptr(stream))

@@ -384,9 +384,10 @@ class MuZeroCollector:
     def _device_path(self, collect_with_pure_policy):
         from ..policy import MuZeroCollectPolicy
         cfg = self.policy_config
-        # MuZero policies only: the device collector's search step is MuZero's (an EfficientZero
-        # policy, a MuZeroCollectPolicy subclass, keeps the host path with its value-prefix / LSTM search)
-        return (isinstance(self._env, DeviceEnvManager) and type(self._policy) is MuZeroCollectPolicy
+        # MuZero and EfficientZero policies (EfficientZeroCollectPolicy subclasses MuZeroCollectPolicy): the
+        # device collector's search step picks the EfficientZero search (value-prefix roots, the reward LSTM)
+        # from the model, as EfficientZeroPolicy._forward_collect does (efficientzero.py:538-656)
+        return (isinstance(self._env, DeviceEnvManager) and isinstance(self._policy, MuZeroCollectPolicy)
                 and not collect_with_pure_policy and not cfg.eps.eps_greedy_exploration_in_collect
                 and cfg.model.frame_stack_num == self._env.frame_stack)
 
@@ -402,7 +403,9 @@ class MuZeroCollector:
                 seed=env.seed, rng_mode=cfg.get('device_rng', 'glibc'), graph=True,
                 poll_every=cfg.get('device_poll_every', 4), record_pred=bool(cfg.use_priority),
                 support_scale=cfg.model.support_scale, env=env.env_kind,
-                categorical_distribution=bool(cfg.model.get('categorical_distribution', True)))
+                categorical_distribution=bool(cfg.model.get('categorical_distribution', True)),
+                search_cfg=dict(discount_factor=float(cfg.get('discount_factor', 0.997)),
+                                lstm_horizon_len=int(cfg.get('lstm_horizon_len', 5))))
         else:
             self._device.set_temperature(temperature)
         return self._device

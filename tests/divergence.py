@@ -97,6 +97,12 @@ def attribute(ra, rb, B, S, A, ez=False, tau=1e-3):
                 max_near_tie_gap=max(near) if near else None, tau=tau,
                 root_value_max_abs_diff_same_counts=float(np.max(np.abs(ra["values"] - rb["values"])[~differ]))
                 if (~differ).any() else None,
+                # roots whose every request matched (the same tree, only the network's rounding differs)
+                root_value_max_abs_diff_same_requests=float(np.max(np.abs(ra["values"] - rb["values"])[first == S]))
+                if (first == S).any() else None,
+                root_value_max_rel_diff_same_requests=float(np.max(
+                    np.abs(ra["values"] - rb["values"])[first == S] / np.maximum(np.abs(ra["values"][first == S]), 1e-6)))
+                if (first == S).any() else None,
                 typical_gap_quantiles={q: float(np.quantile(gaps, q)) for q in (0.01, 0.1, 0.5)} if gaps else None,
                 first_divergences=rows[:64])
 

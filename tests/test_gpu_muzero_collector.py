@@ -154,3 +154,42 @@ def test_device_path_breakout_segments_match_restatement():
         assert e["episode_return"] >= e["reward_segment"].sum()
         assert breakout_synth.replay_episode(fr, e["action_segment"], e["reward_segment"], 150,
                                              episode_return=e["episode_return"]) is None
+
+
+def test_device_path_pong_efficientzero_segments_match_restatement():
+    """config 3's device path through the MuZeroCollector drop-in: an EfficientZeroCollectPolicy on the Pong
+    stand-in (DevicePongEnvManager) takes the device collector (the one-launch EfficientZero search with the
+    reward LSTM in the captured step, lstm_horizon_len from the policy config), and its episodes cut into
+    segments identical to the restatement of the reference's loop fed the same episodes; the logged return is
+    each counted episode's point difference"""
+    import bench
+    from lightzero_amd.envs import DevicePongEnvManager
+    from lightzero_amd.policy import EfficientZeroCollectPolicy, policy_config
+    from lightzero_amd.worker import MuZeroCollector
+    from oracle import pong_synth
+    n, n_ep = 16, 20
+    cfg = policy_config(num_simulations=8, game_segment_length=12, device=DEV, use_priority=True, n_episode=n,
+                        lstm_horizon_len=5,
+                        model=dict(frame_stack_num=4, action_space_size=6, observation_shape=(4, 64, 64),
+                                   image_channel=1, model_type='conv', support_scale=50))
+    model = bench.build_ez_model(DEV, seed=3)
+    col = MuZeroCollector(env=DevicePongEnvManager(n, seed=7, max_episode_steps=90),
+                          policy=EfficientZeroCollectPolicy(cfg, model), policy_config=cfg)
+    segs, meta = col.collect(n_episode=n_ep, policy_kwargs=dict(temperature=1.0, epsilon=0.0))
+    assert col._device is not None and col._device.search.ez, "the EZ policy did not take the device path"
+    assert col._device.search.mcts.last_path == "fused"
+    eps = _played(col.last_schedule)
+    assert sum(len(e) for e in eps) == n_ep
+    env = EpisodeEnv(eps)
+    ref_segs, ref_meta, _ = ref_collect(cfg, env, EpisodeForward(env), n_ep)
+    _compare(segs, meta, ref_segs, ref_meta)
+    for e in sum(eps, []):
+        assert (e["visits"].sum(axis=1) == 8).all() and set(np.unique(e["reward"])) <= {-1.0, 0.0, 1.0}
+    counted = [e for r in col.last_schedule.played for e in r]
+    info = col._episode_info[-n_ep:]
+    assert sorted(d['reward'] for d in info) == sorted(float(e["episode_return"]) for e in counted)
+    for e in counted:
+        fr = np.rint(e["obs_segment"] * 255).astype(np.uint8)
+        assert e["episode_return"] == e["reward_segment"].sum()
+        assert pong_synth.replay_episode(fr, e["action_segment"], e["reward_segment"], 90,
+                                         episode_return=e["episode_return"]) is None

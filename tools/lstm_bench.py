@@ -42,10 +42,14 @@ def main():
     outs = [torch.empty(B, H, device=dev) for _ in range(4)]
     ws = torch.zeros((L.lzm_ez_lstm_workspace_bytes(B, H) + 15) // 16 * 4, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
+    # the rows' split scales (lzm_conv.h ls_row_exp of each row's max)
+    xscale = torch.tensor([14 - int(np.floor(np.log2(max(float(v), 1.0)))) for v in xin.abs().amax(dim=1).cpu()],
+                          dtype=torch.int32, device=dev)
 
     def fused():
-        _lib.call("lzm_ez_lstm_step", B, K, H, P(xin), P(frag), P(bias), P(cpool), P(x), P(slen), 5, P(outs[0]),
-                  P(outs[1]), P(outs[2]), P(outs[3]), P(ws) if a.splitk else None, P(err), _lib.stream_ptr())
+        _lib.call("lzm_ez_lstm_step", B, K, H, P(xin), P(xscale), P(frag), P(bias), P(cpool), P(x), P(slen), 5,
+                  P(outs[0]), P(outs[1]), P(outs[2]), P(outs[3]), P(ws) if a.splitk else None, P(err), None,
+                  _lib.stream_ptr())
 
     def blas():
         gates = torch.addmm(bias, xin, W.t())
