@@ -485,6 +485,33 @@ def algorithmic_bytes(B, A, H, V, dbar):
     return {"traverse": trav, "decode_backprop": dec}
 
 
+def survey_hbm(sims_per_s, A, H, V, dbar, extra=0, note=None):
+    """BASELINE.md's HBM-roofline fraction: sims/s x SURVEY.md §8(d)'s algorithmic bytes per simulation / 8 TB/s,
+    with d-bar the measured mean search_len. Bytes per simulation: select d(16A + 12), leaf record 16, gather
+    4H + 4, scatter 4H, decode 8V + 4A, expand 16A + 16, backup 24(d + 1) + 8 (+ extra: EfficientZero's LSTM
+    state, 4 x 512 x 4 B). H is the latent's float count: 128 for the MLP configs, 64 x 8 x 8 = 4096 for the conv
+    configs (§8(d)'s C3 / C5 figures used 1024, a 64 x 4 x 4 latent: the reference's DownSample ends at 8 x 8 for
+    64 x 64 frames, common.py:258-262)."""
+    per_sim = dbar * (16 * A + 12) + 16 + (4 * H + 4) + 4 * H + (8 * V + 4 * A) + (16 * A + 16) + 24 * (dbar + 1) + 8 \
+        + extra
+    gbs = sims_per_s * per_sim / 1e9
+    out = {"definition": "sims/s x SURVEY.md 8(d) bytes/sim / peak HBM (BASELINE.md)", "bytes_per_sim": round(per_sim, 1),
+           "mean_search_len": round(dbar, 3), "A": A, "H": H, "V": V, "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 6)}
+    if note:
+        out["note"] = note
+    return out
+
+
+def az_mean_depth(m, B, S):
+    """AlphaZero: the mean simulation depth from the exported trees — every simulation adds one visit to each
+    non-root node of its path, so sum over non-root nodes of the visits / (B S) is the mean depth"""
+    visit, _, _, nn = m.export_tree(B)  # [B][1 + 9 (S + 1)] node visits, root first; nodes in use per board
+    used = torch.arange(visit.shape[1], device=visit.device).unsqueeze(0) < nn.unsqueeze(1)
+    used[:, 0] = False
+    return float((visit.double() * used).sum().item() / (B * S))
+
+
 def host_cpu_info():
     """The box's host CPU as the CPU-baseline line records it: nproc (os.cpu_count, the whole
     machine), the affinity mask, the job's thread share (OMP_NUM_THREADS, which the GPU pool sets
@@ -850,6 +877,8 @@ def secondary_breakout(args, world, rank, device):
            "data": "synthetic (random-init conv MuZeroModel; Breakout stand-in env, ALE absent)"}
     if rank == 0:
         out["roofline"] = conv_roofline(step, model, B, S, device)
+        out["hbm_roofline"] = survey_hbm(out["value"] / world, 4, 4096, 601, out["roofline"]["mean_search_len"],
+                                         note="per GPU (the value / n_gpus) against one GPU's HBM")
     return out
 
 
@@ -951,6 +980,7 @@ def config1(args, device, cpu):
            "value": round(B * S * steps / el, 1), "unit": "sims/s", "ms_per_step": round(el / steps * 1e3, 4),
            "steps": steps, "n_gpus": 1, "dtype": "f32", "tie_stream_errors": tie, "search_diag": sdiag,
            "roofline": mlp_roofline(step, B, S, device)}
+    out["hbm_roofline"] = survey_hbm(out["value"], 2, 128, 601, out["roofline"]["mean_search_len"])
     if cpu:
         out["cpu_baseline"] = cpu_baseline_ptree(B, S, 0.15 * args.cpu_baseline_secs)
     return out
@@ -979,6 +1009,7 @@ def config3(args, device, cpu):
            "search_path": step.mcts.last_path, "tie_stream_errors": tie, "search_diag": sdiag,
            "data": "synthetic (random-init conv EfficientZeroModel; Pong stand-in env, ALE absent)",
            "roofline": conv_roofline(step, model, B, S, device)}
+    out["hbm_roofline"] = survey_hbm(out["value"], 6, 4096, 101, out["roofline"]["mean_search_len"], extra=4 * 512 * 4)
     if cpu:
         out["cpu_baseline"] = cpu_baseline_conv("ez", B, S, model, 0.5 * args.cpu_baseline_secs, device)
     return out
@@ -1014,6 +1045,9 @@ def config4(args, device, cpu):
         el = time.perf_counter() - t0
     visits = m.last_visits(B)
     assert bool((visits.sum(dim=1) == S).all()), "AlphaZero root visits do not sum to num_simulations"
+    with torch.no_grad():  # one more search that keeps its trees, for the mean depth
+        m.search_fused(db, ds, fnet, 1.0, True, export_tree=True)
+    dbar = az_mean_depth(m, B, S)
     with torch.no_grad(), FlopCounterMode(display=False) as fc:
         model.compute_policy_value(torch.zeros(B, 3, 3, 3, device=device))
     per_op = {str(k): v for k, v in fc.get_flop_counts().get("Global", {}).items()}
@@ -1033,7 +1067,11 @@ def config4(args, device, cpu):
                         "traffic": pmc_traffic("az_search_fused_kernel"), "traffic_source": pmc_source(),
                         "alg_flops_per_sim": int(flops),
                         "alg_conv_flops_per_sim": int(conv), "launch_us": round(sec * 1e6, 1),
-                        "sims_per_launch": B * S}}
+                        "sims_per_launch": B * S},
+           # the board's 27 state floats stand for the latent (gathered; the tree stores no latent to scatter)
+           "hbm_roofline": survey_hbm(B * S * steps / el, 9, 27, 1, dbar, extra=4 * 9 - 4 * 27 - 8,
+                                      note="AlphaZero: gather = the 27-float board state, decode = 9 policy logits + "
+                                           "the value, no latent scatter")}
     if cpu:
         out["cpu_baseline"] = cpu_baseline_az(model, boards, starts, S, 0.2 * args.cpu_baseline_secs)
     return out
@@ -1120,7 +1158,12 @@ def main():
                 "process_group": (dist.get_backend() if dist.is_initialized() else None) if rccl1 is None
                 else {"world1": rccl1},
                 "tie_stream_errors": tie_errors, "search_diag": sdiag, "ranks": ranks,
-                "trajectory": traj, "roofline": roofline, "cpu_baseline": cpu, "config5": config5, **extra}
+                "trajectory": traj, "roofline": roofline,
+                "hbm_roofline": survey_hbm(value / world, 2, 128, 601, roofline["mean_search_len"],
+                                           note="per GPU (the value / n_gpus) against one GPU's HBM")
+                if roofline and wl == "cartpole" else
+                (survey_hbm(value / world, 4, 4096, 601, roofline["mean_search_len"]) if roofline else None),
+                "cpu_baseline": cpu, "config5": config5, **extra}
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

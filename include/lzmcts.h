@@ -580,11 +580,15 @@ int lzm_ez_lstm_prepare(int K, int H, const float *W, float *out);
  * is split over two workgroups per tile when every workgroup fits on the GPU at once (err: a sticky
  * int32 counting hand-off timeouts, required with the workspace). */
 int64_t lzm_ez_lstm_workspace_bytes(int B, int H);
+/* test support: n workgroups, each holding a CU (its whole LDS) for usec microseconds, on `stream` — another
+ * stream's kernel occupying CUs while a co-resident grid (lzm_search_conv_ez) launches */
+int lzm_debug_hold_cus(int n, int usec, void *stream);
 /* diagnostics: lzm_ez_lstm_step launches record shader-clock stamps into buf [blocks][8] (nullptr: off) */
 int lzm_debug_lstm_stamps(void *buf);
 /* Device address of the handle's sticky error word i (0..7) for kernels launched outside the handle
- * (word 3: lzm_ez_lstm_step's hand-off timeouts, word 4: split-fp16 range errors); lzm_check_errors
- * reports them. */
+ * (word 3: lzm_ez_lstm_step's hand-off timeouts, word 4: split-fp16 range errors, word 5: the one-launch conv
+ * searches' abort word — set by their first wait that times out (200 ms), after which every wait of that launch
+ * returns at once); lzm_check_errors reports them (and clears word 5 with the rest). */
 int32_t *lzm_error_word(lzm_handle *h, int i);
 /* xscale [B]: each row's split scale exponent (lzm_conv_trunk_xin_p writes it; any s with |x 2^s| < 2^15 over the
  * row is correct, 14 - floor(log2 max |row|) keeps the most bits); range_err (nullable): counts split values

@@ -264,6 +264,10 @@ constexpr int kBxAhead = 3;  // default weight read-ahead (chunks)
 // the EZ search's read-ahead: with fp16 terms (two uint4s per chunk) 5 chunks fit its registers and measured
 // 2.49 -> 2.46 ms per Pong search; the Breakout search even at 2, 3, 4, 5 (profiles/r05/ab/ab_ahead.txt)
 constexpr int kBxAheadEz = 5;
+#ifndef LZM_RANGE_DIAG
+#define LZM_RANGE_DIAG 0  // timing experiments only (results invalid): 1 = no max reduction, 2 = + no lane maxima,
+                          // 3 = + max-form ReLU, 4 = + no scale multiplies
+#endif
 constexpr int kBxWExp = 24;   // weight-row scale exponents within +-24
 constexpr int kBxAExp = 100;  // activation scale exponents within +-100: 2^-(e + s) stays a normal f32
 
@@ -344,15 +348,15 @@ __device__ __forceinline__ void bx_prefetch(BxRing<AHEAD> &r, const uint4 *__res
 }
 
 struct BxNoHook {
-  __device__ void operator()() const {}
+  __device__ void operator()(int) const {}
 };
 
 // one convolution for this wave's 16 out-channels x 64 pixels: NCH = 18 chunks (3x3) or 2 (1x1), its
 // first AHEAD chunks already in the ring (bx_prefetch). DIAG = 1: no weight loads (timing
 // experiments only, results invalid). Software pipeline, in issue order (the scheduling barriers keep
 // the compiler from sinking loads next to their first use): weights of chunk s + AHEAD, activations
-// of chunk s + 1, then chunk s's 12 MFMAs. hook(): VALU work run in chunk 1's MFMA shadow (the range
-// bookkeeping's wave reduction).
+// of chunk s + 1, then chunk s's 12 MFMAs. hook(s): a little VALU work in chunk s's MFMA shadow (the range
+// bookkeeping's wave reduction, one butterfly step per chunk).
 template <int NCH, int AHEAD, int DIAG, class Hook = BxNoHook>
 __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restrict__ wf, BxRing<AHEAD> &r, int lane,
                                         bxf4 (&acc)[4], const Hook &hook = Hook()) {
@@ -390,7 +394,7 @@ __device__ __forceinline__ void bx_conv(const uint16_t *in, const uint4 *__restr
     for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(x[t][0]), bx_ash(w[1]), acc[t], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bx_ash(x[t][0]), bx_ash(w[0]), acc[t], 0, 0, 0);
-    if (s == (NCH > 1 ? 1 : 0)) hook();
+    hook(s);
     // issue the next chunks' loads in the MFMA gaps (an MFMA holds the vector issue for half its
     // cycles): weights first (they have the longest way), then one activation read per MFMA
     const int nw = (s + AHEAD < NCH && DIAG != 1) ? kBxTerms : 0, na = s + 1 < NCH ? 4 * kBxTerms : 0;
@@ -420,7 +424,8 @@ __device__ __forceinline__ int bx_ep_pos(int lane, int t, int r) {
 
 // 3x3 epilogue: v = relu(acc f + bias [+ amap] [+ xres]) (f = 2^-(e_c + s_in): the weight row's and the input's
 // scales undone) -> the split planes of `out` as v 2^s_out (so = 2^s_out); KEEP: xres = v. Returns the max of
-// this lane's |v| as bits (NaN above every finite value) for the output's range bookkeeping.
+// this lane's v as unsigned bits (v >= +0 or NaN: a NaN of either sign above every finite value) for the output's
+// range bookkeeping (RELU only).
 // RELU = false: store acc as is (the input latent's staging; f = 1, bias 0)
 template <bool RELU = true>
 __device__ __forceinline__ uint32_t bx_epilogue3(const bxf4 (&acc)[4], uint16_t *out, float f, float bc, bool use_am,
@@ -435,15 +440,18 @@ __device__ __forceinline__ uint32_t bx_epilogue3(const bxf4 (&acc)[4], uint16_t 
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float x = RELU ? __fmaf_rn(acc[t][r], f, bc) : acc[t][r];
+      float x = RELU ? (LZM_RANGE_DIAG >= 4 ? acc[t][r] + bc : __fmaf_rn(acc[t][r], f, bc)) : acc[t][r];
       if (use_am) x += r == 0 ? am[t].x : r == 1 ? am[t].y : r == 2 ? am[t].z : am[t].w;
       if (add_res) x += xres[4 * t + r];
-      if (RELU) x = x < 0.f ? 0.f : x;  // (NaN stays NaN)
+      // relu: NaN stays NaN, -0 becomes +0, so every output's bits order as unsigned integers with a NaN of either
+      // sign above +inf (the range bookkeeping's max needs no masking)
+      if (RELU) x = LZM_RANGE_DIAG >= 3 ? (x > 0.f ? x : 0.f) : (x <= 0.f ? 0.f : x);
       if (keep) xres[4 * t + r] = x;
       v[r] = x;
     }
-    mx = max(mx, max(max(__float_as_uint(v[0]) & 0x7fffffffu, __float_as_uint(v[1]) & 0x7fffffffu),
-                     max(__float_as_uint(v[2]) & 0x7fffffffu, __float_as_uint(v[3]) & 0x7fffffffu)));
+    if (LZM_RANGE_DIAG < 2)
+      mx = max(max(mx, __float_as_uint(v[0])), max(max(__float_as_uint(v[1]), __float_as_uint(v[2])),
+                                                     __float_as_uint(v[3])));
     // lanes 2j, 2j + 1 hold channels c, c + 1 (one dword of a plane row): per pixel pair (2k, 2k + 1)
     // the even lane writes pixel 2k's dword and the odd lane pixel 2k + 1's, after one DPP swap
 #pragma unroll
@@ -451,7 +459,7 @@ __device__ __forceinline__ uint32_t bx_epilogue3(const bxf4 (&acc)[4], uint16_t 
       const float send = odd ? v[2 * k] : v[2 * k + 1];
       const float recv = __builtin_bit_cast(
           float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-      const bxf2 pr = (odd ? bxf2{recv, v[2 * k + 1]} : bxf2{v[2 * k], recv}) * so;  // (channel c & ~1, c | 1)
+      const bxf2 pr = (odd ? bxf2{recv, v[2 * k + 1]} : bxf2{v[2 * k], recv}) * (LZM_RANGE_DIAG >= 4 ? 1.f : so);
       const bxb2 h = __builtin_convertvector(pr, bxb2);
       const bxb2 l = __builtin_convertvector(pr - __builtin_convertvector(h, bxf2), bxb2);
       const int r = 2 * k + odd;
@@ -475,13 +483,15 @@ __device__ __forceinline__ void bx_stage_bounds(float4 *s_bd, const float *w, co
 
 // Range bookkeeping of one workgroup's trunk (every wave holds the same copy): the exact max |x| of the
 // current layer input and of the current block input, the input buffer's scale exponent, a sticky failure.
-// Per layer: the epilogue writes each lane's max (bits) to LDS, unreduced; after the barrier every wave reads
-// four of the 256 and reduces them inside the next convolution's MFMA stream (bx_conv's hook): the max of a
-// layer's output is first needed for the NEXT layer's output scale.
+// Per layer: the epilogue writes each lane's max of its outputs (bits) to LDS, unreduced; after the barrier
+// every lane reads four of the 256 and the wave reduces them inside the next convolution, one butterfly step per
+// weight chunk (bx_range_step as bx_conv's hook), where each step's operand is a chunk old: the max of a layer's
+// output is first needed for the NEXT layer's output scale.
 struct BxRange {
   float m_in, m_blk;
   int s_in, bad;
-  uint4 lm;  // this lane's four of the previous epilogue's 256 lane maxima (read after the barrier)
+  uint32_t m;  // the reduction in flight
+  uint4 lm;    // this lane's four of the previous epilogue's 256 lane maxima (read after the barrier)
 };
 
 // this wave's max (lane maxima as bits) into its LDS slot; read back after the next barrier (bx_read_max)
@@ -508,6 +518,7 @@ __device__ __forceinline__ BxRange bx_range_input(float m) {
   rg.m_in = rg.m_blk = m;
   rg.s_in = bx_scale_exp(m, kBxAExp);
   rg.bad = !(m * bx_pow2(rg.s_in) < 65504.f);
+  rg.m = 0u;
   rg.lm = uint4{0u, 0u, 0u, 0u};
   return rg;
 }
@@ -524,12 +535,26 @@ __device__ __forceinline__ void bx_range_fetch(BxRange &rg, const uint32_t *slot
   rg.lm = reinterpret_cast<const uint4 *>(slots)[lane];
   rg.s_in = s_out;
 }
-// ... reduced (bx_conv's hook, or directly): the layer input's exact max, checked against its scale
+// step s of the reduction (s = 0 .. 7; bx_conv's hook calls it per chunk): then the layer input's exact max,
+// checked against its scale (lane maxima are unsigned bits of outputs >= +0 or NaN: bx_epilogue3)
+__device__ __forceinline__ void bx_range_step(BxRange &rg, int s) {
+  if (LZM_RANGE_DIAG >= 1) return;
+  if (s == 0) rg.m = max(max(rg.lm.x, rg.lm.y), max(rg.lm.z, rg.lm.w));
+  if (s == 1) rg.m = max(rg.m, (uint32_t)xor_partner<32>((int)rg.m));
+  if (s == 2) rg.m = max(rg.m, (uint32_t)xor_partner<16>((int)rg.m));
+  if (s == 3) rg.m = max(rg.m, (uint32_t)xor_partner<8>((int)rg.m));
+  if (s == 4) rg.m = max(rg.m, (uint32_t)xor_partner<4>((int)rg.m));
+  if (s == 5) rg.m = max(rg.m, (uint32_t)xor_partner<2>((int)rg.m));
+  if (s == 6) rg.m = max(rg.m, (uint32_t)xor_partner<1>((int)rg.m));
+  if (s == 7) {
+    const float M = __uint_as_float(rg.m);
+    rg.bad |= !(M * bx_pow2(rg.s_in) < 65504.f);
+    rg.m_in = M;
+  }
+}
 __device__ __forceinline__ void bx_range_reduce(BxRange &rg) {
-  const uint32_t m = (uint32_t)xor_max((int)max(max(rg.lm.x, rg.lm.y), max(rg.lm.z, rg.lm.w)));
-  const float M = __uint_as_float(m);
-  rg.bad |= !(M * bx_pow2(rg.s_in) < 65504.f);
-  rg.m_in = M;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) bx_range_step(rg, s);
 }
 
 // 1x1 layer (<= 32 out channels, waves 0 and 1): relu(conv x inv[c] 2^-s_in + b) -> global [c][p]
@@ -640,8 +665,8 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     }
     bxf4 acc[4];
     const bool gather = i > i0;  // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow
-    bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&]() {
-      if (gather) bx_range_reduce(rg);
+    bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&](int s) {
+      if (gather && s < 8) bx_range_step(rg, s);
     });
     if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
     const int s_out = bx_layer_scale(bdi, i == 0 || second, rg);

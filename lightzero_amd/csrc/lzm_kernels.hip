@@ -3011,6 +3011,28 @@ extern "C" int lzm_search_conv_ez(lzm_handle *h, int num_simulations, int pb_c_b
   return LZM_OK;
 }
 
+// Test support: n workgroups that each occupy a CU (the whole LDS) for `usec` microseconds of the 100 MHz real-time
+// clock, then exit — another stream's kernel holding CUs while a co-resident grid launches (tests only).
+__global__ void hold_cu_kernel(unsigned long long ticks) {
+  extern __shared__ uint4 hold_lds[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) hold_lds[0] = uint4{0u, 0u, 0u, 0u};
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+extern "C" int lzm_debug_hold_cus(int n, int usec, void *stream) {
+  if (n <= 0 || n > 4096 || usec <= 0 || usec > 2000000) {
+    set_err("lzm_debug_hold_cus: 1..4096 workgroups for up to 2 s");
+    return LZM_ERR_ARG;
+  }
+  static hipError_t attr = hipFuncSetAttribute((const void *)hold_cu_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)kMaxLds);
+  LZM_HIP(attr);
+  hipLaunchKernelGGL(hold_cu_kernel, dim3(n), dim3(64), kMaxLds, (hipStream_t)stream, (unsigned long long)usec * 100ull);
+  LZM_CHECK_LAUNCH();
+  return LZM_OK;
+}
+
 extern "C" int lzm_ez_lstm_input(int B, int Kr, int H, const float *r, const float *hpool, const int32_t *x, float *xin,
                                  void *stream) {
   if (B <= 0 || Kr <= 0 || H <= 0 || (Kr & 3) || (H & 3) || !r || !hpool || !x || !xin ||

@@ -101,6 +101,23 @@ struct ConvSearchArgs {
       off_lg, off_seed, off_lmax;
 };
 
+// Bounded waits of the one-launch conv searches (their grid must be co-resident; the host checks the static
+// occupancy bound, which cannot see another stream's kernel holding CUs): a wait gives up after kScSpinTicks
+// of the 100 MHz real-time clock (200 ms: a whole 256 x 50 search takes ~3 ms), counts err[0] and raises the
+// launch's abort word err[5], after which every other wait of the launch returns at once — a grid that is not
+// resident ends after ~one timeout with a search the host discards (mcts_ctree: the eager search restores
+// the tree and runs the generic path), instead of one timeout per wait.
+constexpr unsigned long long kScSpinTicks = 20000000ull;
+__device__ __forceinline__ bool sc_give_up(int32_t *err, unsigned long long t0) {
+  if (__hip_atomic_load(err + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+  if (__builtin_amdgcn_s_memrealtime() - t0 > kScSpinTicks) {
+    atomicAdd(err, 1);
+    __hip_atomic_store(err + 5, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+
 // Parity-mode draw offset of root b in simulation k: the sum of the depth flags of roots < b (the
 // reference's single rand() stream, cnode.cpp:783-796). Wave-wide, b <= 256 (lzm_search_conv checks
 // B <= 256): sc_lookback_issue puts every flag of a lane in flight (four loads), sc_lookback_finish
@@ -123,10 +140,9 @@ __device__ __forceinline__ int sc_lookback_finish(const ConvSearchArgs &p, int k
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int q = 64 * u + lane;
-    long long spins = 0;
+    const unsigned long long t0 = (v[u] >> 32) != epoch ? __builtin_amdgcn_s_memrealtime() : 0ull;
     while ((v[u] >> 32) != epoch) {
-      if (++spins > (1ll << 22)) {
-        atomicAdd(p.err, 1);
+      if (sc_give_up(p.err, t0)) {
         v[u] = epoch << 32;
         break;
       }
@@ -367,12 +383,9 @@ __device__ __forceinline__ float sc_decode(const ConvSearchArgs &p, const float 
 __device__ __forceinline__ unsigned long long sc_wait_word(const unsigned long long *w, unsigned long long epoch,
                                                            int32_t *err) {
   unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  long long spins = 0;
+  const unsigned long long t0 = (v >> 32) != epoch ? __builtin_amdgcn_s_memrealtime() : 0ull;
   while ((v >> 32) != epoch) {
-    if (++spins > (1ll << 22)) {
-      atomicAdd(err, 1);
-      return epoch << 32;
-    }
+    if (sc_give_up(err, t0)) return epoch << 32;
     __builtin_amdgcn_s_sleep(1);
     v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -578,11 +591,9 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         const float wsc = winv[i * 64 + c];
         bxf4 acc[4];
         // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow (the latent's: filed)
-        bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&]() {
-          if (i > 0) {
-            bx_range_reduce(rg);
-            if (i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
-          }
+        bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&](int s) {
+          if (i > 0 && s < 8) bx_range_step(rg, s);
+          if (i > 0 && s == 8 && i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
         });
         if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
         if (i == 0 && late) {
@@ -986,7 +997,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           const float4 no_am[4] = {};
           bx_epilogue3<false>(in4, buf(0), 1.f, 0.f, false, no_am, xres, false, false, bx_pow2(rg.s_in), lane, c);
         }
-        __syncthreads();
+          __syncthreads();
         stamp(1);
         for (int i = 0; i < n3; ++i) {
           const float *w = layer_w(i);
@@ -996,11 +1007,9 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           const float wsc = winv[i * 64 + c];
           bxf4 acc[4];
           // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow (the latent's: filed)
-          bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&]() {
-            if (i > 0) {
-              bx_range_reduce(rg);
-              if (i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
-            }
+          bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&](int s) {
+            if (i > 0 && s < 8) bx_range_step(rg, s);
+            if (i > 0 && s == 8 && i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
           });
           if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
           if (i == 0 && late) {

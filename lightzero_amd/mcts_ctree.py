@@ -680,12 +680,34 @@ class EfficientZeroMCTSCtree(object):
                                step["values"], True, cfg.value_delta_max)
                 else:
                     new_minmax(B, cfg.value_delta_max, dev, out=buf.mm)
+                # eager launches are checked for hand-off timeouts (another stream's kernel can hold
+                # CUs the static occupancy bound counted on): the tree (and the step counter) are kept, and a
+                # search whose waits timed out is discarded and re-run on the generic path
+                guard = bool(cfg.get('guard_handoffs', True)) and not torch.cuda.is_current_stream_capturing()
+                if guard:
+                    snap = self._snapshot(t)
+                    count0 = step["count"].clone() if step_in_kernel else None
                 try:
                     t.search_conv_ez(cz, S, buf.mm, None if step_in_kernel else buf.seeds, buf.vtp_in, buf.pool,
                                      buf.extra[0], buf.extra[1], int(cfg.lstm_horizon_len), int(cfg.pb_c_base),
                                      float(cfg.pb_c_init), float(np.float32(cfg.discount_factor)),
                                      bool(cfg.model.get('categorical_distribution', True)), rec=rec)
                     self.last_path = "fused"
+                    if guard and t.peek_errors()[0]:
+                        t.copy_roots_from(snap)
+                        t.reset_errors()
+                        if step_in_kernel:
+                            step["count"].copy_(count0)
+                            t.set_step()
+                            step_in_kernel = False
+                            step_seeds()
+                        if rec is not None:
+                            rec = _Recorder(S, B, t.A, dev)
+                            rec.is_reset = torch.zeros((S, B), dtype=torch.int32, device=dev)
+                            rec.seeds = buf.seeds.cpu().numpy().view(np.uint32)
+                        self.timeout_fallbacks = getattr(self, "timeout_fallbacks", 0) + 1
+                        self.last_path = "generic (hand-off timeout)"
+                        self._loop(t, model, buf, S, row, Hl, rec)
                 except _lib.ResidencyError:
                     if torch.cuda.is_current_stream_capturing():
                         raise
@@ -716,6 +738,17 @@ class EfficientZeroMCTSCtree(object):
             t.searched()
             roots._last_minmax = buf.mm
             self.last_record = rec
+
+    def _snapshot(self, t):
+        """a copy of tree t (lzm_copy_tree) in a handle kept for the purpose"""
+        key = (t.B, t.A, t.ez, t.fast_rng, str(t.device))
+        s = getattr(self, "_snap", None)
+        if s is None or s[0] != key:
+            s = (key, DeviceTree(t.B, t.A, t.sims_capacity, ez=t.ez, fast_rng=t.fast_rng, device=t.device))
+            self._snap = s
+        s[1].reserve(t.sims_capacity)
+        s[1].copy_roots_from(t)
+        return s[1]
 
     def search_with_reuse(self, roots: Any, model: torch.nn.Module, latent_state_roots: List[Any],
                           reward_hidden_state_roots: List[Any], to_play_batch: Union[int, List[Any]],

@@ -254,6 +254,12 @@ class DeviceTree:
         call("lzm_check_errors", self.h, out, int(bool(clear)), stream_ptr(stream))
         return list(out)
 
+    def peek_errors(self, stream=None):
+        """the sticky error words without raising or clearing them (synchronises the stream)"""
+        out = (ctypes.c_int32 * _lib.LZM_ERR_WORDS)()
+        _lib.load().lzm_check_errors(self.h, out, 0, stream_ptr(stream))
+        return list(out)
+
     def search_diagnostics(self):
         out = torch.zeros(4, dtype=torch.int32, device=self.device)
         call("lzm_search_diagnostics", self.h, ptr(out), stream_ptr())

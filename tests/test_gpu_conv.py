@@ -472,3 +472,32 @@ def test_ez_residency_refusal_falls_back_to_generic_with_same_results(monkeypatc
         with torch.cuda.graph(g):
             mcts.search(roots, model, a["lat0"], a["hidden0"], to_play, seeds=seeds)
     assert mcts.residency_fallbacks == 1
+
+
+def test_ez_handoff_timeout_falls_back_to_generic_with_same_results():
+    """another stream's kernel holds most CUs while the one-launch EZ search launches eagerly (the
+    static occupancy bound accepted the grid): the resident workgroups' hand-off waits give up after 200 ms
+    and abort the launch (error words 0 / 5), EfficientZeroMCTSCtree.search restores the tree it snapshotted
+    and runs the generic path — the same visit counts, values and trajectories as an undisturbed search, the
+    error words clear"""
+    from lightzero_amd import _lib
+    from lightzero_amd.mcts_ctree import EfficientZeroMCTSCtree
+    from lightzero_amd.utils import EasyDict
+    B, S = 64, 10
+    model = conv_model("ez", 21)
+    a = run_search("ez", B, S, seed=22, model=model, record=False)
+    assert a["path"] == "fused"
+    cfg = EasyDict(dict(num_simulations=S, discount_factor=0.997, device=DEV, lstm_horizon_len=5,
+                        model=dict(support_scale=50, categorical_distribution=True)))
+    mcts = EfficientZeroMCTSCtree(cfg)
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    hog = torch.cuda.Stream(device=DEV)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(hog):
+        _lib.call("lzm_debug_hold_cus", cus - 40, 700000, _lib.stream_ptr(hog))  # 700 ms on all but 40 CUs
+    b = run_search("ez", B, S, seed=22, model=model, record=False, mcts=mcts)
+    torch.cuda.synchronize()
+    print(f"path under a CU-holding kernel: {b['path']}, fallbacks {getattr(mcts, 'timeout_fallbacks', 0)}")
+    assert b["path"] == "generic (hand-off timeout)" and mcts.timeout_fallbacks == 1
+    for key in ("dist", "values", "traj"):
+        assert np.array_equal(a[key], b[key]), key
