@@ -188,9 +188,10 @@ def test_game_segment_surface():
     assert torch is not None
 
 
-def test_device_path_routes_plain_muzero_policies_only():
-    """a DeviceEnvManager selects the device collector for a MuZero policy only: an EfficientZero policy
-    (a MuZeroCollectPolicy subclass) keeps the host loop with its value-prefix / LSTM search"""
+def test_device_path_routes_muzero_and_efficientzero_policies():
+    """a DeviceEnvManager selects the device collector for MuZero and EfficientZero policies alike (the
+    device search step picks the value-prefix / LSTM search from the model, efficientzero.py:538-656);
+    collect_with_pure_policy keeps the host loop"""
     from lightzero_amd.envs import DeviceBreakoutEnvManager
     from lightzero_amd.policy import EfficientZeroCollectPolicy, MuZeroCollectPolicy
     cfg = policy_config(num_simulations=4, device='cpu',
@@ -198,7 +199,7 @@ def test_device_path_routes_plain_muzero_policies_only():
                                    image_channel=1, model_type='conv'))
     model = torch.nn.Linear(1, 1)  # (routing only: no forward)
     env = DeviceBreakoutEnvManager(4, seed=1)
-    for cls, device_path in ((MuZeroCollectPolicy, True), (EfficientZeroCollectPolicy, False)):
+    for cls, device_path in ((MuZeroCollectPolicy, True), (EfficientZeroCollectPolicy, True)):
         col = MuZeroCollector(env=env, policy=cls(cfg, model), policy_config=cfg)
         assert col._device_path(False) is device_path, cls.__name__
         assert col._device_path(True) is False  # collect_with_pure_policy: the host loop
