@@ -585,6 +585,10 @@ int64_t lzm_ez_lstm_workspace_bytes(int B, int H);
 int lzm_debug_hold_cus(int n, int usec, void *stream);
 /* diagnostics: lzm_ez_lstm_step launches record shader-clock stamps into buf [blocks][8] (nullptr: off) */
 int lzm_debug_lstm_stamps(void *buf);
+/* diagnostics: lzm_az_search_fused launches add their per-phase shader-clock cycles into the device uint64[8]
+ * buf ({descend, convolutions, 1x1 heads, 0, FC1/LayerNorm/FC2/softmax, expand+backup, kernel, simulations}
+ * summed over workgroups; nullptr: the production instantiation) */
+int lzm_debug_az_stamps(void *buf);
 /* Device address of the handle's sticky error word i (0..7) for kernels launched outside the handle
  * (word 3: lzm_ez_lstm_step's hand-off timeouts, word 4: split-fp16 range errors, word 5: the one-launch conv
  * searches' abort word — set by their first wait that times out (200 ms), after which every wait of that launch

@@ -73,6 +73,7 @@ SIGNATURES = {
     "lzm_ez_lstm_workspace_bytes": [_i, _i],
     "lzm_error_word": [_vp, _i],
     "lzm_debug_lstm_stamps": [_vp],
+    "lzm_debug_az_stamps": [_vp],
     "lzm_debug_hold_cus": [_i, _i, _vp],
     "lzm_ez_lstm_step": [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "lzm_search_conv": [_vp, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _i,

@@ -23,7 +23,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "lzm_az.h"
+#include "lzm_tree.h"  // xor_partner, readlane_f
 
 namespace lzm {
 
@@ -82,7 +85,7 @@ struct AzNetRegs {
   static constexpr int T = AzNetLds<R>::T;
   float b0[2];                  // conv0 fragments (steps w, w + 4)
   float br[4 * NRES][9];        // 3x3 conv fragments (steps 9w .. 9w + 8)
-  float bh[2];                  // 1x1 head fragments (step w, two N tiles)
+  float bh[4];                  // 1x1 head fragments (K steps 0..3 of N tile w & 1)
   int koff[9];                  // im2col offsets of this lane's k for steps 9w + j
   int koff0[2];
   int rb[T], rb0[T];            // row base offsets per tile (activation / input planes)
@@ -135,7 +138,7 @@ __device__ inline void az_net_init(const float *__restrict__ w, const AzNetSmem 
     g.koff[j] = (k / 9) * kAzPlane + ((k % 9) / 3) * 5 + (k % 3);
   }
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) g.bh[nt] = w[L.head + (wv * 2 + nt) * 64 + lane];
+  for (int k = 0; k < 4; ++k) g.bh[k] = w[L.head + (k * 2 + (wv & 1)) * 64 + lane];
 #pragma unroll
   for (int t = 0; t < AzNetLds<R>::T; ++t) {
     const int m = 16 * t + (lane & 15);
@@ -167,12 +170,26 @@ __device__ inline void az_conv_epilogue(const AzNetSmem &s, const float *bias, c
   }
 }
 
+// diagnostics (STAMPS instantiations): thread 0 adds the shader-clock cycles since its last stamp to st[n]
+template <bool STAMPS>
+__device__ inline void az_stamp(unsigned long long *st, unsigned long long &prev, int n) {
+  if (STAMPS && threadIdx.x == 0) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    st[n] += now - prev;
+    prev = now;
+  }
+}
+
 // evaluates the R boards whose input planes are in s.xin; leaves probs [R][9] / value [R] in s.out.
-// Starts and ends with a workgroup barrier.
-template <int R, int NRES>
-__device__ inline void az_net_forward(const AzNetSmem &s, const AzNetRegs<R, NRES> &g) {
+// Starts and ends with a workgroup barrier. STAMPS: phases 1 (convolutions), 2 (1x1 heads), 4 (FC1,
+// LayerNorm, FC2, softmax) into st[] (thread 0's registers)
+template <int R, int NRES, bool STAMPS = false>
+__device__ inline void az_net_forward(const AzNetSmem &s, const AzNetRegs<R, NRES> &g,
+                                      unsigned long long *st = nullptr, unsigned long long *prev = nullptr) {
   constexpr int T = AzNetLds<R>::T;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  unsigned long long pdummy = 0;
+  unsigned long long &pv = prev ? *prev : pdummy;
   __syncthreads();
   // ---- conv0: 3 -> 16
   {
@@ -209,85 +226,95 @@ __device__ inline void az_net_forward(const AzNetSmem &s, const AzNetRegs<R, NRE
     if (l & 1) cur = dst;
   }
   __syncthreads();
-  // ---- 1x1 heads: 16 -> 32 (value 0..15 | policy 16..31), K step = this wave's 4 channels
+  az_stamp<STAMPS>(st, pv, 1);
+  // ---- 1x1 heads: 16 -> 32 (value 0..15 | policy 16..31). (row tile t, N tile nt) pair p = 2 t + nt runs on
+  // wave p % 4 (so nt = wave & 1 and t & 1 = wave >> 1) as one chain of 4 MFMAs over K = 16: no partial sums
   {
     const float *x = s.x[cur];
+    const int nt = wv & 1;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-      const float a = x[g.rb[t] + (4 * wv + (lane >> 4)) * kAzPlane + 6];
+      if ((t & 1) != (wv >> 1)) continue;  // wave-uniform
+      azf4 acc = azf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        azf4 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g.bh[nt], azf4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        *(azf4 *)&s.red[((wv * T + t) * 2 + nt) * 256 + lane * 4] = acc;
+      for (int k = 0; k < 4; ++k)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[g.rb[t] + (4 * k + (lane >> 4)) * kAzPlane + 6], g.bh[k], acc, 0, 0, 0);
+      const int n = 16 * nt + (lane & 15);
+      const float bn = s.bias[16 + 64 * 16 + n];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = 16 * t + 4 * (lane >> 4) + v;
+        const float y = acc[v] + bn;
+        if (m < 9 * R) s.hd[(m / 9) * 288 + n * 9 + (m % 9)] = y > 0.0f ? y : 0.0f;
       }
     }
   }
   __syncthreads();
-  for (int e = tid; e < T * 2 * 256; e += kAzfThreads) {
-    const int t = e >> 9, nt = (e >> 8) & 1, ln = (e >> 2) & 63, v = e & 3;
-    const int m = 16 * t + 4 * (ln >> 4) + v, n = 16 * nt + (ln & 15);
-    if (m >= 9 * R) continue;
-    const int i = e & 511;
-    float acc = s.red[(0 * T + t) * 512 + i];
-    acc += s.red[(1 * T + t) * 512 + i];
-    acc += s.red[(2 * T + t) * 512 + i];
-    acc += s.red[(3 * T + t) * 512 + i];
-    acc += s.bias[16 + 64 * 16 + n];
-    s.hd[(m / 9) * 288 + n * 9 + (m % 9)] = acc > 0.0f ? acc : 0.0f;
-  }
-  __syncthreads();
-  // ---- FC1 per head: (board, head, unit, quarter) -> 4 lanes per dot of 144
+  az_stamp<STAMPS>(st, pv, 2);
+  // ---- per (board, head) pair, on wave pair % 4: FC1 as 8 units x 8 lanes (18 products per lane, an
+  // xor-butterfly sum: every lane of an 8-lane group ends with the same bits), the 8 hidden values to
+  // wave-uniform registers, then LayerNorm(8), ReLU, FC2 and (policy) the softmax over lanes 0..8
   const float *hw = s.heads;
-  for (int e = tid; e < R * 64; e += kAzfThreads) {
-    const int r = e >> 6, head = (e >> 5) & 1, j = (e >> 2) & 7, qq = e & 3;
-    const float *wrow = hw + (head ? kAzP1 : kAzV1) + j * 144 + qq * 36;
-    const float *in = s.hd + r * 288 + head * 144 + qq * 36;
+  for (int pr = wv; pr < 2 * R; pr += 4) {
+    const int r = pr >> 1, head = pr & 1;
+    const int j = lane >> 3, q = lane & 7;
+    const float *wrow = hw + (head ? kAzP1 : kAzV1) + j * 144 + q * 18;
+    const float *in = s.hd + r * 288 + head * 144 + q * 18;
     float acc = 0.0f;
-#pragma unroll 12
-    for (int i = 0; i < 36; ++i) acc = fmaf(wrow[i], in[i], acc);
-    acc += __shfl_xor(acc, 1);
-    acc += __shfl_xor(acc, 2);
-    if (qq == 0) s.hid[r * 16 + head * 8 + j] = acc + hw[(head ? kAzP1b : kAzV1b) + j];
-  }
-  __syncthreads();
-  // ---- LayerNorm(8), ReLU, FC2; softmax over the policy logits
-  if (tid < 2 * R) {
-    const int r = tid >> 1, head = tid & 1;
-    const float *h = s.hid + r * 16 + head * 8;
+#pragma unroll
+    for (int i = 0; i < 18; ++i) acc = fmaf(wrow[i], in[i], acc);
+    acc += xor_partner<1>(acc);
+    acc += xor_partner<2>(acc);
+    acc += xor_partner<4>(acc);
+    acc += hw[(head ? kAzP1b : kAzV1b) + j];
+    float h[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) h[u] = readlane_f(acc, 8 * u);
     float mean = 0.0f;
-    for (int j = 0; j < 8; ++j) mean += h[j];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) mean += h[u];
     mean *= 0.125f;
     float var = 0.0f;
-    for (int j = 0; j < 8; ++j) var = fmaf(h[j] - mean, h[j] - mean, var);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) var = fmaf(h[u] - mean, h[u] - mean, var);
     var *= 0.125f;
     const float rs = 1.0f / sqrtf(var + 1e-5f);
     float y[8];
     const float *gg = hw + (head ? kAzPg : kAzVg), *bb = hw + (head ? kAzPb : kAzVb);
-    for (int j = 0; j < 8; ++j) {
-      const float z = (h[j] - mean) * rs * gg[j] + bb[j];
-      y[j] = z > 0.0f ? z : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float z = (h[u] - mean) * rs * gg[u] + bb[u];
+      y[u] = z > 0.0f ? z : 0.0f;
     }
     if (head == 0) {
       float v = hw[kAzV2b];
-      for (int j = 0; j < 8; ++j) v = fmaf(hw[kAzV2 + j], y[j], v);
-      s.out[R * 9 + r] = v;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v = fmaf(hw[kAzV2 + u], y[u], v);
+      if (lane == 0) s.out[R * 9 + r] = v;
     } else {
-      float lg[9], mx = -3.4e38f;
-      for (int a = 0; a < 9; ++a) {
-        float z = hw[kAzP2b + a];
-        for (int j = 0; j < 8; ++j) z = fmaf(hw[kAzP2 + a * 8 + j], y[j], z);
-        lg[a] = z;
-        mx = fmaxf(mx, z);
+      const int a = lane & 15;
+      float z = -__builtin_inff();
+      if (a < 9) {
+        z = hw[kAzP2b + a];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) z = fmaf(hw[kAzP2 + a * 8 + u], y[u], z);
       }
-      float sum = 0.0f;
-      for (int a = 0; a < 9; ++a) {
-        lg[a] = expf(lg[a] - mx);
-        sum += lg[a];
-      }
-      for (int a = 0; a < 9; ++a) s.out[r * 9 + a] = lg[a] / sum;
+      float mx = z;
+      mx = fmaxf(mx, xor_partner<1>(mx));
+      mx = fmaxf(mx, xor_partner<2>(mx));
+      mx = fmaxf(mx, xor_partner<4>(mx));
+      mx = fmaxf(mx, xor_partner<8>(mx));
+      const float e = a < 9 ? expf(z - mx) : 0.0f;
+      float sum = e;
+      sum += xor_partner<1>(sum);
+      sum += xor_partner<2>(sum);
+      sum += xor_partner<4>(sum);
+      sum += xor_partner<8>(sum);
+      if (lane < 9) s.out[r * 9 + lane] = e / sum;
     }
   }
   __syncthreads();
+  az_stamp<STAMPS>(st, pv, 4);
 }
 
 // ---- standalone evaluation: state [n][3][3][3] -> probs [n][9], value [n]
@@ -326,19 +353,56 @@ struct AzFusedArgs {
   double *probs_out;
   int32_t *action_out;
   AzTree t;  // constants (lut_pb, lut_sqrt, noise) and, when export_tree, the destination of the trees
+  unsigned long long *stamps;  // STAMPS instantiations: [0] descend, [1] convolutions, [2] 1x1 heads, [3] 0,
+                               // [4] FC1 / LayerNorm / FC2 / softmax, [5] expand + backup, [6] kernel total, [7] sims
 };
 
-template <int R>
-struct AzTreeLds {
-  static size_t bytes(int cap, int S) {
-    return (size_t)R * cap * 16 + (size_t)(S + 1) * 16 + 81 * 8 + (size_t)R * (9 + 1 + kAzPath + 4 + 1) * 4 + 64;
+// group argmax of the pUCT scores (16 lanes): the lowest lane among the maxima (the reference's first strict
+// maximum in action order). The double score maps to an order-preserving 64-bit key whose maximum a DPP
+// butterfly finds (no LDS round trip); the lowest lane holding it comes from a ballot.
+__device__ inline int az_group_argmax(double sc, int gbase) {
+  sc += 0.0;  // -0.0 -> +0.0: equal scores, equal keys
+  const uint64_t u = __builtin_bit_cast(uint64_t, sc);
+  const uint64_t k0 = (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+  uint64_t k = k0;
+  auto step = [&](auto dd) __attribute__((always_inline)) {
+    constexpr int D = decltype(dd)::value;
+    const uint32_t lo = (uint32_t)xor_partner<D>((int)(uint32_t)k), hi = (uint32_t)xor_partner<D>((int)(uint32_t)(k >> 32));
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    k = o > k ? o : k;
+  };
+  step(std::integral_constant<int, 1>());
+  step(std::integral_constant<int, 2>());
+  step(std::integral_constant<int, 4>());
+  step(std::integral_constant<int, 8>());
+  return __builtin_ctz(az_group_mask(k0 == k, gbase));
+}
+
+// get_done_winner_cython.pyx on bit masks of the two players' stones (bit i = cell i). The reference scans
+// cells in row-major order and from each stone the directions that stay on the board, returning the first
+// full line: a line is only found from its first cell, so the winner is the owner of the full line with the
+// lowest first cell; no line and no empty cell is a draw.
+__device__ inline void az_done_winner_mask(uint32_t m1, uint32_t m2, int &done, int &winner) {
+  constexpr uint32_t kLine[8] = {0x007, 0x049, 0x111, 0x092, 0x054, 0x124, 0x038, 0x1C0};
+  constexpr int kStart[8] = {0, 0, 0, 1, 2, 2, 3, 6};  // first cell of each line (ascending)
+  winner = -1;
+  int first = 9;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (kStart[i] >= first) continue;
+    if ((m1 & kLine[i]) == kLine[i]) { first = kStart[i]; winner = 1; }
+    else if ((m2 & kLine[i]) == kLine[i]) { first = kStart[i]; winner = 2; }
   }
-};
+  done = winner != -1 || ((m1 | m2) & 0x1ffu) == 0x1ffu;
+}
 
-template <int R, int NRES>
+template <int R, int NRES, bool STAMPS = false>
 __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArgs a) {
   extern __shared__ float az_smem[];
   const int tid = threadIdx.x;
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long st_begin = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
+  unsigned long long st_prev = st_begin;
   const int cap = a.cap, S = a.S;
   // ---- LDS: doubles first (alignment), then the tree, then the network
   double *lut_pb = (double *)az_smem;
@@ -348,12 +412,7 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   float *tvsum = (float *)(tvisit + R * cap);
   float *tprior = tvsum + R * cap;
   int32_t *tmeta = (int32_t *)(tprior + R * cap);  // first (16 bits, 0xffff: leaf) | nch << 16 | act << 20
-  int32_t *rboard = tmeta + R * cap;
-  int32_t *rplayer = rboard + R * 9;
-  int32_t *path = rplayer + R;
-  int32_t *leaf = path + R * kAzPath;  // depth, done, winner, player
-  int32_t *nnodes = leaf + R * 4;
-  float *netp = (float *)(((uintptr_t)(nnodes + R) + 15) & ~(uintptr_t)15);
+  float *netp = (float *)(((uintptr_t)(tmeta + R * cap) + 15) & ~(uintptr_t)15);
   const AzNetSmem s = az_net_carve<R>(netp);
   AzNetRegs<R, NRES> g;
   az_net_init<R, NRES>(a.w, s, g);
@@ -365,94 +424,85 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   const int grp = tid >> 4, l = tid & 15, gbase = (tid & 63) & ~15;
   const int b = blockIdx.x * R + grp;
   const bool active = grp < R && b < a.B;  // group-uniform
+  // The group's search state lives in registers (uniform over its 16 lanes unless noted): the root board
+  // (lane l < 9: cell l), the node count, and between a descent and its expansion the leaf (node, depth,
+  // done, winner, player to move, the move that led to it, lane l < 9: cell l of its board; lane m: the
+  // node at depth m of the path)
+  int root_cell = 0, root_player = 1, nn = 1;
+  int lf_node = 0, lf_depth = 0, lf_done = 0, lf_winner = -1, lf_player = 1, lf_act = 15, lf_cell = 0, lf_path = 0;
   __syncthreads();  // xin zeroed by az_net_init before the roots are written
   if (active) {
-    const int player = a.start_index[b] == 0 ? 1 : 2;
-    const int cell = l < 9 ? a.boards[(size_t)b * 9 + l] : 0;
-    if (l < 9) rboard[grp * 9 + l] = cell;
+    root_player = a.start_index[b] == 0 ? 1 : 2;
+    root_cell = l < 9 ? a.boards[(size_t)b * 9 + l] : 0;
+    lf_cell = root_cell;
     if (l == 0) {
-      rplayer[grp] = player;
       tvisit[grp * cap] = 0;
       tvsum[grp * cap] = 0.0f;
       tprior[grp * cap] = 1.0f;
       tmeta[grp * cap] = 0xffff | (15 << 20);
-      nnodes[grp] = 1;
     }
     if (l < 9) {
-      float *st = s.xin + grp * 3 * kAzPlane;
+      float *pl = s.xin + grp * 3 * kAzPlane;
       const int p = az_interior(l);
-      st[p] = cell == player ? 0.5f : 0.0f;
-      st[kAzPlane + p] = cell == 3 - player ? 0.5f : 0.0f;
-      st[2 * kAzPlane + p] = 0.5f * (float)player;
+      pl[p] = root_cell == root_player ? 0.5f : 0.0f;
+      pl[kAzPlane + p] = root_cell == 3 - root_player ? 0.5f : 0.0f;
+      pl[2 * kAzPlane + p] = 0.5f * (float)root_player;
     }
   }
   const size_t tb = (size_t)grp * cap;
   for (int sim = -1; sim < S; ++sim) {
-    // ---- descend (sim >= 0)
+    az_stamp<STAMPS>(st, st_prev, 5);
+    // ---- descend (sim >= 0): _simulate's walk by the maximal pUCT child, replaying the moves on the
+    // group's registers. Child j of a node is the j-th empty cell of the node's board in action order (the
+    // expansion creates them so), so the chosen move comes from the board's empty mask, not from the tree.
     if (sim >= 0 && active) {
-      int cell = l < 9 ? rboard[grp * 9 + l] : 0;
-      int player = rplayer[grp];
-      int node = 0, d = 0;
-      if (l == 0) path[grp * kAzPath] = 0;
+      int cell = root_cell, player = root_player, node = 0, d = 0, act = 15;
+      lf_path = 0;
       for (; d < kAzPath - 1;) {  // a board fills after 9 moves: bounded descent
         const int meta = tmeta[tb + node];
+        const int pvis = tvisit[tb + node];
         const int f = meta & 0xffff;
         if (f == 0xffff) break;
         const int n = (meta >> 16) & 15;
-        const int pv = tvisit[tb + node];
         double sc = -__builtin_inf();
         if (l < n) {
           const size_t c = tb + f + l;
           const int cv = tvisit[c];
           const float val = cv == 0 ? 0.0f : tvsum[c] / (float)cv;
-          double pb = lut_pb[pv];
-          pb *= lut_sq[pv] / (double)(cv + 1);
+          double pb = lut_pb[pvis];
+          pb *= lut_sq[pvis] / (double)(cv + 1);
           sc = pb * (double)tprior[c] + (double)val;
         }
-        int bi = l;
-#pragma unroll
-        for (int m = 8; m >= 1; m >>= 1) {
-          const double os = __shfl_xor(sc, m, kAzGroup);
-          const int oi = __shfl_xor(bi, m, kAzGroup);
-          if (os > sc || (os == sc && oi < bi)) {
-            sc = os;
-            bi = oi;
-          }
-        }
+        const int bi = az_group_argmax(sc, gbase);
         node = f + bi;
-        const int mv = (tmeta[tb + node] >> 20) & 15;
-        if (l == mv) cell = player;
+        const uint32_t em = az_group_mask(l < 9 && cell == 0, gbase);
+        const bool mine = l < 9 && cell == 0 && __popc(em & ((1u << l) - 1u)) == (uint32_t)bi;
+        act = __builtin_ctz(az_group_mask(mine, gbase));
+        if (mine) cell = player;
         player = 3 - player;
         ++d;
-        if (l == 0) path[grp * kAzPath + d] = node;
+        if (l == d) lf_path = node;
       }
-      int bd[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) bd[k] = __shfl(cell, k, kAzGroup);
       int done, winner;
-      az_done_winner(bd, done, winner);
-      if (l == 0) {
-        leaf[grp * 4 + 0] = d;
-        leaf[grp * 4 + 1] = done;
-        leaf[grp * 4 + 2] = winner;
-        leaf[grp * 4 + 3] = player;
-      }
+      az_done_winner_mask(az_group_mask(l < 9 && cell == 1, gbase), az_group_mask(l < 9 && cell == 2, gbase), done,
+                          winner);
+      lf_node = node; lf_depth = d; lf_done = done; lf_winner = winner; lf_player = player; lf_act = act;
+      lf_cell = cell;
       if (l < 9) {
-        float *st = s.xin + grp * 3 * kAzPlane;
+        float *pl = s.xin + grp * 3 * kAzPlane;
         const int p = az_interior(l);
-        st[p] = cell == player ? 0.5f : 0.0f;
-        st[kAzPlane + p] = cell == 3 - player ? 0.5f : 0.0f;
-        st[2 * kAzPlane + p] = 0.5f * (float)player;
+        pl[p] = cell == player ? 0.5f : 0.0f;
+        pl[kAzPlane + p] = cell == 3 - player ? 0.5f : 0.0f;
+        pl[2 * kAzPlane + p] = 0.5f * (float)player;
       }
-      // the leaf board is re-derived from these planes after the network (xin is read-only there)
     }
-    az_net_forward<R, NRES>(s, g);
+    az_stamp<STAMPS>(st, st_prev, 0);
+    az_net_forward<R, NRES, STAMPS>(s, g, st, &st_prev);
     // ---- expand / back up
     if (active) {
       const float pr = l < 9 ? s.out[grp * 9 + l] : 0.0f;
       if (sim < 0) {
-        const int cell = l < 9 ? rboard[grp * 9 + l] : -1;
-        const bool legal = l < 9 && cell == 0;
+        const bool legal = l < 9 && root_cell == 0;
         const uint32_t gm = az_group_mask(legal, gbase);
         const int n = __popc(gm), rank = __popc(gm & ((1u << l) - 1u));
         if (legal) {
@@ -464,50 +514,42 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
           tprior[c] = p;
           tmeta[c] = 0xffff | (l << 20);
         }
-        if (l == 0) {
-          tmeta[tb] = (n > 0 ? 1 : 0xffff) | (n << 16) | (15 << 20);
-          nnodes[grp] = 1 + n;
-        }
+        if (l == 0) tmeta[tb] = (n > 0 ? 1 : 0xffff) | (n << 16) | (15 << 20);
+        nn = 1 + n;
       } else {
-        const int depth = leaf[grp * 4 + 0], done = leaf[grp * 4 + 1], winner = leaf[grp * 4 + 2],
-                  player = leaf[grp * 4 + 3];
-        const int node = path[grp * kAzPath + depth];
         double lv;
-        if (!done) {
-          // leaf board from the network input planes (own stones -> player, opponent's -> 3 - player)
-          int cell = -1;
-          if (l < 9) {
-            const float *st = s.xin + grp * 3 * kAzPlane;
-            const int p = az_interior(l);
-            cell = st[p] > 0.0f ? player : (st[kAzPlane + p] > 0.0f ? 3 - player : 0);
-          }
-          const bool legal = l < 9 && cell == 0;
+        if (!lf_done) {
+          const bool legal = l < 9 && lf_cell == 0;
           const uint32_t gm = az_group_mask(legal, gbase);
           const int n = __popc(gm), rank = __popc(gm & ((1u << l) - 1u));
-          const int base = nnodes[grp];
           if (legal) {
-            const size_t c = tb + base + rank;
+            const size_t c = tb + nn + rank;
             tvisit[c] = 0;
             tvsum[c] = 0.0f;
             tprior[c] = pr;
             tmeta[c] = 0xffff | (l << 20);
           }
-          if (l == 0) {
-            tmeta[tb + node] = (tmeta[tb + node] & ~0xfffff) | (n > 0 ? base : 0xffff) | (n << 16);
-            nnodes[grp] = base + n;
-          }
+          if (l == 0) tmeta[tb + lf_node] = (n > 0 ? nn : 0xffff) | (n << 16) | (lf_act << 20);
+          nn += n;
           lv = (double)s.out[R * 9 + grp];
         } else {
-          lv = winner == -1 ? 0.0 : (player == winner ? 1.0 : -1.0);
+          lv = lf_winner == -1 ? 0.0 : (lf_player == lf_winner ? 1.0 : -1.0);
         }
+        // update_recursive(-leaf_value): lane m updates the path node at depth m, sign by its distance to the leaf
         const float v = (float)(-lv);
-        if (l <= depth) {
-          const size_t nd = tb + path[grp * kAzPath + depth - l];
+        if (l <= lf_depth) {
+          const size_t nd = tb + lf_path;
           tvisit[nd] += 1;
-          tvsum[nd] += (l & 1) ? -v : v;
+          tvsum[nd] += ((lf_depth - l) & 1) ? -v : v;
         }
       }
     }
+  }
+  az_stamp<STAMPS>(st, st_prev, 5);
+  if (STAMPS && tid == 0 && a.stamps) {
+    st[6] = __builtin_amdgcn_s_memtime() - st_begin;
+    st[7] = S;
+    for (int n = 0; n < 8; ++n) atomicAdd(a.stamps + n, st[n]);
   }
   // ---- finish: root statistics -> visits / probs / action; optional tree export
   if (active && l == 0) {
@@ -520,7 +562,6 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   }
   if (a.export_tree && active) {
     const size_t gb = (size_t)b * cap;
-    const int nn = nnodes[grp];
     for (int i = l; i < cap; i += kAzGroup) {
       const bool live = i < nn;
       const int meta = tmeta[tb + i];

@@ -2309,20 +2309,60 @@ int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int3
 }  // extern "C"
 
 // ---- fused AlphaZero search (lzm_az_fused.h)
-static int az_fused_rows(int B) {
-  // boards per workgroup: the fewest that keep the grid within one wave of workgroups per CU
-  const int cus = device_cus();
-  const char *e = getenv("LZM_AZ_BOARDS_PER_WG");
-  if (e && atoi(e) > 0) return atoi(e);
-  for (int r : {1, 2, 4}) if ((B + r - 1) / r <= cus) return r;
-  return 8;
-}
-
 template <int R>
 static size_t az_fused_lds(int cap, int S) {
-  size_t bytes = (size_t)(2 * (S + 1) + 81) * 8 + (size_t)R * cap * 16 + (size_t)R * (9 + 1 + kAzPath + 4 + 1) * 4;
+  size_t bytes = (size_t)(2 * (S + 1) + 81) * 8 + (size_t)R * cap * 16;
   bytes = (bytes + 15) & ~(size_t)15;
   return bytes + (size_t)AzNetLds<R>::total * 4;
+}
+
+template <int R, int NRES>
+static int az_fused_attr(bool stamps) {
+  static bool attr[2] = {false, false};
+  if (!attr[stamps]) {
+    LZM_HIP(hipFuncSetAttribute(stamps ? (const void *)az_search_fused_kernel<R, NRES, true>
+                                       : (const void *)az_search_fused_kernel<R, NRES, false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr[stamps] = true;
+  }
+  return LZM_OK;
+}
+
+// workgroups of R boards that one CU holds at once (0: the trees do not fit in LDS)
+template <int R, int NRES>
+static int az_fused_per_cu(int cap, int S, bool stamps) {
+  const size_t lds = az_fused_lds<R>(cap, S);
+  if (lds > 160 * 1024) return 0;
+  static size_t memo_lds[2] = {0, 0};
+  static int memo[2] = {0, 0};
+  if (memo_lds[stamps] == lds) return memo[stamps];
+  if (az_fused_attr<R, NRES>(stamps) != LZM_OK) return 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, stamps ? (const void *)az_search_fused_kernel<R, NRES, true>
+                                                                   : (const void *)az_search_fused_kernel<R, NRES, false>,
+                                                   kAzfThreads, lds) != hipSuccess)
+    per_cu = 1;
+  memo_lds[stamps] = lds;
+  memo[stamps] = per_cu;
+  return per_cu;
+}
+
+// boards per workgroup: the fewest whose grid the GPU holds at once (B = 512 on 256 CUs: one board per
+// workgroup, two workgroups per CU, so each CU interleaves two boards' latency chains); else the most that fit
+template <int NRES>
+static int az_fused_rows(int B, int cap, int S, bool stamps) {
+  const char *e = getenv("LZM_AZ_BOARDS_PER_WG");
+  if (e && atoi(e) > 0) return atoi(e);
+  const int cus = device_cus();
+  const int occ[4] = {az_fused_per_cu<1, NRES>(cap, S, stamps), az_fused_per_cu<2, NRES>(cap, S, stamps),
+                      az_fused_per_cu<4, NRES>(cap, S, stamps), az_fused_per_cu<8, NRES>(cap, S, stamps)};
+  int best = 0;
+  for (int i = 0, r = 1; i < 4; ++i, r *= 2) {
+    if (!occ[i]) continue;
+    best = r;
+    if ((B + r - 1) / r <= occ[i] * cus) return r;
+  }
+  return best ? best : 1;
 }
 
 template <int R, int NRES>
@@ -2333,13 +2373,10 @@ static int az_launch_fused(const AzFusedArgs &a, hipStream_t s) {
              R, a.S, lds);
     return LZM_ERR_CAPACITY;
   }
-  static bool attr = false;
-  if (!attr) {
-    LZM_HIP(hipFuncSetAttribute((const void *)az_search_fused_kernel<R, NRES>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
-  }
-  hipLaunchKernelGGL((az_search_fused_kernel<R, NRES>), dim3((a.B + R - 1) / R), dim3(kAzfThreads), lds, s, a);
+  // diagnostics: lzm_debug_az_stamps selects the stamped instantiation
+  if (int rc = az_fused_attr<R, NRES>(a.stamps != nullptr)) return rc;
+  auto fn = a.stamps ? az_search_fused_kernel<R, NRES, true> : az_search_fused_kernel<R, NRES, false>;
+  hipLaunchKernelGGL(fn, dim3((a.B + R - 1) / R), dim3(kAzfThreads), lds, s, a);
   LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
@@ -2371,7 +2408,16 @@ static int az_launch_eval(const float *w, const float *state, int n, float *prob
   return LZM_OK;
 }
 
+static unsigned long long *g_az_stamps = nullptr;  // diagnostics: lzm_debug_az_stamps
+
 extern "C" {
+
+// Diagnostics: a device uint64[8] that the fused AlphaZero search adds its per-phase shader-clock cycles to
+// (AzFusedArgs::stamps); nullptr returns to the production instantiation.
+int lzm_debug_az_stamps(void *buf) {
+  g_az_stamps = reinterpret_cast<unsigned long long *>(buf);
+  return LZM_OK;
+}
 
 int64_t lzm_az_net_floats(int nres) { return nres == 1 || nres == 2 ? az_net_layout(nres).total : -1; }
 
@@ -2440,14 +2486,8 @@ int lzm_az_search_fused(int B, int S, void *ws, int nres, const float *weights, 
   a.B = B; a.S = S; a.cap = a.t.cap; a.with_noise = with_noise; a.sample = sample; a.export_tree = export_tree;
   a.noise_weight = noise_weight; a.temperature = temperature; a.seed = seed; a.counter = counter; a.w = weights;
   a.boards = boards; a.start_index = start_index; a.visits_out = visits; a.probs_out = probs; a.action_out = action;
-  int R = az_fused_rows(B);
-  if (!getenv("LZM_AZ_BOARDS_PER_WG")) {  // fewer boards per workgroup when the trees outgrow LDS
-    auto lds = [&](int r) {
-      return r == 8 ? az_fused_lds<8>(a.cap, S) : r == 4 ? az_fused_lds<4>(a.cap, S) : r == 2 ? az_fused_lds<2>(a.cap, S)
-                                                                                          : az_fused_lds<1>(a.cap, S);
-    };
-    while (R > 1 && lds(R) > 160 * 1024) R /= 2;
-  }
+  a.stamps = g_az_stamps;
+  const int R = nres == 1 ? az_fused_rows<1>(B, a.cap, S, a.stamps != nullptr) : az_fused_rows<2>(B, a.cap, S, a.stamps != nullptr);
   hipStream_t s = (hipStream_t)stream;
   return nres == 1 ? az_launch_fused_r<1>(R, a, s) : az_launch_fused_r<2>(R, a, s);
 }
