@@ -69,7 +69,7 @@ __host__ __device__ inline AzNetLayout az_net_layout(int nres) {
 template <int R>
 struct AzNetLds {
   static constexpr int T = (9 * R + 15) / 16;            // row tiles
-  static constexpr int xin = (R + 1) * 3 * kAzPlane;     // network input planes (+ a zero board)
+  static constexpr int xin = ((R + 1) * 3 * kAzPlane + 3) & ~3;  // network input planes (+ a zero board), 16-B padded
   static constexpr int xbuf = (R + 1) * kAzBoardX;       // one activation buffer
   static constexpr int hd = R * 32 * 9;                  // 1x1 head outputs [R][32][9]
   static constexpr int red = 4 * T * 2 * 256;            // K-split partials
@@ -408,11 +408,13 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   double *lut_pb = (double *)az_smem;
   double *lut_sq = lut_pb + (S + 1);
   double *noise = lut_sq + (S + 1);
-  int32_t *tvisit = (int32_t *)(noise + 81);
-  float *tvsum = (float *)(tvisit + R * cap);
-  float *tprior = tvsum + R * cap;
-  int32_t *tmeta = (int32_t *)(tprior + R * cap);  // first (16 bits, 0xffff: leaf) | nch << 16 | act << 20
-  float *netp = (float *)(((uintptr_t)(tmeta + R * cap) + 15) & ~(uintptr_t)15);
+  // node records {visit, value_sum (f32 bits), prior (f32 bits), meta}: one 16-B LDS read per node or child;
+  // meta = first child (16 bits, 0xffff: leaf) | nch << 16 | act << 20
+  const int ndbl = (2 * (S + 1) + 81 + 1) & ~1;  // the double tables, padded to 16 B
+  int4 *trec = (int4 *)(lut_pb + ndbl);
+  // the network part 16-B aligned, addressed from az_smem (an integer round trip of the pointer would hide
+  // its address space and turn every LDS access of the network into a flat one)
+  float *netp = az_smem + 2 * ndbl + 4 * R * cap;
   const AzNetSmem s = az_net_carve<R>(netp);
   AzNetRegs<R, NRES> g;
   az_net_init<R, NRES>(a.w, s, g);
@@ -436,10 +438,7 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
     root_cell = l < 9 ? a.boards[(size_t)b * 9 + l] : 0;
     lf_cell = root_cell;
     if (l == 0) {
-      tvisit[grp * cap] = 0;
-      tvsum[grp * cap] = 0.0f;
-      tprior[grp * cap] = 1.0f;
-      tmeta[grp * cap] = 0xffff | (15 << 20);
+      trec[grp * cap] = make_int4(0, __float_as_int(0.0f), __float_as_int(1.0f), 0xffff | (15 << 20));
     }
     if (l < 9) {
       float *pl = s.xin + grp * 3 * kAzPlane;
@@ -459,20 +458,21 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
       int cell = root_cell, player = root_player, node = 0, d = 0, act = 15;
       lf_path = 0;
       for (; d < kAzPath - 1;) {  // a board fills after 9 moves: bounded descent
-        const int meta = tmeta[tb + node];
-        const int pvis = tvisit[tb + node];
+        const int4 nr = trec[tb + node];
+        const int meta = nr.w, pvis = nr.x;
         const int f = meta & 0xffff;
         if (f == 0xffff) break;
         const int n = (meta >> 16) & 15;
-        double sc = -__builtin_inf();
-        if (l < n) {
-          const size_t c = tb + f + l;
-          const int cv = tvisit[c];
-          const float val = cv == 0 ? 0.0f : tvsum[c] / (float)cv;
-          double pb = lut_pb[pvis];
-          pb *= lut_sq[pvis] / (double)(cv + 1);
-          sc = pb * (double)tprior[c] + (double)val;
-        }
+        // every read of the level issued at once, no branch: lanes >= n read the node itself
+        const int4 cr = trec[tb + (l < n ? f + l : node)];
+        const double lpb = lut_pb[pvis], lsq = lut_sq[pvis];
+        const int cv = cr.x;
+        const float q = __int_as_float(cr.y) / (float)(cv > 0 ? cv : 1);
+        const float val = cv == 0 ? 0.0f : q;
+        double pb = lpb;
+        pb *= lsq / (double)(cv + 1);
+        double sc = pb * (double)__int_as_float(cr.z) + (double)val;
+        sc = l < n ? sc : -__builtin_inf();
         const int bi = az_group_argmax(sc, gbase);
         node = f + bi;
         const uint32_t em = az_group_mask(l < 9 && cell == 0, gbase);
@@ -509,12 +509,9 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
           const size_t c = tb + 1 + rank;
           float p = pr;
           if (a.with_noise) p = (float)((double)pr * (1.0 - a.noise_weight) + noise[(n - 1) * 9 + rank] * a.noise_weight);
-          tvisit[c] = 0;
-          tvsum[c] = 0.0f;
-          tprior[c] = p;
-          tmeta[c] = 0xffff | (l << 20);
+          trec[c] = make_int4(0, __float_as_int(0.0f), __float_as_int(p), 0xffff | (l << 20));
         }
-        if (l == 0) tmeta[tb] = (n > 0 ? 1 : 0xffff) | (n << 16) | (15 << 20);
+        if (l == 0) trec[tb].w = (n > 0 ? 1 : 0xffff) | (n << 16) | (15 << 20);
         nn = 1 + n;
       } else {
         double lv;
@@ -524,12 +521,9 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
           const int n = __popc(gm), rank = __popc(gm & ((1u << l) - 1u));
           if (legal) {
             const size_t c = tb + nn + rank;
-            tvisit[c] = 0;
-            tvsum[c] = 0.0f;
-            tprior[c] = pr;
-            tmeta[c] = 0xffff | (l << 20);
+            trec[c] = make_int4(0, __float_as_int(0.0f), __float_as_int(pr), 0xffff | (l << 20));
           }
-          if (l == 0) tmeta[tb + lf_node] = (n > 0 ? nn : 0xffff) | (n << 16) | (lf_act << 20);
+          if (l == 0) trec[tb + lf_node].w = (n > 0 ? nn : 0xffff) | (n << 16) | (lf_act << 20);
           nn += n;
           lv = (double)s.out[R * 9 + grp];
         } else {
@@ -538,9 +532,9 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
         // update_recursive(-leaf_value): lane m updates the path node at depth m, sign by its distance to the leaf
         const float v = (float)(-lv);
         if (l <= lf_depth) {
-          const size_t nd = tb + lf_path;
-          tvisit[nd] += 1;
-          tvsum[nd] += ((lf_depth - l) & 1) ? -v : v;
+          int2 *nd = reinterpret_cast<int2 *>(trec + tb + lf_path);
+          const int2 vs = *nd;
+          *nd = make_int2(vs.x + 1, __float_as_int(__int_as_float(vs.y) + (((lf_depth - l) & 1) ? -v : v)));
         }
       }
     }
@@ -555,19 +549,20 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   if (active && l == 0) {
     int v[9];
     for (int k = 0; k < 9; ++k) v[k] = 0;
-    const int meta = tmeta[tb];
+    const int meta = trec[tb].w;
     const int f = meta & 0xffff, n = (meta >> 16) & 15;
-    for (int j = 0; f != 0xffff && j < n; ++j) v[(tmeta[tb + f + j] >> 20) & 15] = tvisit[tb + f + j];
+    for (int j = 0; f != 0xffff && j < n; ++j) v[(trec[tb + f + j].w >> 20) & 15] = trec[tb + f + j].x;
     az_finalize(b, v, a.temperature, a.sample, a.seed, a.counter, a.visits_out, a.probs_out, a.action_out);
   }
   if (a.export_tree && active) {
     const size_t gb = (size_t)b * cap;
     for (int i = l; i < cap; i += kAzGroup) {
       const bool live = i < nn;
-      const int meta = tmeta[tb + i];
-      a.t.visit[gb + i] = live ? tvisit[tb + i] : 0;
-      a.t.vsum[gb + i] = live ? tvsum[tb + i] : 0.0f;
-      a.t.prior[gb + i] = live ? tprior[tb + i] : 0.0f;
+      const int4 rc = trec[tb + i];
+      const int meta = rc.w;
+      a.t.visit[gb + i] = live ? rc.x : 0;
+      a.t.vsum[gb + i] = live ? __int_as_float(rc.y) : 0.0f;
+      a.t.prior[gb + i] = live ? __int_as_float(rc.z) : 0.0f;
       a.t.first[gb + i] = live && (meta & 0xffff) != 0xffff ? (meta & 0xffff) : -1;
       a.t.nch[gb + i] = live ? (meta >> 16) & 15 : 0;
       const int act = (meta >> 20) & 15;

@@ -2311,8 +2311,8 @@ int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int3
 // ---- fused AlphaZero search (lzm_az_fused.h)
 template <int R>
 static size_t az_fused_lds(int cap, int S) {
-  size_t bytes = (size_t)(2 * (S + 1) + 81) * 8 + (size_t)R * cap * 16;
-  bytes = (bytes + 15) & ~(size_t)15;
+  // the double tables padded to 16 B, the node records, the network (az_search_fused_kernel's carve)
+  const size_t bytes = (size_t)((2 * (S + 1) + 81 + 1) & ~1) * 8 + (size_t)R * cap * 16;
   return bytes + (size_t)AzNetLds<R>::total * 4;
 }
 
