@@ -408,8 +408,8 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   double *lut_pb = (double *)az_smem;
   double *lut_sq = lut_pb + (S + 1);
   double *noise = lut_sq + (S + 1);
-  // node records {visit, value_sum (f32 bits), prior (f32 bits), meta}: one 16-B LDS read per node or child;
-  // meta = first child (16 bits, 0xffff: leaf) | nch << 16 | act << 20
+  // node records {meta, visit, value_sum (f32 bits), prior (f32 bits)}: one 16-B LDS read per child, one 8-B
+  // read {meta, visit} per node; meta = first child (16 bits, 0xffff: leaf) | nch << 16 | act << 20
   const int ndbl = (2 * (S + 1) + 81 + 1) & ~1;  // the double tables, padded to 16 B
   int4 *trec = (int4 *)(lut_pb + ndbl);
   // the network part 16-B aligned, addressed from az_smem (an integer round trip of the pointer would hide
@@ -438,7 +438,7 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
     root_cell = l < 9 ? a.boards[(size_t)b * 9 + l] : 0;
     lf_cell = root_cell;
     if (l == 0) {
-      trec[grp * cap] = make_int4(0, __float_as_int(0.0f), __float_as_int(1.0f), 0xffff | (15 << 20));
+      trec[grp * cap] = make_int4(0xffff | (15 << 20), 0, __float_as_int(0.0f), __float_as_int(1.0f));
     }
     if (l < 9) {
       float *pl = s.xin + grp * 3 * kAzPlane;
@@ -458,20 +458,22 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
       int cell = root_cell, player = root_player, node = 0, d = 0, act = 15;
       lf_path = 0;
       for (; d < kAzPath - 1;) {  // a board fills after 9 moves: bounded descent
-        const int4 nr = trec[tb + node];
-        const int meta = nr.w, pvis = nr.x;
+        // {meta, visit} as one 64-bit value: one LDS round trip before the leaf test and the LUT reads (as two
+        // fields the compiler read the visit count only after the test)
+        const uint64_t mv = *reinterpret_cast<const uint64_t *>(trec + tb + node);
+        const int meta = (int)(uint32_t)mv, pvis = (int)(mv >> 32);
         const int f = meta & 0xffff;
         if (f == 0xffff) break;
         const int n = (meta >> 16) & 15;
         // every read of the level issued at once, no branch: lanes >= n read the node itself
         const int4 cr = trec[tb + (l < n ? f + l : node)];
         const double lpb = lut_pb[pvis], lsq = lut_sq[pvis];
-        const int cv = cr.x;
-        const float q = __int_as_float(cr.y) / (float)(cv > 0 ? cv : 1);
+        const int cv = cr.y;
+        const float q = __int_as_float(cr.z) / (float)(cv > 0 ? cv : 1);
         const float val = cv == 0 ? 0.0f : q;
         double pb = lpb;
         pb *= lsq / (double)(cv + 1);
-        double sc = pb * (double)__int_as_float(cr.z) + (double)val;
+        double sc = pb * (double)__int_as_float(cr.w) + (double)val;
         sc = l < n ? sc : -__builtin_inf();
         const int bi = az_group_argmax(sc, gbase);
         node = f + bi;
@@ -509,9 +511,9 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
           const size_t c = tb + 1 + rank;
           float p = pr;
           if (a.with_noise) p = (float)((double)pr * (1.0 - a.noise_weight) + noise[(n - 1) * 9 + rank] * a.noise_weight);
-          trec[c] = make_int4(0, __float_as_int(0.0f), __float_as_int(p), 0xffff | (l << 20));
+          trec[c] = make_int4(0xffff | (l << 20), 0, __float_as_int(0.0f), __float_as_int(p));
         }
-        if (l == 0) trec[tb].w = (n > 0 ? 1 : 0xffff) | (n << 16) | (15 << 20);
+        if (l == 0) trec[tb].x = (n > 0 ? 1 : 0xffff) | (n << 16) | (15 << 20);
         nn = 1 + n;
       } else {
         double lv;
@@ -521,9 +523,9 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
           const int n = __popc(gm), rank = __popc(gm & ((1u << l) - 1u));
           if (legal) {
             const size_t c = tb + nn + rank;
-            trec[c] = make_int4(0, __float_as_int(0.0f), __float_as_int(pr), 0xffff | (l << 20));
+            trec[c] = make_int4(0xffff | (l << 20), 0, __float_as_int(0.0f), __float_as_int(pr));
           }
-          if (l == 0) trec[tb + lf_node].w = (n > 0 ? nn : 0xffff) | (n << 16) | (lf_act << 20);
+          if (l == 0) trec[tb + lf_node].x = (n > 0 ? nn : 0xffff) | (n << 16) | (lf_act << 20);
           nn += n;
           lv = (double)s.out[R * 9 + grp];
         } else {
@@ -532,9 +534,9 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
         // update_recursive(-leaf_value): lane m updates the path node at depth m, sign by its distance to the leaf
         const float v = (float)(-lv);
         if (l <= lf_depth) {
-          int2 *nd = reinterpret_cast<int2 *>(trec + tb + lf_path);
-          const int2 vs = *nd;
-          *nd = make_int2(vs.x + 1, __float_as_int(__int_as_float(vs.y) + (((lf_depth - l) & 1) ? -v : v)));
+          int4 &nd = trec[tb + lf_path];
+          nd.y += 1;
+          nd.z = __float_as_int(__int_as_float(nd.z) + (((lf_depth - l) & 1) ? -v : v));
         }
       }
     }
@@ -549,9 +551,9 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   if (active && l == 0) {
     int v[9];
     for (int k = 0; k < 9; ++k) v[k] = 0;
-    const int meta = trec[tb].w;
+    const int meta = trec[tb].x;
     const int f = meta & 0xffff, n = (meta >> 16) & 15;
-    for (int j = 0; f != 0xffff && j < n; ++j) v[(trec[tb + f + j].w >> 20) & 15] = trec[tb + f + j].x;
+    for (int j = 0; f != 0xffff && j < n; ++j) v[(trec[tb + f + j].x >> 20) & 15] = trec[tb + f + j].y;
     az_finalize(b, v, a.temperature, a.sample, a.seed, a.counter, a.visits_out, a.probs_out, a.action_out);
   }
   if (a.export_tree && active) {
@@ -559,10 +561,10 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
     for (int i = l; i < cap; i += kAzGroup) {
       const bool live = i < nn;
       const int4 rc = trec[tb + i];
-      const int meta = rc.w;
-      a.t.visit[gb + i] = live ? rc.x : 0;
-      a.t.vsum[gb + i] = live ? __int_as_float(rc.y) : 0.0f;
-      a.t.prior[gb + i] = live ? __int_as_float(rc.z) : 0.0f;
+      const int meta = rc.x;
+      a.t.visit[gb + i] = live ? rc.y : 0;
+      a.t.vsum[gb + i] = live ? __int_as_float(rc.z) : 0.0f;
+      a.t.prior[gb + i] = live ? __int_as_float(rc.w) : 0.0f;
       a.t.first[gb + i] = live && (meta & 0xffff) != 0xffff ? (meta & 0xffff) : -1;
       a.t.nch[gb + i] = live ? (meta >> 16) & 15 : 0;
       const int act = (meta >> 20) & 15;
