@@ -598,7 +598,9 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
         if (i == 0 && late) {
           // late draw: the look-back and the tie's draw, then the action's map for the epilogue — by every
-          // wave for itself (no barrier hands the action over); wave 0 files it
+          // wave for itself (no barrier hands the action over); wave 0 files it. A spin timeout is counted
+          // once per wave that met it and may leave the waves with different bases: any count invalidates
+          // the search (lzm_check_errors raises), so such a latent is never used
           const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
           const int base = sc_lookback(p, k, b, epoch, lane);
           if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;
@@ -1014,7 +1016,8 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
           if (i == 0 && late) {
             // late draw: the look-back and the tie's draw, then the action's map for the epilogue — by every
-            // wave for itself (no barrier hands the action over); wave 0 files it
+            // wave for itself (no barrier hands the action over); wave 0 files it (a timeout: as in
+            // search_conv_kernel, counted per wave, and it invalidates the search)
             const unsigned long long lb0 = STAMPS ? __builtin_amdgcn_s_memtime() : 0ull;
             const int base = sc_lookback(p, k, b, epoch, lane);
             if (STAMPS && tid == 0) st_acc[8] += __builtin_amdgcn_s_memtime() - lb0;

@@ -1180,9 +1180,12 @@ __device__ inline int lookback_sum(const SearchArgs &p, int k, int g, int G, uns
   return (part[0] + part[1]) + (part[2] + part[3]);
 }
 
-// lookback_sum by wave 0 alone, for G <= 256 workgroups: lane l polls roots l, l + 64, ... (all
+// lookback_sum by one wave, for G <= 256 workgroups: lane l polls roots l, l + 64, ... (all
 // loads in flight at once), the sum by DPP (exact: float sums of integers < 2^24), no LDS and no
-// barrier. Returns the sum in every lane of wave 0.
+// barrier. Returns the sum in every lane of the calling wave. Every wave of the late draw calls it on
+// its own, so a spin timeout is counted in p.diag once per wave that met it, and two waves may then
+// disagree on the base; any count invalidates the whole search (lzm_check_errors raises at the result
+// getters, the collector and bench.py), so such a search is never used.
 __device__ inline int lookback_sum_w0(const SearchArgs &p, int k, int g, int G, unsigned long long epoch) {
   const int lane = threadIdx.x & 63;
   const unsigned long long ok = epoch << 32;  // a published flag of depth 0
