@@ -214,6 +214,10 @@ int lzm_shutdown(void);
  * __shfl_xor (ds_bpermute) forms they replace, on one wave of in float[64]; out float[16][64] (rows:
  * partner D = 1..32, __shfl_xor D = 1..32, xor_sum, shfl sum, xor_max, shfl max). Tests only. */
 int lzm_debug_xor(const float *in, float *out, void *stream);
+/* The fused AlphaZero search's stone-mask done / winner and DPP pUCT argmax beside the reference-order scans they
+ * replace (get_done_winner's cell scan; the first strict maximum): n boards int32[n][9], scores double[n][16];
+ * out int32[n][6] = {done, winner (scan), done, winner (masks), argmax (DPP), argmax (scan)}. Tests only. */
+int lzm_debug_az_rules(int n, const int32_t *boards, const double *scores, int32_t *out, void *stream);
 
 /* ---- Device collect loop, CartPole-v0 (lzero/worker/muzero_collector.py
  * :399-705, zoo/classic_control/cartpole/envs/cartpole_lightzero_env.py) ----

@@ -96,6 +96,7 @@ SIGNATURES = {
     "lzm_debug_glibc_rand": [_u32, _i, _vp, _vp],
     "lzm_debug_philox": [_vp, _vp, _i, _vp],
     "lzm_debug_xor": [_vp, _vp, _vp],
+    "lzm_debug_az_rules": [_i, _vp, _vp, _vp, _vp],
     "lzm_shutdown": [],
     "lzm_debug_phase_cycles": [_vp, _vp, _i],
     "lzm_cartpole_reset": [_i, _vp, _vp, _vp, _u32, _vp],

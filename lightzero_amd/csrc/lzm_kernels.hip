@@ -635,6 +635,30 @@ __global__ void __launch_bounds__(64) debug_xor_kernel(const float *in, float *o
   out[15 * 64 + l] = m;
 }
 
+// lzm_debug_az_rules: the fused AlphaZero search's mask / DPP forms beside the scans they replace, one board per
+// 16-lane group: out[b][6] = {done, winner by az_done_winner (the reference's cell scan), done, winner by
+// az_done_winner_mask, the lane az_group_argmax picks from scores[b][16], the first strict maximum of a scan}
+__global__ void __launch_bounds__(64) debug_az_rules_kernel(int n, const int32_t *boards, const double *scores,
+                                                            int32_t *out) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 4), l = threadIdx.x & 15, gbase = (threadIdx.x & 63) & ~15;
+  const bool on = b < n;  // group-uniform
+  const int cell = on && l < 9 ? boards[(size_t)b * 9 + l] : 0;
+  const double sc = on ? scores[(size_t)b * 16 + l] : 0.0;
+  const int bi = az_group_argmax(sc, gbase);  // (every lane of the wave takes part)
+  int done_m, win_m;
+  az_done_winner_mask(az_group_mask(l < 9 && cell == 1, gbase), az_group_mask(l < 9 && cell == 2, gbase), done_m, win_m);
+  if (!on || l != 0) return;
+  int bd[9];
+  for (int k = 0; k < 9; ++k) bd[k] = boards[(size_t)b * 9 + k];
+  int done_s, win_s;
+  az_done_winner(bd, done_s, win_s);
+  int best = 0;
+  for (int k = 1; k < 16; ++k)
+    if (scores[(size_t)b * 16 + k] > scores[(size_t)b * 16 + best]) best = k;
+  int32_t *o = out + (size_t)b * 6;
+  o[0] = done_s; o[1] = win_s; o[2] = done_m; o[3] = win_m; o[4] = bi; o[5] = best;
+}
+
 __global__ void debug_philox_kernel(const uint32_t *ck, uint32_t *out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1333,6 +1357,13 @@ int lzm_shutdown(void) {
   g_scratch_parts = 0;
   if (g_debug_jm) LZM_HIP(hipFree(g_debug_jm));
   g_debug_jm = nullptr;
+  return LZM_OK;
+}
+
+int lzm_debug_az_rules(int n, const int32_t *boards, const double *scores, int32_t *out, void *stream) {
+  if (n <= 0 || !boards || !scores || !out) return LZM_ERR_ARG;
+  hipLaunchKernelGGL(debug_az_rules_kernel, dim3((n + 3) / 4), dim3(64), 0, (hipStream_t)stream, n, boards, scores, out);
+  LZM_CHECK_LAUNCH();
   return LZM_OK;
 }
 

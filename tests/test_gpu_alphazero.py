@@ -197,3 +197,30 @@ def test_fused_search_batch_512_properties():
     assert ((boards != 0) <= (v == 0)).all()
     a = act.cpu().numpy()
     assert all(v[i, a[i]] > 0 for i in range(512))
+
+
+def test_fused_rules_equal_reference_scans():
+    """the fused search's stone-mask done / winner against get_done_winner's cell scan (lzm_az.h, the
+    reference's order) on every one of the 3^9 boards, legal or not, and its DPP argmax of order-preserving
+    score keys against the first strict maximum of a scan, on scores with ties, -inf lanes and signed zeros"""
+    from lightzero_amd._lib import call, ptr, stream_ptr
+    grid = np.array(np.meshgrid(*[np.arange(3)] * 9, indexing="ij")).reshape(9, -1).T.astype(np.int32)
+    n = len(grid)
+    rng = np.random.default_rng(3)
+    sc = rng.normal(size=(n, 16)) * 10.0 ** rng.integers(-3, 3, size=(n, 1))
+    k = rng.integers(0, 16, size=n)
+    sc[np.arange(n), k] = sc.max(axis=1)                     # a tie with the maximum
+    sc[rng.random((n, 16)) < 0.2] = -np.inf                  # lanes past the children
+    z = rng.random(n) < 0.05
+    sc[z] = 0.0
+    sc[z, ::2] = -0.0                                        # all-zero rows: +0 / -0 are equal scores
+    sc[0] = -np.inf                                          # (no child: lane 0)
+    boards = torch.from_numpy(grid).cuda()
+    scores = torch.from_numpy(np.ascontiguousarray(sc)).cuda()
+    out = torch.zeros((n, 6), dtype=torch.int32, device="cuda")
+    call("lzm_debug_az_rules", n, ptr(boards), ptr(scores), ptr(out), stream_ptr())
+    o = out.cpu().numpy()
+    assert np.array_equal(o[:, 0], o[:, 2]) and np.array_equal(o[:, 1], o[:, 3])
+    assert (o[:, 1] != -1).sum() > 1000 and o[:, 0].sum() > 1000  # (wins and full boards occur)
+    assert np.array_equal(o[:, 4], o[:, 5])
+    assert np.array_equal(o[:, 5], np.argmax(sc, axis=1))       # numpy's argmax: the first maximum too
