@@ -378,6 +378,23 @@ __device__ inline int az_group_argmax(double sc, int gbase) {
   return __builtin_ctz(az_group_mask(k0 == k, gbase));
 }
 
+// The decision at one node for the 16-lane group: the reference's double pUCT of every child (lane l < n: child
+// f + l) and the first maximum (az_group_argmax). pvis: the node's visit count; node: its index (lanes >= n read it,
+// so every read is unconditional).
+__device__ inline int az_node_decision(const int4 *trec, size_t tb, int node, int f, int n, int pvis, const double *lut_pb,
+                                       const double *lut_sq, int l, int gbase) {
+  const int4 cr = trec[tb + (l < n ? f + l : node)];
+  const double lpb = lut_pb[pvis], lsq = lut_sq[pvis];
+  const int cv = cr.y;
+  const float q = __int_as_float(cr.z) / (float)(cv > 0 ? cv : 1);
+  const float val = cv == 0 ? 0.0f : q;
+  double pb = lpb;
+  pb *= lsq / (double)(cv + 1);
+  double sc = pb * (double)__int_as_float(cr.w) + (double)val;
+  sc = l < n ? sc : -__builtin_inf();
+  return az_group_argmax(sc, gbase);
+}
+
 // get_done_winner_cython.pyx on bit masks of the two players' stones (bit i = cell i). The reference scans
 // cells in row-major order and from each stone the directions that stay on the board, returning the first
 // full line: a line is only found from its first cell, so the winner is the owner of the full line with the
@@ -414,7 +431,7 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
   int4 *trec = (int4 *)(lut_pb + ndbl);
   // the network part 16-B aligned, addressed from az_smem (an integer round trip of the pointer would hide
   // its address space and turn every LDS access of the network into a flat one)
-  float *netp = az_smem + 2 * ndbl + 4 * R * cap;
+  float *netp = az_smem + 2 * ndbl + 4 * R * cap + 32;  // (+ the path words of the decision refresh)
   const AzNetSmem s = az_net_carve<R>(netp);
   AzNetRegs<R, NRES> g;
   az_net_init<R, NRES>(a.w, s, g);
@@ -449,12 +466,43 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
     }
   }
   const size_t tb = (size_t)grp * cap;
+  constexpr bool kCached = R == 1;  // one board per workgroup: cached decisions (below)
+  int *s_path = reinterpret_cast<int *>(trec + R * cap);  // [16] the backed-up path, [16] its depth
   for (int sim = -1; sim < S; ++sim) {
     az_stamp<STAMPS>(st, st_prev, 5);
     // ---- descend (sim >= 0): _simulate's walk by the maximal pUCT child, replaying the moves on the
     // group's registers. Child j of a node is the j-th empty cell of the node's board in action order (the
     // expansion creates them so), so the chosen move comes from the board's empty mask, not from the tree.
-    if (sim >= 0 && active) {
+    if (kCached && sim >= 0 && active) {
+      // R = 1: every node's decision is cached in its meta (bits 24..27, refreshed below for each node the last
+      // backup touched), so the walk is a chain of one LDS read per level; the move is the child's action
+      int cell = root_cell, player = root_player, node = 0, d = 0, act = 15;
+      lf_path = 0;
+      int meta = trec[tb].x;
+      for (; d < kAzPath - 1;) {  // a board fills after 9 moves: bounded descent
+        const int f = meta & 0xffff;
+        if (f == 0xffff) break;
+        node = f + ((meta >> 24) & 15);
+        meta = trec[tb + node].x;
+        act = (meta >> 20) & 15;
+        if (l == act) cell = player;
+        player = 3 - player;
+        ++d;
+        if (l == d) lf_path = node;
+      }
+      int done, winner;
+      az_done_winner_mask(az_group_mask(l < 9 && cell == 1, gbase), az_group_mask(l < 9 && cell == 2, gbase), done,
+                          winner);
+      lf_node = node; lf_depth = d; lf_done = done; lf_winner = winner; lf_player = player; lf_act = act;
+      lf_cell = cell;
+      if (l < 9) {
+        float *pl = s.xin + grp * 3 * kAzPlane;
+        const int p = az_interior(l);
+        pl[p] = cell == player ? 0.5f : 0.0f;
+        pl[kAzPlane + p] = cell == 3 - player ? 0.5f : 0.0f;
+        pl[2 * kAzPlane + p] = 0.5f * (float)player;
+      }
+    } else if (sim >= 0 && active) {
       int cell = root_cell, player = root_player, node = 0, d = 0, act = 15;
       lf_path = 0;
       for (; d < kAzPath - 1;) {  // a board fills after 9 moves: bounded descent
@@ -466,16 +514,7 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
         if (f == 0xffff) break;
         const int n = (meta >> 16) & 15;
         // every read of the level issued at once, no branch: lanes >= n read the node itself
-        const int4 cr = trec[tb + (l < n ? f + l : node)];
-        const double lpb = lut_pb[pvis], lsq = lut_sq[pvis];
-        const int cv = cr.y;
-        const float q = __int_as_float(cr.z) / (float)(cv > 0 ? cv : 1);
-        const float val = cv == 0 ? 0.0f : q;
-        double pb = lpb;
-        pb *= lsq / (double)(cv + 1);
-        double sc = pb * (double)__int_as_float(cr.w) + (double)val;
-        sc = l < n ? sc : -__builtin_inf();
-        const int bi = az_group_argmax(sc, gbase);
+        const int bi = az_node_decision(trec, tb, node, f, n, pvis, lut_pb, lut_sq, l, gbase);
         node = f + bi;
         const uint32_t em = az_group_mask(l < 9 && cell == 0, gbase);
         const bool mine = l < 9 && cell == 0 && __popc(em & ((1u << l) - 1u)) == (uint32_t)bi;
@@ -539,6 +578,29 @@ __global__ void __launch_bounds__(kAzfThreads) az_search_fused_kernel(AzFusedArg
           nd.z = __float_as_int(__int_as_float(nd.z) + (((lf_depth - l) & 1) ? -v : v));
         }
       }
+    }
+    if (kCached) {
+      // refresh the cached decisions of the nodes whose inputs just changed: a node's pUCT scores depend only on
+      // its own visit count and its children's records, which change only when it lies on the backed-up path
+      // (the root after its expansion; then path[0 .. depth], the expanded leaf included). One 16-lane group per
+      // path node over all four waves, between two barriers: the path's argmaxes in parallel instead of one per
+      // level of the next walk. (Measured: wave 0 alone, four nodes per pass and no barriers, 526 vs 502 us per
+      // search.)
+      if (active && l <= lf_depth) s_path[l] = lf_path;
+      if (active && l == 0) s_path[16] = lf_depth;
+      __syncthreads();
+      const int gi = tid >> 4;
+      if (blockIdx.x < a.B && gi <= s_path[16]) {  // group-uniform
+        const int node = s_path[gi];
+        const uint64_t mv = *reinterpret_cast<const uint64_t *>(trec + node);
+        const int meta = (int)(uint32_t)mv, pvis = (int)(mv >> 32);
+        const int f = meta & 0xffff, n = (meta >> 16) & 15;
+        if (f != 0xffff) {
+          const int bi = az_node_decision(trec, 0, node, f, n, pvis, lut_pb, lut_sq, l, gbase);
+          if (l == 0) trec[node].x = (meta & ~(15 << 24)) | (bi << 24);
+        }
+      }
+      __syncthreads();
     }
   }
   az_stamp<STAMPS>(st, st_prev, 5);

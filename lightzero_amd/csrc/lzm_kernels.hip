@@ -2343,7 +2343,7 @@ int lzm_az_export_tree(int B, int S, void *ws, int32_t *visit, float *vsum, int3
 template <int R>
 static size_t az_fused_lds(int cap, int S) {
   // the double tables padded to 16 B, the node records, the network (az_search_fused_kernel's carve)
-  const size_t bytes = (size_t)((2 * (S + 1) + 81 + 1) & ~1) * 8 + (size_t)R * cap * 16;
+  const size_t bytes = (size_t)((2 * (S + 1) + 81 + 1) & ~1) * 8 + (size_t)R * cap * 16 + 128;
   return bytes + (size_t)AzNetLds<R>::total * 4;
 }
 
