@@ -778,6 +778,26 @@ def check_step(step, S, fused):
     return int(sum(tie_errors)), sdiag
 
 
+L2_SHARED_ROWS_GBS_PER_CU = 70.0  # MI355X_MICROARCH.md, "Indexed rows": rows shared by every workgroup, 66-73 GB/s per CU
+
+
+def conv_l2_stream_bytes(model):
+    """Bytes one workgroup (one root) streams from L2 per simulation in the one-launch conv searches: every
+    weight of the recurrent step — the trunk's convolutions (split-fp16: 4 B per weight), the head MLPs (f32) —
+    and, for EfficientZero, its LSTM tile: the tile's K half of 64 gate columns (split-fp16 weights) and of its
+    64 input rows (f32)."""
+    nbytes = 0
+    for net in (model.dynamics_network, model.prediction_network):
+        for m in net.modules():
+            if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear)):
+                nbytes += 4 * m.weight.numel()
+    lstm = getattr(model.dynamics_network, "lstm", None)
+    if lstm is not None:
+        k = lstm.input_size + lstm.hidden_size
+        nbytes += 2 * 64 * (k // 2) * 4
+    return nbytes
+
+
 def conv_roofline(step, model, B, S, device):
     """configs 5 / 3: the dominant kernel, search_conv_kernel / search_conv_ez_kernel (one launch = B x S
     simulations): the trunk's convolutions and EZ's LSTM gate GEMM run on the fp16 matrix pipe as split-fp16
@@ -800,7 +820,16 @@ def conv_roofline(step, model, B, S, device):
             "alg_flops_per_sim": int(flops), "alg_conv_flops_per_sim": int(conv),
             "alg_f32_tflops": round(f32, 2), "alg_f32_frac_of_fp32_peak": round(f32 / FP32_PEAK_TFLOPS, 4),
             "launch_us": round(ms[key] * 1e3, 1), "sims_per_launch": B * S,
-            "mean_search_len": round(dbar, 3)}
+            "mean_search_len": round(dbar, 3), "l2_stream": l2_stream(conv_l2_stream_bytes(model), S, sec)}
+
+
+def l2_stream(bytes_per_sim, S, sec):
+    """the L2 weight stream of one workgroup (one root per CU) against the rate the MI355X guide measured for rows
+    shared by every workgroup (served by the XCD's L2): the practical bound of a stream every CU reads at once"""
+    gbs = bytes_per_sim * S / sec / 1e9
+    return {"bytes_per_sim_per_workgroup": int(bytes_per_sim), "achieved_GBs_per_cu": round(gbs, 1),
+            "ref_GBs_per_cu": L2_SHARED_ROWS_GBS_PER_CU, "frac": round(gbs / L2_SHARED_ROWS_GBS_PER_CU, 3),
+            "ref_source": "MI355X_MICROARCH.md Indexed rows: 2,048 rows shared by every workgroup, 66-73 GB/s per CU"}
 
 
 def mlp_roofline(step, B, S, device):
