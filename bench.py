@@ -866,7 +866,8 @@ def mlp_roofline(step, B, S, device):
                 "l2_weight_bytes_per_launch": int(l2), "l2_achieved_TBs": round(l2 / sec / 1e12, 3),
                 "l2_peak_TBs": L2_PEAK_TBS, "roots_per_workgroup": R,
                 "launch_us": round(ms["search_mlp"] * 1e3, 1), "sims_per_launch": B * S,
-                "mean_search_len": round(dbar, 3)}
+                "mean_search_len": round(dbar, 3),
+                "l2_stream": l2_stream(l2 / (-(-B // R) * S), S, sec)}
     byt = algorithmic_bytes(B, 2, 128, 601, dbar)
     dom = max(ms, key=lambda k: ms[k])
     achieved = byt[dom] / (ms[dom] * 1e-3) / 1e9
