@@ -556,6 +556,29 @@ __device__ __forceinline__ void bx_range_reduce(BxRange &rg) {
 #pragma unroll
   for (int s = 0; s < 8; ++s) bx_range_step(rg, s);
 }
+// The form the kernels use: each wave reduces its epilogue's lane maxima (unsigned bits of outputs >= +0 or NaN:
+// a NaN of either sign above +inf) to one word in its LDS slot before the barrier that follows every epilogue,
+// and after it every lane takes the layer output's exact max from the four slots (bx_range_take). (Measured
+// against the staged reduction above — one butterfly step per weight chunk inside the next convolution —
+// Breakout search 1.665 vs 1.687 ms, Pong even; profiles/r06/range/.)
+__device__ __forceinline__ void bx_post_umax(uint32_t *slot, uint32_t mx, int wv, int lane) {
+  mx = max(mx, (uint32_t)xor_partner<32>((int)mx));
+  mx = max(mx, (uint32_t)xor_partner<16>((int)mx));
+  mx = max(mx, (uint32_t)xor_partner<8>((int)mx));
+  mx = max(mx, (uint32_t)xor_partner<4>((int)mx));
+  mx = max(mx, (uint32_t)xor_partner<2>((int)mx));
+  mx = max(mx, (uint32_t)xor_partner<1>((int)mx));
+  if (lane == 0) slot[wv] = mx;
+}
+// after the barrier that follows an epilogue storing at scale s_out (slot: its four wave maxima): the layer
+// output's exact max, checked against its scale; it is the next layer's input
+__device__ __forceinline__ void bx_range_take(BxRange &rg, const uint32_t *slot, int s_out) {
+  rg.s_in = s_out;
+  if (LZM_RANGE_DIAG >= 1) return;
+  const float M = bx_read_max(slot);
+  rg.bad |= !(M * bx_pow2(s_out) < 65504.f);
+  rg.m_in = M;
+}
 
 // 1x1 layer (<= 32 out channels, waves 0 and 1): relu(conv x inv[c] 2^-s_in + b) -> global [c][p]
 // (SC1: 16-B sc1 buffer stores, for planes another CU reads in the same launch); returns the lane's max |v| (bits)
@@ -613,7 +636,7 @@ template <int AHEAD>
 __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1))) void conv_trunk_bx_kernel(
     ConvTrunkArgs a) {
   extern __shared__ uint4 bx_lds4[];
-  __shared__ uint32_t s_mx[4], s_rmx[2], s_lm[2][kCvThreads];
+  __shared__ uint32_t s_mx[4], s_rmx[2], s_wm[2][4];
   __shared__ float4 s_bd[kBxMaxLayers];
   uint16_t *lds = reinterpret_cast<uint16_t *>(bx_lds4);
   auto buf = [&](int i) { return lds + i * kBxBuf; };
@@ -664,16 +687,15 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       for (int t = 0; t < 4; ++t) am[t] = amap[4 * t + (lane >> 4)];
     }
     bxf4 acc[4];
-    const bool gather = i > i0;  // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow
-    bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&](int s) {
-      if (gather && s < 8) bx_range_step(rg, s);
-    });
+    bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
     if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
     const int s_out = bx_layer_scale(bdi, i == 0 || second, rg);
-    s_lm[i & 1][tid] = bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
-                                    i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c);
+    bx_post_umax(s_wm[i & 1],
+                 bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres, i == 0 || second,
+                              i == 0 || second, bx_pow2(s_out), lane, c),
+                 wv, lane);
     __syncthreads();
-    bx_range_fetch(rg, s_lm[i & 1], s_out, lane);
+    bx_range_take(rg, s_wm[i & 1], s_out);
     if (i == 2 * a.n_dres) {  // the next latent (registers, exact) and the reward planes
       float *dst = a.out_latent + (int64_t)b * kCvCh * kCvPix + c * kCvPix + 4 * (lane >> 4);
 #pragma unroll
@@ -689,7 +711,6 @@ __global__ __launch_bounds__(kCvThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   if (wv < 2)
     bx_conv1_layer<0>(buf(n3 & 1), a.w + L.hw, a.w + L.hb, inv + (n3 + 1) * 64, bx_pow2(-rg.s_in), a.h_ch,
                       a.out_h + (int64_t)b * a.h_ch * kCvPix, lane, wv);
-  bx_range_reduce(rg);  // the last layer's output, checked
   if (a.xscale) {  // the LSTM input row's scale (every wave reaches this barrier)
     __syncthreads();
     if (tid == 0) a.xscale[b] = ls_row_exp(__uint_as_float(max(s_rmx[0], s_rmx[1])));

@@ -480,7 +480,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   auto layer_w = [&](int i) { return p.w + bx_layer_off(L, p.n_dres, i); };
   auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   BxRing<AHEAD> ring;
-  __shared__ uint32_t s_mx[4], s_lm[2][kScThreads];
+  __shared__ uint32_t s_mx[4], s_wm[2][4];
   int range_bad = 0;
   float *lmax = smem + p.off_lmax;  // the exact max |x| of this root's pool latents, by slot (lzm_conv.h "Range")
   {  // slot 0: the root's latent
@@ -590,11 +590,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         const float4 bdi = wbd[i];
         const float wsc = winv[i * 64 + c];
         bxf4 acc[4];
-        // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow (the latent's: filed)
-        bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&](int s) {
-          if (i > 0 && s < 8) bx_range_step(rg, s);
-          if (i > 0 && s == 8 && i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
-        });
+        bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
         if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
         if (i == 0 && late) {
           // late draw: the look-back and the tie's draw, then the action's map for the epilogue — by every
@@ -621,10 +617,13 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           sc_load_amap(am, p.actmap, action, c, lane);
         }
         const int s_out = bx_layer_scale(bdi, i == 0 || second, rg);
-        s_lm[i & 1][tid] = bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
-                                        i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c);
+        bx_post_umax(s_wm[i & 1],
+                     bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
+                                  i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c),
+                     wv, lane);
         __syncthreads();
-        bx_range_fetch(rg, s_lm[i & 1], s_out, lane);
+        bx_range_take(rg, s_wm[i & 1], s_out);  // (the latent's max: filed)
+        if (i == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
         if (i == 2 * p.n_dres) {  // the next latent (registers, exact) and the reward planes
           float *dst = p.pool + ((size_t)(k + 1) * B + b) * (kCvCh * kCvPix) + c * kCvPix + 4 * (lane >> 4);
 #pragma unroll
@@ -638,8 +637,6 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
       if (wv < 2)
         bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, winv + (n3 + 1) * 64, bx_pow2(-rg.s_in), p.h_ch, lhd,
                           lane, wv);
-      bx_range_reduce(rg);  // the last layer's output, checked (and filed when it is the latent)
-      if (n3 - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
       range_bad |= rg.bad;
     }
     __syncthreads();
@@ -893,7 +890,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   auto layer_w = [&](int i) { return p.w + bx_layer_off(L, p.n_dres, i); };
   auto wave_stream = [&](const float *w) { return reinterpret_cast<const uint4 *>(w) + wv * 18 * kBxTerms * 64; };
   BxRing<AHEAD> ring;
-  __shared__ uint32_t s_mx[4], s_rmx[2], s_lm[2][kScThreads];
+  __shared__ uint32_t s_mx[4], s_rmx[2], s_wm[2][4];
   int range_bad = 0;
   float *lmax = smem + p.off_lmax;  // the exact max |x| of this root's pool latents, by slot (lzm_conv.h "Range")
   if (has_root) {  // slot 0: the root's latent
@@ -1008,11 +1005,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           const float4 bdi = wbd[i];
           const float wsc = winv[i * 64 + c];
           bxf4 acc[4];
-          // the input's max: the previous epilogue's lane maxima, reduced in the MFMA shadow (the latent's: filed)
-          bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc, [&](int s) {
-            if (i > 0 && s < 8) bx_range_step(rg, s);
-            if (i > 0 && s == 8 && i - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
-          });
+          bx_conv<18, AHEAD, 0>(buf(i & 1), wave_stream(w), ring, lane, acc);
           if (i + 1 < n3) bx_prefetch<18, AHEAD, 0>(ring, wave_stream(layer_w(i + 1)), lane);
           if (i == 0 && late) {
             // late draw: the look-back and the tie's draw, then the action's map for the epilogue — by every
@@ -1038,10 +1031,13 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
             sc_load_amap(am, p.actmap, action, c, lane);
           }
           const int s_out = bx_layer_scale(bdi, i == 0 || second, rg);
-          s_lm[i & 1][tid] = bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
-                                          i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c);
+          bx_post_umax(s_wm[i & 1],
+                       bx_epilogue3(acc, buf((i + 1) & 1), wsc * bx_pow2(-rg.s_in), bc, i == 0, am, xres,
+                                    i == 0 || second, i == 0 || second, bx_pow2(s_out), lane, c),
+                       wv, lane);
           __syncthreads();
-          bx_range_fetch(rg, s_lm[i & 1], s_out, lane);
+          bx_range_take(rg, s_wm[i & 1], s_out);  // (the latent's max: filed)
+          if (i == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
           if (i == 2 * p.n_dres) {  // the next latent (registers, exact) and the reward planes
             // the latent by sc1 (write-through) stores, which do not keep the line in this XCD's L2: 16 KB
             // per root and simulation that would otherwise push the LSTM weights and the trunk's out of
@@ -1063,8 +1059,6 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
         if (wv < 2)
           bx_conv1_layer<0>(buf(n3 & 1), p.w + L.hw, p.w + L.hb, winv + (n3 + 1) * 64, bx_pow2(-rg.s_in), p.h_ch, lhd,
                             lane, wv);
-        bx_range_reduce(rg);  // the last layer's output, checked (and filed when it is the latent)
-        if (n3 - 1 == 2 * p.n_dres && tid == 0) lmax[k + 1] = rg.m_in;
         range_bad |= rg.bad;
       }
       // publish the LSTM input row: every storing wave drained, one barrier, one flag store
