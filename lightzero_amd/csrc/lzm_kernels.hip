@@ -2861,10 +2861,10 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d simulations > reserved %d (lzm_reserve)", S, h->sims_cap);
     return LZM_ERR_CAPACITY;
   }
-  const int cus = device_cus();
-  if (h->B > cus || h->B > 256) {
-    snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d roots > min(%d CUs, 256) (one co-resident workgroup per root)",
-             h->B, cus);
+  // one workgroup per root; roots beyond the CUs queue behind the first ones (their look-back waits only on
+  // lower roots: lzm_search_conv.h sc_lookback)
+  if (h->B > kScMaxRoots) {
+    snprintf(g_err, sizeof(g_err), "lzm_search_conv: %d roots > %d", h->B, kScMaxRoots);
     return LZM_ERR_ARG;
   }
   int rc = fill_lut(h, pb_c_base, pb_c_init);

@@ -39,6 +39,7 @@
 namespace lzm {
 
 constexpr int kScThreads = 256;
+constexpr int kScMaxRoots = 1024;  // search_conv_kernel: roots per launch (one workgroup each, queued past the CUs)
 
 struct ConvSearchArgs {
   // tree (HBM, whole batch; the kernel stages root b's slice)
@@ -119,16 +120,18 @@ __device__ __forceinline__ bool sc_give_up(int32_t *err, unsigned long long t0) 
 }
 
 // Parity-mode draw offset of root b in simulation k: the sum of the depth flags of roots < b (the
-// reference's single rand() stream, cnode.cpp:783-796). Wave-wide, b <= 256 (lzm_search_conv checks
-// B <= 256): sc_lookback_issue puts every flag of a lane in flight (four loads), sc_lookback_finish
-// spins (bounded, counted in err[0]) on the ones not yet published and returns the wave-uniform
-// sum. The late draw issues before the dynamics conv and finishes after it, so the cross-XCD
-// round trip of the flag loads overlaps the MFMAs.
+// reference's single rand() stream, cnode.cpp:783-796). Wave-wide, in chunks of 256 roots (four flags per
+// lane): sc_lookback_issue puts the first chunk's flags in flight, sc_lookback_finish spins (bounded, counted
+// in err[0]) on the ones not yet published, then issues and sums every further chunk, and returns the
+// wave-uniform sum. The late draw issues before the dynamics conv and finishes after it, so the cross-XCD
+// round trip of the first chunk's loads overlaps the MFMAs. (B above the CU count: the grid is dispatched in
+// block order, every root < 256 is resident from the start and a later root waits only on lower ones, which
+// never wait on it: the waits end within one search.)
 __device__ __forceinline__ void sc_lookback_issue(const ConvSearchArgs &p, int k, int b, unsigned long long epoch,
-                                                  int lane, unsigned long long (&v)[4]) {
+                                                  int lane, unsigned long long (&v)[4], int c0 = 0) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const int q = 64 * u + lane;
+    const int q = c0 + 64 * u + lane;
     v[u] = q < b ? __hip_atomic_load(&p.flags[(size_t)k * p.B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                  : (epoch << 32);
   }
@@ -137,19 +140,22 @@ __device__ __forceinline__ void sc_lookback_issue(const ConvSearchArgs &p, int k
 __device__ __forceinline__ int sc_lookback_finish(const ConvSearchArgs &p, int k, int b, unsigned long long epoch,
                                                   int lane, unsigned long long (&v)[4]) {
   int base = 0;
+  for (int c0 = 0; c0 == 0 || c0 < b; c0 += 256) {  // wave-uniform
+    if (c0 > 0) sc_lookback_issue(p, k, b, epoch, lane, v, c0);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int q = 64 * u + lane;
-    const unsigned long long t0 = (v[u] >> 32) != epoch ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    while ((v[u] >> 32) != epoch) {
-      if (sc_give_up(p.err, t0)) {
-        v[u] = epoch << 32;
-        break;
+    for (int u = 0; u < 4; ++u) {
+      const int q = c0 + 64 * u + lane;
+      const unsigned long long t0 = (v[u] >> 32) != epoch ? __builtin_amdgcn_s_memrealtime() : 0ull;
+      while ((v[u] >> 32) != epoch) {
+        if (sc_give_up(p.err, t0)) {
+          v[u] = epoch << 32;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v[u] = __hip_atomic_load(&p.flags[(size_t)k * p.B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __builtin_amdgcn_s_sleep(1);
-      v[u] = __hip_atomic_load(&p.flags[(size_t)k * p.B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      base += (int)(v[u] & 0xffffffffu);
     }
-    base += (int)(v[u] & 0xffffffffu);
   }
   return xor_sum(base);
 }

@@ -277,12 +277,13 @@ class MuZeroMCTSCtree(object):
 
     def _fused_conv(self, model, t, shape):
         """The native split-precision FoldedConvNet when the whole search can run as one lzm_search_conv
-        launch (conv MuZeroModel, 64 x 8 x 8 latent, packed heads with K multiples of 128, one root
-        per CU); None otherwise (the generic per-simulation path). cfg.fused_search (default on) and
+        launch (conv MuZeroModel, 64 x 8 x 8 latent, packed heads with K multiples of 128, one workgroup
+        per root, up to 1024 roots: past the CU count they queue); None otherwise (the generic
+        per-simulation path). cfg.fused_search (default on) and
         LZM_FUSED_CONV=0 turn it off."""
         if not self._cfg.get('fused_search', True) or t.ez or os.environ.get("LZM_FUSED_CONV", "1") == "0":
             return None
-        if tuple(shape) != (64, 8, 8) or t.B > min(256, _device_cus(t.device)):
+        if tuple(shape) != (64, 8, 8) or t.B > 1024:  # (lzm_search_conv: kScMaxRoots)
             return None
         net = _step_net(self, model)
         hp = getattr(net, "heads", None)

@@ -175,6 +175,21 @@ def test_fused_conv_search_equals_generic(kind, B, S, rng, zero):
         oracle_replay(kind, a, B, S)
 
 
+def test_fused_conv_search_beyond_cu_count():
+    """the one-launch MuZero conv search with more roots than CUs (600: the workgroups past the CU count queue
+    behind the first ones, and each look-back sums three 256-root chunks) — the fused path runs and equals the
+    generic path and the oracle bit for bit"""
+    B, S = 600, 20
+    model = conv_model("mz", 15)
+    a, b = [run_search("mz", B, S, seed=16, model=model, fused=f) for f in (True, False)]
+    assert a["path"] in ("fused", "fused-conv") and b["path"] == "generic", (a["path"], b["path"])
+    for key in ("dist", "values", "traj"):
+        assert np.array_equal(a[key], b[key]), key
+    for key in ("x", "action", "search_len", "decoded", "policy_logits"):
+        assert np.array_equal(a["rec"][key], b["rec"][key]), key
+    oracle_replay("mz", a, B, S)
+
+
 def test_fused_ez_search_pools_equal_generic():
     """the one-launch EZ search files the same latent and LSTM state pools as the generic path
     (next latents, reset-masked h / c slots, mcts_ctree.py:805-816)"""
