@@ -137,24 +137,33 @@ __device__ __forceinline__ void sc_lookback_issue(const ConvSearchArgs &p, int k
   }
 }
 
+__device__ __forceinline__ int sc_lookback_chunk(const ConvSearchArgs &p, int k, int b, unsigned long long epoch,
+                                                  int lane, unsigned long long (&v)[4], int c0) {
+  int base = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int q = c0 + 64 * u + lane;
+    const unsigned long long t0 = (v[u] >> 32) != epoch ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    while ((v[u] >> 32) != epoch) {
+      if (sc_give_up(p.err, t0)) {
+        v[u] = epoch << 32;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      v[u] = __hip_atomic_load(&p.flags[(size_t)k * p.B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    base += (int)(v[u] & 0xffffffffu);
+  }
+  return base;
+}
+
 __device__ __forceinline__ int sc_lookback_finish(const ConvSearchArgs &p, int k, int b, unsigned long long epoch,
                                                   int lane, unsigned long long (&v)[4]) {
-  int base = 0;
-  for (int c0 = 0; c0 == 0 || c0 < b; c0 += 256) {  // wave-uniform
-    if (c0 > 0) sc_lookback_issue(p, k, b, epoch, lane, v, c0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int q = c0 + 64 * u + lane;
-      const unsigned long long t0 = (v[u] >> 32) != epoch ? __builtin_amdgcn_s_memrealtime() : 0ull;
-      while ((v[u] >> 32) != epoch) {
-        if (sc_give_up(p.err, t0)) {
-          v[u] = epoch << 32;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        v[u] = __hip_atomic_load(&p.flags[(size_t)k * p.B + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      base += (int)(v[u] & 0xffffffffu);
+  int base = sc_lookback_chunk(p, k, b, epoch, lane, v, 0);
+  if (b > 256) {  // wave-uniform; the common case (B <= 256) keeps the one-chunk straight line
+    for (int c0 = 256; c0 < b; c0 += 256) {
+      sc_lookback_issue(p, k, b, epoch, lane, v, c0);
+      base += sc_lookback_chunk(p, k, b, epoch, lane, v, c0);
     }
   }
   return xor_sum(base);
