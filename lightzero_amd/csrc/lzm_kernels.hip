@@ -2908,12 +2908,23 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_lg = (int)o; o += round4((size_t)Vr + Vv + h->A);
   p.off_seed = (int)o; o += round4((size_t)S + 32);
   p.off_lmax = (int)o; o += round4((size_t)S + 1);
-  const size_t lds = o * sizeof(float);
-  if (lds > kMaxLds) {
+  if (o * sizeof(float) > kMaxLds) {
     snprintf(g_err, sizeof(g_err), "lzm_search_conv: %zu B of LDS needed (tree too large: lower num_simulations)",
-             lds);
+             o * sizeof(float));
     return LZM_ERR_ARG;
   }
+  // the head hidden layers' first half-head resident in LDS when it fits and every root has a CU of its own
+  // (more roots than CUs: the smaller footprint lets two workgroups share one)
+  constexpr size_t kPinFloats = (size_t)kHdParts * 16 * 32 * 4;
+  const char *pin_env = getenv("LZM_CONV_PIN");
+  const int pin_max = pin_env ? atoi(pin_env) : 1;
+  p.off_wpin = (int)o;
+  p.npin = 0;
+  while (p.npin < pin_max && p.npin < 6 && h->B <= device_cus() && (o + kPinFloats) * sizeof(float) <= kMaxLds) {
+    o += kPinFloats;
+    ++p.npin;
+  }
+  const size_t lds = o * sizeof(float);
   const bool stamps = getenv("LZM_PHASE_TIMING") && atoi(getenv("LZM_PHASE_TIMING")) > 0;
   if (stamps && !h->phase) {
     LZM_HIP(hipMalloc(&h->phase, (64 + 1024) * sizeof(unsigned long long)));

@@ -100,6 +100,7 @@ struct ConvSearchArgs {
   // dynamic LDS plan: float offsets (the two activation buffers come first)
   int off_stat, off_meta, off_val, off_lut, off_legal, off_path, off_pact, off_pbt, off_r, off_hd, off_hid, off_part,
       off_lg, off_seed, off_lmax;
+  int off_wpin, npin;  // LDS copy of the first npin half-heads of w1t (sc_heads_hidden_rs), 64 KiB each
 };
 
 // Bounded waits of the one-launch conv searches (their grid must be co-resident; the host checks the static
@@ -295,6 +296,17 @@ __device__ __forceinline__ void sc_head_hidden_rs(const float *in, int K, const 
   __syncthreads();
 }
 
+// The first npin half-heads of w1t (half s: head s / 2, K steps 16 (s % 2) .. + 15 of every K part) copied
+// into LDS once per launch: the head hidden layers' first half-head then reads LDS instead of joining the
+// shared-rows L2 stream (§5.2 of DESIGN.md), and its exposed first round trip goes away.
+__device__ __forceinline__ void sc_stage_wpin(float4 *pin, int npin, const float *w1t, int tid) {
+  const float4 *w4 = reinterpret_cast<const float4 *>(w1t);
+  for (int e = tid; e < npin * kHdParts * 16 * 32; e += kScThreads) {
+    const int c = e & 31, q = (e >> 5) & 15, pt = (e >> 9) % kHdParts, s = (e >> 9) / kHdParts;
+    pin[e] = w4[(((s >> 1) * kHdParts + pt) * 32 + 16 * (s & 1) + q) * 32 + c];
+  }
+}
+
 // NH hidden layers (heads H0 .. H0 + NH - 1 of w1t) in one pass, sc_head_hidden's arithmetic and
 // order for each head (same bits): the weights stream as 2 NH half-heads of 16 float4s per lane, the
 // next half's loads in flight while the FMAs consume the current one, so the heads' L2 streams run
@@ -304,7 +316,8 @@ __device__ __forceinline__ void sc_head_hidden_rs(const float *in, int K, const 
 // simulation.)
 template <int NH, int H0>
 __device__ __forceinline__ void sc_heads_hidden_rs(const float *const (&in)[NH], const int (&K)[NH], const float *w1t,
-                                                   const float *b1, float *part, float *hid, int tid) {
+                                                   const float *b1, float *part, float *hid, int tid,
+                                                   const float4 *pin = nullptr, int npin = 0) {
   const int pt = tid >> 5, c = tid & 31;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(w1t), 0, 3 * kHdParts * 32 * 32 * 16, 0x00020000);
@@ -318,7 +331,12 @@ __device__ __forceinline__ void sc_heads_hidden_rs(const float *const (&in)[NH],
   for (int h = 0; h < NH; ++h) acc[h] = 0.0f;
   auto load = [&](int s, float4(&W)[16]) __attribute__((always_inline)) {
     const int h = s >> 1, half = s & 1;
-    if (on[h]) {
+    if (s < npin) {  // (uniform) the LDS copy, sc_stage_wpin's layout
+      if (on[h]) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) W[q] = pin[((s * kHdParts + pt) * 16 + q) * 32 + c];
+      }
+    } else if (on[h]) {
 #pragma unroll
       for (int q = 0; q < 16; ++q)
         W[q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
@@ -468,6 +486,8 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   }
   if (!FAST && tid < 31) s_pow[tid] = p.pow16807[tid];
   bx_zero_borders(sc_lds4, tid, kScThreads);
+  float4 *lpin = reinterpret_cast<float4 *>(smem + p.off_wpin);
+  sc_stage_wpin(lpin, p.npin, p.w1t, tid);
   if (tid == 0) {
     s_mm[0] = p.step_fresh ? make_float4(kFloatMin, kFloatMax, p.step_delta, 0.0f) : p.minmax[b];
     s_vtp0 = p.vtp_in[b];
@@ -660,7 +680,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
     {
       const float *const in[3] = {lr, lhd, lhd + p.off_policy};
       const int K[3] = {p.Kr, p.off_policy, p.Khd - p.off_policy};
-      sc_heads_hidden_rs<3, 0>(in, K, p.w1t, p.b1, lpart, lhid, tid);
+      sc_heads_hidden_rs<3, 0>(in, K, p.w1t, p.b1, lpart, lhid, tid, lpin, p.npin);
     }
     stamp(3);
     // output columns (w2q [8][N2][4]: float4 k4 of column j at (k4 * N2 + j), so a wave-instruction
