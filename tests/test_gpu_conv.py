@@ -190,6 +190,24 @@ def test_fused_conv_search_beyond_cu_count():
     oracle_replay("mz", a, B, S)
 
 
+def test_fused_conv_search_head_weight_copy_on_off(monkeypatch):
+    """the Breakout search's LDS copy of the first head half-head (default on when every root has a CU) against
+    LZM_CONV_PIN=0 (every head weight from L2): the same bits, and both equal the oracle"""
+    B, S = 256, 20
+    model = conv_model("mz", 17)
+    runs = []
+    for pin in ("1", "0"):
+        monkeypatch.setenv("LZM_CONV_PIN", pin)
+        runs.append(run_search("mz", B, S, seed=18, model=model, fused=True))
+    a, b = runs
+    assert a["path"] in ("fused", "fused-conv") and b["path"] == a["path"], (a["path"], b["path"])
+    for key in ("dist", "values", "traj"):
+        assert np.array_equal(a[key], b[key]), key
+    for key in ("x", "action", "search_len", "decoded", "policy_logits"):
+        assert np.array_equal(a["rec"][key], b["rec"][key]), key
+    oracle_replay("mz", a, B, S)
+
+
 def test_fused_ez_search_pools_equal_generic():
     """the one-launch EZ search files the same latent and LSTM state pools as the generic path
     (next latents, reset-masked h / c slots, mcts_ctree.py:805-816)"""
