@@ -151,13 +151,17 @@ def test_trajectory_return_gloo_world2(tmp_path, kind, mode):
     """all_gather: every rank ends with every rank's episodes; gather: the learner (rank 0) alone does —
     CartPole vectors and config 5's u8 image frames (one flat byte buffer per rank on the wire, unpacked
     to the reference's float32 frame / 255); the statistics are summed on every rank"""
-    from lightzero_amd.trajectory import TrajBlock, unpack_episodes
     world = 2
     mp.spawn(_traj_worker, args=(world, _free_port(), str(tmp_path), kind, mode), nprocs=world, join=True)
+    _check_gathered(tmp_path, world, kind, mode)
+
+
+def _check_gathered(tmp_path, world, kind, mode):
+    from lightzero_amd.trajectory import TrajBlock, unpack_episodes
     for me in range(world):
         r = np.load(tmp_path / f"r{me}.npz")
         n_eps = sum(len(_fake_records(k)[1]) for k in range(world))
-        assert tuple(r["stats"]) == (30.0, float(n_eps), 0.5)
+        assert tuple(r["stats"]) == (10.0 * world * (world + 1) / 2, float(n_eps), 0.25 * world)
         if mode == "gather" and me != 0:
             assert "f0" not in r.files  # nothing received off the learner
             continue
@@ -225,3 +229,13 @@ def test_image_episode_segments_frame_stack():
         assert np.array_equal(seg.obs_segment[:fs + n], window[s0:s0 + fs + n])
         assert np.array_equal(seg.action_segment, ep["action_segment"][s0:s0 + n])
     assert sum(len(s.action_segment) for _, _, s, _, _ in segs) == L
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["all_gather", "gather"])
+def test_trajectory_return_gloo_world4(tmp_path, mode):
+    """four ranks (the driver's 8-GPU node runs 1, 2, 4 and 8): config 5's u8 frames with ragged episode
+    counts per rank, every receiving rank holding every rank's episodes in rank order"""
+    world = 4
+    mp.spawn(_traj_worker, args=(world, _free_port(), str(tmp_path), "image", mode), nprocs=world, join=True)
+    _check_gathered(tmp_path, world, "image", mode)
