@@ -548,11 +548,11 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)b, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
           return o.x >> 1;
         };
-        d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+        d = descend_wave<false, false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
       } else {
         TieInfo ti;
         auto nodraw = [](int) -> uint32_t { return 0u; };
-        d = descend_wave<false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
+        d = descend_wave<false, true, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
         if (STAMPS && tid == 0) {
           st_acc[10] += __builtin_amdgcn_s_memtime() - st_w0;
           st_acc[11] += d.len;              // levels walked (diagnostics)
@@ -565,7 +565,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
           // the depth depends on the draws: look back, walk with them, then publish
           const int base = sc_lookback(p, k, b, epoch, lane);
           const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, 0, t.depth_cap, p.err + 1);
-          d = descend_wave<false, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+          d = descend_wave<false, false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
           if (lane == 0)
             __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -959,11 +959,11 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
             uint4 o = philox4x32_10(make_uint4((uint32_t)level, (uint32_t)b, 0u, 0u), make_uint2(seed, 0x4c5a4d43u));
             return o.x >> 1;
           };
-          d = descend_wave<true, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+          d = descend_wave<true, false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
         } else {
           TieInfo ti;
           auto nodraw = [](int) -> uint32_t { return 0u; };
-          d = descend_wave<true, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
+          d = descend_wave<true, true, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, nodraw, &ti);
           if (lane == 0 && ti.status != 2)
             __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -971,7 +971,7 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
             // the depth depends on the draws: look back, walk with them, then publish
             const int base = sc_lookback(p, k, b, epoch, lane);
             const LaneDraws draw = lane_draws(p.coef, p.coef_positions, s_z0, base, 0, t.depth_cap, p.err + 1);
-            d = descend_wave<true, false>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
+            d = descend_wave<true, false, true>(t, 0, 0, 1, mm, players, s_vtp0, p.disc, draw, nullptr);
             if (lane == 0)
               __hip_atomic_store(&p.flags[(size_t)k * B + b], (epoch << 32) | (unsigned)d.len, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
