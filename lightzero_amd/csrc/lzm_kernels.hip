@@ -2899,8 +2899,8 @@ extern "C" int lzm_search_conv(lzm_handle *h, int num_simulations, int pb_c_base
   p.off_legal = (int)o; o += round4((size_t)h->A + 1);
   p.off_path = (int)o; o += round4((size_t)h->depth_cap);
   p.off_pact = (int)o; o += round4((size_t)h->depth_cap);
-  p.pbt_rows = ((size_t)h->lut_n * (h->lut_n + 1) / 2 <= 4096) ? h->lut_n : 0;
-  p.off_pbt = (int)o; o += round4((size_t)p.pbt_rows * (p.pbt_rows + 1) / 2);
+  p.pbt_rows = 0;  // (no pb_c table: the MuZero conv walk divides, same bits)
+  p.off_pbt = (int)o;
   p.off_r = (int)o; o += round4((size_t)Kr);
   p.off_hd = (int)o; o += round4((size_t)Khd);
   p.off_hid = (int)o; o += 96;

@@ -469,10 +469,8 @@ __global__ __launch_bounds__(kScThreads) __attribute__((amdgpu_waves_per_eu(1, 1
   for (int e = tid; e < p.lut_n; e += kScThreads) llut[e] = p.lut[e];
   for (int e = tid; e < A; e += kScThreads) llegal[e] = p.legal[(size_t)b * A + e];
   if (tid == 0) llegal[A] = p.nlegal[b];
-  float *lpbt = smem + p.off_pbt;
-  build_pbt(p.lut, p.pbt_rows, lpbt, tid, kScThreads);
   t.stat = ls; t.meta = lm; t.val = lval; t.lut = llut; t.legal = llegal; t.nlegal = llegal + A;
-  t.pbt = p.pbt_rows ? lpbt : nullptr;
+  t.pbt = nullptr;  // the walk divides (same bits) instead of a dependent table read: Breakout walk -3%
   t.path = reinterpret_cast<int32_t *>(smem + p.off_path);
   t.path_act = reinterpret_cast<int32_t *>(smem + p.off_pact);
   t.pathlen = s_len;
